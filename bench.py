@@ -1,0 +1,163 @@
+"""Benchmark: BASELINE.json metric -- Msamples/s (N x d draws) + achieved HBM GB/s,
+LHS + Iman-Conover, d = 32 (config 3: N = 1e8 on one MI355X).
+
+One step = one full `NoOp(*ds).correlate(*ds, corr_mat=C).sample_device(N, method="lhs")`
+through the public DAG API: native LHS fused into the 32 inverse-CDF kernels (norm / gamma /
+triang / poisson x 4, BASELINE config 2 set), then the Iman-Conover reorder of all 32 columns
+(rank + scores + Gram + decorrelate/correlate + rank + gather); outputs stay in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n ROWS] [--d COLS] [--cpu-n ROWS]
+
+With N > 1 (torch.distributed.run, one process per GPU) every rank runs its own full N-row
+problem on its own seed (replicas; weak scaling) -- see DESIGN.md "Multi-GPU".
+Prints ONE JSON line on rank 0.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
+
+
+def kernel_bytes(name, n, k):
+    """Algorithmic HBM bytes of ONE launch of `name` over n rows (k = columns where a launch
+    covers all of them).  SURVEY.md §8(d) per-unit figures."""
+    per_elem = {"k_lhs_ppf": 8, "k_ppf": 16, "k_scatter": 24, "k_upsweep": 8, "k_digit_hist": 8,
+                "k_rank_finish<scores>": 28, "k_rank_finish<gather>": 28, "k_load_keys": 16,
+                "k_elementwise": 24, "k_head_bounds": 8, "k_scan": 0}
+    if name == "k_gram":
+        return 8 * n * k
+    if name == "k_apply":
+        return 16 * n * k
+    return per_elem.get(name, 0) * n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--d", type=int, default=32)
+    ap.add_argument("--cpu-n", type=int, default=262_144)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group("nccl")
+    else:
+        dist = None
+
+    from probabilit_amd import _lib, device
+    from probabilit_amd.modeling import Distribution, NoOp
+
+    dev = device.device()
+    n, d = args.n, args.d
+    base = [("norm", {"loc": 0.0, "scale": 1.0}), ("gamma", {"a": 2.0}), ("triang", {"c": 0.3}),
+            ("poisson", {"mu": 4.0}), ("norm", {"loc": 5.0, "scale": 2.0}), ("gamma", {"a": 0.7, "scale": 3.0}),
+            ("triang", {"c": 0.8, "loc": 1.0, "scale": 2.0}), ("poisson", {"mu": 30.0})]
+    dists = (base * ((d + 7) // 8))[:d]
+    A = np.random.default_rng(0).normal(size=(64, d))
+    C = 0.9 * np.corrcoef(A, rowvar=False) + 0.1 * np.eye(d)
+    ds = [Distribution(name, **kw) for name, kw in dists]
+    root = NoOp(*ds).correlate(*ds, corr_mat=C)
+    seed = args.seed + 1000 * rank
+
+    def step(i):
+        root.sample_device(n, random_state=seed + i, method="lhs")
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+
+    for i in range(args.warmup):
+        step(i)
+    lib = _lib.load()
+    lib.pbh_timing_reset()
+    lib.pbh_timing_enable(1)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    barrier()
+    t1 = time.perf_counter()
+    lib.pbh_timing_enable(0)
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = n * d * world / (ms_per_step / 1e3) / 1e6
+
+    # per-kernel device time inside the timed region (HIP events on the launching stream)
+    import ctypes
+
+    kernels = {}
+    for kid, name in enumerate(_lib.KERNELS):
+        tot, cnt = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(lib.pbh_timing_read(kid, ctypes.byref(tot), ctypes.byref(cnt)))
+        if cnt.value:
+            avg = tot.value / cnt.value
+            b = kernel_bytes(name, n, d)
+            kernels[name] = {"total_ms_per_step": round(tot.value / args.steps, 3), "launches": cnt.value,
+                             "avg_ms": round(avg, 4), "bytes_per_launch": b,
+                             "GBps": round(b / (avg / 1e3) / 1e9, 1) if b else None}
+    dom = max(kernels, key=lambda k: kernels[k]["total_ms_per_step"])
+    dk = kernels[dom]
+    achieved = dk["GBps"] or 0.0
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                "avg_launch_ms": dk["avg_ms"], "bytes_per_launch": dk["bytes_per_launch"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.cpu_n, d)
+
+    if rank == 0:
+        line = {"metric": "Msamples/s (N x d draws), LHS + ImanConover d=32", "value": round(value, 2),
+                "unit": "Msamples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "f64", "data": "synthetic (native LHS quantiles, seeded)",
+                "config": {"workload": "cfg3: d=32 (cfg2 set x4), LHS + ppf + ImanConover, N rows per GPU",
+                           "rows_per_gpu": n, "d": d, "parallelism": "replicas" if world > 1 else "single"},
+                "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels}
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(n, d):
+    """The reference's CPU path (oracle.pipeline: scipy LatinHypercube -> scipy ppf ->
+    Iman-Conover restated in numpy with the reference's calls) on this host."""
+    from threadpoolctl import threadpool_info
+
+    from oracle.pipeline import lhs_ic
+
+    t0 = time.perf_counter()
+    lhs_ic(n, d, 0)
+    dt = time.perf_counter() - t0
+    threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    return {"value": round(n * d / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"cfg3 at N={n}, d={d} ({dt:.1f} s): scipy LHS + scipy ppf + numpy/scipy Iman-Conover; "
+                      f"ppf/sort single-threaded, BLAS on {threads} threads"}
+
+
+if __name__ == "__main__":
+    main()

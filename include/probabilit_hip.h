@@ -1,0 +1,182 @@
+/*
+ * probabilit_hip.h -- C-ABI of libprobabilit_hip.so, the MI355X (gfx950) native library behind
+ * the probabilit_amd drop-in for tommyod/probabilit's Monte Carlo sampling hot path.
+ *
+ * Every entry point is extern "C", takes plain pointers and sizes (device pointers unless
+ * the name says _host), an opaque HIP stream (hipStream_t passed as void*; NULL = legacy
+ * default stream), and returns a pbh_status.  No exception crosses the ABI: on failure the
+ * call returns a non-zero status and pbh_last_error() returns a message (thread-local).
+ *
+ * Each function names the reference interface it replaces (file:line in tommyod/probabilit
+ * @ 2025-09-19, src/probabilit/...; "scipy:" = scipy 1.15.3, the reference's L0 dependency).
+ * The Python side (probabilit_amd/_lib.py) binds these with ctypes; INTEGRATION.md shows the
+ * binding a maintainer of the reference would add.
+ */
+#ifndef PROBABILIT_HIP_H_
+#define PROBABILIT_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum pbh_status {
+  PBH_OK = 0,
+  PBH_ERR_INVALID = 1,     /* bad argument (maps to ValueError / TypeError)                 */
+  PBH_ERR_HIP = 2,         /* HIP runtime failure                                          */
+  PBH_ERR_NOT_PD = 3,      /* IC rank-score correlation not positive definite (ValueError,
+                              correlation.py:399-403)                                      */
+  PBH_ERR_NONFINITE = 4,   /* non-finite input where the reference raises                   */
+  PBH_ERR_WORKSPACE = 5,   /* workspace too small                                          */
+  PBH_ERR_UNSUPPORTED = 6  /* distribution / op without a native kernel                    */
+} pbh_status;
+
+/* ---- distributions with a native inverse-CDF kernel (scipy.stats.<name>.ppf) ---- */
+typedef enum pbh_dist {
+  PBH_DIST_NORM = 0,    /* params: loc, scale                 scipy norm._ppf = ndtri        */
+  PBH_DIST_UNIFORM = 1, /* params: loc, scale                                              */
+  PBH_DIST_EXPON = 2,   /* params: loc, scale                 -log1p(-q)                     */
+  PBH_DIST_LOGNORM = 3, /* params: s, loc, scale              exp(s * ndtri(q))              */
+  PBH_DIST_TRIANG = 4,  /* params: c, loc, scale                                             */
+  PBH_DIST_GAMMA = 5,   /* params: a, loc, scale              gammaincinv(a, q)              */
+  PBH_DIST_POISSON = 6  /* params: mu, loc  (discrete)        smallest k: pdtr(k, mu) >= q   */
+} pbh_dist;
+
+/* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64
+ * (the composite-parameter broadcast of modeling.py:796-802, where a parent node's
+ * samples_ array is passed as the argument). */
+typedef struct pbh_param {
+  const double* ptr;
+  double value;
+} pbh_param;
+
+int pbh_version(void);
+const char* pbh_last_error(void);
+/* Fails (PBH_ERR_HIP) when no gfx950 device is visible; the product never runs without one. */
+int pbh_init(int device);
+
+/* ---------------------------------------------------------------- quantile generators
+ * All generators write column-major quantiles: column c of the (N, d) quantile matrix of
+ * modeling.py:478-489 at q[(c - col0) * ldq + (r - row0)], rows [row0, row0 + nrows).
+ * Rows are counter-addressed, so any row range (a shard) is generated independently. */
+
+/* Native Latin hypercube (replaces scipy.stats.qmc.LatinHypercube._random_lhs reached via
+ * modeling.py:480,488): q = (pi_c(r) + 1 - u_c(r)) / n where pi_c is a keyed bijection of
+ * [0, n) (Feistel network + cycle walking) and u_c(r) a Philox4x32-10 uniform. */
+int pbh_fill_lhs(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col0, int ncols, double* q,
+                 int64_t ldq, void* stream);
+
+/* Native pseudo-random uniforms in [0, 1) (Philox4x32-10), replaces modeling.py:484-486. */
+int pbh_fill_uniform(uint64_t seed, int64_t row0, int64_t nrows, int col0, int ncols, double* q, int64_t ldq,
+                     void* stream);
+
+/* Scrambled Sobol' points, bit-exact with scipy.stats.qmc.Sobol (modeling.py:482,488):
+ * x_r[c] = (shift[c] ^ XOR_{b in gray(r)} sv[c][b]) * 2^-bits.  sv_host is d x bits (row-major),
+ * shift_host has d entries (both produced by the host-side engine setup). */
+int pbh_fill_sobol(const uint32_t* sv_host, const uint32_t* shift_host, int d, int bits, int64_t row0,
+                   int64_t nrows, int col0, int ncols, double* q, int64_t ldq, void* stream);
+
+/* ---------------------------------------------------------------- inverse CDF sweep
+ * Distribution._sample (modeling.py:795-807) -> scipy rv_continuous.ppf / rv_discrete.ppf:
+ * out[i] = ppf(q[i * q_stride]; params) with scipy's argument checks, support bounds at
+ * q == 0 / 1, NaN for invalid input and `_ppf(q) * scale + loc` rounding (no FMA).
+ * When nonfinite_flag != NULL it is set to 1 if any output is non-finite (the check of
+ * modeling.py:600-606, fused into the producing kernel). */
+int pbh_ppf(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_param* params, int nparams,
+            double* out, int32_t* nonfinite_flag, void* stream);
+
+/* Fused generator + inverse CDF (q never touches HBM): column `col` of the native LHS
+ * design of pbh_fill_lhs pushed through `dist`.  Bit-identical to pbh_fill_lhs + pbh_ppf. */
+int pbh_lhs_ppf(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col, int dist,
+                const pbh_param* params, int nparams, double* out, int32_t* nonfinite_flag, void* stream);
+
+/* ---------------------------------------------------------------- Iman-Conover
+ * ImanConover.__call__ (correlation.py:368-425) on device:
+ *   step 1  ranks = rankdata(X, axis=0, 'average') / (N + 1); S = ndtri(ranks)     (:394-395)
+ *   step 2  E = corrcoef(S); E must be PD; L = cholesky(E)                        (:398-405)
+ *   step 3  CS = S L^-T P^T  with P = cholesky(target) (target_chol_host, K x K
+ *           row-major lower triangular, Correlator.set_target :177-178)         (:409-414)
+ *   step 4  idx = rankdata(CS[:, k]).astype(int) - 1; Y[:, k] = sort(X[:, k])[idx]  (:418-423)
+ * X element (r, c) is read at X[r * x_rs + c * x_cs]; Y is written at Y[r * y_rs + c * y_cs].
+ * Returns PBH_ERR_NOT_PD when E is not positive definite, PBH_ERR_NONFINITE for NaN/inf in X.
+ * The optional outputs (device pointers, column-major K x N, may be NULL) expose the
+ * intermediates for parity tests: scores S, correlated scores CS, step-4 indices idx. */
+typedef struct pbh_ic_args {
+  const double* X;
+  int64_t n;
+  int32_t k;
+  int64_t x_rs, x_cs;
+  const double* target_chol_host;
+  double* Y;
+  int64_t y_rs, y_cs;
+  void* ws;
+  size_t ws_bytes;
+  double* scores_out;
+  double* cscores_out;
+  int32_t* idx_out;
+  double* corr_host_out; /* optional K x K host buffer: E = corrcoef(S) */
+} pbh_ic_args;
+
+int pbh_ic_workspace_size(int64_t n, int32_t k, size_t* bytes);
+int pbh_iman_conover(const pbh_ic_args* args, void* stream);
+
+/* rankdata(x, method='average') of one device column (scipy:stats/_stats_py.py _rankdata,
+ * called at correlation.py:394 and :422).  ws >= pbh_rank_workspace_size(n). */
+int pbh_rank_workspace_size(int64_t n, size_t* bytes);
+int pbh_rankdata_average(const double* x, int64_t stride, int64_t n, double* ranks, void* ws, size_t ws_bytes,
+                         void* stream);
+
+/* ---------------------------------------------------------------- transforms
+ * Elementwise Transform nodes (modeling.py:933-1169): Variadic/Binary/UnaryTransform._sample
+ * with numpy dtype semantics.  Operands are device vectors or scalars (ptr == NULL; the
+ * lazily-broadcast Constant._sample of :760-763). */
+typedef enum pbh_dtype { PBH_BOOL = 0, PBH_INT64 = 1, PBH_FLOAT64 = 2 } pbh_dtype;
+
+typedef struct pbh_operand {
+  const void* ptr; /* device vector, or NULL for a scalar                     */
+  int32_t dtype;   /* pbh_dtype of the vector / scalar                        */
+  double f;        /* scalar value when dtype == PBH_FLOAT64 (or BOOL as 0/1)  */
+  int64_t i;       /* scalar value when dtype == PBH_INT64 / PBH_BOOL          */
+} pbh_operand;
+
+typedef enum pbh_op {
+  /* binary */
+  PBH_OP_ADD = 0, PBH_OP_SUB, PBH_OP_MUL, PBH_OP_TRUEDIV, PBH_OP_FLOORDIV, PBH_OP_MOD, PBH_OP_POW,
+  PBH_OP_MAX, PBH_OP_MIN, PBH_OP_AND, PBH_OP_OR, PBH_OP_EQ, PBH_OP_NE, PBH_OP_LT, PBH_OP_LE, PBH_OP_GT,
+  PBH_OP_GE, PBH_OP_ISCLOSE, PBH_OP_ARCTAN2,
+  /* unary */
+  PBH_OP_NEG = 32, PBH_OP_ABS, PBH_OP_LOG, PBH_OP_EXP, PBH_OP_FLOOR, PBH_OP_CEIL, PBH_OP_SIGN, PBH_OP_SQRT,
+  PBH_OP_SQUARE, PBH_OP_LOG10, PBH_OP_SIN, PBH_OP_COS, PBH_OP_TAN, PBH_OP_ARCSIN, PBH_OP_ARCCOS,
+  PBH_OP_ARCTAN, PBH_OP_SINH, PBH_OP_COSH, PBH_OP_TANH, PBH_OP_ARCSINH, PBH_OP_ARCCOSH, PBH_OP_ARCTANH,
+  PBH_OP_CAST = 63
+} pbh_op;
+
+/* out = op(a, b) (b ignored for unary ops) computed in `compute_dtype` and stored as
+ * `out_dtype` (the numpy result dtype decided on the host). */
+int pbh_elementwise(int op, int compute_dtype, int out_dtype, const pbh_operand* a, const pbh_operand* b,
+                    void* out, int64_t n, int32_t* nonfinite_flag, void* stream);
+
+/* Avg (modeling.py:986-990): out = np.average(vstack(parents), axis=0) over m float64 vectors. */
+int pbh_average(const double* const* parents_host, int m, int64_t n, double* out, int32_t* nonfinite_flag,
+                void* stream);
+
+/* Column-major <-> row-major transpose of an (rows x cols) float64 matrix (LDS-tiled). */
+int pbh_transpose(const double* in, int64_t rows, int64_t cols, int64_t ld_in, double* out, int64_t ld_out,
+                  void* stream);
+
+/* ---------------------------------------------------------------- measurement
+ * When enabled, every launch of the library's main kernels is bracketed by two HIP events
+ * recorded on the launching stream; pbh_timing_read returns the summed device time and the
+ * launch count of kernel `id` (names via pbh_kernel_name).  Used by bench.py's roofline. */
+int pbh_timing_enable(int on);
+int pbh_timing_reset(void);
+const char* pbh_kernel_name(int id);
+int pbh_timing_read(int id, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PROBABILIT_HIP_H_ */

@@ -1,0 +1,24 @@
+"""probabilit_amd -- MI355X (gfx950) native drop-in for probabilit's Monte Carlo sampling path.
+
+    import probabilit_amd as probabilit              # same names as `import probabilit`
+    from probabilit_amd.modeling import Distribution, NoOp
+    from probabilit_amd.correlation import ImanConover, nearest_correlation_matrix
+
+All sampling runs in hand-written HIP kernels (libprobabilit_hip.so, C-ABI in
+include/probabilit_hip.h); see DESIGN.md.
+"""
+
+from .modeling import (  # noqa: F401
+    Constant,
+    CumulativeDistribution,
+    DiscreteDistribution,
+    Distribution,
+    EmpiricalDistribution,
+    Equal,
+    MultivariateDistribution,
+    scalar_transform,
+)
+
+__all__ = ["Distribution", "Constant", "EmpiricalDistribution", "CumulativeDistribution", "DiscreteDistribution",
+           "Equal", "scalar_transform", "MultivariateDistribution"]
+__version__ = "0.1.0"

@@ -1,0 +1,131 @@
+"""ctypes binding of libprobabilit_hip.so (C-ABI declared in include/probabilit_hip.h).
+
+The library is the only compute path of probabilit_amd: there is no CPU fallback.  Loading
+fails loudly when the in-tree .so is missing (run `python -m probabilit_amd.build`).
+"""
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libprobabilit_hip.so")
+
+# pbh_status
+OK, ERR_INVALID, ERR_HIP, ERR_NOT_PD, ERR_NONFINITE, ERR_WORKSPACE, ERR_UNSUPPORTED = range(7)
+
+# pbh_dist
+DIST_IDS = {"norm": 0, "uniform": 1, "expon": 2, "lognorm": 3, "triang": 4, "gamma": 5, "poisson": 6}
+
+# pbh_dtype
+BOOL, INT64, FLOAT64 = 0, 1, 2
+
+# pbh_op
+OPS = {}
+for _i, _name in enumerate(["add", "sub", "mul", "truediv", "floordiv", "mod", "pow", "max", "min", "and", "or",
+                            "eq", "ne", "lt", "le", "gt", "ge", "isclose", "arctan2"]):
+    OPS[_name] = _i
+for _i, _name in enumerate(["neg", "abs", "log", "exp", "floor", "ceil", "sign", "sqrt", "square", "log10", "sin",
+                            "cos", "tan", "arcsin", "arccos", "arctan", "sinh", "cosh", "tanh", "arcsinh",
+                            "arccosh", "arctanh"]):
+    OPS[_name] = 32 + _i
+OPS["cast"] = 63
+
+# exported symbols (tests check the .so exports every one of them)
+SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fill_uniform", "pbh_fill_sobol",
+           "pbh_ppf", "pbh_lhs_ppf", "pbh_ic_workspace_size", "pbh_iman_conover", "pbh_rank_workspace_size",
+           "pbh_rankdata_average", "pbh_elementwise", "pbh_average", "pbh_transpose", "pbh_timing_enable",
+           "pbh_timing_reset", "pbh_kernel_name", "pbh_timing_read"]
+
+# kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
+KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
+           "k_rank_finish<gather>", "k_load_keys", "k_gram", "k_apply", "k_elementwise", "k_head_bounds", "k_scan"]
+
+
+class Param(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("value", ctypes.c_double)]
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("dtype", ctypes.c_int32), ("f", ctypes.c_double), ("i", ctypes.c_int64)]
+
+
+class ICArgs(ctypes.Structure):
+    _fields_ = [("X", ctypes.c_void_p), ("n", ctypes.c_int64), ("k", ctypes.c_int32), ("x_rs", ctypes.c_int64),
+                ("x_cs", ctypes.c_int64), ("target_chol_host", ctypes.c_void_p), ("Y", ctypes.c_void_p),
+                ("y_rs", ctypes.c_int64), ("y_cs", ctypes.c_int64), ("ws", ctypes.c_void_p),
+                ("ws_bytes", ctypes.c_size_t), ("scores_out", ctypes.c_void_p), ("cscores_out", ctypes.c_void_p),
+                ("idx_out", ctypes.c_void_p), ("corr_host_out", ctypes.c_void_p)]
+
+
+class NativeError(RuntimeError):
+    """A HIP runtime failure inside libprobabilit_hip."""
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the native library; raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"probabilit_amd native library not built: {LIB_PATH} is missing "
+                          "(run `python -m probabilit_amd.build`)")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, i64, i32, dbl, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
+    u64 = ctypes.c_uint64
+    sig = {
+        "pbh_version": ([], i32),
+        "pbh_last_error": ([], ctypes.c_char_p),
+        "pbh_init": ([i32], i32),
+        "pbh_fill_lhs": ([u64, i64, i64, i64, i32, i32, vp, i64, vp], i32),
+        "pbh_fill_uniform": ([u64, i64, i64, i32, i32, vp, i64, vp], i32),
+        "pbh_fill_sobol": ([vp, vp, i32, i32, i64, i64, i32, i32, vp, i64, vp], i32),
+        "pbh_ppf": ([i32, vp, i64, i64, ctypes.POINTER(Param), i32, vp, vp, vp], i32),
+        "pbh_lhs_ppf": ([u64, i64, i64, i64, i32, i32, ctypes.POINTER(Param), i32, vp, vp, vp], i32),
+        "pbh_ic_workspace_size": ([i64, ctypes.c_int32, ctypes.POINTER(sz)], i32),
+        "pbh_iman_conover": ([ctypes.POINTER(ICArgs), vp], i32),
+        "pbh_rank_workspace_size": ([i64, ctypes.POINTER(sz)], i32),
+        "pbh_rankdata_average": ([vp, i64, i64, vp, vp, sz, vp], i32),
+        "pbh_elementwise": ([i32, i32, i32, ctypes.POINTER(Operand), ctypes.POINTER(Operand), vp, i64, vp, vp], i32),
+        "pbh_average": ([ctypes.POINTER(vp), i32, i64, vp, vp, vp], i32),
+        "pbh_transpose": ([vp, i64, i64, i64, vp, i64, vp], i32),
+        "pbh_timing_enable": ([i32], i32),
+        "pbh_timing_reset": ([], i32),
+        "pbh_kernel_name": ([i32], ctypes.c_char_p),
+        "pbh_timing_read": ([i32, ctypes.POINTER(dbl), ctypes.POINTER(i64)], i32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def last_error():
+    return load().pbh_last_error().decode(errors="replace")
+
+
+def check(status, what=""):
+    """Map a pbh_status to the exception type the reference raises for the same condition."""
+    if status == OK:
+        return
+    msg = last_error()
+    if what:
+        msg = f"{what}: {msg}"
+    if status in (ERR_INVALID, ERR_NOT_PD, ERR_NONFINITE):
+        raise ValueError(msg)
+    if status == ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    if status == ERR_WORKSPACE:
+        raise MemoryError(msg)
+    raise NativeError(msg)
+
+
+def np_ptr(a):
+    """Host pointer of a C-contiguous numpy array."""
+    assert a.flags["C_CONTIGUOUS"]
+    return ctypes.c_void_p(a.ctypes.data)
+

@@ -1,0 +1,239 @@
+"""Drop-in for probabilit.correlation (src/probabilit/correlation.py @ 2025-09-19).
+
+* `ImanConover` keeps the Correlator protocol of the reference (`correlator()`,
+  `.set_target(C)`, `inst(X) -> Y` on (N, K) arrays; correlation.py:161-202, 288-425) and
+  runs the transform on the GPU through pbh_iman_conover.  numpy inputs are uploaded and the
+  result downloaded; torch device tensors stay on the device.
+* `nearest_correlation_matrix` solves the same weighted problem as the reference's cvxpy /
+  SCS formulation (correlation.py:59-150: minimise ||H o (X - G)||_F subject to diag(X) = 1
+  and X - (10 eps / n) I >= 0) with a host ADMM on the K x K matrix (cvxpy is not a
+  dependency).  It returns the optimum to ~1e-10, where SCS stops at its `eps`.
+* `Cholesky` is the next correlator on the roadmap: it raises
+  NotImplementedError instead of silently running on the CPU.
+"""
+
+import ctypes
+
+import numpy as np
+
+from . import _lib, device
+
+
+class CorrelatorError(Exception):
+    pass
+
+
+# ------------------------------------------------------------------ nearest correlation matrix
+def _project_psd(A, floor):
+    w, V = np.linalg.eigh((A + A.T) / 2.0)
+    w = np.maximum(w, floor)
+    return (V * w) @ V.T
+
+
+def nearest_correlation_matrix(matrix, *, weights=None, eps=1e-6, verbose=False):
+    """Nearest correlation matrix to `matrix` in the `weights`-weighted Frobenius norm.
+
+    Same problem as correlation.py:59-150 (Qi & Sun's H-weighted formulation, eq. (3)):
+    minimise ||H o (X - G)||_F  s.t.  diag(X) = 1,  X >= (10 eps / n) I.
+    Solved by ADMM on the splitting X (PSD cone, shifted) = Y (unit diagonal, weighted
+    least squares), which is exact at convergence; feasible inputs are returned as-is.
+    """
+    if not isinstance(matrix, np.ndarray):
+        raise TypeError("Input argument `matrix` must be np.ndarray.")
+    if not matrix.ndim == 2 and matrix.shape[0] == matrix.shape[1]:
+        raise ValueError("Input argument `matrix` must be square.")
+    G = np.array(matrix, dtype=float)
+    H = np.ones_like(G) if weights is None else weights
+    if not isinstance(H, np.ndarray):
+        raise TypeError("Input argument `weights` must be np.ndarray.")
+    if not (H.shape == G.shape):
+        raise ValueError("Argument `weights` must have same shape as `matrix`.")
+    n = G.shape[0]
+    floor = (eps / n) * 10
+
+    # already feasible (to rounding): the optimum is G itself, returned unchanged so that a
+    # valid target reaches the correlator bit for bit (e.g. 0.9 * corrcoef(A) + 0.1 * I)
+    if np.allclose(G, G.T, rtol=0, atol=1e-12) and np.allclose(np.diag(G), 1.0, rtol=0, atol=1e-12):
+        if np.linalg.eigvalsh((G + G.T) / 2).min() >= floor:
+            return G.copy()
+
+    H2 = np.asarray(H, dtype=float) ** 2
+    rho = max(float(np.mean(H2)), 1e-3)
+    Y = (G + G.T) / 2.0
+    np.fill_diagonal(Y, 1.0)
+    U = np.zeros_like(G)
+    X = Y
+    for it in range(20000):
+        X = _project_psd(Y - U, floor)
+        Y_old = Y
+        Y = (H2 * G + rho * (X + U)) / (H2 + rho)
+        np.fill_diagonal(Y, 1.0)
+        U = U + X - Y
+        r = np.linalg.norm(X - Y)
+        s = rho * np.linalg.norm(Y - Y_old)
+        if verbose and it % 100 == 0:
+            print(f"ncm admm it={it} primal={r:.3e} dual={s:.3e} rho={rho:.3e}")
+        if r < 1e-12 * n and s < 1e-12 * n:
+            break
+        if r > 10 * s:  # residual balancing
+            rho *= 2.0
+            U /= 2.0
+        elif s > 10 * r:
+            rho /= 2.0
+            U *= 2.0
+    # exact unit diagonal while keeping the eigenvalue floor: project, rescale, re-project
+    X = _project_psd(X, floor)
+    d = np.sqrt(np.diag(X))
+    X = X / d[:, None] / d[None, :]
+    X = (X + X.T) / 2.0
+    np.fill_diagonal(X, 1.0)
+    is_symmetric = np.allclose(X, X.T)
+    is_PD = np.linalg.eig(X)[0].min() > 0
+    if not (is_symmetric and is_PD) and (eps > 1e-14):
+        if verbose:
+            print(f"Recursively calling solver with eps := {eps} / 10")
+        return nearest_correlation_matrix(G, weights=H, eps=eps / 10, verbose=verbose)
+    return X
+
+
+def _is_positive_definite(X):
+    try:
+        np.linalg.cholesky(X)
+        return True
+    except np.linalg.LinAlgError:
+        return False
+
+
+class Correlator:
+    """Correlator protocol (correlation.py:161-202): set_target validates and factors C."""
+
+    def set_target(self, correlation_matrix):
+        if not isinstance(correlation_matrix, np.ndarray):
+            raise TypeError("Input argument `correlation_matrix` must be NumPy array.")
+        if not correlation_matrix.ndim == 2:
+            raise ValueError("Correlation matrix must be square.")
+        if not correlation_matrix.shape[0] == correlation_matrix.shape[1]:
+            raise ValueError("Correlation matrix must be square.")
+        if not np.allclose(np.diag(correlation_matrix), 1.0):
+            raise ValueError("Correlation matrix must have 1.0 on diagonal.")
+        if not np.allclose(correlation_matrix.T, correlation_matrix):
+            raise ValueError("Correlation matrix must be symmetric.")
+        if not _is_positive_definite(correlation_matrix):
+            raise ValueError("Correlation matrix must be positive definite.")
+        self.C = correlation_matrix.copy()
+        self.P = np.linalg.cholesky(self.C)
+        return self
+
+    def _validate_X(self, X, check_rows_cols=True):
+        if not (hasattr(self, "C") and hasattr(self, "P")):
+            raise CorrelatorError("User must call `set_target` first.")
+        import torch
+
+        if not isinstance(X, (np.ndarray, torch.Tensor)):
+            raise TypeError("Input argument `X` must be NumPy array.")
+        if not X.ndim == 2:
+            raise ValueError("Correlation matrix must be square.")
+        N, K = X.shape
+        if self.P.shape[0] != K:
+            raise ValueError(f"Shape of `X` ({tuple(X.shape)}) does not match shape of correlation matrix "
+                             f"({self.P.shape})")
+        if check_rows_cols and N <= K:
+            raise ValueError(f"The matrix X must have rows > columns. Got shape: {tuple(X.shape)}")
+        return N, K
+
+
+class Cholesky(Correlator):
+    """Cholesky correlator (correlation.py:205-285): next on the device roadmap."""
+
+    def __call__(self, X):
+        raise NotImplementedError("correlator='cholesky' has no device implementation yet "
+                                  "(SURVEY.md §8f, next #1); use 'imanconover'")
+
+
+_NOT_PD_MSG = ("Rank data correlation not positive definite."
+               "There are perfect correlations in the ranked data."
+               "Supply more data (rows in X) or sample differently.")
+
+
+class ImanConover(Correlator):
+    """Iman-Conover rank-correlation induction (correlation.py:288-425) on the GPU.
+
+    Steps 1-4 of the reference run in pbh_iman_conover: van der Waerden scores from
+    'average' ranks, E = corrcoef(scores) with the positive-definiteness check, the
+    forward substitution with cholesky(E) and the multiply by P^T, then every column of X
+    re-ordered by the ranks of the correlated scores (marginals preserved)."""
+
+    def set_target(self, correlation_matrix):
+        super().set_target(correlation_matrix)
+        return self
+
+    def _run(self, X, n, k, x_rs, x_cs, Y, y_rs, y_cs, debug=None):
+        lib = _lib.load()
+        ws_bytes = ctypes.c_size_t()
+        _lib.check(lib.pbh_ic_workspace_size(n, k, ctypes.byref(ws_bytes)))
+        ws = device.empty(int(ws_bytes.value), "uint8")
+        P = np.ascontiguousarray(self.P, dtype=np.float64)
+        args = _lib.ICArgs()
+        args.X, args.n, args.k, args.x_rs, args.x_cs = X.data_ptr(), n, k, x_rs, x_cs
+        args.target_chol_host = P.ctypes.data
+        args.Y, args.y_rs, args.y_cs = Y.data_ptr(), y_rs, y_cs
+        args.ws, args.ws_bytes = ws.data_ptr(), ws_bytes.value
+        if debug is not None:
+            args.scores_out = debug["S"].data_ptr()
+            args.cscores_out = debug["CS"].data_ptr()
+            args.idx_out = debug["idx"].data_ptr()
+            args.corr_host_out = debug["E"].ctypes.data
+        status = lib.pbh_iman_conover(ctypes.byref(args), device.stream())
+        if status in (_lib.ERR_NOT_PD, _lib.ERR_NONFINITE):
+            raise ValueError(_NOT_PD_MSG)
+        _lib.check(status, "pbh_iman_conover")
+        del ws
+
+    def __call__(self, X):
+        """Transform X of shape (N, K); returns a new array (X is not modified)."""
+        import torch
+
+        N, K = self._validate_X(X)
+        on_device = isinstance(X, torch.Tensor)
+        Xd = X.to(device.device(), torch.float64) if on_device else device.to_device(np.asarray(X, dtype=np.float64))
+        Xd = Xd.contiguous()
+        Y = device.empty((N, K))
+        self._run(Xd, N, K, K, 1, Y, K, 1)
+        return Y if on_device else device.to_host(Y)
+
+    def _transform_device(self, block, ev=None):
+        """block: (K, N) contiguous device tensor of the correlated variables (DAG path)."""
+        K, N = block.shape
+        self._validate_X(block.T)
+        Y = device.empty((K, N))
+        self._run(block, N, K, 1, N, Y, 1, N)
+        return Y
+
+    def _call_debug(self, X):
+        """Transform plus the intermediates (scores, correlated scores, step-4 indices,
+        rank correlation E) for parity tests."""
+        N, K = self._validate_X(X)
+        Xd = device.to_device(np.asarray(X, dtype=np.float64)).contiguous()
+        Y = device.empty((N, K))
+        dbg = {"S": device.empty((K, N)), "CS": device.empty((K, N)), "idx": device.empty((K, N), "int32"),
+               "E": np.zeros((K, K))}
+        self._run(Xd, N, K, K, 1, Y, K, 1, debug=dbg)
+        return (device.to_host(Y), device.to_host(dbg["S"]).T, device.to_host(dbg["CS"]).T,
+                device.to_host(dbg["idx"]).T, dbg["E"])
+
+
+def rankdata(x):
+    """scipy.stats.rankdata(x, method='average') of a 1-D array, on the device."""
+    import torch
+
+    on_device = isinstance(x, torch.Tensor)
+    xd = (x.to(device.device(), torch.float64) if on_device else device.to_device(np.asarray(x, np.float64)))
+    n = xd.shape[0]
+    out = device.empty(n)
+    lib = _lib.load()
+    wsb = ctypes.c_size_t()
+    _lib.check(lib.pbh_rank_workspace_size(n, ctypes.byref(wsb)))
+    ws = device.empty(int(wsb.value), "uint8")
+    _lib.check(lib.pbh_rankdata_average(xd.data_ptr(), xd.stride(0), n, out.data_ptr(), ws.data_ptr(), wsb.value,
+                                        device.stream()), "rankdata")
+    return out if on_device else device.to_host(out)

@@ -1,0 +1,275 @@
+// C-ABI entry points that orchestrate several kernels: Iman-Conover and rankdata.
+//
+// Host-side control stays here (plain C++, no Python): the K x K correlation assembly,
+// the positive-definiteness check and the Cholesky factor of correlation.py:398-405 are
+// O(K^3) with K <= 128 and run on the host between two device phases (one 8 KB D2H).
+#include <math.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "pbh_error.h"
+#include "pbh_ic.h"
+#include "pbh_sort.h"
+
+namespace pbh {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+namespace {
+
+struct Carver {
+  char* p;
+  size_t used = 0;
+  explicit Carver(void* base) : p((char*)base) {}
+  void* take(size_t bytes) {
+    void* r = p + used;
+    used += (bytes + 255) & ~(size_t)255;
+    return r;
+  }
+};
+
+size_t small_bytes(int k) { return 4 * (((size_t)k * k * 8 + 255) & ~(size_t)255) + 2 * 256 + 4096; }
+
+size_t ic_bytes(int64_t n, int k, bool carve, void* base, struct IcLayout* out);
+
+struct IcLayout {
+  double* S;
+  double* sorted_x;
+  void* sort_ws;
+  void* tie_ws;
+  double* partials;
+  double* means;
+  double* gram;
+  double* L;
+  double* inv_diag;
+  double* P;
+  int32_t* flag;
+};
+
+size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
+  Carver c(base);
+  void* S = c.take((size_t)n * k * 8);
+  void* sx = c.take((size_t)n * k * 8);
+  void* sws = c.take(sort_workspace_bytes(n));
+  void* tws = c.take(tie_workspace_bytes(n));
+  void* part = c.take(gram_partials_bytes(k));
+  void* means = c.take((size_t)k * 8);
+  void* gram = c.take((size_t)k * k * 8);
+  void* Lm = c.take((size_t)k * k * 8);
+  void* invd = c.take((size_t)k * 8);
+  void* P = c.take((size_t)k * k * 8);
+  void* flag = c.take(256);
+  if (carve) {
+    L->S = (double*)S;
+    L->sorted_x = (double*)sx;
+    L->sort_ws = sws;
+    L->tie_ws = tws;
+    L->partials = (double*)part;
+    L->means = (double*)means;
+    L->gram = (double*)gram;
+    L->L = (double*)Lm;
+    L->inv_diag = (double*)invd;
+    L->P = (double*)P;
+    L->flag = (int32_t*)flag;
+  }
+  return c.used;
+}
+
+// Lower Cholesky (Cholesky-Banachiewicz); false when a pivot is not > 0 (np.linalg.cholesky
+// raises LinAlgError there, which _is_positive_definite turns into False).
+bool cholesky_lower(const std::vector<double>& A, int k, std::vector<double>& L) {
+  L.assign((size_t)k * k, 0.0);
+  for (int j = 0; j < k; ++j) {
+    double s = A[(size_t)j * k + j];
+    for (int m = 0; m < j; ++m) s -= L[(size_t)j * k + m] * L[(size_t)j * k + m];
+    if (!(s > 0.0)) return false;
+    double d = sqrt(s);
+    L[(size_t)j * k + j] = d;
+    for (int i = j + 1; i < k; ++i) {
+      double t = A[(size_t)i * k + j];
+      for (int m = 0; m < j; ++m) t -= L[(size_t)i * k + m] * L[(size_t)j * k + m];
+      L[(size_t)i * k + j] = t / d;
+    }
+  }
+  return true;
+}
+
+}  // namespace
+}  // namespace pbh
+
+using namespace pbh;
+
+extern "C" int pbh_version(void) { return 10000; }  // 1.0.0
+
+extern "C" const char* pbh_last_error(void) { return pbh::g_last_error.c_str(); }
+
+extern "C" int pbh_init(int device) {
+  int count = 0;
+  PBH_CHECK_HIP(hipGetDeviceCount(&count));
+  PBH_REQUIRE(device >= 0 && device < count, "pbh_init: device %d not visible (%d devices)", device, count);
+  hipDeviceProp_t prop;
+  PBH_CHECK_HIP(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_error("pbh_init: device %d is %s; this library is built for gfx950 (MI355X) only", device,
+              prop.gcnArchName);
+    return PBH_ERR_UNSUPPORTED;
+  }
+  PBH_CHECK_HIP(hipSetDevice(device));
+  return PBH_OK;
+}
+
+extern "C" int pbh_ic_workspace_size(int64_t n, int32_t k, size_t* bytes) {
+  PBH_REQUIRE(bytes != nullptr && n >= 1 && k >= 1, "pbh_ic_workspace_size: bad arguments");
+  *bytes = ic_bytes(n, k, false, nullptr, nullptr);
+  return PBH_OK;
+}
+
+extern "C" int pbh_rank_workspace_size(int64_t n, size_t* bytes) {
+  PBH_REQUIRE(bytes != nullptr && n >= 1, "pbh_rank_workspace_size: bad arguments");
+  *bytes = sort_workspace_bytes(n) + tie_workspace_bytes(n) + 512;
+  return PBH_OK;
+}
+
+extern "C" int pbh_rankdata_average(const double* x, int64_t stride, int64_t n, double* ranks, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  PBH_REQUIRE(x && ranks && ws, "pbh_rankdata_average: null pointer");
+  PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "pbh_rankdata_average: n out of range");
+  size_t need = 0;
+  pbh_rank_workspace_size(n, &need);
+  if (ws_bytes < need) {
+    set_error("pbh_rankdata_average: workspace %zu < %zu bytes", ws_bytes, need);
+    return PBH_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  Carver c(ws);
+  SortBuffers sb;
+  sort_carve(c.take(sort_workspace_bytes(n)), n, sb);
+  TieBuffers tb;
+  tie_carve(c.take(tie_workspace_bytes(n)), n, tb);
+  uint32_t hist_host[8 * 256];
+  sb.hist_host = hist_host;
+  int st = load_keys(x, stride, n, sb.keys[0], nullptr, s);
+  if (st) return st;
+  int buf = 0;
+  st = radix_sort_keys(sb, n, s, &buf);
+  if (st) return st;
+  RankOut out = {};
+  out.ranks = ranks;
+  return rank_finish(kModeRanks, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+}
+
+extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
+  PBH_REQUIRE(a != nullptr, "pbh_iman_conover: args must not be NULL");
+  const int64_t n = a->n;
+  const int k = a->k;
+  PBH_REQUIRE(a->X && a->Y && a->ws && a->target_chol_host, "pbh_iman_conover: null pointer argument");
+  PBH_REQUIRE(k >= 1 && k <= 128, "pbh_iman_conover: K = %d outside [1, 128]", k);
+  PBH_REQUIRE(n > k && n < ((int64_t)1 << 32), "pbh_iman_conover: need K < N < 2^32 (N=%lld, K=%d)", (long long)n, k);
+  IcLayout L;
+  size_t need = ic_bytes(n, k, true, a->ws, &L);
+  if (a->ws_bytes < need) {
+    set_error("pbh_iman_conover: workspace %zu < %zu bytes", a->ws_bytes, need);
+    return PBH_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  SortBuffers sb;
+  sort_carve(L.sort_ws, n, sb);
+  TieBuffers tb;
+  tie_carve(L.tie_ws, n, tb);
+  std::vector<uint32_t> hist_host(8 * 256);
+  sb.hist_host = hist_host.data();
+  int st;
+
+  // ---- step 1: van der Waerden scores of every column (+ the sorted column for step 4)
+  PBH_CHECK_HIP(hipMemsetAsync(L.flag, 0, sizeof(int32_t), s));
+  for (int c = 0; c < k; ++c) {
+    st = load_keys(a->X + (int64_t)c * a->x_cs, a->x_rs, n, sb.keys[0], L.flag, s);
+    if (st) return st;
+    int buf = 0;
+    st = radix_sort_keys(sb, n, s, &buf);
+    if (st) return st;
+    RankOut out = {};
+    out.scores = L.S + (int64_t)c * n;
+    out.sorted_x = L.sorted_x + (int64_t)c * n;
+    st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+    if (st) return st;
+  }
+  int32_t flag_host = 0;
+  PBH_CHECK_HIP(hipMemcpyAsync(&flag_host, L.flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (a->scores_out)
+    PBH_CHECK_HIP(hipMemcpyAsync(a->scores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
+
+  // ---- step 2: E = corrcoef(S) on the host from the device Gram matrix
+  st = column_means(L.S, n, k, n, L.partials, L.means, s);
+  if (st) return st;
+  st = centered_gram(L.S, n, k, n, L.means, L.partials, L.gram, s);
+  if (st) return st;
+  std::vector<double> G((size_t)k * k);
+  PBH_CHECK_HIP(hipMemcpyAsync(G.data(), L.gram, (size_t)k * k * 8, hipMemcpyDeviceToHost, s));
+  PBH_CHECK_HIP(hipStreamSynchronize(s));
+  if (flag_host) {
+    set_error("Iman-Conover input contains NaN");
+    return PBH_ERR_NONFINITE;
+  }
+  // np.cov: c = dot(Xc, Xc^T) * (1 / (N - 1)); np.corrcoef: c /= std[:,None]; c /= std[None,:]; clip
+  const double fact = 1.0 / (double)(n - 1);
+  for (auto& v : G) v *= fact;
+  std::vector<double> sd(k);
+  for (int i = 0; i < k; ++i) sd[i] = sqrt(G[(size_t)i * k + i]);
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) {
+      double v = G[(size_t)i * k + j];
+      v /= sd[i];
+      v /= sd[j];
+      G[(size_t)i * k + j] = v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v);
+    }
+  if (a->corr_host_out) memcpy(a->corr_host_out, G.data(), (size_t)k * k * 8);
+  std::vector<double> Lc;
+  if (!cholesky_lower(G, k, Lc)) {
+    set_error(
+        "Rank data correlation not positive definite.There are perfect correlations in the ranked data.Supply more "
+        "data (rows in X) or sample differently.");
+    return PBH_ERR_NOT_PD;
+  }
+  std::vector<double> invd(k), P((size_t)k * k);
+  for (int j = 0; j < k; ++j) invd[j] = 1.0 / Lc[(size_t)j * k + j];
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) P[(size_t)i * k + j] = j <= i ? a->target_chol_host[(size_t)i * k + j] : 0.0;
+  PBH_CHECK_HIP(hipMemcpyAsync(L.L, Lc.data(), (size_t)k * k * 8, hipMemcpyHostToDevice, s));
+  PBH_CHECK_HIP(hipMemcpyAsync(L.inv_diag, invd.data(), (size_t)k * 8, hipMemcpyHostToDevice, s));
+  PBH_CHECK_HIP(hipMemcpyAsync(L.P, P.data(), (size_t)k * k * 8, hipMemcpyHostToDevice, s));
+
+  // ---- step 3: CS = (S L^-T) P^T, in place
+  st = apply_decorrelate_correlate(L.S, n, k, n, L.L, L.inv_diag, L.P, s);
+  if (st) return st;
+  if (a->cscores_out)
+    PBH_CHECK_HIP(hipMemcpyAsync(a->cscores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
+
+  // ---- step 4: Y[:, c] = sort(X[:, c])[rankdata(CS[:, c]).astype(int) - 1]
+  for (int c = 0; c < k; ++c) {
+    st = load_keys(L.S + (int64_t)c * n, 1, n, sb.keys[0], nullptr, s);
+    if (st) return st;
+    int buf = 0;
+    st = radix_sort_keys(sb, n, s, &buf);
+    if (st) return st;
+    RankOut out = {};
+    out.sorted_src = L.sorted_x + (int64_t)c * n;
+    out.y = a->Y + (int64_t)c * a->y_cs;
+    out.y_rs = a->y_rs;
+    out.idx = a->idx_out ? a->idx_out + (int64_t)c * n : nullptr;
+    st = rank_finish(kModeGather, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+    if (st) return st;
+  }
+  return PBH_OK;
+}

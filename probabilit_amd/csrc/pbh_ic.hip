@@ -1,0 +1,506 @@
+// Iman-Conover device kernels (correlation.py:368-425).
+//
+//   rank_finish   : 'average' tie ranks of a sorted column (scipy _rankdata semantics:
+//                   ordinal(first of run) + (count - 1) / 2) -> scores / gather / ranks
+//   centered_gram : (S - mean)^T (S - mean), the np.cov inside np.corrcoef (:398)
+//   apply         : per row, forward substitution with L = cholesky(E) (the
+//                   solve_triangular of :409-411) and the multiply by P^T (:414)
+#include <math.h>
+
+#include "pbh_error.h"
+#include "pbh_ic.h"
+#include "pbh_special.h"
+#include "pbh_timing.h"
+
+namespace pbh {
+namespace {
+
+constexpr int T = kSortThreads;  // 256
+constexpr int IPT = kSortItems;  // 16
+constexpr int TILE = kSortTile;  // 4096
+constexpr int64_t kNoHead = INT64_MAX;
+
+__device__ __forceinline__ int pad(int p) { return p + (p >> 4); }
+
+template <bool IsMax>
+__device__ __forceinline__ int64_t comb(int64_t a, int64_t b) {
+  return IsMax ? (a > b ? a : b) : (a < b ? a : b);
+}
+
+// Exclusive scan across the 256 threads of a block (forward for max, or reverse when Rev).
+template <bool IsMax, bool Rev>
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t identity, int64_t* sh /*>= 8*/) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t y = Rev ? __shfl_down(x, o, 64) : __shfl_up(x, o, 64);
+    bool ok = Rev ? (lane + o < 64) : (lane >= o);
+    if (ok) x = comb<IsMax>(x, y);
+  }
+  // x = inclusive scan within the wave (from the left, or from the right when Rev)
+  if (Rev ? lane == 0 : lane == 63) sh[w] = x;
+  int64_t excl = Rev ? __shfl_down(x, 1, 64) : __shfl_up(x, 1, 64);
+  if (Rev ? lane == 63 : lane == 0) excl = identity;
+  __syncthreads();
+  int64_t other = identity;
+  if (Rev) {
+    for (int i = w + 1; i < 4; ++i) other = comb<IsMax>(other, sh[i]);
+  } else {
+    for (int i = 0; i < w; ++i) other = comb<IsMax>(other, sh[i]);
+  }
+  __syncthreads();
+  return comb<IsMax>(excl, other);
+}
+
+__global__ __launch_bounds__(T) void k_load_keys(const double* __restrict__ x, int64_t stride, int64_t n,
+                                                uint64_t* __restrict__ keys, int32_t* flag) {
+  for (int64_t i = (int64_t)blockIdx.x * T + threadIdx.x; i < n; i += (int64_t)gridDim.x * T) {
+    double v = x[i * stride];
+    keys[i] = f64_to_key(v);
+    flag_nonfinite(flag, isnan(v));  // +-inf sort fine; NaN ranks are undefined (ValueError)
+  }
+}
+
+__global__ __launch_bounds__(T) void k_head_bounds(const uint64_t* __restrict__ keys, int64_t n,
+                                                  int64_t* __restrict__ first_head, int64_t* __restrict__ last_head) {
+  __shared__ int64_t sh[8];
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  int64_t f = kNoHead, l = -1;
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    int64_t i = base + j * T + threadIdx.x;
+    if (i < n) {
+      bool head = (i == 0) || keys[i] != keys[i - 1];
+      if (head) {
+        f = i < f ? i : f;
+        l = i > l ? i : l;
+      }
+    }
+  }
+  // block min / max
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t fo = __shfl_xor(f, o, 64), lo = __shfl_xor(l, o, 64);
+    f = fo < f ? fo : f;
+    l = lo > l ? lo : l;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[w] = f;
+    sh[4 + w] = l;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t ff = sh[0], ll = sh[4];
+    for (int i = 1; i < 4; ++i) {
+      ff = sh[i] < ff ? sh[i] : ff;
+      ll = sh[4 + i] > ll ? sh[4 + i] : ll;
+    }
+    first_head[blockIdx.x] = ff;
+    last_head[blockIdx.x] = ll;
+  }
+}
+
+// prev_head[t] = max(last_head[0..t-1]) (or -1); next_head[t] = min(first_head[t+1..]) (or n).
+__global__ __launch_bounds__(T) void k_head_prefix(const int64_t* __restrict__ first_head,
+                                                  const int64_t* __restrict__ last_head, int64_t ntiles, int64_t n,
+                                                  int64_t* __restrict__ prev_head, int64_t* __restrict__ next_head) {
+  __shared__ int64_t sh[8];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = -1;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < ntiles; b0 += T) {
+    int64_t i = b0 + threadIdx.x;
+    int64_t v = i < ntiles ? last_head[i] : -1;
+    int64_t ex = block_excl_scan<true, false>(v, -1, sh);
+    int64_t c = carry;
+    if (i < ntiles) prev_head[i] = ex > c ? ex : c;
+    __syncthreads();
+    if (threadIdx.x == T - 1) {
+      int64_t tot = comb<true>(ex, v);
+      carry = tot > c ? tot : c;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) carry = n;
+  __syncthreads();
+  for (int64_t e0 = ntiles; e0 > 0; e0 -= T) {
+    int64_t i = e0 - T + threadIdx.x;  // may be negative in the last chunk
+    int64_t v = i >= 0 ? first_head[i] : kNoHead;
+    int64_t ex = block_excl_scan<false, true>(v, kNoHead, sh);
+    int64_t c = carry;
+    if (i >= 0) next_head[i] = ex < c ? ex : c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t tot = comb<false>(ex, v);
+      carry = tot < c ? tot : c;
+    }
+    __syncthreads();
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(T) void k_rank_finish(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ rows,
+                                                  int64_t n, const int64_t* __restrict__ prev_head,
+                                                  const int64_t* __restrict__ next_head, RankOut out) {
+  __shared__ uint64_t sk[TILE + TILE / 16];
+  __shared__ uint32_t sr[TILE + TILE / 16];
+  __shared__ int64_t sh[8];
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int cnt = (int)((n - base) < TILE ? (n - base) : TILE);
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    int p = j * T + t;
+    if (p < cnt) {
+      sk[pad(p)] = keys[base + p];
+      sr[pad(p)] = rows[base + p];
+    }
+  }
+  const uint64_t before = base > 0 ? keys[base - 1] : 0ull;
+  __syncthreads();
+
+  // blocked view: thread t owns positions t*16 .. t*16+15 of the tile
+  uint64_t k[IPT];
+  bool head[IPT];
+  int64_t first_local = kNoHead, last_local = -1;
+#pragma unroll
+  for (int q = 0; q < IPT; ++q) {
+    int p = t * IPT + q;
+    if (p < cnt) {
+      k[q] = sk[pad(p)];
+      uint64_t prev = (p == 0) ? before : sk[pad(p - 1)];
+      head[q] = (base + p == 0) || (k[q] != prev);
+      if (head[q]) {
+        int64_t g = base + p;
+        first_local = g < first_local ? g : first_local;
+        last_local = g;
+      }
+    } else {
+      k[q] = 0;
+      head[q] = false;
+    }
+  }
+  int64_t start = block_excl_scan<true, false>(last_local, -1, sh);
+  start = comb<true>(start, prev_head[blockIdx.x]);
+  int64_t nxt = block_excl_scan<false, true>(first_local, kNoHead, sh);
+  nxt = comb<false>(nxt, next_head[blockIdx.x]);
+
+  int64_t next_after[IPT];
+#pragma unroll
+  for (int q = IPT - 1; q >= 0; --q) {
+    next_after[q] = nxt;
+    if (head[q]) nxt = base + t * IPT + q;
+  }
+  const double np1 = (double)(n + 1);
+#pragma unroll
+  for (int q = 0; q < IPT; ++q) {
+    int p = t * IPT + q;
+    if (p >= cnt) continue;
+    int64_t g = base + p;
+    if (head[q]) start = g;
+    int64_t end = next_after[q] - 1;  // next_after == n when no later head
+    double avg = (double)(start + 1) + (double)(end - start) / 2.0;
+    uint32_t row = sr[pad(p)];
+    if constexpr (MODE == kModeScores) {
+      out.scores[row] = sf::ndtri(avg / np1);
+    } else if constexpr (MODE == kModeGather) {
+      int64_t idx = (int64_t)avg - 1;
+      out.y[(int64_t)row * out.y_rs] = out.sorted_src[idx];
+      if (out.idx) out.idx[row] = (int32_t)idx;
+    } else {
+      out.ranks[row] = avg;
+    }
+  }
+  if constexpr (MODE == kModeScores) {
+    if (out.sorted_x) {
+#pragma unroll
+      for (int j = 0; j < IPT; ++j) {
+        int p = j * T + t;
+        if (p < cnt) out.sorted_x[base + p] = key_to_f64(sk[pad(p)]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- column means
+constexpr int kRedThreads = 256;
+
+__device__ __forceinline__ double block_sum(double v, double* sh /*4*/) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = ((sh[0] + sh[1]) + (sh[2] + sh[3]));
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(kRedThreads) void k_colsum(const double* __restrict__ S, int64_t n, int64_t ld,
+                                                       int64_t chunk, double* __restrict__ partial) {
+  __shared__ double sh[4];
+  const int c = blockIdx.y;
+  const int64_t r0 = (int64_t)blockIdx.x * chunk;
+  int64_t r1 = r0 + chunk;
+  if (r1 > n) r1 = n;
+  double s = 0.0;
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += kRedThreads) s += S[(int64_t)c * ld + r];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) partial[(int64_t)c * gridDim.x + blockIdx.x] = s;
+}
+
+__global__ void k_means(const double* __restrict__ partial, int nb, int k, int64_t n, double* __restrict__ means) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= k) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += partial[(int64_t)c * nb + b];
+  means[c] = s / (double)n;
+}
+
+// ---------------------------------------------------------------- centered Gram
+constexpr int GT = 32;     // Gram tile (columns)
+constexpr int GROWS = 64;  // rows staged per step
+constexpr int kGramBlocksMax = 1024;
+
+__global__ __launch_bounds__(256) void k_gram(const double* __restrict__ S, int64_t n, int k, int64_t ld,
+                                             const double* __restrict__ means, int64_t chunk,
+                                             double* __restrict__ partials) {
+  __shared__ double A[GROWS][GT + 1];  // +1 pad: conflict-free column-wise staging writes
+  __shared__ double B[GROWS][GT + 1];
+  __shared__ double red[4][GT * GT / 4];  // reused for the 4-group reduction in quarters
+  const int t = threadIdx.x, g = t >> 6, l = t & 63;
+  // tile pair (ti <= tj) from blockIdx.y
+  const int nt = (k + GT - 1) / GT;
+  int pair = blockIdx.y, ti = 0;
+  while (pair >= nt - ti) {
+    pair -= nt - ti;
+    ++ti;
+  }
+  const int tj = ti + pair;
+  const int i0 = (l >> 3) * 4, j0 = (l & 7) * 4;
+  double acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+
+  const int64_t r0 = (int64_t)blockIdx.x * chunk;
+  int64_t r1 = r0 + chunk;
+  if (r1 > n) r1 = n;
+  for (int64_t rb = r0; rb < r1; rb += GROWS) {
+#pragma unroll
+    for (int m = 0; m < (GROWS * GT) / 256; ++m) {
+      int idx = t + 256 * m;
+      int col = idx / GROWS, row = idx % GROWS;
+      int64_t r = rb + row;
+      int ca = ti * GT + col, cb = tj * GT + col;
+      A[row][col] = (r < r1 && ca < k) ? S[(int64_t)ca * ld + r] - means[ca] : 0.0;
+      B[row][col] = (r < r1 && cb < k) ? S[(int64_t)cb * ld + r] - means[cb] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int row = g; row < GROWS; row += 4) {
+      double a[4], b[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        a[x] = A[row][i0 + x];
+        b[x] = B[row][j0 + x];
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = __builtin_fma(a[x], b[y], acc[x][y]);
+    }
+    __syncthreads();
+  }
+  // reduce the 4 row groups: group g writes its 16 values; group 0 sums in fixed order
+  double* out = partials + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (GT * GT);
+  for (int q = 0; q < 4; ++q) {  // quarter q of the 1024 entries handled via red[4][256]
+    // thread l of group g holds entries (i0+x, j0+y); map entry to slot within quarter
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        int e = (i0 + x) * GT + (j0 + y);
+        if ((e >> 8) == q) red[g][e & 255] = acc[x][y];
+      }
+    __syncthreads();
+    {
+      int e = t;  // 256 threads cover the quarter
+      double v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+      out[q * 256 + e] = v;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_gram_reduce(const double* __restrict__ partials, int nb, int k, double* __restrict__ gram) {
+  const int nt = (k + GT - 1) / GT;
+  int pair = blockIdx.y, ti = 0;
+  while (pair >= nt - ti) {
+    pair -= nt - ti;
+    ++ti;
+  }
+  const int tj = ti + pair;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= GT * GT) return;
+  const int i = ti * GT + e / GT, j = tj * GT + e % GT;
+  if (i >= k || j >= k) return;
+  const double* p = partials + (int64_t)blockIdx.y * nb * (GT * GT) + e;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += p[(int64_t)b * (GT * GT)];
+  gram[(int64_t)i * k + j] = s;
+  gram[(int64_t)j * k + i] = s;
+}
+
+// ---------------------------------------------------------------- decorrelate + correlate
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_apply(double* __restrict__ S, int64_t n, int k, int64_t ld,
+                                              const double* __restrict__ L, const double* __restrict__ inv_diag,
+                                              const double* __restrict__ P) {
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
+    double v[KMAX];
+#pragma unroll
+    for (int m = 0; m < KMAX; ++m) v[m] = (m < k) ? S[(int64_t)m * ld + r] : 0.0;
+    // D = S L^-T : forward substitution, row by row of L
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+      if (j < k) {
+        double acc = v[j];
+#pragma unroll
+        for (int m = 0; m < j; ++m) acc = __builtin_fma(-L[j * k + m], v[m], acc);
+        v[j] = acc * inv_diag[j];
+      }
+    }
+    // CS = D P^T (P lower triangular), in place from the last column down
+#pragma unroll
+    for (int j = KMAX - 1; j >= 0; --j) {
+      if (j < k) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m <= j; ++m) acc = __builtin_fma(v[m], P[j * k + m], acc);
+        v[j] = acc;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < KMAX; ++m)
+      if (m < k) S[(int64_t)m * ld + r] = v[m];
+  }
+}
+
+}  // namespace
+
+size_t tie_workspace_bytes(int64_t n) {
+  int64_t nt = sort_tiles(n);
+  return 4 * (((size_t)nt * 8 + 255) & ~(size_t)255);
+}
+
+void tie_carve(void* ws, int64_t n, TieBuffers& tb) {
+  int64_t nt = sort_tiles(n);
+  size_t stride = ((size_t)nt * 8 + 255) & ~(size_t)255;
+  char* p = (char*)ws;
+  tb.first_head = (int64_t*)(p);
+  tb.last_head = (int64_t*)(p + stride);
+  tb.prev_head = (int64_t*)(p + 2 * stride);
+  tb.next_head = (int64_t*)(p + 3 * stride);
+}
+
+int load_keys(const double* x, int64_t stride, int64_t n, uint64_t* keys, int32_t* flag, hipStream_t s) {
+  PBH_TIMED(kKLoadKeys, s,
+            hipLaunchKernelGGL(k_load_keys, dim3(grid_for(n, T, 8192)), dim3(T), 0, s, x, stride, n, keys, flag));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int rank_finish(int mode, const uint64_t* keys, const uint32_t* rows, int64_t n, const TieBuffers& tb,
+                const RankOut& out, hipStream_t s) {
+  const int64_t nt = sort_tiles(n);
+  PBH_TIMED(kKHeadBounds, s,
+            hipLaunchKernelGGL(k_head_bounds, dim3((unsigned)nt), dim3(T), 0, s, keys, n, tb.first_head,
+                               tb.last_head);
+            hipLaunchKernelGGL(k_head_prefix, dim3(1), dim3(T), 0, s, tb.first_head, tb.last_head, nt, n,
+                               tb.prev_head, tb.next_head));
+  switch (mode) {
+    case kModeScores:
+      PBH_TIMED(kKRankScores, s,
+                hipLaunchKernelGGL(k_rank_finish<kModeScores>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, n,
+                                   tb.prev_head, tb.next_head, out));
+      break;
+    case kModeGather:
+      PBH_TIMED(kKRankGather, s,
+                hipLaunchKernelGGL(k_rank_finish<kModeGather>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, n,
+                                   tb.prev_head, tb.next_head, out));
+      break;
+    default:
+      hipLaunchKernelGGL(k_rank_finish<kModeRanks>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, n, tb.prev_head,
+                         tb.next_head, out);
+  }
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+static int64_t red_blocks(int64_t n, int64_t* chunk) {
+  int64_t nb = (n + 4095) / 4096;
+  if (nb > kGramBlocksMax) nb = kGramBlocksMax;
+  if (nb < 1) nb = 1;
+  int64_t c = (n + nb - 1) / nb;
+  c = (c + GROWS - 1) / GROWS * GROWS;
+  *chunk = c;
+  return (n + c - 1) / c;
+}
+
+size_t gram_partials_bytes(int k) {
+  int nt = (k + GT - 1) / GT;
+  int pairs = nt * (nt + 1) / 2;
+  size_t a = (size_t)pairs * kGramBlocksMax * GT * GT * 8;
+  size_t b = (size_t)k * kGramBlocksMax * 8;
+  return a > b ? a : b;
+}
+
+int column_means(const double* S, int64_t n, int k, int64_t ld, double* partial, double* means, hipStream_t s) {
+  int64_t chunk;
+  int64_t nb = red_blocks(n, &chunk);
+  hipLaunchKernelGGL(k_colsum, dim3((unsigned)nb, (unsigned)k), dim3(kRedThreads), 0, s, S, n, ld, chunk, partial);
+  hipLaunchKernelGGL(k_means, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, s, partial, (int)nb, k, n, means);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int centered_gram(const double* S, int64_t n, int k, int64_t ld, const double* means, double* partials,
+                  double* gram, hipStream_t s) {
+  int64_t chunk;
+  int64_t nb = red_blocks(n, &chunk);
+  int nt = (k + GT - 1) / GT;
+  int pairs = nt * (nt + 1) / 2;
+  PBH_TIMED(kKGram, s,
+            hipLaunchKernelGGL(k_gram, dim3((unsigned)nb, (unsigned)pairs), dim3(256), 0, s, S, n, k, ld, means,
+                               chunk, partials));
+  hipLaunchKernelGGL(k_gram_reduce, dim3((GT * GT + 255) / 256, (unsigned)pairs), dim3(256), 0, s, partials, (int)nb,
+                     k, gram);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const double* L, const double* inv_diag,
+                                const double* P, hipStream_t s) {
+  dim3 g(grid_for(n, 256, 8192)), b(256);
+  if (k <= 8)
+    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<8>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+  else if (k <= 16)
+    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<16>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+  else if (k <= 32)
+    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<32>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+  else if (k <= 64)
+    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<64>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+  else if (k <= 128)
+    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<128>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+  else {
+    set_error("Iman-Conover: K = %d exceeds the supported maximum of 128 variables", k);
+    return PBH_ERR_UNSUPPORTED;
+  }
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+}  // namespace pbh

@@ -1,0 +1,379 @@
+// Quantile generators and the inverse-CDF sweep (the first half of Node.sample,
+// modeling.py:478-489 and Distribution._sample, modeling.py:795-807).
+//
+// Roofline: the ppf sweep moves 16 B per draw (read q 8 + write x 8), the fused
+// generator + ppf 8 B per draw (write x only); norm / uniform / expon / triang / lognorm
+// are HBM-bound, gamma (igami) and per-element poisson searches are FP64-VALU-bound.
+#include <math.h>
+
+#include "pbh_error.h"
+#include "pbh_rng.h"
+#include "pbh_special.h"
+#include "pbh_timing.h"
+
+namespace pbh {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr double kInf = sf::kInf;
+constexpr double kNaN = sf::kNaN;
+
+struct Params {
+  const double* ptr[3];
+  double val[3];
+  PBH_DI double at(int j, int64_t i) const { return ptr[j] ? ptr[j][i] : val[j]; }
+};
+
+struct PoissonTable {
+  const double* cdf;  // cdf[j] = pdtr(k_lo + j, mu) for scalar mu, else NULL
+  int64_t k_lo;
+  int64_t len;
+};
+
+// smallest k >= 0 with pdtr(k, mu) >= q, by stepping from a Cornish-Fisher guess.
+PBH_DI double poisson_search(double q, double mu) {
+  if (mu == 0.0) return 0.0;
+  double z = sf::ndtri(q);
+  double g = floor(mu + sqrt(mu) * z + (z * z - 1.0) / 6.0);
+  if (!(g >= 0.0)) g = 0.0;
+  if (g > 9.0e15) g = 9.0e15;
+  double k = g;
+  if (sf::pdtr(k, mu) >= q) {
+    while (k > 0.0 && sf::pdtr(k - 1.0, mu) >= q) k -= 1.0;
+  } else {
+    do {
+      k += 1.0;
+    } while (sf::pdtr(k, mu) < q && k < 1.0e18);
+  }
+  return k;
+}
+
+PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
+  int64_t lo = 0, hi = t.len;  // first j with cdf[j] >= q
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (t.cdf[mid] >= q)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  if (lo == t.len || (lo == 0 && t.k_lo > 0)) return poisson_search(q, mu);  // outside coverage
+  return (double)(t.k_lo + lo);
+}
+
+// ppf of one element for distribution D; p = (shape..., loc, scale) already resolved.
+template <int D>
+PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTable& pt) {
+  if constexpr (D == PBH_DIST_POISSON) {
+    double mu = p0, loc = p1;
+    bool cond0 = (mu >= 0.0) && (loc == loc);
+    if (q == 0.0) return -1.0 + loc;
+    if (cond0 && q == 1.0) return kInf + loc;
+    if (cond0 && q > 0.0 && q < 1.0) {
+      double k = pt.cdf ? poisson_from_table(q, mu, pt) : poisson_search(q, mu);
+      return k + loc;
+    }
+    return kNaN;
+  } else {
+    double shape = 0.0, loc, scale;
+    bool arg_ok = true;
+    double lower = 0.0, upper = kInf;
+    if constexpr (D == PBH_DIST_NORM || D == PBH_DIST_UNIFORM || D == PBH_DIST_EXPON) {
+      loc = p0;
+      scale = p1;
+    } else {
+      shape = p0;
+      loc = p1;
+      scale = p2;
+    }
+    if constexpr (D == PBH_DIST_NORM) lower = -kInf;
+    if constexpr (D == PBH_DIST_UNIFORM || D == PBH_DIST_TRIANG) upper = 1.0;
+    if constexpr (D == PBH_DIST_TRIANG) arg_ok = (shape >= 0.0) && (shape <= 1.0);
+    if constexpr (D == PBH_DIST_GAMMA || D == PBH_DIST_LOGNORM) arg_ok = shape > 0.0;
+    bool cond0 = arg_ok && (scale > 0.0) && (loc == loc);
+    if (!cond0) return kNaN;
+    if (q == 0.0) return lower * scale + loc;
+    if (q == 1.0) return upper * scale + loc;
+    if (!(q > 0.0 && q < 1.0)) return kNaN;
+    double x;
+    if constexpr (D == PBH_DIST_NORM) {
+      x = sf::ndtri(q);
+    } else if constexpr (D == PBH_DIST_UNIFORM) {
+      x = q;
+    } else if constexpr (D == PBH_DIST_EXPON) {
+      x = -sf::log1p_(-q);  // scipy expon._ppf: -sc.log1p(-q), the Cephes log1p
+    } else if constexpr (D == PBH_DIST_LOGNORM) {
+      x = exp(shape * sf::ndtri(q));
+    } else if constexpr (D == PBH_DIST_TRIANG) {
+      // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
+      x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
+    } else {  // gamma
+      x = sf::igami(shape, q);
+    }
+    return x * scale + loc;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_ppf(const double* __restrict__ q, int64_t q_stride, int64_t n,
+                                                Params prm, PoissonTable pt, double* __restrict__ out,
+                                                int32_t* flag) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t step = (int64_t)gridDim.x * kBlock;
+  for (; i < n; i += step) {
+    double x = ppf_one<D>(q[i * q_stride], prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
+    out[i] = x;
+    flag_nonfinite(flag, !isfinite(x));
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_lhs_ppf(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
+                                                    uint32_t col, Params prm, PoissonTable pt,
+                                                    double* __restrict__ out, int32_t* flag) {
+  Philox ph(seed);
+  FeistelPerm fp(ph, (uint64_t)n, col);
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t step = (int64_t)gridDim.x * kBlock;
+  for (; i < nrows; i += step) {
+    double q = lhs_quantile(ph, fp, (uint64_t)(row0 + i), col);
+    double x = ppf_one<D>(q, prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
+    out[i] = x;
+    flag_nonfinite(flag, !isfinite(x));
+  }
+}
+
+__global__ void k_poisson_table(double mu, int64_t k_lo, int64_t len, double* cdf) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < len) cdf[j] = sf::pdtr((double)(k_lo + j), mu);
+}
+
+// ---------------------------------------------------------------- generators
+__global__ __launch_bounds__(kBlock) void k_fill_lhs(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
+                                                     int col0, double* __restrict__ q, int64_t ldq) {
+  const uint32_t col = (uint32_t)(col0 + blockIdx.y);
+  Philox ph(seed);
+  FeistelPerm fp(ph, (uint64_t)n, col);
+  double* qc = q + (int64_t)blockIdx.y * ldq;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock)
+    qc[i] = lhs_quantile(ph, fp, (uint64_t)(row0 + i), col);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_uniform(uint64_t seed, int64_t row0, int64_t nrows, int col0,
+                                                         double* __restrict__ q, int64_t ldq) {
+  const uint32_t col = (uint32_t)(col0 + blockIdx.y);
+  Philox ph(seed);
+  double* qc = q + (int64_t)blockIdx.y * ldq;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock)
+    qc[i] = ph.uniform((uint64_t)(row0 + i), col, kPurposeUniform);
+}
+
+constexpr int kSobolColsPerLaunch = 16;
+struct SobolArgs {
+  uint32_t sv[kSobolColsPerLaunch][32];
+  uint32_t shift[kSobolColsPerLaunch];
+};
+
+__global__ __launch_bounds__(kBlock) void k_fill_sobol(SobolArgs a, double scale, int64_t row0, int64_t nrows,
+                                                       double* __restrict__ q, int64_t ldq) {
+  const int c = blockIdx.y;
+  double* qc = q + (int64_t)c * ldq;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
+    uint64_t r = (uint64_t)(row0 + i);
+    uint64_t g = r ^ (r >> 1);
+    uint32_t x = a.shift[c];
+    while (g) {
+      x ^= a.sv[c][__builtin_ctzll(g)];
+      g &= g - 1;
+    }
+    qc[i] = (double)x * scale;
+  }
+}
+
+unsigned ppf_grid(int64_t n) { return grid_for(n, kBlock, 256 * 16); }
+
+int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& prm, const PoissonTable& pt,
+               double* out, int32_t* flag, hipStream_t s) {
+  dim3 g(ppf_grid(n)), b(kBlock);
+  switch (dist) {
+#define PBH_CASE(D) \
+  case D:           \
+    PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf<D>, g, b, 0, s, q, qs, n, prm, pt, out, flag)); break;
+    PBH_CASE(PBH_DIST_NORM)
+    PBH_CASE(PBH_DIST_UNIFORM)
+    PBH_CASE(PBH_DIST_EXPON)
+    PBH_CASE(PBH_DIST_LOGNORM)
+    PBH_CASE(PBH_DIST_TRIANG)
+    PBH_CASE(PBH_DIST_GAMMA)
+    PBH_CASE(PBH_DIST_POISSON)
+#undef PBH_CASE
+    default:
+      set_error("pbh_ppf: unsupported distribution id %d", dist);
+      return PBH_ERR_UNSUPPORTED;
+  }
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int launch_lhs_ppf(int dist, uint64_t seed, int64_t n, int64_t row0, int64_t nrows, uint32_t col,
+                   const Params& prm, const PoissonTable& pt, double* out, int32_t* flag, hipStream_t s) {
+  dim3 g(ppf_grid(nrows)), b(kBlock);
+  switch (dist) {
+#define PBH_CASE(D) \
+  case D:           \
+    PBH_TIMED(kKLhsPpf, s,                                                                         \
+              hipLaunchKernelGGL(k_lhs_ppf<D>, g, b, 0, s, seed, n, row0, nrows, col, prm, pt, out, flag)); \
+    break;
+    PBH_CASE(PBH_DIST_NORM)
+    PBH_CASE(PBH_DIST_UNIFORM)
+    PBH_CASE(PBH_DIST_EXPON)
+    PBH_CASE(PBH_DIST_LOGNORM)
+    PBH_CASE(PBH_DIST_TRIANG)
+    PBH_CASE(PBH_DIST_GAMMA)
+    PBH_CASE(PBH_DIST_POISSON)
+#undef PBH_CASE
+    default:
+      set_error("pbh_lhs_ppf: unsupported distribution id %d", dist);
+      return PBH_ERR_UNSUPPORTED;
+  }
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int expected_nparams(int dist) {
+  switch (dist) {
+    case PBH_DIST_NORM:
+    case PBH_DIST_UNIFORM:
+    case PBH_DIST_EXPON:
+    case PBH_DIST_POISSON:
+      return 2;
+    case PBH_DIST_LOGNORM:
+    case PBH_DIST_TRIANG:
+    case PBH_DIST_GAMMA:
+      return 3;
+    default:
+      return -1;
+  }
+}
+
+// Scalar-mu poisson: build the CDF table pdtr(k, mu), k in [k_lo, k_lo + len), in a
+// stream-ordered allocation; elements outside its coverage fall back to the search.
+int with_params(int dist, const pbh_param* params, int nparams, Params& prm, PoissonTable& pt, double** table,
+                hipStream_t s) {
+  int want = expected_nparams(dist);
+  if (want < 0) {
+    set_error("unsupported distribution id %d", dist);
+    return PBH_ERR_UNSUPPORTED;
+  }
+  PBH_REQUIRE(nparams == want, "distribution %d expects %d parameters, got %d", dist, want, nparams);
+  PBH_REQUIRE(params != nullptr, "params must not be NULL");
+  for (int j = 0; j < 3; ++j) {
+    prm.ptr[j] = j < nparams ? params[j].ptr : nullptr;
+    prm.val[j] = j < nparams ? params[j].value : 0.0;
+  }
+  pt = PoissonTable{nullptr, 0, 0};
+  *table = nullptr;
+  if (dist == PBH_DIST_POISSON && params[0].ptr == nullptr) {
+    double mu = params[0].value;
+    if (mu > 0.0 && mu < 1.0e12) {
+      double sd = sqrt(mu);
+      double lo = floor(mu - 12.0 * sd - 12.0);
+      int64_t k_lo = lo > 0.0 ? (int64_t)lo : 0;
+      int64_t k_hi = (int64_t)ceil(mu + 20.0 * sd + 40.0);
+      int64_t len = k_hi - k_lo + 1;
+      PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)len * sizeof(double), s));
+      hipLaunchKernelGGL(k_poisson_table, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, mu, k_lo, len,
+                         *table);
+      PBH_CHECK_LAUNCH();
+      pt = PoissonTable{*table, k_lo, len};
+    }
+  }
+  return PBH_OK;
+}
+
+}  // namespace
+}  // namespace pbh
+
+using namespace pbh;
+
+extern "C" int pbh_ppf(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_param* params,
+                       int nparams, double* out, int32_t* nonfinite_flag, void* stream) {
+  PBH_REQUIRE(n >= 0, "pbh_ppf: n must be >= 0");
+  if (n == 0) return PBH_OK;
+  PBH_REQUIRE(q != nullptr && out != nullptr, "pbh_ppf: q and out must be device pointers");
+  hipStream_t s = as_stream(stream);
+  Params prm;
+  PoissonTable pt;
+  double* table = nullptr;
+  int st = with_params(dist, params, nparams, prm, pt, &table, s);
+  if (st != PBH_OK) return st;
+  st = launch_ppf(dist, q, q_stride, n, prm, pt, out, nonfinite_flag, s);
+  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));
+  return st;
+}
+
+extern "C" int pbh_lhs_ppf(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col, int dist,
+                           const pbh_param* params, int nparams, double* out, int32_t* nonfinite_flag,
+                           void* stream) {
+  PBH_REQUIRE(n >= 1 && row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "pbh_lhs_ppf: bad row range");
+  PBH_REQUIRE(col >= 0, "pbh_lhs_ppf: bad column");
+  if (nrows == 0) return PBH_OK;
+  hipStream_t s = as_stream(stream);
+  Params prm;
+  PoissonTable pt;
+  double* table = nullptr;
+  int st = with_params(dist, params, nparams, prm, pt, &table, s);
+  if (st != PBH_OK) return st;
+  st = launch_lhs_ppf(dist, seed, n, row0, nrows, (uint32_t)col, prm, pt, out, nonfinite_flag, s);
+  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));
+  return st;
+}
+
+extern "C" int pbh_fill_lhs(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col0, int ncols,
+                            double* q, int64_t ldq, void* stream) {
+  PBH_REQUIRE(n >= 1 && row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "pbh_fill_lhs: bad row range");
+  PBH_REQUIRE(ncols >= 0 && col0 >= 0 && ncols <= 65535, "pbh_fill_lhs: bad column range");
+  PBH_REQUIRE(ldq >= nrows, "pbh_fill_lhs: ldq < nrows");
+  if (nrows == 0 || ncols == 0) return PBH_OK;
+  dim3 g(grid_for(nrows, kBlock, 4096), (unsigned)ncols);
+  hipLaunchKernelGGL(k_fill_lhs, g, dim3(kBlock), 0, as_stream(stream), seed, n, row0, nrows, col0, q, ldq);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+extern "C" int pbh_fill_uniform(uint64_t seed, int64_t row0, int64_t nrows, int col0, int ncols, double* q,
+                                int64_t ldq, void* stream) {
+  PBH_REQUIRE(row0 >= 0 && nrows >= 0, "pbh_fill_uniform: bad row range");
+  PBH_REQUIRE(ncols >= 0 && col0 >= 0 && ncols <= 65535, "pbh_fill_uniform: bad column range");
+  PBH_REQUIRE(ldq >= nrows, "pbh_fill_uniform: ldq < nrows");
+  if (nrows == 0 || ncols == 0) return PBH_OK;
+  dim3 g(grid_for(nrows, kBlock, 4096), (unsigned)ncols);
+  hipLaunchKernelGGL(k_fill_uniform, g, dim3(kBlock), 0, as_stream(stream), seed, row0, nrows, col0, q, ldq);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+extern "C" int pbh_fill_sobol(const uint32_t* sv_host, const uint32_t* shift_host, int d, int bits, int64_t row0,
+                              int64_t nrows, int col0, int ncols, double* q, int64_t ldq, void* stream) {
+  PBH_REQUIRE(sv_host && shift_host, "pbh_fill_sobol: sv/shift must be host arrays");
+  PBH_REQUIRE(bits >= 1 && bits <= 32, "pbh_fill_sobol: bits must be in [1, 32]");
+  PBH_REQUIRE(col0 >= 0 && ncols >= 0 && col0 + ncols <= d, "pbh_fill_sobol: bad column range");
+  PBH_REQUIRE(row0 >= 0 && nrows >= 0 && (row0 + nrows) <= (int64_t)1 << bits, "pbh_fill_sobol: rows exceed 2^bits");
+  PBH_REQUIRE(ldq >= nrows, "pbh_fill_sobol: ldq < nrows");
+  if (nrows == 0 || ncols == 0) return PBH_OK;
+  const double scale = 1.0 / (double)((uint64_t)1 << bits);
+  for (int c0 = 0; c0 < ncols; c0 += kSobolColsPerLaunch) {
+    int nc = ncols - c0 < kSobolColsPerLaunch ? ncols - c0 : kSobolColsPerLaunch;
+    SobolArgs a = {};
+    for (int c = 0; c < nc; ++c) {
+      int col = col0 + c0 + c;
+      for (int b = 0; b < bits; ++b) a.sv[c][b] = sv_host[(int64_t)col * bits + b];
+      a.shift[c] = shift_host[col];
+    }
+    dim3 g(grid_for(nrows, kBlock, 4096), (unsigned)nc);
+    hipLaunchKernelGGL(k_fill_sobol, g, dim3(kBlock), 0, as_stream(stream), a, scale, row0, nrows,
+                       q + (int64_t)c0 * ldq, ldq);
+    PBH_CHECK_LAUNCH();
+  }
+  return PBH_OK;
+}

@@ -1,0 +1,144 @@
+// Counter-based random streams for the native quantile generators.
+//
+// Philox4x32-10 (Salmon et al., SC'11) keyed by the 64-bit seed; the counter carries
+// (row, column, purpose), so every (row, column) draw is independent of launch geometry
+// and of how rows are sharded across GPUs.
+//
+// The LHS permutation of column c is a keyed bijection of [0, n): a balanced Feistel
+// network on the smallest even bit width 2h with 2^(2h) >= n, restricted to [0, n) by
+// cycle walking (Black & Rogaway 2002).  Both directions are cheap, so a row's stratum and
+// a stratum's row are computed, never stored.
+#pragma once
+
+#include "pbh_common.h"
+
+namespace pbh {
+
+struct Philox {
+  uint32_t k0, k1;
+  PBH_HD explicit Philox(uint64_t seed) : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)) {}
+
+  PBH_HD static inline void mulhilo(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
+    uint64_t p = (uint64_t)a * (uint64_t)b;
+    hi = (uint32_t)(p >> 32);
+    lo = (uint32_t)p;
+  }
+
+  // 10 rounds on counter c[0..3]; returns 4 words in c.
+  PBH_HD inline void operator()(uint32_t c[4]) const {
+    uint32_t a0 = k0, a1 = k1;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      uint32_t hi0, lo0, hi1, lo1;
+      mulhilo(0xD2511F53u, c[0], hi0, lo0);
+      mulhilo(0xCD9E8D57u, c[2], hi1, lo1);
+      uint32_t n0 = hi1 ^ c[1] ^ a0;
+      uint32_t n2 = hi0 ^ c[3] ^ a1;
+      c[0] = n0;
+      c[1] = lo1;
+      c[2] = n2;
+      c[3] = lo0;
+      a0 += 0x9E3779B9u;
+      a1 += 0xBB67AE85u;
+    }
+  }
+
+  // Uniform double in [0, 1) with 53 random bits: (u64 >> 11) * 2^-53 (numpy's next_double).
+  PBH_HD inline double uniform(uint64_t row, uint32_t col, uint32_t purpose) const {
+    uint32_t c[4] = {(uint32_t)row, (uint32_t)(row >> 32), col, purpose};
+    (*this)(c);
+    uint64_t u = ((uint64_t)c[1] << 32) | c[0];
+    return (double)(u >> 11) * 0x1.0p-53;
+  }
+};
+
+enum : uint32_t {
+  kPurposeLhsU = 0x4C485355u,   // 'LHSU'
+  kPurposeFeistel = 0x46454953u,  // 'FEIS'
+  kPurposeUniform = 0x50524E47u   // 'PRNG'
+};
+
+PBH_HD inline uint32_t mix32(uint32_t x) {  // lowbias32 finalizer
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+struct FeistelPerm {
+  static constexpr int kRounds = 6;
+  uint64_t n;
+  uint32_t half_bits, mask;
+  uint32_t rk[kRounds];
+
+  PBH_HD FeistelPerm(const Philox& ph, uint64_t n_, uint32_t col) : n(n_) {
+    uint32_t bits = 0;
+    while (bits < 64 && (1ull << bits) < n_) ++bits;
+    if (bits & 1u) ++bits;
+    if (bits < 2) bits = 2;
+    half_bits = bits / 2;
+    mask = (half_bits >= 32) ? 0xFFFFFFFFu : ((1u << half_bits) - 1u);
+    uint32_t c[4] = {col, 0u, 0u, kPurposeFeistel};
+    ph(c);
+    uint32_t d[4] = {col, 1u, 0u, kPurposeFeistel};
+    ph(d);
+    rk[0] = c[0];
+    rk[1] = c[1];
+    rk[2] = c[2];
+    rk[3] = c[3];
+    rk[4] = d[0];
+    rk[5] = d[1];
+  }
+
+  PBH_HD inline uint32_t F(uint32_t r, uint32_t k) const { return mix32(r * 0x9E3779B1u ^ k) & mask; }
+
+  PBH_HD inline uint64_t round_trip(uint64_t x) const {
+    uint32_t L = (uint32_t)(x >> half_bits), R = (uint32_t)(x & mask);
+#pragma unroll
+    for (int i = 0; i < kRounds; ++i) {
+      uint32_t t = L ^ F(R, rk[i]);
+      L = R;
+      R = t;
+    }
+    return ((uint64_t)L << half_bits) | R;
+  }
+
+  PBH_HD inline uint64_t round_trip_inv(uint64_t y) const {
+    uint32_t L = (uint32_t)(y >> half_bits), R = (uint32_t)(y & mask);
+#pragma unroll
+    for (int i = kRounds - 1; i >= 0; --i) {
+      uint32_t t = R ^ F(L, rk[i]);
+      R = L;
+      L = t;
+    }
+    return ((uint64_t)L << half_bits) | R;
+  }
+
+  // Bijection of [0, n) by cycle walking.
+  PBH_HD inline uint64_t operator()(uint64_t x) const {
+    if (n <= 1) return 0;
+    do {
+      x = round_trip(x);
+    } while (x >= n);
+    return x;
+  }
+  PBH_HD inline uint64_t inverse(uint64_t y) const {
+    if (n <= 1) return 0;
+    do {
+      y = round_trip_inv(y);
+    } while (y >= n);
+    return y;
+  }
+};
+
+// q = (perm + 1 - u) / n: scipy's `(perms - samples) / n` with perms in 1..n
+// (scipy:stats/_qmc.py LatinHypercube._random_lhs).
+PBH_HD inline double lhs_quantile(const Philox& ph, const FeistelPerm& fp, uint64_t row, uint32_t col) {
+  uint64_t p = fp(row);
+  double u = ph.uniform(row, col, kPurposeLhsU);
+  return ((double)(p + 1) - u) / (double)fp.n;
+}
+
+}  // namespace pbh

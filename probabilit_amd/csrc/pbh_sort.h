@@ -1,0 +1,44 @@
+// Device radix sort of one column of float64 keys with a uint32 row payload.
+//
+// This is the "argsort" inside scipy.stats.rankdata (scipy:stats/_stats_py.py _rankdata,
+// reached from correlation.py:394 and :422) and the np.sort of correlation.py:423.
+// Stable LSD radix sort over the order-preserving 64-bit image of the doubles, 8-bit
+// digits, tiles of 4096 keys per 256-thread workgroup:
+//   upsweep  : per-tile digit histogram                       (read 8 B/key)
+//   scan     : exclusive scan of the [digit][tile] count table
+//   scatter  : stable in-tile ranking with wave64 ballots, LDS-staged so that every
+//              digit run leaves the tile as one contiguous burst (read 12, write 12 B/key)
+// Byte positions on which every key agrees are skipped (one histogram pass up front).
+#pragma once
+
+#include "pbh_common.h"
+
+namespace pbh {
+
+struct SortBuffers {
+  uint64_t* keys[2];
+  uint32_t* vals[2];
+  uint32_t* counts;    // 256 * ntiles
+  uint32_t* partials;  // scan partials
+  uint32_t* hist;      // 8 * 256 digit histogram
+  uint32_t* hist_host; // pinned host mirror of hist (8 * 256)
+};
+
+constexpr int kSortThreads = 256;
+constexpr int kSortItems = 16;
+constexpr int kSortTile = kSortThreads * kSortItems;  // 4096
+
+inline int64_t sort_tiles(int64_t n) { return (n + kSortTile - 1) / kSortTile; }
+inline int64_t scan_partials_count(int64_t m) { return (m + 2047) / 2048; }
+
+// Workspace (bytes) for sorting n keys, excluding nothing: keys x2, vals x2, counts,
+// partials, histogram.
+size_t sort_workspace_bytes(int64_t n);
+void sort_carve(void* ws, int64_t n, SortBuffers& b);
+
+// Sorts keys in b.keys[0] (payload: row index, generated) and returns the index (0/1) of
+// the buffer holding the sorted keys / payload.  `stream` ordered; synchronises once to read
+// the digit histogram (pass skipping).  Returns < 0 and sets the last error on failure.
+int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf);
+
+}  // namespace pbh

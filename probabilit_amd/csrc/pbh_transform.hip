@@ -1,0 +1,319 @@
+// Elementwise Transform nodes (modeling.py:933-1169) with numpy semantics, plus the
+// Avg reduction (modeling.py:986-990) and an LDS-tiled transpose.
+//
+// The host decides numpy's result dtype and passes (compute dtype, output dtype); the
+// kernel is HBM-bound (8 B per float64 operand vector read, 8 B written per element).
+#include <math.h>
+
+#include "pbh_error.h"
+#include "pbh_timing.h"
+
+namespace pbh {
+namespace {
+
+constexpr int kBlock = 256;
+
+PBH_DI double ld_f(const pbh_operand& o, int64_t i) {
+  if (!o.ptr) return o.dtype == PBH_FLOAT64 ? o.f : (double)o.i;
+  switch (o.dtype) {
+    case PBH_FLOAT64:
+      return ((const double*)o.ptr)[i];
+    case PBH_INT64:
+      return (double)((const int64_t*)o.ptr)[i];
+    default:
+      return ((const uint8_t*)o.ptr)[i] ? 1.0 : 0.0;
+  }
+}
+
+PBH_DI int64_t ld_i(const pbh_operand& o, int64_t i) {
+  if (!o.ptr) return o.dtype == PBH_FLOAT64 ? (int64_t)o.f : o.i;
+  switch (o.dtype) {
+    case PBH_FLOAT64:
+      return (int64_t)((const double*)o.ptr)[i];
+    case PBH_INT64:
+      return ((const int64_t*)o.ptr)[i];
+    default:
+      return ((const uint8_t*)o.ptr)[i] ? 1 : 0;
+  }
+}
+
+// numpy npy_divmod / npy_floor_divide / npy_remainder for float64
+PBH_DI double np_divmod(double a, double b, double* modp) {
+  double mod = fmod(a, b);
+  if (b == 0.0) {
+    *modp = mod;
+    return a / b;
+  }
+  double div = (a - mod) / b;
+  if (mod != 0.0) {
+    if ((b < 0) != (mod < 0)) {
+      mod += b;
+      div -= 1.0;
+    }
+  } else {
+    mod = copysign(0.0, b);
+  }
+  double floordiv;
+  if (div != 0.0) {
+    floordiv = floor(div);
+    if (div - floordiv > 0.5) floordiv += 1.0;
+  } else {
+    floordiv = copysign(0.0, a / b);
+  }
+  *modp = mod;
+  return floordiv;
+}
+PBH_DI double np_floordiv(double a, double b) {
+  if (b == 0.0) return a / b;
+  double m;
+  return np_divmod(a, b, &m);
+}
+PBH_DI double np_remainder(double a, double b) {
+  if (b == 0.0) return fmod(a, b);
+  double m;
+  np_divmod(a, b, &m);
+  return m;
+}
+
+PBH_DI int64_t i_floordiv(int64_t a, int64_t b) {
+  if (b == 0) return 0;
+  if (a == INT64_MIN && b == -1) return INT64_MIN;
+  int64_t q = a / b;
+  if (((a % b) != 0) && ((a < 0) != (b < 0))) q -= 1;
+  return q;
+}
+PBH_DI int64_t i_mod(int64_t a, int64_t b) {
+  if (b == 0) return 0;
+  if (b == -1) return 0;
+  int64_t r = a % b;
+  if (r != 0 && ((r < 0) != (b < 0))) r += b;
+  return r;
+}
+PBH_DI int64_t i_pow(int64_t a, int64_t b) {
+  uint64_t r = 1, base = (uint64_t)a;
+  while (b > 0) {
+    if (b & 1) r *= base;
+    base *= base;
+    b >>= 1;
+  }
+  return (int64_t)r;
+}
+
+PBH_DI double f_binary(int op, double a, double b) {
+  switch (op) {
+    case PBH_OP_ADD: return a + b;
+    case PBH_OP_SUB: return a - b;
+    case PBH_OP_MUL: return a * b;
+    case PBH_OP_TRUEDIV: return a / b;
+    case PBH_OP_FLOORDIV: return np_floordiv(a, b);
+    case PBH_OP_MOD: return np_remainder(a, b);
+    case PBH_OP_POW: return pow(a, b);
+    case PBH_OP_MAX: return (a >= b || isnan(a)) ? a : b;
+    case PBH_OP_MIN: return (a <= b || isnan(a)) ? a : b;
+    case PBH_OP_ARCTAN2: return atan2(a, b);
+    case PBH_OP_AND: return (a != 0.0 && b != 0.0) ? 1.0 : 0.0;
+    case PBH_OP_OR: return (a != 0.0 || b != 0.0) ? 1.0 : 0.0;
+    case PBH_OP_EQ: return a == b;
+    case PBH_OP_NE: return a != b;
+    case PBH_OP_LT: return a < b;
+    case PBH_OP_LE: return a <= b;
+    case PBH_OP_GT: return a > b;
+    case PBH_OP_GE: return a >= b;
+    case PBH_OP_ISCLOSE: {  // np.isclose(a, b) with rtol=1e-5, atol=1e-8, equal_nan=False
+      bool fin = isfinite(a) && isfinite(b);
+      return fin ? (fabs(a - b) <= 1e-08 + 1e-05 * fabs(b)) : (a == b);
+    }
+    default: return __builtin_nan("");
+  }
+}
+
+PBH_DI double f_unary(int op, double a) {
+  switch (op) {
+    case PBH_OP_NEG: return -a;
+    case PBH_OP_ABS: return fabs(a);
+    case PBH_OP_LOG: return log(a);
+    case PBH_OP_EXP: return exp(a);
+    case PBH_OP_FLOOR: return floor(a);
+    case PBH_OP_CEIL: return ceil(a);
+    case PBH_OP_SIGN: return a > 0.0 ? 1.0 : (a < 0.0 ? -1.0 : (a == 0.0 ? 0.0 : a));
+    case PBH_OP_SQRT: return sqrt(a);
+    case PBH_OP_SQUARE: return a * a;
+    case PBH_OP_LOG10: return log10(a);
+    case PBH_OP_SIN: return sin(a);
+    case PBH_OP_COS: return cos(a);
+    case PBH_OP_TAN: return tan(a);
+    case PBH_OP_ARCSIN: return asin(a);
+    case PBH_OP_ARCCOS: return acos(a);
+    case PBH_OP_ARCTAN: return atan(a);
+    case PBH_OP_SINH: return sinh(a);
+    case PBH_OP_COSH: return cosh(a);
+    case PBH_OP_TANH: return tanh(a);
+    case PBH_OP_ARCSINH: return asinh(a);
+    case PBH_OP_ARCCOSH: return acosh(a);
+    case PBH_OP_ARCTANH: return atanh(a);
+    default: return a;  // CAST
+  }
+}
+
+PBH_DI int64_t i_binary(int op, int64_t a, int64_t b, bool* neg_pow) {
+  switch (op) {
+    case PBH_OP_ADD: return (int64_t)((uint64_t)a + (uint64_t)b);
+    case PBH_OP_SUB: return (int64_t)((uint64_t)a - (uint64_t)b);
+    case PBH_OP_MUL: return (int64_t)((uint64_t)a * (uint64_t)b);
+    case PBH_OP_FLOORDIV: return i_floordiv(a, b);
+    case PBH_OP_MOD: return i_mod(a, b);
+    case PBH_OP_POW:
+      if (b < 0) *neg_pow = true;
+      return i_pow(a, b);
+    case PBH_OP_MAX: return a > b ? a : b;
+    case PBH_OP_MIN: return a < b ? a : b;
+    case PBH_OP_AND: return (a != 0 && b != 0);
+    case PBH_OP_OR: return (a != 0 || b != 0);
+    case PBH_OP_EQ: return a == b;
+    case PBH_OP_NE: return a != b;
+    case PBH_OP_LT: return a < b;
+    case PBH_OP_LE: return a <= b;
+    case PBH_OP_GT: return a > b;
+    case PBH_OP_GE: return a >= b;
+    default: return 0;
+  }
+}
+
+PBH_DI int64_t i_unary(int op, int64_t a) {
+  switch (op) {
+    case PBH_OP_NEG: return (int64_t)(0ull - (uint64_t)a);
+    case PBH_OP_ABS: return a < 0 ? (int64_t)(0ull - (uint64_t)a) : a;
+    case PBH_OP_SIGN: return (a > 0) - (a < 0);
+    case PBH_OP_SQUARE: return (int64_t)((uint64_t)a * (uint64_t)a);
+    case PBH_OP_FLOOR:
+    case PBH_OP_CEIL:
+    default: return a;  // CAST
+  }
+}
+
+PBH_DI void flag_bits(int32_t* flag, bool cond, int bit) {
+  if (flag == nullptr) return;
+  unsigned long long m = __ballot(cond);
+  if (m != 0ull && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(m)) atomicOr(flag, bit);
+}
+
+__global__ __launch_bounds__(kBlock) void k_elementwise(int op, int cdt, int odt, pbh_operand a, pbh_operand b,
+                                                        void* __restrict__ out, int64_t n, int32_t* flag) {
+  const bool unary = op >= PBH_OP_NEG;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    bool bad = false, negpow = false;
+    if (cdt == PBH_FLOAT64) {
+      double x = unary ? f_unary(op, ld_f(a, i)) : f_binary(op, ld_f(a, i), ld_f(b, i));
+      if (odt == PBH_FLOAT64) {
+        ((double*)out)[i] = x;
+        bad = !isfinite(x);
+      } else if (odt == PBH_INT64) {
+        ((int64_t*)out)[i] = (int64_t)x;
+      } else {
+        ((uint8_t*)out)[i] = x != 0.0;
+      }
+    } else {  // INT64 or BOOL compute: integer arithmetic on 0/1 for bool
+      int64_t x;
+      if (unary) {
+        x = i_unary(op, ld_i(a, i));
+      } else {
+        int64_t u = ld_i(a, i), v = ld_i(b, i);
+        if (cdt == PBH_BOOL) {  // numpy bool arithmetic: + is or, * is and
+          if (op == PBH_OP_ADD) op = PBH_OP_OR;
+          if (op == PBH_OP_MUL) op = PBH_OP_AND;
+        }
+        x = i_binary(op, u, v, &negpow);
+      }
+      if (odt == PBH_FLOAT64)
+        ((double*)out)[i] = (double)x;
+      else if (odt == PBH_INT64)
+        ((int64_t*)out)[i] = x;
+      else
+        ((uint8_t*)out)[i] = x != 0;
+    }
+    flag_bits(flag, bad, 1);
+    flag_bits(flag, negpow, 2);
+  }
+}
+
+struct AvgArgs {
+  const double* p[32];
+};
+
+__global__ __launch_bounds__(kBlock) void k_average(AvgArgs args, int m, int64_t n, double* __restrict__ out,
+                                                    int32_t* flag) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    double s = args.p[0][i];
+    for (int j = 1; j < m; ++j) s += args.p[j][i];
+    double x = s / (double)m;
+    out[i] = x;
+    flag_bits(flag, !isfinite(x), 1);
+  }
+}
+
+constexpr int TT = 32;
+__global__ __launch_bounds__(TT * 8) void k_transpose(const double* __restrict__ in, int64_t rows, int64_t cols,
+                                                      int64_t ld_in, double* __restrict__ out, int64_t ld_out) {
+  // in: rows x cols, element (r, c) at in[r * ld_in + c]; out(c, r) at out[c * ld_out + r]
+  __shared__ double tile[TT][TT + 1];
+  const int64_t r0 = (int64_t)blockIdx.x * TT, c0 = (int64_t)blockIdx.y * TT;
+  for (int y = threadIdx.y; y < TT; y += 8) {
+    int64_t r = r0 + y, c = c0 + threadIdx.x;
+    if (r < rows && c < cols) tile[y][threadIdx.x] = in[r * ld_in + c];
+  }
+  __syncthreads();
+  for (int y = threadIdx.y; y < TT; y += 8) {
+    int64_t c = c0 + y, r = r0 + threadIdx.x;
+    if (r < rows && c < cols) out[c * ld_out + r] = tile[threadIdx.x][y];
+  }
+}
+
+}  // namespace
+}  // namespace pbh
+
+using namespace pbh;
+
+extern "C" int pbh_elementwise(int op, int compute_dtype, int out_dtype, const pbh_operand* a, const pbh_operand* b,
+                               void* out, int64_t n, int32_t* nonfinite_flag, void* stream) {
+  PBH_REQUIRE(a != nullptr && out != nullptr, "pbh_elementwise: a and out required");
+  PBH_REQUIRE(compute_dtype >= PBH_BOOL && compute_dtype <= PBH_FLOAT64, "pbh_elementwise: bad compute dtype");
+  PBH_REQUIRE(out_dtype >= PBH_BOOL && out_dtype <= PBH_FLOAT64, "pbh_elementwise: bad output dtype");
+  const bool unary = op >= PBH_OP_NEG;
+  PBH_REQUIRE((op >= PBH_OP_ADD && op <= PBH_OP_ARCTAN2) || (op >= PBH_OP_NEG && op <= PBH_OP_ARCTANH) ||
+                  op == PBH_OP_CAST,
+              "pbh_elementwise: unknown op %d", op);
+  PBH_REQUIRE(unary || b != nullptr, "pbh_elementwise: binary op needs b");
+  if (n <= 0) return PBH_OK;
+  pbh_operand bb = unary ? *a : *b;
+  hipStream_t s = as_stream(stream);
+  PBH_TIMED(kKElementwise, s,
+            hipLaunchKernelGGL(k_elementwise, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, op, compute_dtype,
+                               out_dtype, *a, bb, out, n, nonfinite_flag));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+extern "C" int pbh_average(const double* const* parents_host, int m, int64_t n, double* out, int32_t* nonfinite_flag,
+                           void* stream) {
+  PBH_REQUIRE(m >= 1 && m <= 32, "pbh_average: 1 <= m <= 32 parents supported");
+  PBH_REQUIRE(parents_host && out, "pbh_average: null pointer");
+  if (n <= 0) return PBH_OK;
+  AvgArgs a = {};
+  for (int j = 0; j < m; ++j) a.p[j] = parents_host[j];
+  hipLaunchKernelGGL(k_average, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, as_stream(stream), a, m, n, out,
+                     nonfinite_flag);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+extern "C" int pbh_transpose(const double* in, int64_t rows, int64_t cols, int64_t ld_in, double* out,
+                             int64_t ld_out, void* stream) {
+  PBH_REQUIRE(in && out, "pbh_transpose: null pointer");
+  PBH_REQUIRE(ld_in >= cols && ld_out >= rows, "pbh_transpose: bad leading dimension");
+  if (rows <= 0 || cols <= 0) return PBH_OK;
+  PBH_REQUIRE((cols + TT - 1) / TT <= 65535, "pbh_transpose: too many columns per launch");
+  dim3 g((unsigned)((rows + TT - 1) / TT), (unsigned)((cols + TT - 1) / TT)), b(TT, 8);
+  hipLaunchKernelGGL(k_transpose, g, b, 0, as_stream(stream), in, rows, cols, ld_in, out, ld_out);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}

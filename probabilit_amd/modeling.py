@@ -1,0 +1,831 @@
+"""Drop-in for probabilit.modeling (tommyod/probabilit @ 2025-09-19, src/probabilit/modeling.py).
+
+The modeling language is unchanged: Node / Constant / Distribution / Transform classes with
+overloaded operators build a lazy DAG, `Node.sample(size, random_state, method, correlator,
+gc_strategy)` draws quantiles and `Node.sample_from_quantiles(quantiles, ...)` evaluates the
+graph.  What changes is where the numbers live and who computes them:
+
+* every node's samples are a device vector in HBM (torch-allocated, `cuda:<LOCAL_RANK>`);
+  `node.samples_` is a numpy view materialised lazily on first access (one D2H copy);
+* quantile columns come from GPU generators (probabilit_amd.qmc), the inverse CDFs from
+  HIP kernels (pbh_ppf / fused pbh_lhs_ppf), transforms from pbh_elementwise, and the
+  Iman-Conover reorder from pbh_iman_conover;
+* Constants stay scalars until someone reads `.samples_` (Constant._sample of :760-763 is
+  an `np.ones(size) * value` broadcast; no kernel needs it materialised);
+* the non-finite check of :600-606 is fused into the producing kernels (one device flag
+  per node, read once at the end; the first offending node in topological order raises).
+
+Node-visiting order, quantile-column assignment (initial sampling nodes by creation id,
+then the rest in networkx topological order), correlation validation, garbage collection
+and the errors raised follow the reference line by line (citations below).
+"""
+
+import abc
+import copy
+import ctypes
+import functools
+import itertools
+import numbers
+
+import networkx as nx
+import numpy as np
+import scipy.stats
+
+from . import _lib, device, qmc
+from .correlation import Cholesky, ImanConover, nearest_correlation_matrix
+from .garbage_collector import GarbageCollector
+from .utils import build_corrmat
+
+__all__ = ["Node", "Constant", "Distribution", "EmpiricalDistribution", "CumulativeDistribution",
+           "DiscreteDistribution", "Transform", "VariadicTransform", "BinaryTransform", "UnaryTransform",
+           "NoOp", "Avg", "scalar_transform", "MultivariateDistribution", "MarginalDistribution"]
+
+
+def python_to_prob(argument):
+    """Numbers become Constants, Nodes pass through (modeling.py:272-279)."""
+    if isinstance(argument, numbers.Number):
+        return Constant(argument)
+    if isinstance(argument, Node):
+        return argument
+    raise ValueError(f"Type not compatible with probabilit: {argument}")
+
+
+# =============================================================================
+# device sample containers
+# =============================================================================
+_PBH_DTYPE = {np.dtype(bool): _lib.BOOL, np.dtype(np.int64): _lib.INT64, np.dtype(np.float64): _lib.FLOAT64}
+
+
+def _canonical(dt):
+    """The device dtype used for numpy dtype `dt` (bool / int64 / float64)."""
+    dt = np.dtype(dt)
+    if dt == np.bool_:
+        return np.dtype(bool)
+    if np.issubdtype(dt, np.integer):
+        return np.dtype(np.int64)
+    if np.issubdtype(dt, np.floating):
+        return np.dtype(np.float64)
+    raise TypeError(f"probabilit_amd: samples of dtype {dt} are not supported on the device")
+
+
+class _Broadcast:
+    """A Constant's `np.ones(size, dtype=type(value)) * value` kept as a scalar."""
+
+    __slots__ = ("value", "n", "dtype")
+
+    def __init__(self, value, n, dtype=None):
+        self.dtype = _canonical(np.dtype(type(value)) if dtype is None else dtype)
+        self.value = self.dtype.type(value)
+        self.n = int(n)
+
+    def host(self):
+        return np.full(self.n, self.value, dtype=self.dtype)
+
+    def operand(self):
+        v = self.value
+        if self.dtype == np.float64:
+            return _lib.Operand(None, _lib.FLOAT64, float(v), 0)
+        return _lib.Operand(None, _PBH_DTYPE[self.dtype], float(v), int(v))
+
+
+def _dtype_of(x):
+    if isinstance(x, _Broadcast):
+        return x.dtype
+    import torch
+
+    return {torch.float64: np.dtype(np.float64), torch.int64: np.dtype(np.int64),
+            torch.bool: np.dtype(bool)}[x.dtype]
+
+
+def _operand(x):
+    if isinstance(x, _Broadcast):
+        return x.operand()
+    return _lib.Operand(x.data_ptr(), _PBH_DTYPE[_dtype_of(x)], 0.0, 0)
+
+
+def _to_device_samples(value):
+    import torch
+
+    if value is None or isinstance(value, _Broadcast):
+        return value
+    if isinstance(value, torch.Tensor):
+        return value
+    a = np.asarray(value)
+    return device.to_device(a.astype(_canonical(a.dtype), copy=False))
+
+
+def _alloc(n, dt):
+    return device.empty(n, _canonical(dt).name)
+
+
+def _as_float_vector(x, n):
+    """float64 device vector or python float for a distribution parameter."""
+    if isinstance(x, _Broadcast):
+        return float(x.value)
+    if _dtype_of(x) == np.float64:
+        return x
+    return _elementwise("cast", x, None, n, np.dtype(np.float64), np.dtype(np.float64), flag=None)
+
+
+class _Evaluation:
+    """Per-sample() state: one non-finite flag per node, the current size."""
+
+    def __init__(self, size, nodes):
+        self.size = size
+        self.slot = {node: i for i, node in enumerate(nodes)}
+        self.flags = device.zeros(max(len(nodes), 1), "int32")
+
+    def flag_ptr(self, node):
+        return self.flags.data_ptr() + 4 * self.slot[node]
+
+
+# =============================================================================
+# device kernels behind the Transform nodes
+# =============================================================================
+_NP_BINARY = {"add": np.add, "sub": np.subtract, "mul": np.multiply, "truediv": np.true_divide,
+              "floordiv": np.floor_divide, "mod": np.mod, "pow": np.power, "max": np.maximum,
+              "min": np.minimum, "and": np.logical_and, "or": np.logical_or, "eq": np.equal,
+              "ne": np.not_equal, "lt": np.less, "le": np.less_equal, "gt": np.greater,
+              "ge": np.greater_equal, "isclose": np.isclose, "arctan2": np.arctan2}
+_NP_UNARY = {"neg": np.negative, "abs": np.absolute, "log": np.log, "exp": np.exp, "floor": np.floor,
+             "ceil": np.ceil, "sign": np.sign, "sqrt": np.sqrt, "square": np.square, "log10": np.log10,
+             "sin": np.sin, "cos": np.cos, "tan": np.tan, "arcsin": np.arcsin, "arccos": np.arccos,
+             "arctan": np.arctan, "sinh": np.sinh, "cosh": np.cosh, "tanh": np.tanh, "arcsinh": np.arcsinh,
+             "arccosh": np.arccosh, "arctanh": np.arctanh}
+_COMPARISONS = {"eq", "ne", "lt", "le", "gt", "ge", "isclose"}
+
+
+def _numpy_result(op, dta, dtb=None):
+    """numpy's own answer for the result dtype (and its TypeError for e.g. bool - bool)."""
+    a = np.ones(1, dtype=dta)
+    with np.errstate(all="ignore"):
+        if dtb is None:
+            return _NP_UNARY[op](a).dtype
+        return _NP_BINARY[op](a, np.ones(1, dtype=dtb)).dtype
+
+
+def _elementwise(op, a, b, n, out_dt, compute_dt, flag):
+    out = _alloc(n, out_dt)
+    oa = _operand(a)
+    ob = _operand(b) if b is not None else oa
+    lib = _lib.load()
+    _lib.check(lib.pbh_elementwise(_lib.OPS[op], _PBH_DTYPE[_canonical(compute_dt)], _PBH_DTYPE[_canonical(out_dt)],
+                                   oa, ob, out.data_ptr(), n, flag, device.stream()), f"transform {op}")
+    return out
+
+
+def _binary(op, a, b, n, flag=None):
+    dta, dtb = _dtype_of(a), _dtype_of(b)
+    res = _numpy_result(op, dta, dtb)
+    if isinstance(a, _Broadcast) and isinstance(b, _Broadcast):
+        with np.errstate(all="ignore"):
+            v = _NP_BINARY[op](np.ones(1, dta) * a.value, np.ones(1, dtb) * b.value)
+        if op == "pow" and np.issubdtype(res, np.integer) and b.value < 0:
+            raise ValueError("Integers to negative integer powers are not allowed.")
+        return _Broadcast(v[0], n, res)
+    out_dt = _canonical(res)
+    if op in _COMPARISONS or op in ("and", "or"):
+        compute = _canonical(np.result_type(dta, dtb))
+        if op in ("isclose", "and", "or"):
+            compute = np.dtype(np.float64)
+    else:
+        compute = out_dt
+    return _elementwise(op, a, b, n, out_dt, compute, flag)
+
+
+def _unary(op, a, n, flag=None):
+    dta = _dtype_of(a)
+    res = _numpy_result(op, dta)
+    if isinstance(a, _Broadcast):
+        with np.errstate(all="ignore"):
+            v = _NP_UNARY[op](np.ones(1, dta) * a.value)
+        return _Broadcast(v[0], n, res)
+    out_dt = _canonical(res)
+    compute = out_dt
+    if op not in ("neg", "abs", "sign", "square", "floor", "ceil") and out_dt != np.float64:
+        compute = np.dtype(np.float64)
+    return _elementwise(op, a, None, n, out_dt, compute, flag)
+
+
+# =============================================================================
+# COMPUTATIONAL GRAPH AND MODELING LANGUAGE
+# =============================================================================
+class Node(abc.ABC):
+    """A node in the computational graph (modeling.py:335-680)."""
+
+    id_iter = itertools.count()  # creation order = the ISN column order (modeling.py:525)
+
+    def __init__(self):
+        self._id = next(self.id_iter)
+        self._correlations = []
+
+    def __eq__(self, other):
+        if not isinstance(other, Node):
+            return NotImplemented
+        return self._id == other._id
+
+    def __hash__(self):
+        return self._id
+
+    # ---- samples: device vector + lazily materialised numpy view ----------------
+    @property
+    def samples_(self):
+        d = self.__dict__
+        if "_smp" not in d:
+            raise AttributeError(f"'{type(self).__name__}' object has no attribute 'samples_'")
+        dev = d["_smp"]
+        if dev is None:
+            return None
+        if d.get("_host") is None:
+            d["_host"] = dev.host() if isinstance(dev, _Broadcast) else device.to_host(dev)
+        return d["_host"]
+
+    @samples_.setter
+    def samples_(self, value):
+        self.__dict__["_smp"] = _to_device_samples(value)
+        self.__dict__["_host"] = value if isinstance(value, np.ndarray) else None
+
+    @samples_.deleter
+    def samples_(self):
+        if "_smp" not in self.__dict__:
+            raise AttributeError("samples_")
+        del self.__dict__["_smp"]
+        self.__dict__.pop("_host", None)
+
+    @property
+    def samples_device(self):
+        """The device tensor behind `samples_` (a scalar broadcast is materialised)."""
+        dev = self.__dict__["_smp"]
+        if isinstance(dev, _Broadcast):
+            dev = _elementwise("cast", dev, None, dev.n, dev.dtype, dev.dtype, None)
+        return dev
+
+    def _set_device(self, dev):
+        self.__dict__["_smp"] = dev
+        self.__dict__["_host"] = None
+
+    def _dev(self):
+        return self.__dict__["_smp"]
+
+    # ---- graph -------------------------------------------------------------------
+    def copy(self):
+        """Copy the node and the graph above it (modeling.py:353-404)."""
+        new = {}
+
+        def remap(item):
+            return new[item._id] if isinstance(item, Node) else copy.deepcopy(item)
+
+        for node in nx.topological_sort(self.to_graph()):
+            dup = copy.copy(node)
+            dup.__dict__ = dict(node.__dict__)
+            new[dup._id] = dup
+            dev = dup.__dict__.get("_smp")
+            if dev is not None and not isinstance(dev, _Broadcast):
+                dup.__dict__["_smp"] = dev.clone()
+                dup.__dict__["_host"] = None
+            dup._correlations = copy.deepcopy(dup._correlations)
+            if isinstance(dup, (AbstractDistribution, ScalarFunctionTransform)) and hasattr(dup, "args"):
+                dup.args = tuple(remap(a) for a in dup.args)
+                dup.kwargs = {k: remap(v) for k, v in dup.kwargs.items()}
+            elif isinstance(dup, (VariadicTransform, BinaryTransform)):
+                dup.parents = tuple(remap(p) for p in dup.parents)
+            elif isinstance(dup, UnaryTransform):
+                dup.parent = remap(dup.parent)
+            elif isinstance(dup, MarginalDistribution):
+                dup.distr = remap(dup.distr)
+            elif isinstance(dup, Constant):
+                dup.value = remap(dup.value)
+        return new[self._id]
+
+    def nodes(self):
+        """Yield self and all ancestors, depth first (modeling.py:406-423)."""
+        stack = [self]
+        while stack:
+            node = stack.pop()
+            yield node
+            stack.extend(node.get_parents())
+
+    def num_distribution_nodes(self):
+        return sum(1 for node in set(self.nodes()) if isinstance(node, AbstractDistribution))
+
+    def to_graph(self):
+        """networkx MultiDiGraph of the expression (modeling.py:663-680)."""
+        nodes = list(self.nodes())
+        if len(nodes) == 1:
+            G = nx.MultiDiGraph()
+            G.add_node(self)
+            return G
+        return nx.MultiDiGraph([(parent, node) for node in nodes for parent in node.get_parents()
+                                if not node.is_leaf])
+
+    def _is_initial_sampling_node(self):
+        """A Distribution none of whose ancestors is a Distribution (modeling.py:616-626)."""
+        if not isinstance(self, AbstractDistribution):
+            return False
+        return not any(isinstance(n, AbstractDistribution) for n in set(self.nodes()) - {self})
+
+    def correlate(self, *variables, corr_mat):
+        """Record a correlation between ancestor variables (modeling.py:628-661)."""
+        assert corr_mat.ndim == 2
+        assert corr_mat.shape[0] == corr_mat.shape[1]
+        assert corr_mat.shape[0] == len(variables)
+        assert len(variables) == len(set(variables))
+        ancestors = set(self.nodes())
+        for var in variables:
+            if var not in ancestors:
+                raise ValueError(f"{var} is not an ancestor of {self}")
+        self._correlations.append((list(variables), np.copy(corr_mat)))
+        return self
+
+    # ---- sampling ----------------------------------------------------------------
+    def sample(self, size=None, random_state=None, method=None, correlator="imanconover", gc_strategy=None):
+        """Sample this node and assign `.samples_` on every ancestor (modeling.py:431-493).
+
+        The quantile matrix is generated on the GPU (see probabilit_amd.qmc) and never
+        materialised for method="lhs" (generator fused into the inverse-CDF kernels)."""
+        size = 1 if size is None else size
+        d = self.num_distribution_nodes()
+        if method is not None and method.lower().strip() not in ("lhs", "halton", "sobol"):
+            raise KeyError(method.lower().strip())
+        source = qmc.make_source(method, size, d, random_state)
+        return self._evaluate(source, correlator, gc_strategy, to_host=True)
+
+    def sample_from_quantiles(self, quantiles, correlator="imanconover", gc_strategy=None):
+        """Evaluate the graph on given quantiles, shape (samples, dimensions) (modeling.py:495-614)."""
+        src = qmc.DeviceMatrixSource(quantiles)
+        return self._evaluate(src, correlator, gc_strategy, to_host=True)
+
+    def sample_device(self, size=None, random_state=None, method=None, correlator="imanconover",
+                      gc_strategy=None):
+        """As sample(), but return the sink's device tensor (no D2H copy)."""
+        size = 1 if size is None else size
+        source = qmc.make_source(method, size, self.num_distribution_nodes(), random_state)
+        return self._evaluate(source, correlator, gc_strategy, to_host=False)
+
+    def _evaluate(self, source, correlator, gc_strategy, to_host):
+        assert nx.is_directed_acyclic_graph(self.to_graph())
+        size, n_dim = source.n, source.d
+        assert n_dim == self.num_distribution_nodes()
+
+        if isinstance(correlator, str):
+            correlator = {"imanconover": ImanConover, "cholesky": Cholesky}[correlator.lower()]
+
+        for node in set(self.nodes()):
+            if "_smp" in node.__dict__:
+                del node.samples_
+
+        gc = GarbageCollector(strategy=gc_strategy).set_sink(self)
+        isns = sorted({n for n in self.nodes() if n._is_initial_sampling_node()}, key=lambda n: n._id)
+        G = self.to_graph()
+        ev = _Evaluation(size, list(G.nodes))
+
+        # correlations are a property of the graph: gather and validate them first so that
+        # the correlated ISNs can be written straight into one (K, N) block (:542-568)
+        correlations = []
+        for node in set(self.nodes()):
+            correlations.extend(getattr(node, "_correlations", []))
+        variable_sets = [set(v) for (v, _) in correlations]
+        all_variables = sorted(functools.reduce(set.union, variable_sets, set()), key=lambda n: n._id)
+        block, block_row = None, {}
+        if correlations and set(all_variables) <= set(isns):
+            block = device.empty((len(all_variables), size))
+            block_row = {v: j for j, v in enumerate(all_variables)}
+
+        for node in isns:  # (:529-538)
+            for anc in nx.topological_sort(G.subgraph(nx.ancestors(G, node))):
+                assert isinstance(anc, (Constant, Transform))
+                anc._set_device(anc._sample_device(ev))
+            assert isinstance(node, AbstractDistribution)
+            out = block[block_row[node]] if node in block_row else None
+            node._set_device(node._sample_device(ev, source.next_column(), out=out))
+
+        for variables, _ in correlations:  # (:548-551)
+            for variable in variables:
+                if variable not in isns:
+                    raise ValueError(f"Cannot correlate variable: {variable}")
+        for vars1, vars2 in itertools.combinations(variable_sets, 2):  # (:554-558)
+            common = vars1.intersection(vars2)
+            if len(common) > 1:
+                raise ValueError(f"Correlations specified more than once: {common}")
+
+        if correlations:  # (:571-583)
+            var_to_int = {v: i for (i, v) in enumerate(all_variables)}
+            indexed = [(tuple(var_to_int[v] for v in vs), cm) for (vs, cm) in correlations]
+            C = nearest_correlation_matrix(build_corrmat(indexed))
+            inst = correlator().set_target(C)
+            if isinstance(inst, ImanConover):
+                Y = inst._transform_device(block, ev)
+                for j, var in enumerate(all_variables):
+                    var._set_device(Y[j])
+            else:  # a user correlator class: the reference's (N, K) ndarray protocol
+                X = np.vstack([v.samples_ for v in all_variables]).T
+                Yh = inst(X)
+                for var, col in zip(all_variables, Yh.T):
+                    var.samples_ = np.copy(col)
+
+        for node in nx.topological_sort(G):  # (:586-612)
+            if "_smp" in node.__dict__:
+                pass
+            elif isinstance(node, Constant):
+                node._set_device(node._sample_device(ev))
+            elif isinstance(node, AbstractDistribution):
+                node._set_device(node._sample_device(ev, source.next_column()))
+            elif isinstance(node, Transform):
+                node._set_device(node._sample_device(ev))
+            else:
+                raise TypeError("Node must be Constant, AbstractDistribution or Transform.")
+            gc.decrement_and_delete(node)
+
+        # fused non-finite check (:600-606): first flagged node in topological order raises
+        flags = device.to_host(ev.flags)
+        if flags.any():
+            for node in nx.topological_sort(G):
+                if flags[ev.slot[node]] & 2:  # numpy's integer power check
+                    raise ValueError("Integers to negative integer powers are not allowed.")
+                if flags[ev.slot[node]]:
+                    shown = node.samples_ if "_smp" in node.__dict__ else "(garbage collected)"
+                    raise ValueError(f"Sampling this node gave non-finite values: {node}\n{shown}")
+
+        if not to_host:
+            return None if self._dev() is None else self.samples_device
+        return self.samples_
+
+
+class OverloadMixin:
+    """Arithmetic and comparison operators build Transform nodes (modeling.py:683-748)."""
+
+    def __add__(self, other): return Add(self, other)
+    def __radd__(self, other): return Add(self, other)
+    def __mul__(self, other): return Multiply(self, other)
+    def __rmul__(self, other): return Multiply(self, other)
+    def __floordiv__(self, other): return FloorDivide(self, other)
+    def __rfloordiv__(self, other): return FloorDivide(other, self)
+    def __truediv__(self, other): return Divide(self, other)
+    def __rtruediv__(self, other): return Divide(other, self)
+    def __mod__(self, other): return Mod(self, other)
+    def __rmod__(self, other): return Mod(other, self)
+    def __sub__(self, other): return Subtract(self, other)
+    def __rsub__(self, other): return Subtract(other, self)
+    def __pow__(self, other): return Power(self, other)
+    def __rpow__(self, other): return Power(other, self)
+    def __neg__(self): return Negate(self)
+    def __abs__(self): return Abs(self)
+    def __lt__(self, other): return LessThan(self, other)
+    def __le__(self, other): return LessThanOrEqual(self, other)
+    def __gt__(self, other): return GreaterThan(self, other)
+    def __ge__(self, other): return GreaterThanOrEqual(self, other)
+
+
+class Constant(Node, OverloadMixin):
+    """A number; sampled as a lazily broadcast scalar (modeling.py:751-769)."""
+
+    is_leaf = True
+
+    def __init__(self, value):
+        self.value = value.value if isinstance(value, Constant) else value
+        super().__init__()
+
+    def _sample(self, size=None):
+        if size is None:
+            return self.value
+        return np.ones(size, dtype=type(self.value)) * self.value
+
+    def _sample_device(self, ev):
+        return _Broadcast(self.value, ev.size)
+
+    def get_parents(self):
+        yield from []
+
+    def __repr__(self):
+        return f"{type(self).__name__}({self.value})"
+
+
+class AbstractDistribution(Node, OverloadMixin, abc.ABC):
+    pass
+
+
+# scipy.stats parameter layout of the distributions with native kernels: shape names,
+# then loc (and scale for continuous ones) -- scipy's rv_generic._parse_args.
+_DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "triang": ("c",),
+                "gamma": ("a",), "poisson": ("mu",)}
+_DISCRETE = {"poisson"}
+
+
+def _parse_scipy_args(name, args, kwargs):
+    shapes = _DIST_SHAPES[name]
+    names = list(shapes) + (["loc"] if name in _DISCRETE else ["loc", "scale"])
+    defaults = {"loc": 0.0, "scale": 1.0}
+    if len(args) > len(names):
+        raise TypeError(f"_parse_args() takes from {len(shapes)} to {len(names)} positional arguments but "
+                        f"{len(args)} were given")
+    vals = dict(zip(names, args))
+    for k, v in kwargs.items():
+        if k not in names:
+            raise TypeError(f"_parse_args() got an unexpected keyword argument '{k}'")
+        if k in vals:
+            raise TypeError(f"_parse_args() got multiple values for argument '{k}'")
+        vals[k] = v
+    missing = [s for s in shapes if s not in vals]
+    if missing:
+        raise TypeError(f"_parse_args() missing {len(missing)} required positional argument: '{missing[0]}'")
+    return [vals.get(nm, defaults.get(nm)) for nm in names]
+
+
+class Distribution(AbstractDistribution):
+    """A scipy.stats distribution sampled by inverse CDF on the GPU (modeling.py:776-822)."""
+
+    def __init__(self, distr, *args, **kwargs):
+        self.distr = distr
+        self.args = args
+        self.kwargs = kwargs
+        super().__init__()
+
+    def __repr__(self):
+        args = ", ".join(repr(arg) for arg in self.args)
+        kwargs = ", ".join(f"{k}={repr(v)}" for (k, v) in self.kwargs.items())
+        out = f'{type(self).__name__}("{self.distr}"'
+        if args:
+            out += f", {args}"
+        if kwargs:
+            out += f", {kwargs}"
+        return out + ")"
+
+    def _params(self, n):
+        name = self.distr
+        getattr(scipy.stats, name)  # AttributeError for unknown names, as getattr(stats, ...) at :805
+        if name not in _DIST_SHAPES:
+            raise NotImplementedError(f"Distribution('{name}') has no native inverse-CDF kernel yet; supported: "
+                                      f"{sorted(_DIST_SHAPES)}")
+
+        def resolve(v):
+            if isinstance(v, Node):
+                return _as_float_vector(v._dev(), n)
+            a = np.asarray(v, dtype=np.float64)
+            if a.ndim == 0:
+                return float(a)
+            if a.shape != (n,):
+                raise NotImplementedError(f"array-valued parameter of shape {a.shape} for size {n}")
+            return device.to_device(a)
+
+        return [resolve(v) for v in _parse_scipy_args(name, self.args, self.kwargs)]
+
+    def _sample_device(self, ev, column, out=None):
+        n = ev.size
+        params = self._params(n)
+        keep = [p for p in params if not isinstance(p, float)]  # keep vectors alive over the launch
+        arr = (_lib.Param * len(params))(*[_lib.Param(None, p) if isinstance(p, float) else _lib.Param(p.data_ptr(), 0.0)
+                                            for p in params])
+        out = device.empty(n) if out is None else out
+        lib = _lib.load()
+        dist = _lib.DIST_IDS[self.distr]
+        if column[0] == "lhs":
+            _, seed, n_total, col = column
+            _lib.check(lib.pbh_lhs_ppf(seed, n_total, 0, n, col, dist, arr, len(params), out.data_ptr(),
+                                       ev.flag_ptr(self), device.stream()), f"{self}")
+        else:
+            _, q, stride = column
+            _lib.check(lib.pbh_ppf(dist, q.data_ptr(), stride, n, arr, len(params), out.data_ptr(),
+                                   ev.flag_ptr(self), device.stream()), f"{self}")
+        del keep
+        return out
+
+    def get_parents(self):
+        for arg in self.args + tuple(self.kwargs.values()):
+            if isinstance(arg, Node):
+                yield arg
+
+    @property
+    def is_leaf(self):
+        return list(self.get_parents()) == []
+
+
+class _TableDistribution(AbstractDistribution):
+    is_leaf = True
+
+    def get_parents(self):
+        yield from []
+
+    def _sample_device(self, ev, column, out=None):
+        raise NotImplementedError(f"{type(self).__name__} has no native kernel yet (SURVEY.md §8f, next #3)")
+
+
+class EmpiricalDistribution(_TableDistribution):
+    """np.quantile of data (modeling.py:825-844)."""
+
+    def __init__(self, data, **kwargs):
+        self.data = np.array(data)
+        self.kwargs = kwargs
+        super().__init__()
+
+    def __repr__(self):
+        return f"{type(self).__name__}()"
+
+    def _sample(self, q):
+        return np.quantile(a=self.data, q=q, **self.kwargs)
+
+
+class CumulativeDistribution(_TableDistribution):
+    """Piecewise-linear inverse CDF (modeling.py:847-882)."""
+
+    def __init__(self, quantiles, cumulatives):
+        self.q = np.array(quantiles)
+        self.cumulatives = np.array(cumulatives)
+        if not np.all(np.diff(self.q) > 0):
+            raise ValueError("The quantiles must be strictly increasing.")
+        if not np.all(np.diff(self.cumulatives) > 0):
+            raise ValueError("The cumulatives must be strictly increasing.")
+        if not (np.isclose(np.min(self.q), 0) and np.isclose(np.max(self.q), 1)):
+            raise ValueError("Lowest quantile must be 0 and highest must be 1.")
+        super().__init__()
+
+    def __repr__(self):
+        return f"{type(self).__name__}(quantiles={repr(self.q)}, cumulatives={repr(self.cumulatives)})"
+
+    def _sample(self, q):
+        return np.interp(x=q, xp=self.q, fp=self.cumulatives)
+
+
+class DiscreteDistribution(_TableDistribution):
+    """Categorical values with probabilities (modeling.py:885-927)."""
+
+    def __init__(self, values, probabilities=None):
+        self.values = np.array(values)
+        if probabilities is None:
+            self.probabilities = np.ones(len(self.values), dtype=float) / len(self.values)
+        else:
+            self.probabilities = np.array(probabilities)
+        if not len(self.values) == len(self.probabilities):
+            raise ValueError(f"Length mismatch: {len(self.values)=}  {len(self.probabilities)=}")
+        if not np.isclose(np.sum(self.probabilities), 1.0):
+            raise ValueError(f"Probabilities must sum to 1. {sum(self.probabilities)=}")
+        if np.any(self.probabilities < 0):
+            raise ValueError("Probabilities are not non-negative.")
+        super().__init__()
+
+    def __repr__(self):
+        return f"{type(self).__name__}(values={repr(self.values)}, probabilities={repr(self.probabilities)})"
+
+    def _sample(self, q):
+        return self.values[np.searchsorted(np.cumsum(self.probabilities), v=q, side="right")]
+
+
+# =============================================================================
+# Transforms (modeling.py:933-1169)
+# =============================================================================
+class Transform(Node, OverloadMixin, abc.ABC):
+    is_leaf = False
+
+    def __repr__(self):
+        return f"{type(self).__name__}({', '.join(repr(p) for p in self.get_parents())})"
+
+
+class VariadicTransform(Transform):
+    """functools.reduce(op, parents' samples) (modeling.py:943-959)."""
+
+    op_name = None
+
+    def __init__(self, *args):
+        self.parents = tuple(python_to_prob(arg) for arg in args)
+        super().__init__()
+
+    def _sample_device(self, ev):
+        n = ev.size
+        acc = self.parents[0]._dev()
+        for p in self.parents[1:]:
+            acc = _binary(self.op_name, acc, p._dev(), n, ev.flag_ptr(self))
+        return acc
+
+    def get_parents(self):
+        yield from self.parents
+
+
+class Avg(VariadicTransform):
+    """np.average(np.vstack(samples), axis=0) (modeling.py:986-990)."""
+
+    def _sample_device(self, ev):
+        n = ev.size
+        f64 = np.dtype(np.float64)
+        vecs = [_as_float_vector(p._dev(), n) for p in self.parents]
+        vecs = [_elementwise("cast", _Broadcast(v, n), None, n, f64, f64, None) if isinstance(v, float) else v
+                for v in vecs]
+        out = device.empty(n)
+        lib = _lib.load()
+        ptrs = (ctypes.c_void_p * len(vecs))(*[v.data_ptr() for v in vecs])
+        _lib.check(lib.pbh_average(ptrs, len(vecs), n, out.data_ptr(), ev.flag_ptr(self), device.stream()), "Avg")
+        return out
+
+
+class NoOp(VariadicTransform):
+    """Sample all ancestors, produce nothing (modeling.py:993-997)."""
+
+    def _sample_device(self, ev):
+        return None
+
+
+class BinaryTransform(Transform):
+    """op(left, right) (modeling.py:1000-1012)."""
+
+    op_name = None
+
+    def __init__(self, *args):
+        self.parents = tuple(python_to_prob(arg) for arg in args)
+        super().__init__()
+
+    def _sample_device(self, ev):
+        a, b = (p._dev() for p in self.parents)
+        return _binary(self.op_name, a, b, ev.size, ev.flag_ptr(self))
+
+    def get_parents(self):
+        yield from self.parents
+
+
+class UnaryTransform(Transform):
+    """op(parent) (modeling.py:1063-1075)."""
+
+    op_name = None
+
+    def __init__(self, arg):
+        self.parent = python_to_prob(arg)
+        super().__init__()
+
+    def _sample_device(self, ev):
+        return _unary(self.op_name, self.parent._dev(), ev.size, ev.flag_ptr(self))
+
+    def get_parents(self):
+        yield self.parent
+
+
+def _define(base, table):
+    for name, op in table.items():
+        globals()[name] = type(name, (base,), {"op_name": op, "__module__": __name__})
+        __all__.append(name)
+
+
+_define(VariadicTransform, {"Add": "add", "Multiply": "mul", "Max": "max", "Min": "min", "All": "and",
+                            "Any": "or"})
+_define(BinaryTransform, {"FloorDivide": "floordiv", "Mod": "mod", "Divide": "truediv", "Power": "pow",
+                          "Subtract": "sub", "Equal": "eq", "NotEqual": "ne", "LessThan": "lt",
+                          "LessThanOrEqual": "le", "GreaterThan": "gt", "GreaterThanOrEqual": "ge",
+                          "IsClose": "isclose", "Arctan2": "arctan2"})
+_define(UnaryTransform, {"Negate": "neg", "Abs": "abs", "Log": "log", "Exp": "exp", "Floor": "floor",
+                         "Ceil": "ceil", "Sign": "sign", "Sqrt": "sqrt", "Square": "square", "Log10": "log10",
+                         "Sin": "sin", "Cos": "cos", "Tan": "tan", "Arcsin": "arcsin", "Arccos": "arccos",
+                         "Arctan": "arctan", "Sinh": "sinh", "Cosh": "cosh", "Tanh": "tanh", "Arcsinh": "arcsinh",
+                         "Arccosh": "arccosh", "Arctanh": "arctanh"})
+
+
+class ScalarFunctionTransform(Transform):
+    """A Python function applied sample by sample (modeling.py:1172-1201).  Inherently a
+    scalar host loop: out of scope for the device path."""
+
+    def __init__(self, func, args, kwargs):
+        self.func = func
+        self.args = args
+        self.kwargs = kwargs
+        super().__init__()
+
+    def _sample_device(self, ev):
+        raise NotImplementedError("scalar_transform runs a Python function per sample; it has no device path")
+
+    def get_parents(self):
+        for arg in self.args + tuple(self.kwargs.values()):
+            if isinstance(arg, Node):
+                yield arg
+
+
+def scalar_transform(func):
+    @functools.wraps(func)
+    def transformed_function(*args, **kwargs):
+        return ScalarFunctionTransform(func, args, kwargs)
+
+    return transformed_function
+
+
+class MarginalDistribution(Transform):
+    """Slice of a multivariate distribution (modeling.py:1215-1243); pseudo-random .rvs only
+    in the reference, so no inverse-CDF device path."""
+
+    is_leaf = False
+
+    def __init__(self, distr, d):
+        self.distr = distr
+        self.d = d
+        super().__init__()
+
+    def _sample_device(self, ev):
+        raise NotImplementedError("multivariate distributions have no device path (SURVEY.md §2 #2)")
+
+    def get_parents(self):
+        yield self.distr
+
+    def __repr__(self):
+        return f"{type(self).__name__}({self.distr}, d={self.d})"
+
+
+def MultivariateDistribution(distr, *args, **kwargs):
+    """Marginals of a multivariate scipy distribution (modeling.py:1246-1264)."""
+    dist = Distribution(distr, *args, **kwargs)
+    frozen = getattr(scipy.stats, distr)(*args, **kwargs)
+    d = len(np.atleast_1d(frozen.rvs(size=1, random_state=0)).squeeze())
+    yield from (MarginalDistribution(dist, d=i) for i in range(d))
+

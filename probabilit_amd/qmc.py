@@ -1,0 +1,235 @@
+"""Quantile sources for Node.sample (modeling.py:478-489), generated on the GPU.
+
+    method=None     native Philox4x32-10 uniforms            (pbh_fill_uniform)
+    method="lhs"    native Latin hypercube: per column a keyed Feistel bijection of the
+                    strata plus a Philox jitter, fused into the ppf kernel (pbh_lhs_ppf)
+    method="sobol"  scrambled Sobol', bit-exact with scipy.stats.qmc.Sobol (pbh_fill_sobol);
+                    only the O(d * bits^2) engine setup (direction numbers, LMS scramble,
+                    digital shift) runs on the host, consuming the numpy Generator exactly
+                    as scipy does.
+
+"Native" streams are statistically the same designs as scipy's but are counter-based, so
+any row range can be generated independently (row-sharding across GPUs) — they are not
+numpy's PCG64 / MT19937 bit streams.  Bit-level parity with the reference is defined at
+Node.sample_from_quantiles: identical quantiles in give identical samples out.
+"""
+
+import os
+import warnings
+
+import numpy as np
+
+from . import _lib, device
+
+MASK63 = (1 << 63) - 1
+
+
+# ------------------------------------------------------------------ seeds
+def seed_from(random_state):
+    """A 64-bit seed for the native counter-based streams.
+
+    int -> that int; None -> fresh OS entropy; np.random.Generator / RandomState -> one
+    draw from it (so successive calls with one generator give different streams)."""
+    if random_state is None:
+        return int(np.random.SeedSequence().entropy) & ((1 << 64) - 1)
+    if isinstance(random_state, (int, np.integer)):
+        if random_state < 0:
+            raise ValueError("Seed must be non-negative")
+        return int(random_state) & ((1 << 64) - 1)
+    if isinstance(random_state, np.random.Generator):
+        return int(random_state.integers(0, MASK63, dtype=np.int64))
+    if isinstance(random_state, np.random.RandomState):
+        return int(random_state.randint(0, MASK63, dtype=np.int64))
+    raise ValueError(f"{random_state!r} cannot be used to seed a numpy.random.Generator instance")
+
+
+def engine_rng(rng):
+    """The Generator a scipy QMC engine owns when built as `Engine(d=d, rng=rng)`
+    (modeling.py:488): scipy's `_transition_to_rng` normalises the keyword with
+    np.random.default_rng, and QMCEngine._initialize spawns an owned child from it
+    (scipy:stats/_qmc.py)."""
+    g = np.random.default_rng(rng)
+    bg = g.bit_generator
+    return np.random.Generator(type(bg)(bg.seed_seq.spawn(1)[0]))
+
+
+# ------------------------------------------------------------------ Sobol' engine setup
+_DIRECTION = {}
+
+
+def _direction_numbers():
+    """Joe & Kuo direction numbers as shipped by the pinned scipy (data file, read once)."""
+    if not _DIRECTION:
+        import scipy.stats
+
+        path = os.path.join(os.path.dirname(scipy.stats.__file__), "_sobol_direction_numbers.npz")
+        with np.load(path, allow_pickle=False) as z:
+            _DIRECTION["poly"] = z["poly"].astype(np.int64)
+            _DIRECTION["vinit"] = z["vinit"].astype(np.int64)
+    return _DIRECTION["poly"], _DIRECTION["vinit"]
+
+
+MAXDIM = 21201
+
+
+def sobol_direction_matrix(d, bits=30):
+    """Unscrambled direction matrix v (d x bits), Bratley & Fox recurrence."""
+    poly, vinit = _direction_numbers()
+    v = np.zeros((d, bits), dtype=np.uint64)
+    if d == 0:
+        return v.astype(np.uint32)
+    v[0, :] = 1
+    for k in range(1, d):
+        p = int(poly[k])
+        m = p.bit_length() - 1
+        for j in range(m):
+            v[k, j] = vinit[k, j]
+        for j in range(m, bits):
+            newv = int(v[k, j - m])
+            pow2 = 1
+            for i in range(m):
+                pow2 <<= 1
+                if (p >> (m - 1 - i)) & 1:
+                    newv ^= pow2 * int(v[k, j - i - 1])
+            v[k, j] = newv
+    scale = np.array([1 << (bits - 1 - j) for j in range(bits)], dtype=np.uint64)
+    return (v * scale[None, :]).astype(np.uint32 if bits <= 32 else np.uint64)
+
+
+def _lms_scramble(sv, ltm, bits):
+    """Linear matrix scramble: each direction number times a random lower-triangular binary
+    matrix (unit diagonal) over GF(2), MSB first."""
+    d = sv.shape[0]
+    ltm = ltm.copy()
+    idx = np.arange(bits)
+    ltm[:, idx, idx] = 1
+    weights = np.array([1 << (bits - 1 - i) for i in range(bits)], dtype=object)
+    out = np.zeros_like(sv)
+    for k in range(d):
+        rows = [int(sum(int(x) * w for x, w in zip(ltm[k, p, :], weights))) for p in range(bits)]
+        for j in range(bits):
+            vkj = int(sv[k, j])
+            t2, l = 0, 1
+            for p in range(bits - 1, -1, -1):
+                t1 = bin(rows[p] & vkj).count("1") & 1
+                t2 += t1 * l
+                l <<= 1
+            out[k, j] = t2
+    return out
+
+
+def sobol_setup(d, rng=None, bits=30, scramble=True):
+    """(sv, shift) of scipy.stats.qmc.Sobol(d, rng=rng, bits=bits, scramble=scramble)."""
+    if d > MAXDIM:
+        raise ValueError(f"Maximum supported dimensionality is {MAXDIM}.")
+    if bits > 32:
+        raise NotImplementedError("native Sobol' supports bits <= 32")
+    sv = sobol_direction_matrix(d, bits)
+    if not scramble:
+        return sv, np.zeros(d, dtype=np.uint32)
+    g = engine_rng(rng)
+    shift = np.dot(g.integers(0, 2, size=(d, bits), dtype=np.uint32),
+                   2 ** np.arange(bits, dtype=np.uint32)).astype(np.uint32)
+    ltm = np.tril(g.integers(0, 2, size=(d, bits, bits), dtype=np.uint32))
+    return _lms_scramble(sv, ltm, bits).astype(np.uint32), shift
+
+
+# ------------------------------------------------------------------ sources
+class QuantileSource:
+    """Yields the columns of an (n, d) quantile matrix in order (the iterator of
+    modeling.py:510).  Each column is either a device vector with a stride or a fused
+    generator descriptor understood by Distribution._sample."""
+
+    def __init__(self, n, d):
+        self.n, self.d, self._next = int(n), int(d), 0
+
+    def next_column(self):
+        if self._next >= self.d:
+            raise StopIteration("quantile columns exhausted")
+        c = self._next
+        self._next += 1
+        return self.column(c)
+
+
+class DeviceMatrixSource(QuantileSource):
+    """User-supplied quantiles (numpy or device tensor), shape (n, d), any layout."""
+
+    def __init__(self, quantiles):
+        import torch
+
+        if isinstance(quantiles, torch.Tensor):
+            q = quantiles.to(device.device(), dtype=torch.float64)
+        else:
+            q = device.to_device(np.asarray(quantiles, dtype=np.float64))
+        if q.dim() != 2:
+            raise ValueError("quantiles must be a 2-D array of shape (samples, dimensions)")
+        super().__init__(q.shape[0], q.shape[1])
+        self.q = q
+
+    def column(self, c):
+        col = self.q[:, c]
+        return ("vector", col, col.stride(0))
+
+
+class UniformSource(QuantileSource):
+    def __init__(self, n, d, seed):
+        super().__init__(n, d)
+        self.seed = seed
+
+    def column(self, c):
+        out = device.empty(self.n)
+        lib = _lib.load()
+        _lib.check(lib.pbh_fill_uniform(self.seed, 0, self.n, c, 1, out.data_ptr(), max(self.n, 1),
+                                        device.stream()), "pbh_fill_uniform")
+        return ("vector", out, 1)
+
+
+class LHSSource(QuantileSource):
+    def __init__(self, n, d, seed):
+        super().__init__(n, d)
+        self.seed = seed
+
+    def column(self, c):
+        return ("lhs", self.seed, self.n, c)
+
+    def materialize(self, c):
+        out = device.empty(self.n)
+        lib = _lib.load()
+        _lib.check(lib.pbh_fill_lhs(self.seed, self.n, 0, self.n, c, 1, out.data_ptr(), max(self.n, 1),
+                                    device.stream()), "pbh_fill_lhs")
+        return out
+
+
+class SobolSource(QuantileSource):
+    def __init__(self, n, d, rng, bits=30):
+        super().__init__(n, d)
+        if n > 2 ** bits:
+            raise ValueError(f"At most 2**{bits}={2 ** bits} distinct points can be generated. "
+                             f"0 points have been previously generated, then: n=0+{n}={n}. "
+                             "Consider increasing `bits`.")
+        if n > 1 and (n & (n - 1)) != 0:
+            warnings.warn("The balance properties of Sobol' points require n to be a power of 2.", stacklevel=3)
+        self.bits = bits
+        self.sv, self.shift = sobol_setup(d, rng, bits)
+
+    def column(self, c):
+        out = device.empty(self.n)
+        lib = _lib.load()
+        sv = np.ascontiguousarray(self.sv, dtype=np.uint32)
+        sh = np.ascontiguousarray(self.shift, dtype=np.uint32)
+        _lib.check(lib.pbh_fill_sobol(_lib.np_ptr(sv), _lib.np_ptr(sh), self.d, self.bits, 0, self.n, c, 1,
+                                      out.data_ptr(), max(self.n, 1), device.stream()), "pbh_fill_sobol")
+        return ("vector", out, 1)
+
+
+def make_source(method, n, d, random_state):
+    if method is None:
+        return UniformSource(n, d, seed_from(random_state))
+    m = method.lower().strip()
+    if m == "lhs":
+        return LHSSource(n, d, seed_from(random_state))
+    if m == "sobol":
+        return SobolSource(n, d, random_state)
+    if m == "halton":
+        raise NotImplementedError("method='halton' has no native generator yet (supported: None, 'lhs', 'sobol')")
+    raise KeyError(method)
