@@ -103,7 +103,25 @@ int pbh_lhs_ppf(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col, 
  * Returns PBH_ERR_NOT_PD when E is not positive definite, PBH_ERR_NONFINITE for NaN/inf in X.
  * The optional outputs (device pointers, column-major K x N, may be NULL) expose the
  * intermediates for parity tests: scores S, correlated scores CS, step-4 indices idx. */
+/* An Iman-Conover input column that is GENERATED instead of read: column `lhs_col` of the
+ * native LHS design of pbh_fill_lhs(seed, n) pushed through distribution `dist` (scalar
+ * params).  This is how the DAG evaluator hands over initial sampling nodes that feed a
+ * correlate() (modeling.py:529-538, 571-583): their pre-correlation samples are never
+ * observable, so the device generates each column directly in sorted (stratum) order,
+ * verifies it is non-decreasing, and derives the step-1 ranks from the LHS permutation --
+ * no sort of X.  A column whose ppf is not monotone on the grid falls back to the sort path.
+ * nonfinite_flag (optional, device) is set when a generated value is NaN / inf. */
+typedef struct pbh_ic_column {
+  uint64_t seed;
+  int32_t lhs_col;
+  int32_t dist;
+  double params[3];
+  int32_t nparams;
+  int32_t* nonfinite_flag;
+} pbh_ic_column;
+
 typedef struct pbh_ic_args {
+  const pbh_ic_column* columns; /* host array of k generated columns, or NULL: read X */
   const double* X;
   int64_t n;
   int32_t k;

@@ -38,7 +38,8 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
-           "k_rank_finish<gather>", "k_load_keys", "k_gram", "k_apply", "k_elementwise", "k_head_bounds", "k_scan"]
+           "k_rank_finish<gather>", "k_load_keys", "k_gram", "k_apply", "k_elementwise", "k_head_bounds", "k_scan",
+           "k_lhs_sorted_ppf", "k_perm_scores"]
 
 
 class Param(ctypes.Structure):
@@ -49,8 +50,13 @@ class Operand(ctypes.Structure):
     _fields_ = [("ptr", ctypes.c_void_p), ("dtype", ctypes.c_int32), ("f", ctypes.c_double), ("i", ctypes.c_int64)]
 
 
+class ICColumn(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("lhs_col", ctypes.c_int32), ("dist", ctypes.c_int32),
+                ("params", ctypes.c_double * 3), ("nparams", ctypes.c_int32), ("nonfinite_flag", ctypes.c_void_p)]
+
+
 class ICArgs(ctypes.Structure):
-    _fields_ = [("X", ctypes.c_void_p), ("n", ctypes.c_int64), ("k", ctypes.c_int32), ("x_rs", ctypes.c_int64),
+    _fields_ = [("columns", ctypes.POINTER(ICColumn)), ("X", ctypes.c_void_p), ("n", ctypes.c_int64), ("k", ctypes.c_int32), ("x_rs", ctypes.c_int64),
                 ("x_cs", ctypes.c_int64), ("target_chol_host", ctypes.c_void_p), ("Y", ctypes.c_void_p),
                 ("y_rs", ctypes.c_int64), ("y_cs", ctypes.c_int64), ("ws", ctypes.c_void_p),
                 ("ws_bytes", ctypes.c_size_t), ("scores_out", ctypes.c_void_p), ("cscores_out", ctypes.c_void_p),
@@ -72,6 +78,11 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"probabilit_amd native library not built: {LIB_PATH} is missing "
                           "(run `python -m probabilit_amd.build`)")
+    # torch loads its own libamdhip64.so.7 by path; importing it first makes this library's
+    # NEEDED libamdhip64.so.7 resolve (by SONAME) to that same runtime instance instead of
+    # loading a second HIP runtime into the process.
+    import torch  # noqa: F401
+
     lib = ctypes.CDLL(LIB_PATH)
     vp, i64, i32, dbl, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
     u64 = ctypes.c_uint64

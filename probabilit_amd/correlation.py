@@ -167,14 +167,17 @@ class ImanConover(Correlator):
         super().set_target(correlation_matrix)
         return self
 
-    def _run(self, X, n, k, x_rs, x_cs, Y, y_rs, y_cs, debug=None):
+    def _run(self, X, n, k, x_rs, x_cs, Y, y_rs, y_cs, debug=None, columns=None):
         lib = _lib.load()
         ws_bytes = ctypes.c_size_t()
         _lib.check(lib.pbh_ic_workspace_size(n, k, ctypes.byref(ws_bytes)))
         ws = device.empty(int(ws_bytes.value), "uint8")
         P = np.ascontiguousarray(self.P, dtype=np.float64)
         args = _lib.ICArgs()
-        args.X, args.n, args.k, args.x_rs, args.x_cs = X.data_ptr(), n, k, x_rs, x_cs
+        if columns is not None:
+            arr = (_lib.ICColumn * k)(*columns)
+            args.columns = ctypes.cast(arr, ctypes.POINTER(_lib.ICColumn))
+        args.X, args.n, args.k, args.x_rs, args.x_cs = (X.data_ptr() if X is not None else None), n, k, x_rs, x_cs
         args.target_chol_host = P.ctypes.data
         args.Y, args.y_rs, args.y_cs = Y.data_ptr(), y_rs, y_cs
         args.ws, args.ws_bytes = ws.data_ptr(), ws_bytes.value
@@ -207,6 +210,21 @@ class ImanConover(Correlator):
         self._validate_X(block.T)
         Y = device.empty((K, N))
         self._run(block, N, K, 1, N, Y, 1, N)
+        return Y
+
+    def _transform_generated(self, columns, n):
+        """DAG fast path: K natively generated LHS columns (list of _lib.ICColumn) are
+        generated, correlated and returned as a (K, N) device block without ever
+        materialising the uncorrelated samples (see pbh_ic_column)."""
+        K = len(columns)
+        if not (hasattr(self, "C") and hasattr(self, "P")):
+            raise CorrelatorError("User must call `set_target` first.")
+        if self.P.shape[0] != K:
+            raise ValueError(f"Shape of `X` ({(n, K)}) does not match shape of correlation matrix ({self.P.shape})")
+        if n <= K:
+            raise ValueError(f"The matrix X must have rows > columns. Got shape: {(n, K)}")
+        Y = device.empty((K, n))
+        self._run(None, n, K, 1, n, Y, 1, n, columns=columns)
         return Y
 
     def _call_debug(self, X):

@@ -11,6 +11,7 @@
 
 #include "pbh_error.h"
 #include "pbh_ic.h"
+#include "pbh_lhs.h"
 #include "pbh_sort.h"
 
 namespace pbh {
@@ -55,6 +56,8 @@ struct IcLayout {
   double* inv_diag;
   double* P;
   int32_t* flag;
+  double* tmp;                  // n doubles: tied-column average ranks / fallback X column
+  unsigned long long* counts;   // ties, inversions of a generated sorted column
 };
 
 size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
@@ -70,7 +73,11 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* invd = c.take((size_t)k * 8);
   void* P = c.take((size_t)k * k * 8);
   void* flag = c.take(256);
+  void* tmp = c.take((size_t)n * 8);
+  void* counts = c.take(256);
   if (carve) {
+    L->tmp = (double*)tmp;
+    L->counts = (unsigned long long*)counts;
     L->S = (double*)S;
     L->sorted_x = (double*)sx;
     L->sort_ws = sws;
@@ -173,7 +180,8 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   PBH_REQUIRE(a != nullptr, "pbh_iman_conover: args must not be NULL");
   const int64_t n = a->n;
   const int k = a->k;
-  PBH_REQUIRE(a->X && a->Y && a->ws && a->target_chol_host, "pbh_iman_conover: null pointer argument");
+  PBH_REQUIRE((a->X || a->columns) && a->Y && a->ws && a->target_chol_host,
+              "pbh_iman_conover: null pointer argument");
   PBH_REQUIRE(k >= 1 && k <= 128, "pbh_iman_conover: K = %d outside [1, 128]", k);
   PBH_REQUIRE(n > k && n < ((int64_t)1 << 32), "pbh_iman_conover: need K < N < 2^32 (N=%lld, K=%d)", (long long)n, k);
   IcLayout L;
@@ -194,14 +202,51 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   // ---- step 1: van der Waerden scores of every column (+ the sorted column for step 4)
   PBH_CHECK_HIP(hipMemsetAsync(L.flag, 0, sizeof(int32_t), s));
   for (int c = 0; c < k; ++c) {
-    st = load_keys(a->X + (int64_t)c * a->x_cs, a->x_rs, n, sb.keys[0], L.flag, s);
+    double* S_c = L.S + (int64_t)c * n;
+    double* sx_c = L.sorted_x + (int64_t)c * n;
+    const double* x_c = a->X ? a->X + (int64_t)c * a->x_cs : nullptr;
+    int64_t x_stride = a->x_rs;
+    if (a->columns) {
+      // generated LHS column: sorted order straight from the inverse permutation
+      const pbh_ic_column& g = a->columns[c];
+      pbh_param prm[3];
+      for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
+      st = lhs_sorted_ppf(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, sx_c, g.nonfinite_flag, s);
+      if (st) return st;
+      st = check_sorted(sx_c, n, L.counts, s);
+      if (st) return st;
+      unsigned long long cnt[2];
+      PBH_CHECK_HIP(hipMemcpyAsync(cnt, L.counts, sizeof(cnt), hipMemcpyDeviceToHost, s));
+      PBH_CHECK_HIP(hipStreamSynchronize(s));
+      if (cnt[1] == 0) {
+        const double* avg = nullptr;
+        if (cnt[0] != 0) {  // ties (discrete ppf): 'average' ranks of the runs, in stratum order
+          st = load_keys(sx_c, 1, n, sb.keys[0], nullptr, s);
+          if (st) return st;
+          RankOut ro = {};
+          ro.ranks = L.tmp;
+          st = rank_finish(kModeRanks, sb.keys[0], nullptr, n, tb, ro, s);
+          if (st) return st;
+          avg = L.tmp;
+        }
+        st = perm_scores(g.seed, n, g.lhs_col, avg, S_c, s);
+        if (st) return st;
+        continue;
+      }
+      // not monotone on this grid: materialise the column in row order and sort it
+      st = pbh_lhs_ppf(g.seed, n, 0, n, g.lhs_col, g.dist, prm, g.nparams, L.tmp, nullptr, stream);
+      if (st) return st;
+      x_c = L.tmp;
+      x_stride = 1;
+    }
+    st = load_keys(x_c, x_stride, n, sb.keys[0], L.flag, s);
     if (st) return st;
     int buf = 0;
     st = radix_sort_keys(sb, n, s, &buf);
     if (st) return st;
     RankOut out = {};
-    out.scores = L.S + (int64_t)c * n;
-    out.sorted_x = L.sorted_x + (int64_t)c * n;
+    out.scores = S_c;
+    out.sorted_x = sx_c;
     st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
     if (st) return st;
   }

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(T) void k_rank_finish(const uint64_t* __restrict__ 
     int p = j * T + t;
     if (p < cnt) {
       sk[pad(p)] = keys[base + p];
-      sr[pad(p)] = rows[base + p];
+      sr[pad(p)] = rows ? rows[base + p] : (uint32_t)(base + p);  // NULL payload: identity
     }
   }
   const uint64_t before = base > 0 ? keys[base - 1] : 0ull;

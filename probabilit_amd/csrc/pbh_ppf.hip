@@ -24,10 +24,14 @@ struct Params {
   PBH_DI double at(int j, int64_t i) const { return ptr[j] ? ptr[j][i] : val[j]; }
 };
 
+// Per-launch constants of the distribution (scalar parameters only).
 struct PoissonTable {
-  const double* cdf;  // cdf[j] = pdtr(k_lo + j, mu) for scalar mu, else NULL
+  const double* cdf;  // poisson: cdf[j] = pdtr(k_lo + j, mu) for scalar mu, else NULL
   int64_t k_lo;
   int64_t len;
+  int has_gamma;      // gamma with scalar a: hoisted GammaAux + z-grid guide
+  sf::GammaAux aux;
+  sf::GammaGuide guide;
 };
 
 // smallest k >= 0 with pdtr(k, mu) >= q, by stepping from a Cornish-Fisher guess.
@@ -108,7 +112,7 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
     } else {  // gamma
-      x = sf::igami(shape, q);
+      x = pt.has_gamma ? sf::igami_guided(shape, q, &pt.aux, pt.guide) : sf::igami(shape, q);
     }
     return x * scale + loc;
   }
@@ -141,6 +145,65 @@ __global__ __launch_bounds__(kBlock) void k_lhs_ppf(uint64_t seed, int64_t n, in
     out[i] = x;
     flag_nonfinite(flag, !isfinite(x));
   }
+}
+
+// The same LHS column in stratum order: out[t] = ppf(q) for the row pi^-1(t) that holds
+// stratum t.  Bit-identical to k_lhs_ppf's value for that row; non-decreasing in t whenever
+// the ppf is monotone, which k_check_sorted verifies before anything relies on it.
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_lhs_sorted_ppf(uint64_t seed, int64_t n, uint32_t col, Params prm,
+                                                           PoissonTable pt, double* __restrict__ out, int32_t* flag) {
+  Philox ph(seed);
+  FeistelPerm fp(ph, (uint64_t)n, col);
+  int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t step = (int64_t)gridDim.x * kBlock;
+  for (; t < n; t += step) {
+    uint64_t row = fp.inverse((uint64_t)t);
+    double u = ph.uniform(row, col, kPurposeLhsU);
+    double q = ((double)(t + 1) - u) / (double)n;
+    double x = ppf_one<D>(q, prm.val[0], prm.val[1], prm.val[2], pt);
+    out[t] = x;
+    flag_nonfinite(flag, !isfinite(x));
+  }
+}
+
+// counts[0] += #(x[t] == x[t+1]), counts[1] += #(x[t] > x[t+1] or unordered)
+__global__ __launch_bounds__(kBlock) void k_check_sorted(const double* __restrict__ x, int64_t n,
+                                                         unsigned long long* counts) {
+  unsigned long long ties = 0, inv = 0;
+  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t + 1 < n; t += (int64_t)gridDim.x * kBlock) {
+    double a = x[t], b = x[t + 1];
+    ties += (a == b);
+    inv += !(a <= b);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ties += __shfl_xor(ties, o, 64);
+    inv += __shfl_xor(inv, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && (ties | inv)) {
+    atomicAdd(&counts[0], ties);
+    atomicAdd(&counts[1], inv);
+  }
+}
+
+// Van der Waerden scores of an untied LHS column, in row order: the rank of row r is
+// pi(r) + 1, so S[r] = ndtri((pi(r) + 1) / (n + 1)) (correlation.py:394-395), no sort.
+__global__ __launch_bounds__(kBlock) void k_perm_scores(uint64_t seed, int64_t n, uint32_t col,
+                                                        const double* __restrict__ avg, double* __restrict__ S) {
+  Philox ph(seed);
+  FeistelPerm fp(ph, (uint64_t)n, col);
+  const double np1 = (double)(n + 1);
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n; r += (int64_t)gridDim.x * kBlock) {
+    uint64_t t = fp((uint64_t)r);
+    double rank = avg ? avg[t] : (double)(t + 1);  // tied column: 'average' rank of stratum t
+    S[r] = sf::ndtri(rank / np1);
+  }
+}
+
+__global__ void k_gamma_guide(double a, double z0, double h, int m, double* y, double* dy) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < m) sf::gamma_guide_entry(a, z0 + j * h, &y[j], &dy[j]);
 }
 
 __global__ void k_poisson_table(double mu, int64_t k_lo, int64_t len, double* cdf) {
@@ -271,8 +334,20 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
     prm.ptr[j] = j < nparams ? params[j].ptr : nullptr;
     prm.val[j] = j < nparams ? params[j].value : 0.0;
   }
-  pt = PoissonTable{nullptr, 0, 0};
+  pt = PoissonTable{};
   *table = nullptr;
+  if (dist == PBH_DIST_GAMMA && params[0].ptr == nullptr && params[0].value > 0.0 && isfinite(params[0].value)) {
+    const double a = params[0].value;
+    const double z0 = -12.0, h = 1.0 / 64.0;
+    const int m = (int)((8.125 - z0) / h) + 1;
+    PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)2 * m * sizeof(double), s));
+    hipLaunchKernelGGL(k_gamma_guide, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a, z0, h, m, *table,
+                       *table + m);
+    PBH_CHECK_LAUNCH();
+    pt.has_gamma = 1;
+    pt.aux = sf::gamma_aux(a);
+    pt.guide = sf::GammaGuide{*table, *table + m, m, z0, h, 1.0 / h};
+  }
   if (dist == PBH_DIST_POISSON && params[0].ptr == nullptr) {
     double mu = params[0].value;
     if (mu > 0.0 && mu < 1.0e12) {
@@ -285,13 +360,63 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
       hipLaunchKernelGGL(k_poisson_table, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, mu, k_lo, len,
                          *table);
       PBH_CHECK_LAUNCH();
-      pt = PoissonTable{*table, k_lo, len};
+      pt.cdf = *table;
+      pt.k_lo = k_lo;
+      pt.len = len;
     }
   }
   return PBH_OK;
 }
 
 }  // namespace
+
+int lhs_sorted_ppf(uint64_t seed, int64_t n, int col, int dist, const pbh_param* params, int nparams, double* out,
+                   int32_t* flag, hipStream_t s) {
+  for (int j = 0; j < nparams; ++j)
+    PBH_REQUIRE(params[j].ptr == nullptr, "stratum-ordered LHS generation needs scalar parameters");
+  Params prm;
+  PoissonTable pt;
+  double* table = nullptr;
+  int st = with_params(dist, params, nparams, prm, pt, &table, s);
+  if (st != PBH_OK) return st;
+  dim3 g(ppf_grid(n)), b(kBlock);
+  switch (dist) {
+#define PBH_CASE(D)                                                                                                 \
+  case D:                                                                                                           \
+    PBH_TIMED(kKLhsSorted, s,                                                                                       \
+              hipLaunchKernelGGL(k_lhs_sorted_ppf<D>, g, b, 0, s, seed, n, (uint32_t)col, prm, pt, out, flag)); \
+    break;
+    PBH_CASE(PBH_DIST_NORM)
+    PBH_CASE(PBH_DIST_UNIFORM)
+    PBH_CASE(PBH_DIST_EXPON)
+    PBH_CASE(PBH_DIST_LOGNORM)
+    PBH_CASE(PBH_DIST_TRIANG)
+    PBH_CASE(PBH_DIST_GAMMA)
+    PBH_CASE(PBH_DIST_POISSON)
+#undef PBH_CASE
+    default:
+      set_error("unsupported distribution id %d", dist);
+      return PBH_ERR_UNSUPPORTED;
+  }
+  PBH_CHECK_LAUNCH();
+  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));
+  return PBH_OK;
+}
+
+int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStream_t s) {
+  PBH_CHECK_HIP(hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, x, n, counts);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int perm_scores(uint64_t seed, int64_t n, int col, const double* avg, double* S, hipStream_t s) {
+  PBH_TIMED(kKPermScores, s,
+            hipLaunchKernelGGL(k_perm_scores, dim3(ppf_grid(n)), dim3(kBlock), 0, s, seed, n, (uint32_t)col, avg, S));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
 }  // namespace pbh
 
 using namespace pbh;

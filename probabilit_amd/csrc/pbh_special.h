@@ -399,14 +399,24 @@ PBH_HD inline double lanczos_sum_expg_scaled(double x) {
 
 // ---------------------------------------------------------------- incomplete gamma
 // x^a e^{-x} / Gamma(a)
-PBH_HD inline double igam_fac(double a, double x) {
+// Functions of the shape parameter alone, hoisted out of per-element loops when `a` is a
+// scalar (the same values the per-call code computes, so results are unchanged).
+struct GammaAux {
+  double lga;      // lgam(a)
+  double lg1pa;    // lgam1p(a)
+  double lanczos;  // lanczos_sum_expg_scaled(a)
+};
+
+PBH_HD inline GammaAux gamma_aux(double a);
+
+PBH_HD inline double igam_fac(double a, double x, const GammaAux* g = nullptr) {
   if (fabs(a - x) > 0.4 * fabs(a)) {
-    double ax = a * log(x) - x - lgam(a);
+    double ax = a * log(x) - x - (g ? g->lga : lgam(a));
     if (ax < -kMaxLog) return 0.0;
     return exp(ax);
   }
   double fac = a + kLanczosG - 0.5;
-  double res = sqrt(fac / exp(1.0)) / lanczos_sum_expg_scaled(a);
+  double res = sqrt(fac / exp(1.0)) / (g ? g->lanczos : lanczos_sum_expg_scaled(a));
   if ((a < 200) && (x < 200)) {
     res *= exp(a - x) * pow(x / fac, a);
   } else {
@@ -416,9 +426,9 @@ PBH_HD inline double igam_fac(double a, double x) {
   return res;
 }
 
-PBH_HD inline double igamc_cf(double a, double x) {  // DLMF 8.9.2
+PBH_HD inline double igamc_cf(double a, double x, const GammaAux* g = nullptr) {  // DLMF 8.9.2
   const double big = 4.503599627370496e15, biginv = 2.22044604925031308085e-16;
-  double ax = igam_fac(a, x);
+  double ax = igam_fac(a, x, g);
   if (ax == 0.0) return 0.0;
   double y = 1.0 - a, z = x + y + 1.0, c = 0.0;
   double pkm2 = 1.0, qkm2 = x, pkm1 = x + 1.0, qkm1 = z * x;
@@ -452,8 +462,8 @@ PBH_HD inline double igamc_cf(double a, double x) {  // DLMF 8.9.2
   return ans * ax;
 }
 
-PBH_HD inline double igam_series(double a, double x) {  // DLMF 8.11.4
-  double ax = igam_fac(a, x);
+PBH_HD inline double igam_series(double a, double x, const GammaAux* g = nullptr) {  // DLMF 8.11.4
+  double ax = igam_fac(a, x, g);
   if (ax == 0.0) return 0.0;
   double r = a, c = 1.0, ans = 1.0;
   for (int i = 0; i < 2000; ++i) {
@@ -465,7 +475,7 @@ PBH_HD inline double igam_series(double a, double x) {  // DLMF 8.11.4
   return ans * ax / a;
 }
 
-PBH_HD inline double igamc_series(double a, double x) {  // DLMF 8.7.3
+PBH_HD inline double igamc_series(double a, double x, const GammaAux* g = nullptr) {  // DLMF 8.7.3
   double fac = 1, sum = 0;
   for (int n = 1; n < 2000; ++n) {
     fac *= -x / n;
@@ -474,8 +484,8 @@ PBH_HD inline double igamc_series(double a, double x) {  // DLMF 8.7.3
     if (fabs(term) <= kMachEp * fabs(sum)) break;
   }
   double logx = log(x);
-  double term = -expm1_(a * logx - lgam1p(a));
-  return term - exp(a * logx - lgam(a)) * sum;
+  double term = -expm1_(a * logx - (g ? g->lg1pa : lgam1p(a)));
+  return term - exp(a * logx - (g ? g->lga : lgam(a))) * sum;
 }
 
 // Temme uniform asymptotic expansion, DLMF 8.12.3 / 8.12.4; igam when upper == false.
@@ -517,9 +527,9 @@ PBH_HD inline double igam_asymptotic(double a, double x, bool upper) {
   return res;
 }
 
-PBH_HD inline double igamc(double a, double x);
+PBH_HD inline double igamc(double a, double x, const GammaAux* g = nullptr);
 
-PBH_HD inline double igam(double a, double x) {  // regularized lower P(a, x)
+PBH_HD inline double igam(double a, double x, const GammaAux* g = nullptr) {  // regularized lower P(a, x)
   if (x < 0 || a < 0) return kNaN;
   if (a == 0) return x > 0 ? 1.0 : kNaN;
   if (x == 0) return 0.0;
@@ -528,11 +538,11 @@ PBH_HD inline double igam(double a, double x) {  // regularized lower P(a, x)
   double absxma_a = fabs(x - a) / a;
   if ((a > 20) && (a < 200) && (absxma_a < 0.3)) return igam_asymptotic(a, x, false);
   if ((a > 200) && (absxma_a < 4.5 / sqrt(a))) return igam_asymptotic(a, x, false);
-  if ((x > 1.0) && (x > a)) return 1.0 - igamc(a, x);
-  return igam_series(a, x);
+  if ((x > 1.0) && (x > a)) return 1.0 - igamc(a, x, g);
+  return igam_series(a, x, g);
 }
 
-PBH_HD inline double igamc(double a, double x) {  // regularized upper Q(a, x)
+PBH_HD inline double igamc(double a, double x, const GammaAux* g) {  // regularized upper Q(a, x)
   if (x < 0 || a < 0) return kNaN;
   if (a == 0) return x > 0 ? 0.0 : kNaN;
   if (x == 0) return 1.0;
@@ -542,16 +552,18 @@ PBH_HD inline double igamc(double a, double x) {  // regularized upper Q(a, x)
   if ((a > 20) && (a < 200) && (absxma_a < 0.3)) return igam_asymptotic(a, x, true);
   if ((a > 200) && (absxma_a < 4.5 / sqrt(a))) return igam_asymptotic(a, x, true);
   if (x > 1.1) {
-    if (x < a) return 1.0 - igam_series(a, x);
-    return igamc_cf(a, x);
+    if (x < a) return 1.0 - igam_series(a, x, g);
+    return igamc_cf(a, x, g);
   }
   if (x <= 0.5) {
-    if (-0.4 / log(x) < a) return 1.0 - igam_series(a, x);
-    return igamc_series(a, x);
+    if (-0.4 / log(x) < a) return 1.0 - igam_series(a, x, g);
+    return igamc_series(a, x, g);
   }
-  if (x * 1.1 < a) return 1.0 - igam_series(a, x);
-  return igamc_series(a, x);
+  if (x * 1.1 < a) return 1.0 - igam_series(a, x, g);
+  return igamc_series(a, x, g);
 }
+
+PBH_HD inline GammaAux gamma_aux(double a) { return GammaAux{lgam(a), lgam1p(a), lanczos_sum_expg_scaled(a)}; }
 
 // ---------------------------------------------------------------- inverse incomplete gamma
 PBH_HD inline double didonato_eq25(double a, double y) {
@@ -686,6 +698,62 @@ PBH_HD inline double igamci(double a, double q) {  // x with Q(a, x) = q
       x = x - f_fp / (1.0 - 0.5 * f_fp * fpp_fp);
   }
   return x;
+}
+
+// ---------------------------------------------------------------- table-guided gammaincinv
+// For a scalar shape `a`, log(igami(a, Phi(z))) is tabulated on a uniform z grid (value and
+// z-derivative = phi(z) / igam_fac(a, x)); an element's initial guess is the cubic Hermite
+// interpolant at z = ndtri(p) (relative error ~1e-10), and one Halley step of igami's own
+// iteration (igam for p <= 0.9, the igamc form of igamci above) lands on the root.  This
+// replaces DiDonato-Morris + 3 Halley steps per element by 1 step; elements outside the
+// table or next to an invalid (under/overflowed) entry use the full igami.
+struct GammaGuide {
+  const double* y;   // log x at z_j = z0 + j h
+  const double* dy;  // d log x / dz at z_j
+  int m;
+  double z0, h, inv_h;
+};
+
+PBH_HD inline double ndtr(double a) {
+  double x = a * 0.70710678118654752440;
+  double z = fabs(x);
+  if (z < 1.0) return 0.5 + 0.5 * erf_(x);
+  double y = 0.5 * erfc_(z);
+  return x > 0 ? 1.0 - y : y;
+}
+
+PBH_HD inline double gamma_halley(double a, double p, double x, const GammaAux* g) {
+  double fac = igam_fac(a, x, g);
+  if (fac == 0.0) return x;
+  double f_fp = (p > 0.9) ? (igamc(a, x, g) - (1 - p)) * x / (-fac) : (igam(a, x, g) - p) * x / fac;
+  double fpp_fp = -1.0 + (a - 1) / x;
+  return isinf(fpp_fp) ? x - f_fp : x - f_fp / (1.0 - 0.5 * f_fp * fpp_fp);
+}
+
+PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const GammaGuide& T) {
+  if (!(p > 0.0 && p < 1.0)) return igami(a, p);
+  double z = ndtri(p);
+  double u = (z - T.z0) * T.inv_h;
+  if (!(u >= 0.0 && u < (double)(T.m - 1))) return igami(a, p);
+  int j = (int)u;
+  double t = u - (double)j;
+  double y0 = T.y[j], y1 = T.y[j + 1], d0 = T.dy[j] * T.h, d1 = T.dy[j + 1] * T.h;
+  if (!isfinite(y0 + y1 + d0 + d1)) return igami(a, p);
+  double t2 = t * t, t3 = t2 * t;
+  double y = (2 * t3 - 3 * t2 + 1) * y0 + (t3 - 2 * t2 + t) * d0 + (3 * t2 - 2 * t3) * y1 + (t3 - t2) * d1;
+  return gamma_halley(a, p, exp(y), g);
+}
+
+// Table entry j of GammaGuide for shape a (NaN when the entry is unusable).
+PBH_HD inline void gamma_guide_entry(double a, double z, double* y, double* dy) {
+  double q = ndtr(z);
+  double x = igami(a, q);
+  double fac = igam_fac(a, x);
+  double phi = exp(-0.5 * z * z) / kSqrt2Pi;
+  double ly = log(x), d = phi / fac;
+  bool ok = q > 0.0 && q < 1.0 && x > 0.0 && isfinite(ly) && isfinite(d) && fac > 0.0;
+  *y = ok ? ly : kNaN;
+  *dy = ok ? d : kNaN;
 }
 
 // Poisson CDF P[X <= k] = Q(k + 1, m) for integer k >= 0 (scipy.special.pdtr).

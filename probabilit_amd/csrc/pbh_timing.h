@@ -20,6 +20,8 @@ enum KernelId {
   kKElementwise,
   kKHeadBounds,
   kKScan,
+  kKLhsSorted,
+  kKPermScores,
   kKCount
 };
 

@@ -387,7 +387,16 @@ class Node(abc.ABC):
         variable_sets = [set(v) for (v, _) in correlations]
         all_variables = sorted(functools.reduce(set.union, variable_sets, set()), key=lambda n: n._id)
         block, block_row = None, {}
-        if correlations and set(all_variables) <= set(isns):
+        # Fast path: correlated ISNs drawn from the native LHS with plain-number parameters
+        # are handed to Iman-Conover as generator descriptors; their uncorrelated samples are
+        # overwritten by the correlator anyway (:582-583), so they are never materialised.
+        generated = (bool(correlations) and isinstance(source, qmc.LHSSource)
+                     and isinstance(correlator, type) and issubclass(correlator, ImanConover)
+                     and set(all_variables) <= set(isns)
+                     and all(type(v) is Distribution and v.distr in _DIST_SHAPES and v.is_leaf
+                             for v in all_variables))
+        deferred = {}
+        if correlations and set(all_variables) <= set(isns) and not generated:
             block = device.empty((len(all_variables), size))
             block_row = {v: j for j, v in enumerate(all_variables)}
 
@@ -396,6 +405,9 @@ class Node(abc.ABC):
                 assert isinstance(anc, (Constant, Transform))
                 anc._set_device(anc._sample_device(ev))
             assert isinstance(node, AbstractDistribution)
+            if generated and node in all_variables:
+                deferred[node] = source.next_column()
+                continue
             out = block[block_row[node]] if node in block_row else None
             node._set_device(node._sample_device(ev, source.next_column(), out=out))
 
@@ -413,7 +425,17 @@ class Node(abc.ABC):
             indexed = [(tuple(var_to_int[v] for v in vs), cm) for (vs, cm) in correlations]
             C = nearest_correlation_matrix(build_corrmat(indexed))
             inst = correlator().set_target(C)
-            if isinstance(inst, ImanConover):
+            if generated:
+                cols = []
+                for var in all_variables:
+                    _, seed, n_total, col = deferred[var]
+                    params = [float(p) for p in var._params(size)]
+                    cols.append(_lib.ICColumn(seed, col, _lib.DIST_IDS[var.distr], (ctypes.c_double * 3)(*params),
+                                              len(params), ev.flag_ptr(var)))
+                Y = inst._transform_generated(cols, size)
+                for j, var in enumerate(all_variables):
+                    var._set_device(Y[j])
+            elif isinstance(inst, ImanConover):
                 Y = inst._transform_device(block, ev)
                 for j, var in enumerate(all_variables):
                     var._set_device(Y[j])

@@ -24,10 +24,12 @@ RTOL = 1e-10
 POISSON_DOMAIN = (1e-150, 1.0 - 2.0**-52)
 
 
-def _check_poisson(q, out, exp, mu):
+def _check_poisson(q, out, exp, mu, loc=0.0):
     import scipy.special as sc
 
     q = np.asarray(q)
+    out = np.asarray(out) - loc
+    exp = np.asarray(exp) - loc
     inside = (q >= POISSON_DOMAIN[0]) & (q <= POISSON_DOMAIN[1])
     np.testing.assert_array_equal(out[inside | ~np.isfinite(exp)], exp[inside | ~np.isfinite(exp)])
     mu = np.broadcast_to(mu, q.shape)
@@ -54,7 +56,7 @@ def test_ppf_golden(gpu, ppf_golden, case):
     out = native.ppf(name, ppf_golden["q"], **kw)
     exp = ppf_golden[case]
     if name == "poisson":
-        _check_poisson(ppf_golden["q"], out, exp, kw["mu"])
+        _check_poisson(ppf_golden["q"], out, exp, kw["mu"], kw.get("loc", 0.0))
     else:
         assert_close(out, exp, rtol=RTOL, what=case)
 
