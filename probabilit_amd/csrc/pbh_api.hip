@@ -58,7 +58,36 @@ struct IcLayout {
   int32_t* flag;
   double* tmp;                  // n doubles: tied-column average ranks / fallback X column
   unsigned long long* counts;   // ties, inversions of a generated sorted column
+  void* codemap;                // CodeMap base[] / scale[] (step 4)
 };
+
+// Host tables of the step-4 code map, built once; uploaded into the workspace per call.
+CodeMap upload_code_map(void* dev, hipStream_t s, int* st) {
+  struct Host {
+    std::vector<uint32_t> base;
+    std::vector<double> scale;
+    double x0 = 0, w = 0;
+    Host() : base(kCodeSegments + 1), scale(kCodeSegments) { code_map_host(base.data(), scale.data(), &x0, &w); }
+  };
+  static const Host h;
+  const size_t base_bytes = ((kCodeSegments + 1) * 4 + 255) / 256 * 256;
+  CodeMap cm;
+  cm.x0 = h.x0;
+  cm.w = h.w;
+  cm.inv_w = 1.0 / h.w;
+  cm.m = kCodeSegments;
+  cm.base = (const uint32_t*)dev;
+  cm.scale = (const double*)((char*)dev + base_bytes);
+  *st = PBH_OK;
+  hipError_t e = hipMemcpyAsync(dev, h.base.data(), (kCodeSegments + 1) * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync((char*)dev + base_bytes, h.scale.data(), kCodeSegments * 8, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    set_error("code map upload: %s", hipGetErrorString(e));
+    *st = PBH_ERR_HIP;
+  }
+  return cm;
+}
 
 size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   Carver c(base);
@@ -75,7 +104,9 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* flag = c.take(256);
   void* tmp = c.take((size_t)n * 8);
   void* counts = c.take(256);
+  void* codemap = c.take(code_map_bytes());
   if (carve) {
+    L->codemap = codemap;
     L->tmp = (double*)tmp;
     L->counts = (unsigned long long*)counts;
     L->S = (double*)S;
@@ -302,17 +333,39 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     PBH_CHECK_HIP(hipMemcpyAsync(a->cscores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
 
   // ---- step 4: Y[:, c] = sort(X[:, c])[rankdata(CS[:, c]).astype(int) - 1]
+  // The correlated scores are ~N(0, 1): sort 32-bit order-preserving codes (4 passes instead
+  // of 8), then order the (short) runs of equal codes by the full float64 value.  A run
+  // longer than kMaxRun sends that column through the 64-bit sort instead.
+  const CodeMap cm = upload_code_map(L.codemap, s, &st);
+  if (st) return st;
+  uint8_t* eqprev = (uint8_t*)L.tmp;
   for (int c = 0; c < k; ++c) {
-    st = load_keys(L.S + (int64_t)c * n, 1, n, sb.keys[0], nullptr, s);
-    if (st) return st;
-    int buf = 0;
-    st = radix_sort_keys(sb, n, s, &buf);
-    if (st) return st;
+    const double* cs_c = L.S + (int64_t)c * n;
     RankOut out = {};
     out.sorted_src = L.sorted_x + (int64_t)c * n;
     out.y = a->Y + (int64_t)c * a->y_cs;
     out.y_rs = a->y_rs;
     out.idx = a->idx_out ? a->idx_out + (int64_t)c * n : nullptr;
+    int buf = 0;
+    st = make_codes(cs_c, n, cm, (uint32_t*)sb.keys[0], s);
+    if (st) return st;
+    st = radix_sort_keys32(sb, n, s, &buf);
+    if (st) return st;
+    PBH_CHECK_HIP(hipMemsetAsync(L.counts, 0, sizeof(int32_t), s));
+    st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], cs_c, n, eqprev, (int32_t*)L.counts, s);
+    if (st) return st;
+    int32_t long_run = 0;
+    PBH_CHECK_HIP(hipMemcpyAsync(&long_run, L.counts, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+    if (!long_run) {
+      st = rank_finish(kModeGather, nullptr, sb.vals[buf], n, tb, out, s, eqprev);
+      if (st) return st;
+      continue;
+    }
+    st = load_keys(cs_c, 1, n, sb.keys[0], nullptr, s);
+    if (st) return st;
+    st = radix_sort_keys(sb, n, s, &buf);
+    if (st) return st;
     st = rank_finish(kModeGather, sb.keys[buf], sb.vals[buf], n, tb, out, s);
     if (st) return st;
   }

@@ -35,8 +35,30 @@ void tie_carve(void* ws, int64_t n, TieBuffers& tb);
 int load_keys(const double* x, int64_t stride, int64_t n, uint64_t* keys, int32_t* flag, hipStream_t s);
 
 // Given keys sorted ascending with row payload, resolve 'average' tie ranks and emit per mode.
+// With eqprev != NULL, ties come from eqprev[i] (element i equals element i - 1) and keys may
+// be NULL (gather / ranks modes only).
 int rank_finish(int mode, const uint64_t* keys, const uint32_t* rows, int64_t n, const TieBuffers& tb,
-                const RankOut& out, hipStream_t s);
+                const RankOut& out, hipStream_t s, const uint8_t* eqprev = nullptr);
+
+// 32-bit order-preserving codes of approximately N(0, 1) data: a piecewise-linear map through
+// Phi on m uniform segments of [x0, x0 + m w].  code(x) is non-decreasing in x for every
+// double (segment index and in-segment offset are both monotone), so sorting by code and
+// then ordering equal-code runs by the full value yields the exact float64 order.
+struct CodeMap {
+  double x0, w, inv_w;
+  int m;
+  const uint32_t* base;  // m + 1 strictly increasing code bases
+  const double* scale;   // m slopes (codes per unit x)
+};
+constexpr int kCodeSegments = 8192;
+size_t code_map_bytes();
+// Host: fill base / scale for N(0, 1)-shaped data into the host buffers.
+void code_map_host(uint32_t* base, double* scale, double* x0, double* w);
+int make_codes(const double* x, int64_t n, const CodeMap& cm, uint32_t* codes, hipStream_t s);
+// Order every run of equal codes (length <= 16) by the full value x[row] and flag exact
+// ties in eqprev; sets *long_flag when a run is longer (caller falls back to 64-bit keys).
+int resolve_code_runs(const uint32_t* codes, uint32_t* rows, const double* x, int64_t n, uint8_t* eqprev,
+                      int32_t* long_flag, hipStream_t s);
 
 // Column sums (k columns of length n, column stride ld) into sums[k] (device), fixed order.
 int column_means(const double* S, int64_t n, int k, int64_t ld, double* partial, double* means, hipStream_t s);

@@ -62,8 +62,9 @@ __global__ __launch_bounds__(T) void k_load_keys(const double* __restrict__ x, i
   }
 }
 
-__global__ __launch_bounds__(T) void k_head_bounds(const uint64_t* __restrict__ keys, int64_t n,
-                                                  int64_t* __restrict__ first_head, int64_t* __restrict__ last_head) {
+__global__ __launch_bounds__(T) void k_head_bounds(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ eqprev,
+                                                  int64_t n, int64_t* __restrict__ first_head,
+                                                  int64_t* __restrict__ last_head) {
   __shared__ int64_t sh[8];
   const int64_t base = (int64_t)blockIdx.x * TILE;
   int64_t f = kNoHead, l = -1;
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(T) void k_head_bounds(const uint64_t* __restrict__ 
   for (int j = 0; j < IPT; ++j) {
     int64_t i = base + j * T + threadIdx.x;
     if (i < n) {
-      bool head = (i == 0) || keys[i] != keys[i - 1];
+      bool head = (i == 0) || (eqprev ? !eqprev[i] : keys[i] != keys[i - 1]);
       if (head) {
         f = i < f ? i : f;
         l = i > l ? i : l;
@@ -142,7 +143,8 @@ __global__ __launch_bounds__(T) void k_head_prefix(const int64_t* __restrict__ f
 
 template <int MODE>
 __global__ __launch_bounds__(T) void k_rank_finish(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ rows,
-                                                  int64_t n, const int64_t* __restrict__ prev_head,
+                                                  const uint8_t* __restrict__ eqprev, int64_t n,
+                                                  const int64_t* __restrict__ prev_head,
                                                   const int64_t* __restrict__ next_head, RankOut out) {
   __shared__ uint64_t sk[TILE + TILE / 16];
   __shared__ uint32_t sr[TILE + TILE / 16];
@@ -154,11 +156,12 @@ __global__ __launch_bounds__(T) void k_rank_finish(const uint64_t* __restrict__ 
   for (int j = 0; j < IPT; ++j) {
     int p = j * T + t;
     if (p < cnt) {
-      sk[pad(p)] = keys[base + p];
+      // with eqprev the key slot carries the "equals previous" flag instead of the key
+      sk[pad(p)] = eqprev ? (uint64_t)eqprev[base + p] : keys[base + p];
       sr[pad(p)] = rows ? rows[base + p] : (uint32_t)(base + p);  // NULL payload: identity
     }
   }
-  const uint64_t before = base > 0 ? keys[base - 1] : 0ull;
+  const uint64_t before = (base > 0 && !eqprev) ? keys[base - 1] : 0ull;
   __syncthreads();
 
   // blocked view: thread t owns positions t*16 .. t*16+15 of the tile
@@ -170,8 +173,12 @@ __global__ __launch_bounds__(T) void k_rank_finish(const uint64_t* __restrict__ 
     int p = t * IPT + q;
     if (p < cnt) {
       k[q] = sk[pad(p)];
-      uint64_t prev = (p == 0) ? before : sk[pad(p - 1)];
-      head[q] = (base + p == 0) || (k[q] != prev);
+      if (eqprev) {
+        head[q] = (base + p == 0) || k[q] == 0;
+      } else {
+        uint64_t prev = (p == 0) ? before : sk[pad(p - 1)];
+        head[q] = (base + p == 0) || (k[q] != prev);
+      }
       if (head[q]) {
         int64_t g = base + p;
         first_local = g < first_local ? g : first_local;
@@ -414,26 +421,26 @@ int load_keys(const double* x, int64_t stride, int64_t n, uint64_t* keys, int32_
 }
 
 int rank_finish(int mode, const uint64_t* keys, const uint32_t* rows, int64_t n, const TieBuffers& tb,
-                const RankOut& out, hipStream_t s) {
+                const RankOut& out, hipStream_t s, const uint8_t* eqprev) {
   const int64_t nt = sort_tiles(n);
   PBH_TIMED(kKHeadBounds, s,
-            hipLaunchKernelGGL(k_head_bounds, dim3((unsigned)nt), dim3(T), 0, s, keys, n, tb.first_head,
+            hipLaunchKernelGGL(k_head_bounds, dim3((unsigned)nt), dim3(T), 0, s, keys, eqprev, n, tb.first_head,
                                tb.last_head);
             hipLaunchKernelGGL(k_head_prefix, dim3(1), dim3(T), 0, s, tb.first_head, tb.last_head, nt, n,
                                tb.prev_head, tb.next_head));
   switch (mode) {
     case kModeScores:
       PBH_TIMED(kKRankScores, s,
-                hipLaunchKernelGGL(k_rank_finish<kModeScores>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, n,
+                hipLaunchKernelGGL(k_rank_finish<kModeScores>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, eqprev, n,
                                    tb.prev_head, tb.next_head, out));
       break;
     case kModeGather:
       PBH_TIMED(kKRankGather, s,
-                hipLaunchKernelGGL(k_rank_finish<kModeGather>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, n,
+                hipLaunchKernelGGL(k_rank_finish<kModeGather>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, eqprev, n,
                                    tb.prev_head, tb.next_head, out));
       break;
     default:
-      hipLaunchKernelGGL(k_rank_finish<kModeRanks>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, n, tb.prev_head,
+      hipLaunchKernelGGL(k_rank_finish<kModeRanks>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, eqprev, n, tb.prev_head,
                          tb.next_head, out);
   }
   PBH_CHECK_LAUNCH();
@@ -499,6 +506,100 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
     set_error("Iman-Conover: K = %d exceeds the supported maximum of 128 variables", k);
     return PBH_ERR_UNSUPPORTED;
   }
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+// ---------------------------------------------------------------- 32-bit codes of the scores
+__device__ __forceinline__ uint32_t code_of(double x, const CodeMap& c) {
+  double u = (x - c.x0) * c.inv_w;
+  if (!(u >= 0.0)) return 0u;
+  if (u >= (double)c.m) return 0xFFFFFFFFu;
+  int j = (int)u;
+  double lo = c.x0 + (double)j * c.w;
+  uint32_t b0 = c.base[j], cnt = c.base[j + 1] - b0;
+  double off = floor((x - lo) * c.scale[j]);
+  uint32_t o = off <= 0.0 ? 0u : (off >= (double)(cnt - 1) ? cnt - 1 : (uint32_t)off);
+  return b0 + o;
+}
+
+static __global__ __launch_bounds__(256) void k_make_codes(const double* __restrict__ x, int64_t n, CodeMap cm,
+                                                          uint32_t* __restrict__ codes) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    codes[i] = code_of(x[i], cm);
+}
+
+constexpr int kMaxRun = 16;
+
+static __global__ __launch_bounds__(256) void k_code_runs(const uint32_t* __restrict__ code, uint32_t* __restrict__ rows,
+                                                         const double* __restrict__ x, int64_t n,
+                                                         uint8_t* __restrict__ eqprev, int32_t* long_flag) {
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const uint32_t c = code[t];
+    if (t > 0 && code[t - 1] == c) continue;  // inside a run: handled by its first element
+    if (t + 1 >= n || code[t + 1] != c) {
+      eqprev[t] = 0;
+      continue;
+    }
+    int len = 2;
+    while (t + len < n && code[t + len] == c && len <= kMaxRun) ++len;
+    if (len > kMaxRun) {
+      atomicOr(long_flag, 1);
+      continue;
+    }
+    uint32_t r[kMaxRun];
+    double v[kMaxRun];
+    for (int i = 0; i < len; ++i) {
+      r[i] = rows[t + i];
+      v[i] = x[r[i]];
+    }
+    for (int i = 1; i < len; ++i) {  // insertion sort by value (ties keep their order)
+      uint32_t ri = r[i];
+      double vi = v[i];
+      int j = i - 1;
+      while (j >= 0 && v[j] > vi) {
+        v[j + 1] = v[j];
+        r[j + 1] = r[j];
+        --j;
+      }
+      v[j + 1] = vi;
+      r[j + 1] = ri;
+    }
+    for (int i = 0; i < len; ++i) {
+      rows[t + i] = r[i];
+      eqprev[t + i] = (i > 0 && v[i] == v[i - 1]) ? 1 : 0;
+    }
+  }
+}
+
+size_t code_map_bytes() { return ((kCodeSegments + 1) * 4 + 255) / 256 * 256 + kCodeSegments * 8; }
+
+void code_map_host(uint32_t* base, double* scale, double* x0, double* w) {
+  const int m = kCodeSegments;
+  *x0 = -8.5;
+  *w = 17.0 / m;
+  const double span = 4294967295.0 - m;
+  for (int j = 0; j <= m; ++j) {
+    double lo = *x0 + (double)j * (*w);
+    double phi = 0.5 * erfc(-lo * 0.70710678118654752440);
+    double b = floor(phi * span) + j;
+    base[j] = (uint32_t)(b > 4294967295.0 ? 4294967295.0 : b);
+  }
+  for (int j = 0; j < m; ++j) scale[j] = (double)(base[j + 1] - base[j]) / (*w);
+}
+
+int make_codes(const double* x, int64_t n, const CodeMap& cm, uint32_t* codes, hipStream_t s) {
+  PBH_TIMED(kKMakeCodes, s,
+            hipLaunchKernelGGL(k_make_codes, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, x, n, cm, codes));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int resolve_code_runs(const uint32_t* codes, uint32_t* rows, const double* x, int64_t n, uint8_t* eqprev,
+                      int32_t* long_flag, hipStream_t s) {
+  PBH_TIMED(kKCodeRuns, s,
+            hipLaunchKernelGGL(k_code_runs, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, codes, rows, x, n, eqprev,
+                               long_flag));
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }

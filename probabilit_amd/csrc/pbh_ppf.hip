@@ -338,8 +338,8 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
   *table = nullptr;
   if (dist == PBH_DIST_GAMMA && params[0].ptr == nullptr && params[0].value > 0.0 && isfinite(params[0].value)) {
     const double a = params[0].value;
-    const double z0 = -12.0, h = 1.0 / 64.0;
-    const int m = (int)((8.125 - z0) / h) + 1;
+    const double z0 = sf::kGammaGuideZ0, h = sf::kGammaGuideH;
+    const int m = sf::kGammaGuideM;
     PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)2 * m * sizeof(double), s));
     hipLaunchKernelGGL(k_gamma_guide, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a, z0, h, m, *table,
                        *table + m);

@@ -67,19 +67,24 @@ PBH_HD inline uint32_t mix32(uint32_t x) {  // lowbias32 finalizer
   return x;
 }
 
+// Alternating (unbalanced) Feistel network on b = ceil(log2 n) bits: the high part L
+// (b - b/2 bits) and the low part R (b/2 bits) take turns being xored with a keyed round
+// function of the other part.  Every round is an involution on its half, so the network is
+// a bijection of [0, 2^b) for any split, and 2^b < 2n keeps cycle walking short (expected
+// < 2 walks; the wave-wide maximum, which is what a SIMD lane waits for, stays ~3-4).
 struct FeistelPerm {
   static constexpr int kRounds = 6;
   uint64_t n;
-  uint32_t half_bits, mask;
+  uint32_t r_bits, mask_l, mask_r;
   uint32_t rk[kRounds];
 
   PBH_HD FeistelPerm(const Philox& ph, uint64_t n_, uint32_t col) : n(n_) {
     uint32_t bits = 0;
     while (bits < 64 && (1ull << bits) < n_) ++bits;
-    if (bits & 1u) ++bits;
-    if (bits < 2) bits = 2;
-    half_bits = bits / 2;
-    mask = (half_bits >= 32) ? 0xFFFFFFFFu : ((1u << half_bits) - 1u);
+    r_bits = bits / 2;
+    uint32_t l_bits = bits - r_bits;
+    mask_r = (r_bits >= 32) ? 0xFFFFFFFFu : ((1u << r_bits) - 1u);
+    mask_l = (l_bits >= 32) ? 0xFFFFFFFFu : ((1u << l_bits) - 1u);
     uint32_t c[4] = {col, 0u, 0u, kPurposeFeistel};
     ph(c);
     uint32_t d[4] = {col, 1u, 0u, kPurposeFeistel};
@@ -92,28 +97,30 @@ struct FeistelPerm {
     rk[5] = d[1];
   }
 
-  PBH_HD inline uint32_t F(uint32_t r, uint32_t k) const { return mix32(r * 0x9E3779B1u ^ k) & mask; }
+  PBH_HD inline uint32_t F(uint32_t v, uint32_t k) const { return mix32(v * 0x9E3779B1u ^ k); }
 
   PBH_HD inline uint64_t round_trip(uint64_t x) const {
-    uint32_t L = (uint32_t)(x >> half_bits), R = (uint32_t)(x & mask);
+    uint32_t L = (uint32_t)(x >> r_bits), R = (uint32_t)(x & mask_r);
 #pragma unroll
     for (int i = 0; i < kRounds; ++i) {
-      uint32_t t = L ^ F(R, rk[i]);
-      L = R;
-      R = t;
+      if (i & 1)
+        R ^= F(L, rk[i]) & mask_r;
+      else
+        L ^= F(R, rk[i]) & mask_l;
     }
-    return ((uint64_t)L << half_bits) | R;
+    return ((uint64_t)L << r_bits) | R;
   }
 
   PBH_HD inline uint64_t round_trip_inv(uint64_t y) const {
-    uint32_t L = (uint32_t)(y >> half_bits), R = (uint32_t)(y & mask);
+    uint32_t L = (uint32_t)(y >> r_bits), R = (uint32_t)(y & mask_r);
 #pragma unroll
     for (int i = kRounds - 1; i >= 0; --i) {
-      uint32_t t = R ^ F(L, rk[i]);
-      R = L;
-      L = t;
+      if (i & 1)
+        R ^= F(L, rk[i]) & mask_r;
+      else
+        L ^= F(R, rk[i]) & mask_l;
     }
-    return ((uint64_t)L << half_bits) | R;
+    return ((uint64_t)L << r_bits) | R;
   }
 
   // Bijection of [0, n) by cycle walking.

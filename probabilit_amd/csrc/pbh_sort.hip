@@ -10,25 +10,28 @@ constexpr int IPT = kSortItems;
 constexpr int TILE = kSortTile;
 
 // ------------------------------------------------------------------ full digit histogram
-__global__ __launch_bounds__(256) void k_digit_hist(const uint64_t* __restrict__ keys, int64_t n,
+template <typename K>
+__global__ __launch_bounds__(256) void k_digit_hist(const K* __restrict__ keys, int64_t n,
                                                     uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[8][256];
-  for (int i = threadIdx.x; i < 8 * 256; i += 256) (&h[0][0])[i] = 0;
+  constexpr int NB = sizeof(K);
+  __shared__ uint32_t h[NB][256];
+  for (int i = threadIdx.x; i < NB * 256; i += 256) (&h[0][0])[i] = 0;
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    uint64_t k = keys[i];
+    K k = keys[i];
 #pragma unroll
-    for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(k >> (8 * p)) & 255u], 1u);
+    for (int p = 0; p < NB; ++p) atomicAdd(&h[p][(k >> (8 * p)) & 255u], 1u);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 8 * 256; i += 256) {
+  for (int i = threadIdx.x; i < NB * 256; i += 256) {
     uint32_t v = (&h[0][0])[i];
     if (v) atomicAdd(&hist[i], v);
   }
 }
 
 // ------------------------------------------------------------------ upsweep
-__global__ __launch_bounds__(T) void k_upsweep(const uint64_t* __restrict__ keys, int64_t n, int shift,
+template <typename K>
+__global__ __launch_bounds__(T) void k_upsweep(const K* __restrict__ keys, int64_t n, int shift,
                                               uint32_t* __restrict__ counts, int64_t ntiles) {
   __shared__ uint32_t h[256];
   h[threadIdx.x] = 0;
@@ -127,10 +130,11 @@ int exclusive_scan_u32(uint32_t* a, int64_t m, uint32_t* partials, hipStream_t s
 }
 
 // ------------------------------------------------------------------ stable scatter
-__global__ __launch_bounds__(T) void k_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                              uint64_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n,
+template <typename K>
+__global__ __launch_bounds__(T) void k_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                              K* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n,
                                               int shift, const uint32_t* __restrict__ offsets, int64_t ntiles) {
-  __shared__ uint64_t skeys[TILE];
+  __shared__ K skeys[TILE];
   __shared__ uint32_t svals[TILE];
   __shared__ uint32_t run[256];
   __shared__ uint32_t chunk[2][4][256];  // double-buffered by item parity
@@ -142,14 +146,14 @@ __global__ __launch_bounds__(T) void k_scatter(const uint64_t* __restrict__ kin,
   const int64_t base = tile * TILE;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
-  uint64_t key[IPT];
+  K key[IPT];
   uint32_t val[IPT];
   uint32_t rank[IPT];
 #pragma unroll
   for (int j = 0; j < IPT; ++j) {
     int64_t i = base + j * T + t;
     bool valid = i < n;
-    key[j] = valid ? kin[i] : 0ull;
+    key[j] = valid ? kin[i] : (K)0;
     val[j] = valid ? (vin ? vin[i] : (uint32_t)i) : 0u;
   }
   run[t] = 0;
@@ -203,7 +207,7 @@ __global__ __launch_bounds__(T) void k_scatter(const uint64_t* __restrict__ kin,
   for (int j = 0; j < IPT; ++j) {
     int p = j * T + t;
     if (p < cnt) {
-      uint64_t k = skeys[p];
+      K k = skeys[p];
       uint32_t d = (uint32_t)(k >> shift) & 255u;
       int64_t o = (int64_t)gbase[d] + (p - (int64_t)dstart[d]);
       kout[o] = k;
@@ -247,18 +251,21 @@ void sort_carve(void* ws, int64_t n, SortBuffers& sb) {
   sb.hist = (uint32_t*)take(8 * 256 * 4);
 }
 
-int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
+template <typename K>
+int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
+  constexpr int NB = sizeof(K);
   PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "radix sort: n out of range");
   const int64_t nt = sort_tiles(n);
+  K* keys[2] = {(K*)b.keys[0], (K*)b.keys[1]};
   // which byte positions vary?
   PBH_CHECK_HIP(hipMemsetAsync(b.hist, 0, 8 * 256 * 4, s));
-  PBH_TIMED(kKSortDigitHist, s,
-            hipLaunchKernelGGL(k_digit_hist, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, b.keys[0], n, b.hist));
+  PBH_TIMED(NB == 8 ? kKSortDigitHist : kKSortDigitHist32, s,
+            hipLaunchKernelGGL(k_digit_hist<K>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, keys[0], n, b.hist));
   PBH_CHECK_LAUNCH();
-  PBH_CHECK_HIP(hipMemcpyAsync(b.hist_host, b.hist, 8 * 256 * 4, hipMemcpyDeviceToHost, s));
+  PBH_CHECK_HIP(hipMemcpyAsync(b.hist_host, b.hist, NB * 256 * 4, hipMemcpyDeviceToHost, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));
   int passes[8], npass = 0;
-  for (int p = 0; p < 8; ++p) {
+  for (int p = 0; p < NB; ++p) {
     int nonzero = 0;
     for (int d = 0; d < 256; ++d) nonzero += b.hist_host[p * 256 + d] != 0;
     if (nonzero > 1) passes[npass++] = p;
@@ -267,20 +274,28 @@ int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
   int cur = 0;
   for (int ip = 0; ip < npass; ++ip) {
     const int shift = 8 * passes[ip];
-    PBH_TIMED(kKSortUpsweep, s,
-              hipLaunchKernelGGL(k_upsweep, dim3((unsigned)nt), dim3(T), 0, s, b.keys[cur], n, shift, b.counts, nt));
+    PBH_TIMED(NB == 8 ? kKSortUpsweep : kKSortUpsweep32, s,
+              hipLaunchKernelGGL(k_upsweep<K>, dim3((unsigned)nt), dim3(T), 0, s, keys[cur], n, shift, b.counts, nt));
     PBH_CHECK_LAUNCH();
     int st = exclusive_scan_u32(b.counts, 256 * nt, b.partials, s);
     if (st != PBH_OK) return st;
-    PBH_TIMED(kKSortScatter, s,
-              hipLaunchKernelGGL(k_scatter, dim3((unsigned)nt), dim3(T), 0, s, b.keys[cur],
-                                 ip == 0 ? nullptr : b.vals[cur], b.keys[cur ^ 1], b.vals[cur ^ 1], n, shift, b.counts,
+    PBH_TIMED(NB == 8 ? kKSortScatter : kKSortScatter32, s,
+              hipLaunchKernelGGL(k_scatter<K>, dim3((unsigned)nt), dim3(T), 0, s, keys[cur],
+                                 ip == 0 ? nullptr : b.vals[cur], keys[cur ^ 1], b.vals[cur ^ 1], n, shift, b.counts,
                                  nt));
     PBH_CHECK_LAUNCH();
     cur ^= 1;
   }
   *out_buf = cur;
   return PBH_OK;
+}
+
+int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
+  return radix_sort_impl<uint64_t>(b, n, s, out_buf);
+}
+
+int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
+  return radix_sort_impl<uint32_t>(b, n, s, out_buf);
 }
 
 }  // namespace pbh

@@ -707,6 +707,10 @@ PBH_HD inline double igamci(double a, double q) {  // x with Q(a, x) = q
 // iteration (igam for p <= 0.9, the igamc form of igamci above) lands on the root.  This
 // replaces DiDonato-Morris + 3 Halley steps per element by 1 step; elements outside the
 // table or next to an invalid (under/overflowed) entry use the full igami.
+constexpr double kGammaGuideZ0 = -12.0;       // grid start (Phi(z0) ~ 1.8e-33)
+constexpr double kGammaGuideH = 1.0 / 64.0;   // grid step
+constexpr int kGammaGuideM = 1289;            // entries: z0 .. z0 + (m - 1) h = 8.125 (1 - Phi ~ 2.2e-16)
+
 struct GammaGuide {
   const double* y;   // log x at z_j = z0 + j h
   const double* dy;  // d log x / dz at z_j
@@ -741,17 +745,26 @@ PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const G
   if (!isfinite(y0 + y1 + d0 + d1)) return igami(a, p);
   double t2 = t * t, t3 = t2 * t;
   double y = (2 * t3 - 3 * t2 + 1) * y0 + (t3 - 2 * t2 + t) * d0 + (3 * t2 - 2 * t3) * y1 + (t3 - t2) * d1;
+  if (y < -680.0) return igami(a, p);  // x near the subnormal range: keep igami's own iteration
   return gamma_halley(a, p, exp(y), g);
 }
 
 // Table entry j of GammaGuide for shape a (NaN when the entry is unusable).
+// The upper half is tabulated through the complement Q = Phi(-z), which keeps every entry
+// consistent with its z (Phi(z) itself rounds to 1 - k ulp for z >~ 5).
 PBH_HD inline void gamma_guide_entry(double a, double z, double* y, double* dy) {
-  double q = ndtr(z);
-  double x = igami(a, q);
+  double x, tail;
+  if (z > 0.0) {
+    tail = ndtr(-z);
+    x = igamci(a, tail);
+  } else {
+    tail = ndtr(z);
+    x = igami(a, tail);
+  }
   double fac = igam_fac(a, x);
   double phi = exp(-0.5 * z * z) / kSqrt2Pi;
   double ly = log(x), d = phi / fac;
-  bool ok = q > 0.0 && q < 1.0 && x > 0.0 && isfinite(ly) && isfinite(d) && fac > 0.0;
+  bool ok = tail > 0.0 && tail < 1.0 && x > 0.0 && isfinite(ly) && isfinite(d) && fac > 0.0;
   *y = ok ? ly : kNaN;
   *dy = ok ? d : kNaN;
 }

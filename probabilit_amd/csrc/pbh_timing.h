@@ -22,6 +22,11 @@ enum KernelId {
   kKScan,
   kKLhsSorted,
   kKPermScores,
+  kKCodeRuns,
+  kKMakeCodes,
+  kKSortScatter32,
+  kKSortUpsweep32,
+  kKSortDigitHist32,
   kKCount
 };
 

@@ -1,0 +1,92 @@
+"""CPU sweep of the device special functions (pbh_special.h compiled for the host by
+tests/native/special_host.cpp) against scipy 1.15.3, the reference's ppf backend
+(modeling.py:807 -> scipy.special.ndtri / gammaincinv / pdtr).
+
+Gate: 1e-10 relative (BASELINE north_star).  The host build uses glibc's libm where the
+device uses its own math library, so this pins the algorithms; tests/test_gpu_ppf.py pins
+the device results."""
+
+import ctypes
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+import scipy.special as sp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "native", "special_host.cpp")
+OUT = os.path.join(HERE, "native", "_build", "libpbh_special_host.so")
+
+
+@pytest.fixture(scope="module")
+def sfh():
+    hipcc = "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else shutil.which("hipcc")
+    if hipcc is None:
+        pytest.skip("hipcc not available")
+    deps = [SRC] + [os.path.join(ROOT, "probabilit_amd", "csrc", f) for f in ("pbh_special.h", "pbh_common.h",
+                                                                            "pbh_tables.inc")]
+    if not os.path.exists(OUT) or any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps):
+        os.makedirs(os.path.dirname(OUT), exist_ok=True)
+        subprocess.run([hipcc, "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+                        "-I", os.path.join(ROOT, "probabilit_amd", "csrc"), "-I", os.path.join(ROOT, "include"),
+                        SRC, "-o", OUT], check=True, capture_output=True)
+    return ctypes.CDLL(OUT)
+
+
+def _call(lib, fn, *scalars_then_array):
+    *scal, arr = scalars_then_array
+    arr = np.ascontiguousarray(arr, dtype=np.float64)
+    out = np.empty_like(arr)
+    P = ctypes.c_void_p
+    args = [ctypes.c_double(s) for s in scal]
+    getattr(lib, fn)(*args, P(arr.ctypes.data), ctypes.c_long(arr.size), P(out.ctypes.data))
+    return out
+
+
+def _quantiles():
+    rng = np.random.default_rng(0)
+    return np.concatenate([rng.random(60000), 1 - 10 ** rng.uniform(-16, -1, 20000),
+                           10 ** rng.uniform(-300, -1, 20000), 10 ** rng.uniform(-323.5, -300, 2000),
+                           [0.0, 5e-324, 1e-300, 2.0 ** -53, 0.5, 1 - 2.0 ** -53, 1.0]])
+
+
+def _rel(x, ref):
+    with np.errstate(invalid="ignore", divide="ignore"):
+        r = np.abs(x - ref) / np.abs(ref)
+    r[(x == ref) | (np.isnan(x) & np.isnan(ref))] = 0.0
+    return r
+
+
+def test_ndtri_matches_scipy(sfh):
+    q = _quantiles()
+    r = _rel(_call(sfh, "sfh_ndtri", q), sp.ndtri(q))
+    assert r.max() <= 1e-13
+
+
+@pytest.mark.parametrize("a", [0.05, 0.1, 0.3, 0.7, 1.0, 2.0, 5.0, 20.0, 45.0, 100.0, 250.0, 1e3, 1e4, 1e5])
+def test_gammaincinv_and_guided_table(sfh, a):
+    q = _quantiles()
+    ref = sp.gammaincinv(a, q)
+    direct = _call(sfh, "sfh_igami", a, q)
+    guided = _call(sfh, "sfh_igami_guided", a, q)
+    assert (np.isnan(direct) == np.isnan(ref)).all() and (np.isnan(guided) == np.isnan(ref)).all()
+    assert _rel(direct, ref).max() <= 1e-12, "igami restatement"
+    assert _rel(guided, ref).max() <= 1e-10, "guide-table igami"
+
+
+@pytest.mark.parametrize("mu", [0.5, 4.0, 30.0, 1000.0])
+def test_pdtr_matches_scipy(sfh, mu):
+    k = np.arange(0, int(mu + 20 * np.sqrt(mu) + 40), dtype=np.float64)
+    r = _rel(_pdtr(sfh, k, mu), sp.pdtr(k, mu))
+    assert r.max() <= 1e-12
+
+
+def _pdtr(lib, k, mu):
+    k = np.ascontiguousarray(k)
+    out = np.empty_like(k)
+    P = ctypes.c_void_p
+    lib.sfh_pdtr(P(k.ctypes.data), ctypes.c_double(mu), ctypes.c_long(k.size), P(out.ctypes.data))
+    return out

@@ -1,10 +1,18 @@
 set -o pipefail
+# One GPU round: smoke, GPU tests, ppf microbench, bench, rocprofv3 kernel stats.
+# Ordinary failures (exit 1) continue to the next step; a crash, abort or time limit ends the script.
 TAG=${1:-rX}
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
-timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/${TAG}_smoke.log 2>&1; echo "smoke exit $?" >> gpurun_out/${TAG}_smoke.log
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf --maxfail=30 -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1; echo "pytest exit $?" >> gpurun_out/${TAG}_tests.log
+stop_if_crashed() {  # $1 = exit status, $2 = step name
+  echo "$2 exit $1"
+  if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "stopping after $2 (status $1)"; exit "$1"; fi
+}
+timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/${TAG}_smoke.log 2>&1
+stop_if_crashed $? smoke
+timeout -k 10 900 python -m pytest tests -m gpu -q -rf --maxfail=30 -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
+stop_if_crashed $? pytest
 timeout -k 10 300 python tools/microbench_ppf.py > gpurun_out/${TAG}_micro.json 2> gpurun_out/${TAG}_micro.err || exit 1
 timeout -k 10 700 python bench.py --steps 3 --warmup 1 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit 1
 cd /tmp && export TMPDIR=/tmp
