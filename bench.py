@@ -28,8 +28,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 
 def kernel_bytes(name, n, k):
     """Algorithmic HBM bytes of ONE launch of `name` over n rows (k = columns where a launch
     covers all of them).  SURVEY.md §8(d) per-unit figures."""
-    per_elem = {"k_lhs_ppf": 8, "k_ppf": 16, "k_scatter": 24, "k_upsweep": 8, "k_digit_hist": 8,
-                "k_rank_finish<scores>": 28, "k_rank_finish<gather>": 28, "k_load_keys": 16,
+    per_elem = {"k_lhs_ppf": 8, "k_ppf": 16, "k_lhs_sorted_ppf": 8, "k_perm_scores": 8,
+                "k_scatter": 24, "k_upsweep": 8, "k_digit_hist": 8,               # u64 key + u32 row
+                "k_scatter<u32>": 16, "k_upsweep<u32>": 4, "k_digit_hist<u32>": 4,  # u32 code + u32 row
+                "k_rank_finish<scores>": 28,  # read key 8 + row 4, write score 8 + sorted x 8
+                "k_rank_finish<gather>": 21,  # read eqprev 1 + row 4 + sorted x 8, write y 8 (idx only in debug calls)
+                "k_load_keys": 16, "k_make_codes": 12, "k_code_runs": 13,  # runs: codes 4 + row 4 + out 4 + eqprev 1
                 "k_elementwise": 24, "k_head_bounds": 8, "k_scan": 0}
     if name == "k_gram":
         return 8 * n * k

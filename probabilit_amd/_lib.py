@@ -40,7 +40,8 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
            "k_rank_finish<gather>", "k_load_keys", "k_gram", "k_apply", "k_elementwise", "k_head_bounds", "k_scan",
            "k_lhs_sorted_ppf", "k_perm_scores", "k_code_runs",
-           "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>"]
+           "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>",
+           "k_upsweep<place>", "k_scatter<place>", "k_place"]
 
 
 class Param(ctypes.Structure):

@@ -352,13 +352,29 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     st = radix_sort_keys32(sb, n, s, &buf);
     if (st) return st;
     PBH_CHECK_HIP(hipMemsetAsync(L.counts, 0, sizeof(int32_t), s));
-    st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], cs_c, n, eqprev, (int32_t*)L.counts, s);
+    st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], sb.vals[buf ^ 1], cs_c, n, eqprev,
+                           (int32_t*)L.counts, s);
     if (st) return st;
-    int32_t long_run = 0;
-    PBH_CHECK_HIP(hipMemcpyAsync(&long_run, L.counts, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    int32_t run_flags = 0;
+    PBH_CHECK_HIP(hipMemcpyAsync(&run_flags, L.counts, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     PBH_CHECK_HIP(hipStreamSynchronize(s));
-    if (!long_run) {
-      st = rank_finish(kModeGather, nullptr, sb.vals[buf], n, tb, out, s, eqprev);
+    if (run_flags == 0 && out.idx == nullptr) {
+      // no ties: rank - 1 is the sorted position, so Y[rows[p]] = sorted_x[p]
+      PlaceBuffers pb;
+      pb.rows[0] = sb.vals[buf];
+      pb.vals[0] = (double*)sb.keys[buf ^ 1];
+      pb.rows[1] = sb.vals[buf ^ 1];
+      pb.vals[1] = (double*)sb.keys[buf];
+      pb.counts = sb.counts;
+      pb.partials = sb.partials;
+      pb.status = sb.status;
+      pb.bases = sb.bases;
+      st = place_by_row(sb.vals[buf ^ 1], out.sorted_src, n, out.y, out.y_rs, pb, s);
+      if (st) return st;
+      continue;
+    }
+    if (!(run_flags & 1)) {
+      st = rank_finish(kModeGather, nullptr, sb.vals[buf ^ 1], n, tb, out, s, eqprev);
       if (st) return st;
       continue;
     }

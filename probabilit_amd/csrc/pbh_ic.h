@@ -55,10 +55,11 @@ size_t code_map_bytes();
 // Host: fill base / scale for N(0, 1)-shaped data into the host buffers.
 void code_map_host(uint32_t* base, double* scale, double* x0, double* w);
 int make_codes(const double* x, int64_t n, const CodeMap& cm, uint32_t* codes, hipStream_t s);
-// Order every run of equal codes (length <= 16) by the full value x[row] and flag exact
-// ties in eqprev; sets *long_flag when a run is longer (caller falls back to 64-bit keys).
-int resolve_code_runs(const uint32_t* codes, uint32_t* rows, const double* x, int64_t n, uint8_t* eqprev,
-                      int32_t* long_flag, hipStream_t s);
+// rows_out = rows with every run of equal codes (length <= 16) ordered by the full value
+// x[row]; eqprev[i] = element i equals element i - 1.  *flags |= 1 when a run is longer
+// (the caller falls back to 64-bit keys), |= 2 when any exact tie exists.
+int resolve_code_runs(const uint32_t* codes, const uint32_t* rows, uint32_t* rows_out, const double* x, int64_t n,
+                      uint8_t* eqprev, int32_t* flags, hipStream_t s);
 
 // Column sums (k columns of length n, column stride ld) into sums[k] (device), fixed order.
 int column_means(const double* S, int64_t n, int k, int64_t ld, double* partial, double* means, hipStream_t s);

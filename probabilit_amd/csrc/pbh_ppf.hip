@@ -201,9 +201,14 @@ __global__ __launch_bounds__(kBlock) void k_perm_scores(uint64_t seed, int64_t n
   }
 }
 
-__global__ void k_gamma_guide(double a, double z0, double h, int m, double* y, double* dy) {
+__global__ void k_gamma_guide(double a, sf::GammaGuide T, double* y, double* d1, double* d2) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < m) sf::gamma_guide_entry(a, z0 + j * h, &y[j], &dy[j]);
+  if (j < T.m) sf::gamma_guide_entry(a, T.z0 + j * T.h, &y[j], &d1[j], &d2[j]);
+}
+
+__global__ void k_gamma_guide_check(double a, sf::GammaGuide T, double* ok) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < T.m) ok[j] = (j < T.m - 1) ? sf::gamma_guide_check(a, T, j) : 0.0;
 }
 
 __global__ void k_poisson_table(double mu, int64_t k_lo, int64_t len, double* cdf) {
@@ -340,13 +345,17 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
     const double a = params[0].value;
     const double z0 = sf::kGammaGuideZ0, h = sf::kGammaGuideH;
     const int m = sf::kGammaGuideM;
-    PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)2 * m * sizeof(double), s));
-    hipLaunchKernelGGL(k_gamma_guide, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a, z0, h, m, *table,
-                       *table + m);
+    PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)4 * m * sizeof(double), s));
+    double* tb = *table;
+    sf::GammaGuide T{tb, tb + m, tb + 2 * m, tb + 3 * m, m, z0, h, 1.0 / h};
+    const unsigned g = (unsigned)((m + 63) / 64);
+    hipLaunchKernelGGL(k_gamma_guide, dim3(g), dim3(64), 0, s, a, T, tb, tb + m, tb + 2 * m);
+    PBH_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_gamma_guide_check, dim3(g), dim3(64), 0, s, a, T, tb + 3 * m);
     PBH_CHECK_LAUNCH();
     pt.has_gamma = 1;
     pt.aux = sf::gamma_aux(a);
-    pt.guide = sf::GammaGuide{*table, *table + m, m, z0, h, 1.0 / h};
+    pt.guide = T;
   }
   if (dist == PBH_DIST_POISSON && params[0].ptr == nullptr) {
     double mu = params[0].value;

@@ -22,6 +22,8 @@ struct SortBuffers {
   uint32_t* partials;  // scan partials
   uint32_t* hist;      // 8 * 256 digit histogram
   uint32_t* hist_host; // pinned host mirror of hist (8 * 256)
+  uint64_t* status;    // one-sweep look-back words (256 * ntiles) + tile counter
+  uint32_t* bases;     // one-sweep global digit bases (8 * 256)
 };
 
 constexpr int kSortThreads = 256;
@@ -42,5 +44,23 @@ void sort_carve(void* ws, int64_t n, SortBuffers& b);
 int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf);
 // The same on uint32 keys stored in b.keys[0] (reinterpreted): at most 4 passes.
 int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf);
+
+// Y[rows[p] * y_rs] = v[p] for a permutation `rows` of [0, n): the inverse-permutation write
+// of Iman-Conover step 4 (correlation.py:423) without random 8-byte stores.  LSD bucket passes
+// on row >> kPlaceShift (the stable scatter above, payload = value) bring every block of
+// kPlaceRows consecutive rows together; k_place then assembles each block in LDS and writes it
+// out as one contiguous run.  rows/vals: two ping-pong staging pairs of n entries each.
+constexpr int kPlaceShift = 13;
+constexpr int kPlaceRows = 1 << kPlaceShift;  // 8192 rows = 64 KB of LDS per block
+struct PlaceBuffers {
+  uint32_t* rows[2];
+  double* vals[2];
+  uint32_t* counts;    // 256 * sort_tiles(n)
+  uint32_t* partials;  // scan partials
+  uint64_t* status;    // one-sweep look-back words
+  uint32_t* bases;     // 256 digit bases
+};
+int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, int64_t y_rs, const PlaceBuffers& pb,
+                 hipStream_t s);
 
 }  // namespace pbh

@@ -1,3 +1,6 @@
+#include <stdlib.h>
+#include <string.h>
+
 #include "pbh_error.h"
 #include "pbh_sort.h"
 #include "pbh_timing.h"
@@ -130,12 +133,12 @@ int exclusive_scan_u32(uint32_t* a, int64_t m, uint32_t* partials, hipStream_t s
 }
 
 // ------------------------------------------------------------------ stable scatter
-template <typename K>
-__global__ __launch_bounds__(T) void k_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                              K* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n,
+template <typename K, typename V = uint32_t>
+__global__ __launch_bounds__(T) void k_scatter(const K* __restrict__ kin, const V* __restrict__ vin,
+                                              K* __restrict__ kout, V* __restrict__ vout, int64_t n,
                                               int shift, const uint32_t* __restrict__ offsets, int64_t ntiles) {
   __shared__ K skeys[TILE];
-  __shared__ uint32_t svals[TILE];
+  __shared__ V svals[TILE];
   __shared__ uint32_t run[256];
   __shared__ uint32_t chunk[2][4][256];  // double-buffered by item parity
   __shared__ uint32_t dstart[256 + 8];
@@ -147,14 +150,11 @@ __global__ __launch_bounds__(T) void k_scatter(const K* __restrict__ kin, const 
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
   K key[IPT];
-  uint32_t val[IPT];
   uint32_t rank[IPT];
 #pragma unroll
   for (int j = 0; j < IPT; ++j) {
     int64_t i = base + j * T + t;
-    bool valid = i < n;
-    key[j] = valid ? kin[i] : (K)0;
-    val[j] = valid ? (vin ? vin[i] : (uint32_t)i) : 0u;
+    key[j] = i < n ? kin[i] : (K)0;
   }
   run[t] = 0;
 #pragma unroll
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(T) void k_scatter(const K* __restrict__ kin, const 
       uint32_t d = (uint32_t)(key[j] >> shift) & 255u;
       uint32_t lp = dstart[d] + rank[j];
       skeys[lp] = key[j];
-      svals[lp] = val[j];
+      svals[lp] = vin ? vin[i] : (V)i;  // NULL payload: the identity (row index)
     }
   }
   __syncthreads();
@@ -216,7 +216,227 @@ __global__ __launch_bounds__(T) void k_scatter(const K* __restrict__ kin, const 
   }
 }
 
+// ------------------------------------------------------------------ one-sweep scatter
+// One launch per digit pass, no upsweep / scan: every tile ranks its keys per wave (one
+// wave-private digit counter array, no block barrier inside the ranking loop), publishes its
+// digit counts, and finds the count of each digit in all earlier tiles by decoupled
+// look-back over the published (flag | count) words (Merrill & Garland's single-pass scan,
+// as in Adinets & Merrill's Onesweep).  Global digit bases come from the one up-front
+// histogram.  Tile ids are taken from an atomic counter, so a tile only ever waits on tiles
+// that started before it: the look-back always terminates.
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62, kCountMask = (1ull << 62) - 1;
+
+template <typename K, typename V>
+__global__ __launch_bounds__(T) void k_onesweep(const K* __restrict__ kin, const V* __restrict__ vin,
+                                               K* __restrict__ kout, V* __restrict__ vout, int64_t n, int shift,
+                                               const uint32_t* __restrict__ digit_base, uint64_t* status,
+                                               uint32_t* tile_counter) {
+  __shared__ K skeys[TILE];
+  __shared__ V svals[TILE];
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t dstart[256 + 8];
+  __shared__ int64_t gbase[256];
+  __shared__ uint32_t tile_sh;
+
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) tile_sh = atomicAdd(tile_counter, 1u);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wcnt[w][lane + 64 * q] = 0;
+  __syncthreads();
+  const int64_t tile = tile_sh;
+  const int64_t base = tile * TILE;
+  const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  // wave w owns tile positions [w * 1024, (w + 1) * 1024), item-major: j * 64 + lane
+  K key[IPT];
+  V val[IPT];
+  uint32_t rank[IPT];
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    const int64_t i = base + w * (IPT * 64) + j * 64 + lane;
+    const bool valid = i < n;
+    key[j] = valid ? kin[i] : (K)0;
+    val[j] = valid ? (vin ? vin[i] : (V)i) : (V)0;
+  }
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    const int64_t i = base + w * (IPT * 64) + j * 64 + lane;
+    const bool valid = i < n;
+    const uint32_t d = (uint32_t)(key[j] >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bb = __ballot(valid && ((d >> b) & 1u));
+      peers &= ((d >> b) & 1u) ? bb : ~bb;
+    }
+    const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt);
+    const uint32_t c = valid ? wcnt[w][d] : 0u;
+    rank[j] = c + below;
+    if (valid && below == 0) wcnt[w][d] = c + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // thread t = digit t
+  const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+  const uint32_t tot = c0 + c1 + c2 + c3;
+  uint64_t* my = status + tile * 256 + t;
+  if (tile == 0)
+    __hip_atomic_store(my, kFlagInc | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    __hip_atomic_store(my, kFlagAgg | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t ex = block_exclusive_scan_256(tot, dstart, nullptr);
+  uint64_t excl = 0;
+  if (tile > 0) {
+    int64_t tp = tile - 1;
+    uint32_t spins = 0;
+    while (true) {
+      const uint64_t sv = __hip_atomic_load(status + tp * 256 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t flag = sv & ~kCountMask;
+      if (flag == 0) {  // tile tp has not published yet
+        if (++spins > (1u << 26)) {  // cannot happen (see above); never hang the device on a bug
+          atomicOr(tile_counter + 1, 1u);
+          break;
+        }
+        continue;
+      }
+      excl += sv & kCountMask;
+      if (flag == kFlagInc) break;
+      --tp;
+    }
+    __hip_atomic_store(my, kFlagInc | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  dstart[t] = ex;
+  wcnt[0][t] = 0;
+  wcnt[1][t] = c0;
+  wcnt[2][t] = c0 + c1;
+  wcnt[3][t] = c0 + c1 + c2;
+  gbase[t] = (int64_t)digit_base[t] + (int64_t)excl - (int64_t)ex;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    const int64_t i = base + w * (IPT * 64) + j * 64 + lane;
+    if (i < n) {
+      const uint32_t d = (uint32_t)(key[j] >> shift) & 255u;
+      const uint32_t lp = dstart[d] + wcnt[w][d] + rank[j];
+      skeys[lp] = key[j];
+      svals[lp] = val[j];
+    }
+  }
+  __syncthreads();
+  const int cnt = (int)((n - base) < TILE ? (n - base) : TILE);
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    const int p = j * T + t;
+    if (p < cnt) {
+      const K k = skeys[p];
+      const uint32_t d = (uint32_t)(k >> shift) & 255u;
+      const int64_t o = gbase[d] + p;
+      kout[o] = k;
+      vout[o] = svals[p];
+    }
+  }
+}
+
+// bases[p * 256 + d] = exclusive scan over digits of hist[p * 256 + d], for np byte positions
+__global__ __launch_bounds__(256) void k_digit_bases(const uint32_t* __restrict__ hist, uint32_t* __restrict__ bases) {
+  __shared__ uint32_t sh[264];
+  const uint32_t v = hist[blockIdx.x * 256 + threadIdx.x];
+  bases[blockIdx.x * 256 + threadIdx.x] = block_exclusive_scan_256(v, sh, nullptr);
+}
+
+// digit bases of the row keys of place_by_row: rows are a permutation of [0, n), so digit d at
+// `shift` counts the rows r < n with (r >> shift) & 255 == d, in closed form.
+__global__ __launch_bounds__(256) void k_place_bases(int64_t n, int shift, uint32_t* __restrict__ bases) {
+  __shared__ uint32_t sh[264];
+  const uint32_t d = threadIdx.x;
+  const int64_t span = (int64_t)1 << shift;
+  uint64_t count = 0;
+  for (int64_t h = 0;; ++h) {
+    const int64_t lo = ((h << 8) + d) << shift;
+    if (lo >= n) break;
+    count += (uint64_t)((n - lo) < span ? (n - lo) : span);
+  }
+  bases[d] = block_exclusive_scan_256((uint32_t)count, sh, nullptr);
+}
+
+bool onesweep_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PBH_SORT");
+    return !(e && strcmp(e, "classic") == 0);
+  }();
+  return on;
+}
+
+// ------------------------------------------------------------------ row placement
+// Bucket b = rows [b * kPlaceRows, (b + 1) * kPlaceRows).  Because `rows` is a permutation,
+// after the bucket passes bucket b occupies exactly positions [b * kPlaceRows, ...) of the
+// staging arrays; one workgroup assembles its bucket in LDS and writes it out contiguously.
+__global__ __launch_bounds__(T) void k_place(const uint32_t* __restrict__ rows, const double* __restrict__ v,
+                                            int64_t n, double* __restrict__ y, int64_t y_rs) {
+  __shared__ double buf[kPlaceRows];
+  const int64_t r0 = (int64_t)blockIdx.x * kPlaceRows;
+  const int cnt = (int)((n - r0) < kPlaceRows ? (n - r0) : kPlaceRows);
+  for (int p = threadIdx.x; p < cnt; p += T) buf[rows[r0 + p] - (uint32_t)r0] = v[r0 + p];
+  __syncthreads();
+  if (y_rs == 1) {
+    for (int p = threadIdx.x; p < cnt; p += T) y[r0 + p] = buf[p];
+  } else {
+    for (int p = threadIdx.x; p < cnt; p += T) y[(r0 + p) * y_rs] = buf[p];
+  }
+}
+
 }  // namespace
+
+int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, int64_t y_rs, const PlaceBuffers& pb,
+                 hipStream_t s) {
+  PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "place_by_row: n out of range");
+  int bits = 0;
+  while (((int64_t)1 << bits) < n) ++bits;
+  const int64_t nt = sort_tiles(n);
+  const uint32_t* rin = rows;
+  const double* vin = v;
+  int cur = 0;
+  for (int shift = kPlaceShift; shift < bits; shift += 8) {
+    if (onesweep_enabled()) {
+      hipLaunchKernelGGL(k_place_bases, dim3(1), dim3(256), 0, s, n, shift, pb.bases);
+      PBH_CHECK_LAUNCH();
+      PBH_CHECK_HIP(hipMemsetAsync(pb.status, 0, (size_t)nt * 256 * 8 + 256, s));  // words, counter, flag
+      PBH_TIMED(kKPlaceScatter, s,
+                hipLaunchKernelGGL((k_onesweep<uint32_t, double>), dim3((unsigned)nt), dim3(T), 0, s, rin, vin,
+                                   pb.rows[cur], pb.vals[cur], n, shift, pb.bases, pb.status,
+                                   (uint32_t*)(pb.status + nt * 256)));
+      PBH_CHECK_LAUNCH();
+      rin = pb.rows[cur];
+      vin = pb.vals[cur];
+      cur ^= 1;
+      continue;
+    }
+    PBH_TIMED(kKPlaceUpsweep, s,
+              hipLaunchKernelGGL(k_upsweep<uint32_t>, dim3((unsigned)nt), dim3(T), 0, s, rin, n, shift, pb.counts, nt));
+    PBH_CHECK_LAUNCH();
+    int st = exclusive_scan_u32(pb.counts, 256 * nt, pb.partials, s);
+    if (st != PBH_OK) return st;
+    PBH_TIMED(kKPlaceScatter, s,
+              hipLaunchKernelGGL((k_scatter<uint32_t, double>), dim3((unsigned)nt), dim3(T), 0, s, rin, vin,
+                                 pb.rows[cur], pb.vals[cur], n, shift, pb.counts, nt));
+    PBH_CHECK_LAUNCH();
+    rin = pb.rows[cur];
+    vin = pb.vals[cur];
+    cur ^= 1;
+  }
+  const int64_t nb = (n + kPlaceRows - 1) / kPlaceRows;
+  PBH_TIMED(kKPlace, s, hipLaunchKernelGGL(k_place, dim3((unsigned)nb), dim3(T), 0, s, rin, vin, n, y, y_rs));
+  PBH_CHECK_LAUNCH();
+  if (onesweep_enabled() && bits > kPlaceShift) {
+    uint32_t stuck = 0;
+    PBH_CHECK_HIP(hipMemcpyAsync(&stuck, (uint32_t*)(pb.status + nt * 256) + 1, 4, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+    if (stuck) {
+      set_error("row placement: one-sweep look-back did not complete");
+      return PBH_ERR_HIP;
+    }
+  }
+  return PBH_OK;
+}
 
 size_t sort_workspace_bytes(int64_t n) {
   int64_t nt = sort_tiles(n);
@@ -230,6 +450,8 @@ size_t sort_workspace_bytes(int64_t n) {
   add((size_t)m * 4);
   add((size_t)scan_partials_count(m) * 4);
   add(8 * 256 * 4);
+  add((size_t)m * 8 + 256);  // one-sweep status words + tile counter
+  add(8 * 256 * 4);          // digit bases
   return b;
 }
 
@@ -249,6 +471,8 @@ void sort_carve(void* ws, int64_t n, SortBuffers& sb) {
   sb.counts = (uint32_t*)take((size_t)m * 4);
   sb.partials = (uint32_t*)take((size_t)scan_partials_count(m) * 4);
   sb.hist = (uint32_t*)take(8 * 256 * 4);
+  sb.status = (uint64_t*)take((size_t)m * 8 + 256);
+  sb.bases = (uint32_t*)take(8 * 256 * 4);
 }
 
 template <typename K>
@@ -272,6 +496,30 @@ int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
   }
   if (npass == 0) passes[npass++] = 0;  // all keys equal: one pass yields the identity payload
   int cur = 0;
+  if (onesweep_enabled()) {
+    hipLaunchKernelGGL(k_digit_bases, dim3(NB), dim3(256), 0, s, b.hist, b.bases);
+    PBH_CHECK_LAUNCH();
+    PBH_CHECK_HIP(hipMemsetAsync(b.status + nt * 256, 0, 256, s));  // tile counter + stuck flag
+    for (int ip = 0; ip < npass; ++ip) {
+      const int shift = 8 * passes[ip];
+      PBH_CHECK_HIP(hipMemsetAsync(b.status, 0, (size_t)nt * 256 * 8 + 4, s));  // words + tile counter
+      PBH_TIMED(NB == 8 ? kKSortScatter : kKSortScatter32, s,
+                hipLaunchKernelGGL((k_onesweep<K, uint32_t>), dim3((unsigned)nt), dim3(T), 0, s, keys[cur],
+                                   ip == 0 ? nullptr : b.vals[cur], keys[cur ^ 1], b.vals[cur ^ 1], n, shift,
+                                   b.bases + passes[ip] * 256, b.status, (uint32_t*)(b.status + nt * 256)));
+      PBH_CHECK_LAUNCH();
+      cur ^= 1;
+    }
+    uint32_t stuck = 0;
+    PBH_CHECK_HIP(hipMemcpyAsync(&stuck, (uint32_t*)(b.status + nt * 256) + 1, 4, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+    if (stuck) {
+      set_error("radix sort: one-sweep look-back did not complete");
+      return PBH_ERR_HIP;
+    }
+    *out_buf = cur;
+    return PBH_OK;
+  }
   for (int ip = 0; ip < npass; ++ip) {
     const int shift = 8 * passes[ip];
     PBH_TIMED(NB == 8 ? kKSortUpsweep : kKSortUpsweep32, s,

@@ -27,6 +27,9 @@ enum KernelId {
   kKSortScatter32,
   kKSortUpsweep32,
   kKSortDigitHist32,
+  kKPlaceUpsweep,
+  kKPlaceScatter,
+  kKPlace,
   kKCount
 };
 

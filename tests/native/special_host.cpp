@@ -25,11 +25,24 @@ void sfh_pdtr(const double* k, double mu, long n, double* out) {
 // gamma ppf through the scalar-shape guide table, exactly as the device kernels use it.
 void sfh_igami_guided(double a, const double* p, long n, double* out) {
   const int m = sf::kGammaGuideM;
-  std::vector<double> y(m), dy(m);
-  for (int j = 0; j < m; ++j) sf::gamma_guide_entry(a, sf::kGammaGuideZ0 + j * sf::kGammaGuideH, &y[j], &dy[j]);
-  sf::GammaGuide T{y.data(), dy.data(), m, sf::kGammaGuideZ0, sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
+  std::vector<double> tb(4 * (size_t)m);
+  sf::GammaGuide T{tb.data(), tb.data() + m, tb.data() + 2 * m, tb.data() + 3 * m, m, sf::kGammaGuideZ0,
+                   sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
+  for (int j = 0; j < m; ++j) sf::gamma_guide_entry(a, T.z0 + j * T.h, &tb[j], &tb[m + j], &tb[2 * m + j]);
+  for (int j = 0; j < m; ++j) tb[3 * m + j] = j < m - 1 ? sf::gamma_guide_check(a, T, j) : 0.0;
   sf::GammaAux aux = sf::gamma_aux(a);
   for (long i = 0; i < n; ++i) out[i] = sf::igami_guided(a, p[i], &aux, T);
 }
 
+// fraction of guide intervals that passed the midpoint check
+double sfh_guide_ok_fraction(double a) {
+  const int m = sf::kGammaGuideM;
+  std::vector<double> tb(4 * (size_t)m);
+  sf::GammaGuide T{tb.data(), tb.data() + m, tb.data() + 2 * m, tb.data() + 3 * m, m, sf::kGammaGuideZ0,
+                   sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
+  for (int j = 0; j < m; ++j) sf::gamma_guide_entry(a, T.z0 + j * T.h, &tb[j], &tb[m + j], &tb[2 * m + j]);
+  int ok = 0;
+  for (int j = 0; j < m - 1; ++j) ok += sf::gamma_guide_check(a, T, j) != 0.0;
+  return (double)ok / (m - 1);
+}
 }

@@ -73,6 +73,21 @@ def test_ic_vs_oracle_bit_exact_indices(gpu, n, k):
     assert_close(S, ref["S"], rtol=1e-14, atol=1e-300, what="scores")
 
 
+@pytest.mark.parametrize("n,k", [(8_192, 2), (3_000_017, 4)])
+def test_ic_outputs_vs_oracle_placement_path(gpu, n, k):
+    """Y without the debug outputs (the production step 4: 32-bit code sort, run fix-up and
+    the LDS row placement with 0 / 2 bucket passes) equals the oracle's Y exactly."""
+    from oracle import ic as oic
+    from oracle.pipeline import cfg3_corr, cfg_dists, lhs_quantiles, ppf_columns
+    from probabilit_amd.correlation import ImanConover
+
+    X = ppf_columns(lhs_quantiles(n, k, 5), cfg_dists(k))
+    C = cfg3_corr(k)
+    ref = oic.iman_conover(X, C)
+    Y = ImanConover().set_target(C)(X)
+    np.testing.assert_array_equal(Y, ref["Y"])
+
+
 def test_ic_properties_large(gpu):
     """N = 4M, K = 32: marginals preserved exactly, rank correlation near the target."""
     import torch

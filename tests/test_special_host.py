@@ -90,3 +90,12 @@ def _pdtr(lib, k, mu):
     P = ctypes.c_void_p
     lib.sfh_pdtr(P(k.ctypes.data), ctypes.c_double(mu), ctypes.c_long(k.size), P(out.ctypes.data))
     return out
+
+
+@pytest.mark.parametrize("a,floor", [(0.05, 0.75), (0.1, 0.9), (0.7, 0.99), (2.0, 0.99), (45.0, 0.99), (1e4, 0.99)])
+def test_guide_table_mostly_interpolates(sfh, a, floor):
+    """The quintic guide must cover (nearly) the whole grid; otherwise the Halley fallback
+    silently carries the cost.  For small a the lower grid maps to x below 1e-290 (x ~ p^(1/a)),
+    which is deliberately left to igami."""
+    sfh.sfh_guide_ok_fraction.restype = ctypes.c_double
+    assert sfh.sfh_guide_ok_fraction(ctypes.c_double(a)) >= floor
