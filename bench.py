@@ -8,8 +8,10 @@ triang / poisson x 4, BASELINE config 2 set), then the Iman-Conover reorder of a
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n ROWS] [--d COLS] [--cpu-n ROWS]
 
-With N > 1 (torch.distributed.run, one process per GPU) every rank runs its own full N-row
-problem on its own seed (replicas; weak scaling) -- see DESIGN.md "Multi-GPU".
+With N > 1 (torch.distributed.run, one process per GPU, RCCL) the same N-row problem is
+row-sharded across the ranks (BASELINE config 4; strong scaling): rank r generates and
+scores rows [N r / R, N (r + 1) / R), the Gram matrix is all-reduced, and the step-4 rank
+of each column runs on its owner between two all-to-alls (probabilit_amd/distributed.py).
 Prints ONE JSON line on rank 0.
 """
 
@@ -63,7 +65,8 @@ def main():
         import torch.distributed as dist
 
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        dist.init_process_group("nccl")
+        # RCCL; PBH_DIST_BACKEND=gloo rehearses the sharded path with several ranks on one GPU
+        dist.init_process_group(os.environ.get("PBH_DIST_BACKEND", "nccl"))
     else:
         dist = None
 
@@ -80,10 +83,10 @@ def main():
     C = 0.9 * np.corrcoef(A, rowvar=False) + 0.1 * np.eye(d)
     ds = [Distribution(name, **kw) for name, kw in dists]
     root = NoOp(*ds).correlate(*ds, corr_mat=C)
-    seed = args.seed + 1000 * rank
+    group = dist.group.WORLD if dist is not None else None
 
     def step(i):
-        root.sample_device(n, random_state=seed + i, method="lhs")
+        root.sample_device(n, random_state=args.seed + i, method="lhs", group=group)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -108,7 +111,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
-    value = n * d * world / (ms_per_step / 1e3) / 1e6
+    value = n * d / (ms_per_step / 1e3) / 1e6  # the whole job: N x d draws per step
 
     # per-kernel device time inside the timed region (HIP events on the launching stream)
     import ctypes
@@ -137,10 +140,14 @@ def main():
     if rank == 0:
         line = {"metric": "Msamples/s (N x d draws), LHS + ImanConover d=32", "value": round(value, 2),
                 "unit": "Msamples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+                "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+                "scaling": "strong" if world > 1 else "weak",
                 "vs_baseline": None, "dtype": "f64", "data": "synthetic (native LHS quantiles, seeded)",
-                "config": {"workload": "cfg3: d=32 (cfg2 set x4), LHS + ppf + ImanConover, N rows per GPU",
-                           "rows_per_gpu": n, "d": d, "parallelism": "replicas" if world > 1 else "single"},
+                "config": {"workload": ("cfg4: " if world > 1 else "cfg3: ") +
+                                       "d=32 (cfg2 set x4), LHS + ppf + ImanConover, N rows",
+                           "rows": n, "d": d,
+                           "parallelism": f"row-sharded x{world} (RCCL all-reduce + all-to-all)" if world > 1
+                           else "single"},
                 "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels}
         print(json.dumps(line))
     if dist is not None:

@@ -140,6 +140,55 @@ typedef struct pbh_ic_args {
 int pbh_ic_workspace_size(int64_t n, int32_t k, size_t* bytes);
 int pbh_iman_conover(const pbh_ic_args* args, void* stream);
 
+/* ---------------------------------------------------------------- Iman-Conover phases
+ * The four steps of pbh_iman_conover as separate calls, for row-sharded execution across
+ * GPUs (probabilit_amd/distributed.py): every rank holds rows
+ * [row0, row0 + nrows) of the N-row problem, sums its Gram partials with the other ranks
+ * (one K x K all-reduce), and each column's step 4 runs on the rank that owns the column. */
+
+/* Sorted values of a generated LHS column for the strata [t0, t0 + nt) (t = rank - 1 of the
+ * point in its column): out[t - t0] = ppf((t + 1 - u) / n).  params_host: the scalar
+ * parameters in pbh_dist order.  This is np.sort(X[:, k]) of correlation.py:423 for a
+ * column the DAG generates (modeling.py:480, 488 + 807). */
+int pbh_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist,
+                       const double* params_host, int nparams, double* out, int32_t* nonfinite_flag,
+                       void* stream);
+/* Adjacent-pair check of a column: *ties = #(x[t] == x[t+1]), *inversions = #!(x[t] <= x[t+1]).
+ * ws: 256 bytes of device memory.  Synchronises the stream. */
+int pbh_sorted_check(const double* x, int64_t n, int64_t* ties, int64_t* inversions, void* ws, void* stream);
+/* Run heads of a sorted segment x[0..m) = strata [t0, t0 + m): the positions whose value
+ * differs from the previous one (scipy _rankdata's `obs` flags, reached from
+ * correlation.py:394).  With first_is_prev, x[0] is the value of stratum t0 - 1 and is not
+ * itself reported.  heads (device, u32) receive t values in order; *count their number. */
+int pbh_run_heads_workspace_size(int64_t m, size_t* bytes);
+int pbh_run_heads(const double* x, int64_t m, int64_t t0, int first_is_prev, uint32_t* heads, int64_t* count,
+                  void* ws, size_t ws_bytes, void* stream);
+/* Step 1 for rows [row0, row0 + nrows) of a generated LHS column (correlation.py:394-395):
+ * S[r - row0] = ndtri(rank / (N + 1)), rank = pi(r) + 1, or the 'average' rank of the run of
+ * stratum pi(r) when heads (all run heads of the sorted column, heads[0] == 0) is given. */
+int pbh_lhs_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, const uint32_t* heads,
+                   int64_t nheads, double* S, void* stream);
+/* Step 2 pieces (correlation.py:398): column sums and the centered Gram matrix sum over rows
+ * (S - means)^T (S - means) of a column-major block S (column stride ld); K x K row-major. */
+int pbh_gram_workspace_size(int32_t k, size_t* bytes);
+int pbh_column_sums(const double* S, int64_t n, int32_t k, int64_t ld, double* sums, void* ws, size_t ws_bytes,
+                    void* stream);
+int pbh_centered_gram(const double* S, int64_t n, int32_t k, int64_t ld, const double* means, double* gram,
+                      void* ws, size_t ws_bytes, void* stream);
+/* Host: E = corrcoef from the summed Gram matrix over n rows (np.cov / np.corrcoef order),
+ * the positive-definiteness check and L = cholesky(E) (correlation.py:398-405).  Returns
+ * PBH_ERR_NOT_PD with the reference's message. */
+int pbh_ic_factor(const double* gram_host, int64_t n, int32_t k, double* corr_host_out, double* L_host_out);
+/* Step 3 in place (correlation.py:409-414): S <- (S L^-T) P^T, P = cholesky(target).
+ * ws >= (2 K^2 + K) doubles of device memory. */
+int pbh_ic_apply(double* S, int64_t n, int32_t k, int64_t ld, const double* L_host, const double* target_chol_host,
+                 void* ws, size_t ws_bytes, void* stream);
+/* Step 4 for one column (correlation.py:418-423): y[r * y_rs] = sorted_src[rank(cs[r]) - 1],
+ * idx_out[r] = rank - 1 (optional). */
+int pbh_ic_reorder_workspace_size(int64_t n, size_t* bytes);
+int pbh_ic_reorder(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx_out,
+                   void* ws, size_t ws_bytes, void* stream);
+
 /* rankdata(x, method='average') of one device column (scipy:stats/_stats_py.py _rankdata,
  * called at correlation.py:394 and :422).  ws >= pbh_rank_workspace_size(n). */
 int pbh_rank_workspace_size(int64_t n, size_t* bytes);

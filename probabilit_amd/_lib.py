@@ -34,7 +34,10 @@ OPS["cast"] = 63
 SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fill_uniform", "pbh_fill_sobol",
            "pbh_ppf", "pbh_lhs_ppf", "pbh_ic_workspace_size", "pbh_iman_conover", "pbh_rank_workspace_size",
            "pbh_rankdata_average", "pbh_elementwise", "pbh_average", "pbh_transpose", "pbh_timing_enable",
-           "pbh_timing_reset", "pbh_kernel_name", "pbh_timing_read"]
+           "pbh_timing_reset", "pbh_kernel_name", "pbh_timing_read", "pbh_lhs_sorted_ppf", "pbh_sorted_check",
+           "pbh_run_heads_workspace_size", "pbh_run_heads", "pbh_lhs_scores", "pbh_gram_workspace_size",
+           "pbh_column_sums", "pbh_centered_gram", "pbh_ic_factor", "pbh_ic_apply", "pbh_ic_reorder_workspace_size",
+           "pbh_ic_reorder"]
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
@@ -108,6 +111,18 @@ def load():
         "pbh_timing_reset": ([], i32),
         "pbh_kernel_name": ([i32], ctypes.c_char_p),
         "pbh_timing_read": ([i32, ctypes.POINTER(dbl), ctypes.POINTER(i64)], i32),
+        "pbh_lhs_sorted_ppf": ([u64, i64, i64, i64, i32, i32, vp, i32, vp, vp, vp], i32),
+        "pbh_sorted_check": ([vp, i64, ctypes.POINTER(i64), ctypes.POINTER(i64), vp, vp], i32),
+        "pbh_run_heads_workspace_size": ([i64, ctypes.POINTER(sz)], i32),
+        "pbh_run_heads": ([vp, i64, i64, i32, vp, ctypes.POINTER(i64), vp, sz, vp], i32),
+        "pbh_lhs_scores": ([u64, i64, i32, i64, i64, vp, i64, vp, vp], i32),
+        "pbh_gram_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
+        "pbh_column_sums": ([vp, i64, ctypes.c_int32, i64, vp, vp, sz, vp], i32),
+        "pbh_centered_gram": ([vp, i64, ctypes.c_int32, i64, vp, vp, vp, sz, vp], i32),
+        "pbh_ic_factor": ([vp, i64, ctypes.c_int32, vp, vp], i32),
+        "pbh_ic_apply": ([vp, i64, ctypes.c_int32, i64, vp, vp, vp, sz, vp], i32),
+        "pbh_ic_reorder_workspace_size": ([i64, ctypes.POINTER(sz)], i32),
+        "pbh_ic_reorder": ([vp, i64, vp, vp, i64, vp, vp, sz, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

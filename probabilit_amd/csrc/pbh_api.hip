@@ -40,15 +40,12 @@ struct Carver {
   }
 };
 
-size_t small_bytes(int k) { return 4 * (((size_t)k * k * 8 + 255) & ~(size_t)255) + 2 * 256 + 4096; }
-
-size_t ic_bytes(int64_t n, int k, bool carve, void* base, struct IcLayout* out);
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 struct IcLayout {
   double* S;
   double* sorted_x;
-  void* sort_ws;
-  void* tie_ws;
+  void* reorder_ws;             // step 4 (its sort / tie buffers also serve step 1's sorts)
   double* partials;
   double* means;
   double* gram;
@@ -56,45 +53,16 @@ struct IcLayout {
   double* inv_diag;
   double* P;
   int32_t* flag;
-  double* tmp;                  // n doubles: tied-column average ranks / fallback X column
+  double* tmp;                  // n doubles: fallback X column, or the run heads (u32) of a tied column
   unsigned long long* counts;   // ties, inversions of a generated sorted column
-  void* codemap;                // CodeMap base[] / scale[] (step 4)
+  void* heads_ws;
 };
-
-// Host tables of the step-4 code map, built once; uploaded into the workspace per call.
-CodeMap upload_code_map(void* dev, hipStream_t s, int* st) {
-  struct Host {
-    std::vector<uint32_t> base;
-    std::vector<double> scale;
-    double x0 = 0, w = 0;
-    Host() : base(kCodeSegments + 1), scale(kCodeSegments) { code_map_host(base.data(), scale.data(), &x0, &w); }
-  };
-  static const Host h;
-  const size_t base_bytes = ((kCodeSegments + 1) * 4 + 255) / 256 * 256;
-  CodeMap cm;
-  cm.x0 = h.x0;
-  cm.w = h.w;
-  cm.inv_w = 1.0 / h.w;
-  cm.m = kCodeSegments;
-  cm.base = (const uint32_t*)dev;
-  cm.scale = (const double*)((char*)dev + base_bytes);
-  *st = PBH_OK;
-  hipError_t e = hipMemcpyAsync(dev, h.base.data(), (kCodeSegments + 1) * 4, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync((char*)dev + base_bytes, h.scale.data(), kCodeSegments * 8, hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) {
-    set_error("code map upload: %s", hipGetErrorString(e));
-    *st = PBH_ERR_HIP;
-  }
-  return cm;
-}
 
 size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   Carver c(base);
   void* S = c.take((size_t)n * k * 8);
   void* sx = c.take((size_t)n * k * 8);
-  void* sws = c.take(sort_workspace_bytes(n));
-  void* tws = c.take(tie_workspace_bytes(n));
+  void* rws = c.take(reorder_ws_bytes(n));
   void* part = c.take(gram_partials_bytes(k));
   void* means = c.take((size_t)k * 8);
   void* gram = c.take((size_t)k * k * 8);
@@ -104,15 +72,11 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* flag = c.take(256);
   void* tmp = c.take((size_t)n * 8);
   void* counts = c.take(256);
-  void* codemap = c.take(code_map_bytes());
+  void* hws = c.take(run_heads_ws_bytes(n));
   if (carve) {
-    L->codemap = codemap;
-    L->tmp = (double*)tmp;
-    L->counts = (unsigned long long*)counts;
     L->S = (double*)S;
     L->sorted_x = (double*)sx;
-    L->sort_ws = sws;
-    L->tie_ws = tws;
+    L->reorder_ws = rws;
     L->partials = (double*)part;
     L->means = (double*)means;
     L->gram = (double*)gram;
@@ -120,27 +84,11 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
     L->inv_diag = (double*)invd;
     L->P = (double*)P;
     L->flag = (int32_t*)flag;
+    L->tmp = (double*)tmp;
+    L->counts = (unsigned long long*)counts;
+    L->heads_ws = hws;
   }
   return c.used;
-}
-
-// Lower Cholesky (Cholesky-Banachiewicz); false when a pivot is not > 0 (np.linalg.cholesky
-// raises LinAlgError there, which _is_positive_definite turns into False).
-bool cholesky_lower(const std::vector<double>& A, int k, std::vector<double>& L) {
-  L.assign((size_t)k * k, 0.0);
-  for (int j = 0; j < k; ++j) {
-    double s = A[(size_t)j * k + j];
-    for (int m = 0; m < j; ++m) s -= L[(size_t)j * k + m] * L[(size_t)j * k + m];
-    if (!(s > 0.0)) return false;
-    double d = sqrt(s);
-    L[(size_t)j * k + j] = d;
-    for (int i = j + 1; i < k; ++i) {
-      double t = A[(size_t)i * k + j];
-      for (int m = 0; m < j; ++m) t -= L[(size_t)i * k + m] * L[(size_t)j * k + m];
-      L[(size_t)i * k + j] = t / d;
-    }
-  }
-  return true;
 }
 
 }  // namespace
@@ -222,13 +170,11 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     return PBH_ERR_WORKSPACE;
   }
   hipStream_t s = as_stream(stream);
-  SortBuffers sb;
-  sort_carve(L.sort_ws, n, sb);
-  TieBuffers tb;
-  tie_carve(L.tie_ws, n, tb);
-  std::vector<uint32_t> hist_host(8 * 256);
-  sb.hist_host = hist_host.data();
-  int st;
+  ReorderWs rw;
+  int st = reorder_carve(L.reorder_ws, n, rw, s);
+  if (st) return st;
+  SortBuffers& sb = rw.sb;
+  TieBuffers& tb = rw.tb;
 
   // ---- step 1: van der Waerden scores of every column (+ the sorted column for step 4)
   PBH_CHECK_HIP(hipMemsetAsync(L.flag, 0, sizeof(int32_t), s));
@@ -242,7 +188,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       const pbh_ic_column& g = a->columns[c];
       pbh_param prm[3];
       for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
-      st = lhs_sorted_ppf(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, sx_c, g.nonfinite_flag, s);
+      st = lhs_sorted_ppf(g.seed, n, 0, n, g.lhs_col, g.dist, prm, g.nparams, sx_c, g.nonfinite_flag, s);
       if (st) return st;
       st = check_sorted(sx_c, n, L.counts, s);
       if (st) return st;
@@ -250,17 +196,14 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       PBH_CHECK_HIP(hipMemcpyAsync(cnt, L.counts, sizeof(cnt), hipMemcpyDeviceToHost, s));
       PBH_CHECK_HIP(hipStreamSynchronize(s));
       if (cnt[1] == 0) {
-        const double* avg = nullptr;
-        if (cnt[0] != 0) {  // ties (discrete ppf): 'average' ranks of the runs, in stratum order
-          st = load_keys(sx_c, 1, n, sb.keys[0], nullptr, s);
+        uint32_t* heads = nullptr;
+        int64_t nheads = 0;
+        if (cnt[0] != 0) {  // ties (discrete ppf): 'average' ranks from the runs of the sorted column
+          heads = (uint32_t*)L.tmp;
+          st = run_heads(sx_c, n, 0, false, heads, &nheads, L.heads_ws, s);
           if (st) return st;
-          RankOut ro = {};
-          ro.ranks = L.tmp;
-          st = rank_finish(kModeRanks, sb.keys[0], nullptr, n, tb, ro, s);
-          if (st) return st;
-          avg = L.tmp;
         }
-        st = perm_scores(g.seed, n, g.lhs_col, avg, S_c, s);
+        st = perm_scores(g.seed, n, g.lhs_col, 0, n, heads, nheads, S_c, s);
         if (st) return st;
         continue;
       }
@@ -291,33 +234,15 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   if (st) return st;
   st = centered_gram(L.S, n, k, n, L.means, L.partials, L.gram, s);
   if (st) return st;
-  std::vector<double> G((size_t)k * k);
+  std::vector<double> G((size_t)k * k), Lc((size_t)k * k);
   PBH_CHECK_HIP(hipMemcpyAsync(G.data(), L.gram, (size_t)k * k * 8, hipMemcpyDeviceToHost, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));
   if (flag_host) {
     set_error("Iman-Conover input contains NaN");
     return PBH_ERR_NONFINITE;
   }
-  // np.cov: c = dot(Xc, Xc^T) * (1 / (N - 1)); np.corrcoef: c /= std[:,None]; c /= std[None,:]; clip
-  const double fact = 1.0 / (double)(n - 1);
-  for (auto& v : G) v *= fact;
-  std::vector<double> sd(k);
-  for (int i = 0; i < k; ++i) sd[i] = sqrt(G[(size_t)i * k + i]);
-  for (int i = 0; i < k; ++i)
-    for (int j = 0; j < k; ++j) {
-      double v = G[(size_t)i * k + j];
-      v /= sd[i];
-      v /= sd[j];
-      G[(size_t)i * k + j] = v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v);
-    }
-  if (a->corr_host_out) memcpy(a->corr_host_out, G.data(), (size_t)k * k * 8);
-  std::vector<double> Lc;
-  if (!cholesky_lower(G, k, Lc)) {
-    set_error(
-        "Rank data correlation not positive definite.There are perfect correlations in the ranked data.Supply more "
-        "data (rows in X) or sample differently.");
-    return PBH_ERR_NOT_PD;
-  }
+  st = ic_factor(G.data(), n, k, a->corr_host_out, Lc.data());
+  if (st) return st;
   std::vector<double> invd(k), P((size_t)k * k);
   for (int j = 0; j < k; ++j) invd[j] = 1.0 / Lc[(size_t)j * k + j];
   for (int i = 0; i < k; ++i)
@@ -333,57 +258,11 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     PBH_CHECK_HIP(hipMemcpyAsync(a->cscores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
 
   // ---- step 4: Y[:, c] = sort(X[:, c])[rankdata(CS[:, c]).astype(int) - 1]
-  // The correlated scores are ~N(0, 1): sort 32-bit order-preserving codes (4 passes instead
-  // of 8), then order the (short) runs of equal codes by the full float64 value.  A run
-  // longer than kMaxRun sends that column through the 64-bit sort instead.
-  const CodeMap cm = upload_code_map(L.codemap, s, &st);
-  if (st) return st;
-  uint8_t* eqprev = (uint8_t*)L.tmp;
   for (int c = 0; c < k; ++c) {
-    const double* cs_c = L.S + (int64_t)c * n;
-    RankOut out = {};
-    out.sorted_src = L.sorted_x + (int64_t)c * n;
-    out.y = a->Y + (int64_t)c * a->y_cs;
-    out.y_rs = a->y_rs;
-    out.idx = a->idx_out ? a->idx_out + (int64_t)c * n : nullptr;
-    int buf = 0;
-    st = make_codes(cs_c, n, cm, (uint32_t*)sb.keys[0], s);
-    if (st) return st;
-    st = radix_sort_keys32(sb, n, s, &buf);
-    if (st) return st;
-    PBH_CHECK_HIP(hipMemsetAsync(L.counts, 0, sizeof(int32_t), s));
-    st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], sb.vals[buf ^ 1], cs_c, n, eqprev,
-                           (int32_t*)L.counts, s);
-    if (st) return st;
-    int32_t run_flags = 0;
-    PBH_CHECK_HIP(hipMemcpyAsync(&run_flags, L.counts, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    PBH_CHECK_HIP(hipStreamSynchronize(s));
-    if (run_flags == 0 && out.idx == nullptr) {
-      // no ties: rank - 1 is the sorted position, so Y[rows[p]] = sorted_x[p]
-      PlaceBuffers pb;
-      pb.rows[0] = sb.vals[buf];
-      pb.vals[0] = (double*)sb.keys[buf ^ 1];
-      pb.rows[1] = sb.vals[buf ^ 1];
-      pb.vals[1] = (double*)sb.keys[buf];
-      pb.counts = sb.counts;
-      pb.partials = sb.partials;
-      pb.status = sb.status;
-      pb.bases = sb.bases;
-      st = place_by_row(sb.vals[buf ^ 1], out.sorted_src, n, out.y, out.y_rs, pb, s);
-      if (st) return st;
-      continue;
-    }
-    if (!(run_flags & 1)) {
-      st = rank_finish(kModeGather, nullptr, sb.vals[buf ^ 1], n, tb, out, s, eqprev);
-      if (st) return st;
-      continue;
-    }
-    st = load_keys(cs_c, 1, n, sb.keys[0], nullptr, s);
-    if (st) return st;
-    st = radix_sort_keys(sb, n, s, &buf);
-    if (st) return st;
-    st = rank_finish(kModeGather, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+    st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
+                        a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s);
     if (st) return st;
   }
+  PBH_CHECK_HIP(hipStreamSynchronize(s));  // host vectors above were sources of async copies
   return PBH_OK;
 }

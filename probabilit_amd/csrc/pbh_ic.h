@@ -61,7 +61,14 @@ int make_codes(const double* x, int64_t n, const CodeMap& cm, uint32_t* codes, h
 int resolve_code_runs(const uint32_t* codes, const uint32_t* rows, uint32_t* rows_out, const double* x, int64_t n,
                       uint8_t* eqprev, int32_t* flags, hipStream_t s);
 
-// Column sums (k columns of length n, column stride ld) into sums[k] (device), fixed order.
+// dst = src, then dst[p] = src[s + (e - s) / 2] inside every tie run [s, e] flagged by eqprev:
+// the value every member of a tie run receives in step 4 (int of the 'average' rank).
+int tie_fix_values(const uint8_t* eqprev, int64_t n, const double* src, double* dst, hipStream_t s);
+
+// out[c] = (sum of column c) / divisor, k columns of length n (column stride ld), fixed order.
+int column_sums(const double* S, int64_t n, int k, int64_t ld, double* partial, double* out, double divisor,
+                hipStream_t s);
+// Column means (k columns of length n, column stride ld) into means[k] (device), fixed order.
 int column_means(const double* S, int64_t n, int k, int64_t ld, double* partial, double* means, hipStream_t s);
 size_t gram_partials_bytes(int k);
 // Centered Gram matrix G = (S - m)^T (S - m), k x k row-major into gram (device), fixed order.
@@ -71,5 +78,28 @@ int centered_gram(const double* S, int64_t n, int k, int64_t ld, const double* m
 // then cs_j = sum_{m<=j} P_jm d_m.   L, P: k x k row-major device, inv_diag: k.
 int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const double* L, const double* inv_diag,
                                 const double* P, hipStream_t s);
+
+// ---------------------------------------------------------------- shared orchestration pieces
+// Host, step 2 (correlation.py:398-405): G = centered Gram (k x k, row-major) of scores over n
+// rows is scaled in place to np.corrcoef (np.cov's 1/(n-1), the two divisions by the standard
+// deviations, the clip to [-1, 1]); corr_out (optional) receives it; Lc = cholesky.  Returns
+// PBH_ERR_NOT_PD with the reference's message when a pivot is not positive.
+int ic_factor(double* G, int64_t n, int k, double* corr_out, double* Lc);
+
+// Step 4 (correlation.py:418-423) for one column, with its workspace.
+struct ReorderWs {
+  SortBuffers sb;
+  TieBuffers tb;
+  CodeMap cm;
+  uint8_t* eqprev;
+  int32_t* flags;
+  uint32_t hist_host[8 * 256];
+};
+size_t reorder_ws_bytes(int64_t n);
+// Carves ws and uploads the code map (stream ordered).
+int reorder_carve(void* ws, int64_t n, ReorderWs& w, hipStream_t s);
+// y[r * y_rs] = sorted_src[rank(cs[r]) - 1]; idx[r] = rank - 1 when idx != NULL.
+int reorder_column(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx,
+                   ReorderWs& w, hipStream_t s);
 
 }  // namespace pbh

@@ -257,12 +257,13 @@ __global__ __launch_bounds__(kRedThreads) void k_colsum(const double* __restrict
   if (threadIdx.x == 0) partial[(int64_t)c * gridDim.x + blockIdx.x] = s;
 }
 
-__global__ void k_means(const double* __restrict__ partial, int nb, int k, int64_t n, double* __restrict__ means) {
+__global__ void k_means(const double* __restrict__ partial, int nb, int k, double divisor,
+                        double* __restrict__ means) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= k) return;
   double s = 0.0;
   for (int b = 0; b < nb; ++b) s += partial[(int64_t)c * nb + b];
-  means[c] = s / (double)n;
+  means[c] = s / divisor;
 }
 
 // ---------------------------------------------------------------- centered Gram
@@ -361,66 +362,68 @@ __global__ void k_gram_reduce(const double* __restrict__ partials, int nb, int k
   gram[(int64_t)j * k + i] = s;
 }
 
-// Row-streaming Gram for K <= 32: lane l of every wave takes row r0 + l of a 64-row group
-// and keeps the (centered) row in registers; wave w accumulates the entries (i, j >= i) with
-// i = w (mod 4) of the upper triangle, so no LDS is needed and each row is read from HBM
-// once (the four waves of a block share it through L1/L2).  Lane sums are reduced at the end
-// of the block's row chunk in a fixed order (deterministic).
-// partials[(block * KC + i) * KC + j], i <= j.
-template <int KC, int W>
-__device__ __forceinline__ void gram_rows_wave(const double* __restrict__ S, int64_t ld, int k,
-                                               const double* __restrict__ means, int64_t r0, int64_t r1,
-                                               double* __restrict__ out) {
-  constexpr int NE = [] {
-    int c = 0;
-    for (int i = W; i < KC; i += 4) c += KC - i;
-    return c;
-  }();
-  const int lane = threadIdx.x & 63;
-  double mu[KC];
-#pragma unroll
-  for (int c = 0; c < KC; ++c) mu[c] = c < k ? means[c] : 0.0;
-  double acc[NE];
-#pragma unroll
-  for (int e = 0; e < NE; ++e) acc[e] = 0.0;
-  for (int64_t rb = r0; rb < r1; rb += 64) {
-    const int64_t r = rb + lane;
-    double v[KC];
-#pragma unroll
-    for (int c = 0; c < KC; ++c) v[c] = (c < k && r < r1) ? S[(int64_t)c * ld + r] - mu[c] : 0.0;
-    int e = 0;
-#pragma unroll
-    for (int i = W; i < KC; i += 4)
-#pragma unroll
-      for (int j = i; j < KC; ++j) {
-        acc[e] = __builtin_fma(v[i], v[j], acc[e]);
-        ++e;
-      }
-  }
-  int e = 0;
-#pragma unroll
-  for (int i = W; i < KC; i += 4)
-#pragma unroll
-    for (int j = i; j < KC; ++j) {
-      double x = acc[e++];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-      if (lane == 0) out[i * KC + j] = x;
-    }
-}
+// Gram for K <= 32 on the f64 matrix cores.  A block stages GM_ROWS rows x 32 columns of the
+// centered scores in LDS (one coalesced 512-byte column load per wave instruction, zero
+// padding for columns >= k and rows past the chunk), then every wave feeds row quads to
+// v_mfma_f64_16x16x4_f64: with A[m][q] = B[q][m] = S[row q][16 I + m], the three tiles
+// (0,0), (0,1), (1,1) of the 32 x 32 upper block triangle accumulate in 12 registers.
+// The four waves' tiles are summed through LDS in a fixed order at the end (deterministic).
+// partials[(block * 32 + i) * 32 + j] for i <= j, as k_gram_rows_reduce<32> expects.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int GM_ROWS = 128;
 
-template <int KC>
-__global__ __launch_bounds__(256) void k_gram_rows(const double* __restrict__ S, int64_t n, int k, int64_t ld,
+__global__ __launch_bounds__(256) void k_gram_mfma(const double* __restrict__ S, int64_t n, int k, int64_t ld,
                                                   const double* __restrict__ means, int64_t chunk,
                                                   double* __restrict__ partials) {
+  __shared__ double smem[GM_ROWS * 33];  // staging tile [row][col], reused for the wave reduction
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * chunk;
   const int64_t r1 = (r0 + chunk) < n ? (r0 + chunk) : n;
-  double* out = partials + (int64_t)blockIdx.x * KC * KC;
-  switch (threadIdx.x >> 6) {
-    case 0: gram_rows_wave<KC, 0>(S, ld, k, means, r0, r1, out); break;
-    case 1: gram_rows_wave<KC, 1>(S, ld, k, means, r0, r1, out); break;
-    case 2: gram_rows_wave<KC, 2>(S, ld, k, means, r0, r1, out); break;
-    default: gram_rows_wave<KC, 3>(S, ld, k, means, r0, r1, out); break;
+  double mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mu[j] = (w * 8 + j) < k ? means[w * 8 + j] : 0.0;
+  f64x4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c11 = c00;
+  for (int64_t rb = r0; rb < r1; rb += GM_ROWS) {
+#pragma unroll
+    for (int h = 0; h < GM_ROWS / 64; ++h) {
+      const int row = h * 64 + lane;
+      const int64_t r = rb + row;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = w * 8 + j;
+        smem[row * 33 + c] = (c < k && r < r1) ? S[(int64_t)c * ld + r] - mu[j] : 0.0;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int qi = 0; qi < GM_ROWS / 16; ++qi) {
+      const int row = (w + 4 * qi) * 4 + (lane >> 4);
+      const double a0 = smem[row * 33 + (lane & 15)];
+      const double a1 = smem[row * 33 + 16 + (lane & 15)];
+      c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a0, c00, 0, 0, 0);
+      c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a1, c01, 0, 0, 0);
+      c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, a1, c11, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // wave reduction: red[w][tile][reg][lane]
+  double* red = smem;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    red[((w * 3 + 0) * 4 + g) * 64 + lane] = c00[g];
+    red[((w * 3 + 1) * 4 + g) * 64 + lane] = c01[g];
+    red[((w * 3 + 2) * 4 + g) * 64 + lane] = c11[g];
+  }
+  __syncthreads();
+  double* out = partials + (int64_t)blockIdx.x * 32 * 32;
+  for (int e = t; e < 3 * 4 * 64; e += 256) {  // e = (tile * 4 + reg) * 64 + lane
+    const int tile = e / 256, g = (e >> 6) & 3, l = e & 63;
+    const double v = ((red[((0 * 3 + tile) * 4 + g) * 64 + l] + red[((1 * 3 + tile) * 4 + g) * 64 + l]) +
+                      red[((2 * 3 + tile) * 4 + g) * 64 + l]) +
+                     red[((3 * 3 + tile) * 4 + g) * 64 + l];
+    const int i = (l >> 4) + 4 * g + (tile == 2 ? 16 : 0);
+    const int j = (l & 15) + (tile >= 1 ? 16 : 0);
+    if (i <= j) out[i * 32 + j] = v;
   }
 }
 
@@ -544,34 +547,34 @@ size_t gram_partials_bytes(int k) {
   return a > b ? a : b;
 }
 
-int column_means(const double* S, int64_t n, int k, int64_t ld, double* partial, double* means, hipStream_t s) {
+int column_sums(const double* S, int64_t n, int k, int64_t ld, double* partial, double* out, double divisor,
+                hipStream_t s) {
   int64_t chunk;
   int64_t nb = red_blocks(n, &chunk);
   hipLaunchKernelGGL(k_colsum, dim3((unsigned)nb, (unsigned)k), dim3(kRedThreads), 0, s, S, n, ld, chunk, partial);
-  hipLaunchKernelGGL(k_means, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, s, partial, (int)nb, k, n, means);
+  hipLaunchKernelGGL(k_means, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, s, partial, (int)nb, k, divisor, out);
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
 
-template <int KC>
-static int gram_rows(const double* S, int64_t n, int k, int64_t ld, const double* means, double* partials,
-                     double* gram, hipStream_t s) {
-  int64_t nb = kGramBlocksMax;
-  int64_t chunk = ((n + nb - 1) / nb + 63) / 64 * 64;
-  nb = (n + chunk - 1) / chunk;
-  PBH_TIMED(kKGram, s,
-            hipLaunchKernelGGL(k_gram_rows<KC>, dim3((unsigned)nb), dim3(256), 0, s, S, n, k, ld, means, chunk,
-                               partials));
-  hipLaunchKernelGGL(k_gram_rows_reduce<KC>, dim3((k * k + 255) / 256), dim3(256), 0, s, partials, (int)nb, k, gram);
-  PBH_CHECK_LAUNCH();
-  return PBH_OK;
+int column_means(const double* S, int64_t n, int k, int64_t ld, double* partial, double* means, hipStream_t s) {
+  return column_sums(S, n, k, ld, partial, means, (double)n, s);
 }
 
 int centered_gram(const double* S, int64_t n, int k, int64_t ld, const double* means, double* partials,
                   double* gram, hipStream_t s) {
-  if (k <= 8) return gram_rows<8>(S, n, k, ld, means, partials, gram, s);
-  if (k <= 16) return gram_rows<16>(S, n, k, ld, means, partials, gram, s);
-  if (k <= 32) return gram_rows<32>(S, n, k, ld, means, partials, gram, s);
+  if (k <= 32) {
+    int64_t nb = kGramBlocksMax;
+    int64_t chunk = ((n + nb - 1) / nb + GM_ROWS - 1) / GM_ROWS * GM_ROWS;
+    nb = (n + chunk - 1) / chunk;
+    PBH_TIMED(kKGram, s,
+              hipLaunchKernelGGL(k_gram_mfma, dim3((unsigned)nb), dim3(256), 0, s, S, n, k, ld, means, chunk,
+                                 partials));
+    hipLaunchKernelGGL(k_gram_rows_reduce<32>, dim3((k * k + 255) / 256), dim3(256), 0, s, partials, (int)nb, k,
+                       gram);
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
   int64_t chunk;
   int64_t nb = red_blocks(n, &chunk);
   int nt = (k + GT - 1) / GT;
@@ -694,6 +697,40 @@ static __global__ __launch_bounds__(256) void k_code_runs(const uint32_t* __rest
     }
     for (int64_t p = p0; p < p0 + 4 && p < n; ++p) code_run_one(code, rows, rows_out, x, n, eqprev, flags, p);
   }
+}
+
+// dst[p] = src[s + (e - s) / 2] for every position p of a tie run [s, e] (eqprev marks the
+// non-head members): the int('average' rank) - 1 of correlation.py:422 that all members of
+// the run share.  dst already holds src elsewhere.  16 positions per thread.
+static __global__ __launch_bounds__(256) void k_tie_fix(const uint8_t* __restrict__ eqprev, int64_t n,
+                                                       const double* __restrict__ src, double* __restrict__ dst) {
+  const int64_t nq = (n + 15) / 16;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+    const int64_t p0 = q * 16;
+    bool any = false;
+    if (p0 + 16 <= n) {
+      const uint4 v = *(const uint4*)(eqprev + p0);
+      any = (v.x | v.y | v.z | v.w) != 0u || (p0 + 16 < n && eqprev[p0 + 16] != 0);
+    } else {
+      for (int64_t p = p0; p < n; ++p) any |= eqprev[p] != 0;
+    }
+    if (!any) continue;
+    for (int64_t p = p0; p < p0 + 16 && p < n; ++p) {
+      const bool member = eqprev[p] != 0 || (p + 1 < n && eqprev[p + 1] != 0);
+      if (!member) continue;
+      int64_t st = p, e = p;
+      while (st > 0 && eqprev[st] != 0) --st;
+      while (e + 1 < n && eqprev[e + 1] != 0) ++e;
+      dst[p] = src[st + (e - st) / 2];
+    }
+  }
+}
+
+int tie_fix_values(const uint8_t* eqprev, int64_t n, const double* src, double* dst, hipStream_t s) {
+  PBH_CHECK_HIP(hipMemcpyAsync(dst, src, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(k_tie_fix, dim3(grid_for((n + 15) / 16, 256, 4096)), dim3(256), 0, s, eqprev, n, src, dst);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
 }
 
 size_t code_map_bytes() { return ((kCodeSegments + 1) * 4 + 255) / 256 * 256 + kCodeSegments * 8; }

@@ -1,0 +1,277 @@
+// Iman-Conover phases shared by the single-call orchestrator (pbh_iman_conover, pbh_api.hip)
+// and exported one by one for row-sharded multi-GPU execution (probabilit_amd/distributed.py):
+//
+//   step 1   pbh_lhs_sorted_ppf + pbh_run_heads + pbh_lhs_scores   (generated LHS columns)
+//   step 2   pbh_column_sums, pbh_centered_gram (per shard; summed across ranks), pbh_ic_factor
+//   step 3   pbh_ic_apply                                           (per shard)
+//   step 4   pbh_ic_reorder                                         (per column, on its owner)
+#include <math.h>
+#include <string.h>
+
+#include <vector>
+
+#include "pbh_error.h"
+#include "pbh_ic.h"
+#include "pbh_lhs.h"
+#include "pbh_sort.h"
+
+namespace pbh {
+
+namespace {
+
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// Lower Cholesky (Cholesky-Banachiewicz); false when a pivot is not > 0 (np.linalg.cholesky
+// raises LinAlgError there, which _is_positive_definite turns into False).
+bool cholesky_lower(const double* A, int k, double* L) {
+  for (int i = 0; i < k * k; ++i) L[i] = 0.0;
+  for (int j = 0; j < k; ++j) {
+    double s = A[(size_t)j * k + j];
+    for (int m = 0; m < j; ++m) s -= L[(size_t)j * k + m] * L[(size_t)j * k + m];
+    if (!(s > 0.0)) return false;
+    double d = sqrt(s);
+    L[(size_t)j * k + j] = d;
+    for (int i = j + 1; i < k; ++i) {
+      double t = A[(size_t)i * k + j];
+      for (int m = 0; m < j; ++m) t -= L[(size_t)i * k + m] * L[(size_t)j * k + m];
+      L[(size_t)i * k + j] = t / d;
+    }
+  }
+  return true;
+}
+
+struct CodeMapHost {
+  std::vector<uint32_t> base;
+  std::vector<double> scale;
+  double x0 = 0, w = 0;
+  CodeMapHost() : base(kCodeSegments + 1), scale(kCodeSegments) { code_map_host(base.data(), scale.data(), &x0, &w); }
+};
+
+}  // namespace
+
+int ic_factor(double* G, int64_t n, int k, double* corr_out, double* Lc) {
+  // np.cov: c = dot(Xc, Xc^T) * (1 / (N - 1)); np.corrcoef: c /= std[:,None]; c /= std[None,:]; clip
+  const double fact = 1.0 / (double)(n - 1);
+  for (int i = 0; i < k * k; ++i) G[i] *= fact;
+  std::vector<double> sd(k);
+  for (int i = 0; i < k; ++i) sd[i] = sqrt(G[(size_t)i * k + i]);
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) {
+      double v = G[(size_t)i * k + j];
+      v /= sd[i];
+      v /= sd[j];
+      G[(size_t)i * k + j] = v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v);
+    }
+  if (corr_out) memcpy(corr_out, G, (size_t)k * k * 8);
+  if (!cholesky_lower(G, k, Lc)) {
+    set_error(
+        "Rank data correlation not positive definite.There are perfect correlations in the ranked data.Supply more "
+        "data (rows in X) or sample differently.");
+    return PBH_ERR_NOT_PD;
+  }
+  return PBH_OK;
+}
+
+size_t reorder_ws_bytes(int64_t n) {
+  return align256(sort_workspace_bytes(n)) + align256(tie_workspace_bytes(n)) + align256(code_map_bytes()) +
+         align256((size_t)n) + 256;
+}
+
+int reorder_carve(void* ws, int64_t n, ReorderWs& w, hipStream_t s) {
+  static const CodeMapHost h;
+  char* p = (char*)ws;
+  sort_carve(p, n, w.sb);
+  p += align256(sort_workspace_bytes(n));
+  tie_carve(p, n, w.tb);
+  p += align256(tie_workspace_bytes(n));
+  char* cmap = p;
+  p += align256(code_map_bytes());
+  w.eqprev = (uint8_t*)p;
+  p += align256((size_t)n);
+  w.flags = (int32_t*)p;
+  w.sb.hist_host = w.hist_host;
+  const size_t base_bytes = align256((kCodeSegments + 1) * 4);
+  w.cm.x0 = h.x0;
+  w.cm.w = h.w;
+  w.cm.inv_w = 1.0 / h.w;
+  w.cm.m = kCodeSegments;
+  w.cm.base = (const uint32_t*)cmap;
+  w.cm.scale = (const double*)(cmap + base_bytes);
+  PBH_CHECK_HIP(hipMemcpyAsync(cmap, h.base.data(), (kCodeSegments + 1) * 4, hipMemcpyHostToDevice, s));
+  PBH_CHECK_HIP(hipMemcpyAsync(cmap + base_bytes, h.scale.data(), kCodeSegments * 8, hipMemcpyHostToDevice, s));
+  return PBH_OK;
+}
+
+// The correlated scores are ~N(0, 1): sort 32-bit order-preserving codes (4 passes instead of
+// 8), then order the (short) runs of equal codes by the full float64 value.  Without ties the
+// rank - 1 of row r is its sorted position, and Y is written by the LDS row placement; exact
+// ties use the tie-aware gather, and a run longer than kMaxRun the 64-bit sort.
+int reorder_column(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx,
+                   ReorderWs& w, hipStream_t s) {
+  SortBuffers& sb = w.sb;
+  RankOut out = {};
+  out.sorted_src = sorted_src;
+  out.y = y;
+  out.y_rs = y_rs;
+  out.idx = idx;
+  int buf = 0;
+  int st = make_codes(cs, n, w.cm, (uint32_t*)sb.keys[0], s);
+  if (st) return st;
+  st = radix_sort_keys32(sb, n, s, &buf);
+  if (st) return st;
+  PBH_CHECK_HIP(hipMemsetAsync(w.flags, 0, sizeof(int32_t), s));
+  st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], sb.vals[buf ^ 1], cs, n, w.eqprev, w.flags, s);
+  if (st) return st;
+  int32_t run_flags = 0;
+  PBH_CHECK_HIP(hipMemcpyAsync(&run_flags, w.flags, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  PBH_CHECK_HIP(hipStreamSynchronize(s));
+  if (!(run_flags & 1) && idx == nullptr) {
+    const double* vals = sorted_src;
+    if (run_flags & 2) {  // exact ties: every member of a run takes the same sorted value
+      double* fixed = (double*)sb.keys[buf];  // the codes are consumed; pass 2 of the placement reuses it
+      st = tie_fix_values(w.eqprev, n, sorted_src, fixed, s);
+      if (st) return st;
+      vals = fixed;
+    }
+    PlaceBuffers pb;
+    pb.rows[0] = sb.vals[buf];
+    pb.vals[0] = (double*)sb.keys[buf ^ 1];
+    pb.rows[1] = sb.vals[buf ^ 1];
+    pb.vals[1] = (double*)sb.keys[buf];
+    pb.counts = sb.counts;
+    pb.partials = sb.partials;
+    pb.status = sb.status;
+    pb.bases = sb.bases;
+    return place_by_row(sb.vals[buf ^ 1], vals, n, y, y_rs, pb, s);
+  }
+  if (!(run_flags & 1)) return rank_finish(kModeGather, nullptr, sb.vals[buf ^ 1], n, w.tb, out, s, w.eqprev);
+  st = load_keys(cs, 1, n, sb.keys[0], nullptr, s);
+  if (st) return st;
+  st = radix_sort_keys(sb, n, s, &buf);
+  if (st) return st;
+  return rank_finish(kModeGather, sb.keys[buf], sb.vals[buf], n, w.tb, out, s);
+}
+
+}  // namespace pbh
+
+using namespace pbh;
+
+// ---------------------------------------------------------------- exported phases
+extern "C" int pbh_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist,
+                                  const double* params_host, int nparams, double* out, int32_t* nonfinite_flag,
+                                  void* stream) {
+  PBH_REQUIRE(out != nullptr && nparams >= 0 && nparams <= 3 && (nparams == 0 || params_host),
+              "pbh_lhs_sorted_ppf: bad arguments");
+  pbh_param prm[3];
+  for (int j = 0; j < nparams; ++j) prm[j] = pbh_param{nullptr, params_host[j]};
+  return lhs_sorted_ppf(seed, n, t0, nt, col, dist, prm, nparams, out, nonfinite_flag, as_stream(stream));
+}
+
+extern "C" int pbh_sorted_check(const double* x, int64_t n, int64_t* ties, int64_t* inversions, void* ws,
+                                void* stream) {
+  PBH_REQUIRE(x && ws && ties && inversions && n >= 0, "pbh_sorted_check: bad arguments");
+  hipStream_t s = as_stream(stream);
+  unsigned long long c[2] = {0, 0};
+  if (n > 1) {
+    int st = check_sorted(x, n, (unsigned long long*)ws, s);
+    if (st) return st;
+    PBH_CHECK_HIP(hipMemcpyAsync(c, ws, sizeof(c), hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+  }
+  *ties = (int64_t)c[0];
+  *inversions = (int64_t)c[1];
+  return PBH_OK;
+}
+
+extern "C" int pbh_run_heads_workspace_size(int64_t n, size_t* bytes) {
+  PBH_REQUIRE(bytes && n >= 0, "pbh_run_heads_workspace_size: bad arguments");
+  *bytes = run_heads_ws_bytes(n);
+  return PBH_OK;
+}
+
+extern "C" int pbh_run_heads(const double* x, int64_t m, int64_t t0, int first_is_prev, uint32_t* heads,
+                             int64_t* count, void* ws, size_t ws_bytes, void* stream) {
+  PBH_REQUIRE(x && heads && count && ws && m >= 0, "pbh_run_heads: bad arguments");
+  if (ws_bytes < run_heads_ws_bytes(m)) {
+    set_error("pbh_run_heads: workspace %zu < %zu bytes", ws_bytes, run_heads_ws_bytes(m));
+    return PBH_ERR_WORKSPACE;
+  }
+  return run_heads(x, m, t0, first_is_prev != 0, heads, count, ws, as_stream(stream));
+}
+
+extern "C" int pbh_lhs_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, const uint32_t* heads,
+                              int64_t nheads, double* S, void* stream) {
+  PBH_REQUIRE(S != nullptr && (heads == nullptr || nheads >= 1), "pbh_lhs_scores: bad arguments");
+  PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "pbh_lhs_scores: n out of range");
+  return perm_scores(seed, n, col, row0, nrows, heads, nheads, S, as_stream(stream));
+}
+
+extern "C" int pbh_gram_workspace_size(int32_t k, size_t* bytes) {
+  PBH_REQUIRE(bytes && k >= 1 && k <= 128, "pbh_gram_workspace_size: bad arguments");
+  *bytes = align256(gram_partials_bytes(k)) + align256((size_t)k * 8);
+  return PBH_OK;
+}
+
+extern "C" int pbh_column_sums(const double* S, int64_t n, int32_t k, int64_t ld, double* sums, void* ws,
+                               size_t ws_bytes, void* stream) {
+  size_t need = 0;
+  pbh_gram_workspace_size(k, &need);
+  PBH_REQUIRE(S && sums && ws && n >= 1 && ws_bytes >= need, "pbh_column_sums: bad arguments / workspace");
+  return column_sums(S, n, k, ld, (double*)ws, sums, 1.0, as_stream(stream));
+}
+
+extern "C" int pbh_centered_gram(const double* S, int64_t n, int32_t k, int64_t ld, const double* means,
+                                 double* gram, void* ws, size_t ws_bytes, void* stream) {
+  size_t need = 0;
+  pbh_gram_workspace_size(k, &need);
+  PBH_REQUIRE(S && means && gram && ws && n >= 1 && ws_bytes >= need, "pbh_centered_gram: bad arguments / workspace");
+  return centered_gram(S, n, k, ld, means, (double*)ws, gram, as_stream(stream));
+}
+
+extern "C" int pbh_ic_factor(const double* gram_host, int64_t n, int32_t k, double* corr_host_out,
+                             double* L_host_out) {
+  PBH_REQUIRE(gram_host && L_host_out && k >= 1 && n > 1, "pbh_ic_factor: bad arguments");
+  std::vector<double> G(gram_host, gram_host + (size_t)k * k);
+  return ic_factor(G.data(), n, k, corr_host_out, L_host_out);
+}
+
+extern "C" int pbh_ic_apply(double* S, int64_t n, int32_t k, int64_t ld, const double* L_host,
+                            const double* target_chol_host, void* ws, size_t ws_bytes, void* stream) {
+  PBH_REQUIRE(S && L_host && target_chol_host && ws && k >= 1 && k <= 128 && n >= 0, "pbh_ic_apply: bad arguments");
+  PBH_REQUIRE(ws_bytes >= (size_t)(2 * k * k + k) * 8, "pbh_ic_apply: workspace too small");
+  hipStream_t s = as_stream(stream);
+  std::vector<double> host((size_t)2 * k * k + k);
+  double* Lh = host.data();
+  double* Ph = Lh + (size_t)k * k;
+  double* ih = Ph + (size_t)k * k;
+  for (int i = 0; i < k * k; ++i) Lh[i] = L_host[i];
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) Ph[(size_t)i * k + j] = j <= i ? target_chol_host[(size_t)i * k + j] : 0.0;
+  for (int j = 0; j < k; ++j) ih[j] = 1.0 / L_host[(size_t)j * k + j];
+  double* dev = (double*)ws;
+  PBH_CHECK_HIP(hipMemcpyAsync(dev, host.data(), host.size() * 8, hipMemcpyHostToDevice, s));
+  PBH_CHECK_HIP(hipStreamSynchronize(s));  // `host` is pageable and goes out of scope
+  if (n == 0) return PBH_OK;
+  return apply_decorrelate_correlate(S, n, k, ld, dev, dev + 2 * (size_t)k * k, dev + (size_t)k * k, s);
+}
+
+extern "C" int pbh_ic_reorder_workspace_size(int64_t n, size_t* bytes) {
+  PBH_REQUIRE(bytes && n >= 1, "pbh_ic_reorder_workspace_size: bad arguments");
+  *bytes = reorder_ws_bytes(n);
+  return PBH_OK;
+}
+
+extern "C" int pbh_ic_reorder(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs,
+                              int32_t* idx_out, void* ws, size_t ws_bytes, void* stream) {
+  PBH_REQUIRE(cs && sorted_src && y && ws, "pbh_ic_reorder: null pointer");
+  PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "pbh_ic_reorder: n out of range");
+  if (ws_bytes < reorder_ws_bytes(n)) {
+    set_error("pbh_ic_reorder: workspace %zu < %zu bytes", ws_bytes, reorder_ws_bytes(n));
+    return PBH_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  ReorderWs w;
+  int st = reorder_carve(ws, n, w, s);
+  if (st) return st;
+  return reorder_column(cs, n, sorted_src, y, y_rs, idx_out, w, s);
+}

@@ -9,6 +9,7 @@
 #include "pbh_error.h"
 #include "pbh_rng.h"
 #include "pbh_special.h"
+#include "pbh_sort.h"
 #include "pbh_timing.h"
 
 namespace pbh {
@@ -151,18 +152,20 @@ __global__ __launch_bounds__(kBlock) void k_lhs_ppf(uint64_t seed, int64_t n, in
 // stratum t.  Bit-identical to k_lhs_ppf's value for that row; non-decreasing in t whenever
 // the ppf is monotone, which k_check_sorted verifies before anything relies on it.
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_lhs_sorted_ppf(uint64_t seed, int64_t n, uint32_t col, Params prm,
-                                                           PoissonTable pt, double* __restrict__ out, int32_t* flag) {
+__global__ __launch_bounds__(kBlock) void k_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt,
+                                                           uint32_t col, Params prm, PoissonTable pt,
+                                                           double* __restrict__ out, int32_t* flag) {
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
-  int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t step = (int64_t)gridDim.x * kBlock;
-  for (; t < n; t += step) {
+  for (; i < nt; i += step) {
+    const int64_t t = t0 + i;
     uint64_t row = fp.inverse((uint64_t)t);
     double u = ph.uniform(row, col, kPurposeLhsU);
     double q = ((double)(t + 1) - u) / (double)n;
     double x = ppf_one<D>(q, prm.val[0], prm.val[1], prm.val[2], pt);
-    out[t] = x;
+    out[i] = x;
     flag_nonfinite(flag, !isfinite(x));
   }
 }
@@ -187,17 +190,87 @@ __global__ __launch_bounds__(kBlock) void k_check_sorted(const double* __restric
   }
 }
 
-// Van der Waerden scores of an untied LHS column, in row order: the rank of row r is
-// pi(r) + 1, so S[r] = ndtri((pi(r) + 1) / (n + 1)) (correlation.py:394-395), no sort.
-__global__ __launch_bounds__(kBlock) void k_perm_scores(uint64_t seed, int64_t n, uint32_t col,
-                                                        const double* __restrict__ avg, double* __restrict__ S) {
+// 'average' rank of stratum t given the run heads (sorted, heads[0] = 0) of the sorted
+// column: the run [s, e] holding t has ranks s+1 .. e+1, average s + 1 + (e - s) / 2
+// (scipy _rankdata; the same formula as k_rank_finish).
+__device__ __forceinline__ double run_average_rank(const uint32_t* __restrict__ heads, int64_t nheads, int64_t n,
+                                                   int64_t t) {
+  int64_t lo = 0, hi = nheads;  // first head > t
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)heads[mid] <= t)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  const int64_t s = heads[lo - 1];
+  const int64_t e = (lo < nheads ? (int64_t)heads[lo] : n) - 1;
+  return (double)(s + 1) + (double)(e - s) / 2.0;
+}
+
+// Van der Waerden scores of an LHS column, rows [row0, row0 + nrows), in row order: the rank
+// of row r is pi(r) + 1 (untied), or the run average of stratum pi(r) (heads != NULL), so
+// S[r] = ndtri(rank / (n + 1)) (correlation.py:394-395) without sorting anything.
+__global__ __launch_bounds__(kBlock) void k_perm_scores(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
+                                                        int64_t nrows, const uint32_t* __restrict__ heads,
+                                                        int64_t nheads, double* __restrict__ S) {
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
   const double np1 = (double)(n + 1);
-  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n; r += (int64_t)gridDim.x * kBlock) {
-    uint64_t t = fp((uint64_t)r);
-    double rank = avg ? avg[t] : (double)(t + 1);  // tied column: 'average' rank of stratum t
-    S[r] = sf::ndtri(rank / np1);
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
+    const uint64_t t = fp((uint64_t)(row0 + i));
+    const double rank = heads ? run_average_rank(heads, nheads, n, (int64_t)t) : (double)(t + 1);
+    S[i] = sf::ndtri(rank / np1);
+  }
+}
+
+// Run heads of a sorted segment x[0..m): position p is a head when p == 0 (unless x[0] is
+// the value before the segment, first_is_prev) or x[p] != x[p - 1]; heads are reported as
+// t0 + p (t0 - 1 + p with first_is_prev).  Two passes: per-tile counts, then ordered writes.
+constexpr int kHeadTile = kBlock * 16;
+
+__device__ __forceinline__ bool is_head(const double* __restrict__ x, int64_t p, bool first_is_prev) {
+  return p == 0 ? !first_is_prev : x[p] != x[p - 1];
+}
+
+__global__ __launch_bounds__(kBlock) void k_heads_count(const double* __restrict__ x, int64_t m, int first_is_prev,
+                                                        uint32_t* __restrict__ counts) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  const int64_t base = (int64_t)blockIdx.x * kHeadTile;
+  uint32_t c = 0;
+  for (int j = 0; j < 16; ++j) {
+    const int64_t p = base + j * kBlock + threadIdx.x;
+    c += (p < m && is_head(x, p, first_is_prev)) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ __launch_bounds__(kBlock) void k_heads_write(const double* __restrict__ x, int64_t m, int first_is_prev,
+                                                        int64_t t0, const uint32_t* __restrict__ offsets,
+                                                        uint32_t* __restrict__ heads) {
+  __shared__ uint32_t wcount[kBlock / 64];
+  __shared__ uint32_t running;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kHeadTile;
+  const int64_t shift = first_is_prev ? t0 - 1 : t0;
+  if (threadIdx.x == 0) running = offsets[blockIdx.x];
+  __syncthreads();
+  for (int j = 0; j < 16; ++j) {  // tile order = position order: row j of 256 positions
+    const int64_t p = base + j * kBlock + threadIdx.x;
+    const bool h = p < m && is_head(x, p, first_is_prev);
+    const uint64_t bal = __ballot(h);
+    const uint32_t below = (uint32_t)__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+    if (lane == 0) wcount[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t off = running;
+    for (int v = 0; v < w; ++v) off += wcount[v];
+    if (h) heads[off + below] = (uint32_t)(shift + p);
+    __syncthreads();
+    if (threadIdx.x == 0) running += wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    __syncthreads();
   }
 }
 
@@ -379,8 +452,11 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
 
 }  // namespace
 
-int lhs_sorted_ppf(uint64_t seed, int64_t n, int col, int dist, const pbh_param* params, int nparams, double* out,
-                   int32_t* flag, hipStream_t s) {
+int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist, const pbh_param* params,
+                   int nparams, double* out, int32_t* flag, hipStream_t s) {
+  PBH_REQUIRE(t0 >= 0 && nt >= 0 && t0 + nt <= n, "lhs_sorted_ppf: strata [%lld, %lld) outside [0, %lld)",
+              (long long)t0, (long long)(t0 + nt), (long long)n);
+  if (nt == 0) return PBH_OK;
   for (int j = 0; j < nparams; ++j)
     PBH_REQUIRE(params[j].ptr == nullptr, "stratum-ordered LHS generation needs scalar parameters");
   Params prm;
@@ -388,12 +464,13 @@ int lhs_sorted_ppf(uint64_t seed, int64_t n, int col, int dist, const pbh_param*
   double* table = nullptr;
   int st = with_params(dist, params, nparams, prm, pt, &table, s);
   if (st != PBH_OK) return st;
-  dim3 g(ppf_grid(n)), b(kBlock);
+  dim3 g(ppf_grid(nt)), b(kBlock);
   switch (dist) {
-#define PBH_CASE(D)                                                                                                 \
-  case D:                                                                                                           \
-    PBH_TIMED(kKLhsSorted, s,                                                                                       \
-              hipLaunchKernelGGL(k_lhs_sorted_ppf<D>, g, b, 0, s, seed, n, (uint32_t)col, prm, pt, out, flag)); \
+#define PBH_CASE(D)                                                                                         \
+  case D:                                                                                                   \
+    PBH_TIMED(kKLhsSorted, s,                                                                               \
+              hipLaunchKernelGGL(k_lhs_sorted_ppf<D>, g, b, 0, s, seed, n, t0, nt, (uint32_t)col, prm, pt, \
+                                 out, flag));                                                               \
     break;
     PBH_CASE(PBH_DIST_NORM)
     PBH_CASE(PBH_DIST_UNIFORM)
@@ -419,10 +496,43 @@ int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStre
   return PBH_OK;
 }
 
-int perm_scores(uint64_t seed, int64_t n, int col, const double* avg, double* S, hipStream_t s) {
+int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, const uint32_t* heads,
+                int64_t nheads, double* S, hipStream_t s) {
+  PBH_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "perm_scores: rows outside [0, n)");
+  if (nrows == 0) return PBH_OK;
   PBH_TIMED(kKPermScores, s,
-            hipLaunchKernelGGL(k_perm_scores, dim3(ppf_grid(n)), dim3(kBlock), 0, s, seed, n, (uint32_t)col, avg, S));
+            hipLaunchKernelGGL(k_perm_scores, dim3(ppf_grid(nrows)), dim3(kBlock), 0, s, seed, n, (uint32_t)col, row0,
+                               nrows, heads, nheads, S));
   PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+size_t run_heads_ws_bytes(int64_t m) {
+  const int64_t nb = (m + kHeadTile - 1) / kHeadTile;
+  return ((size_t)nb * 4 + 255) / 256 * 256 + ((size_t)scan_partials_count(nb) * 4 + 255) / 256 * 256 + 256;
+}
+
+int run_heads(const double* x, int64_t m, int64_t t0, bool first_is_prev, uint32_t* heads, int64_t* count,
+              void* ws, hipStream_t s) {
+  if (m <= 0) {
+    *count = 0;
+    return PBH_OK;
+  }
+  const int64_t nb = (m + kHeadTile - 1) / kHeadTile;
+  uint32_t* counts = (uint32_t*)ws;
+  uint32_t* partials = (uint32_t*)((char*)ws + ((size_t)nb * 4 + 255) / 256 * 256);
+  hipLaunchKernelGGL(k_heads_count, dim3((unsigned)nb), dim3(kBlock), 0, s, x, m, (int)first_is_prev, counts);
+  PBH_CHECK_LAUNCH();
+  uint32_t last = 0, last_off = 0;
+  PBH_CHECK_HIP(hipMemcpyAsync(&last, counts + nb - 1, 4, hipMemcpyDeviceToHost, s));
+  int st = exclusive_scan_u32(counts, nb, partials, s);
+  if (st) return st;
+  PBH_CHECK_HIP(hipMemcpyAsync(&last_off, counts + nb - 1, 4, hipMemcpyDeviceToHost, s));
+  hipLaunchKernelGGL(k_heads_write, dim3((unsigned)nb), dim3(kBlock), 0, s, x, m, (int)first_is_prev, t0, counts,
+                     heads);
+  PBH_CHECK_LAUNCH();
+  PBH_CHECK_HIP(hipStreamSynchronize(s));
+  *count = (int64_t)last_off + last;
   return PBH_OK;
 }
 

@@ -42,6 +42,8 @@ void sort_carve(void* ws, int64_t n, SortBuffers& b);
 // the buffer holding the sorted keys / payload.  `stream` ordered; synchronises once to read
 // the digit histogram (pass skipping).  Returns < 0 and sets the last error on failure.
 int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf);
+// In-place exclusive scan of m uint32 counts (partials: scan_partials_count(m) entries).
+int exclusive_scan_u32(uint32_t* a, int64_t m, uint32_t* partials, hipStream_t s);
 // The same on uint32 keys stored in b.keys[0] (reinterpreted): at most 4 passes.
 int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf);
 

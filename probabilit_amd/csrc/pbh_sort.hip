@@ -123,6 +123,9 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, int
   }
 }
 
+
+}  // namespace
+
 int exclusive_scan_u32(uint32_t* a, int64_t m, uint32_t* partials, hipStream_t s) {
   int64_t np = scan_partials_count(m);
   PBH_TIMED(kKScan, s, hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)np), dim3(256), 0, s, a, m, partials);
@@ -131,6 +134,8 @@ int exclusive_scan_u32(uint32_t* a, int64_t m, uint32_t* partials, hipStream_t s
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
+
+namespace {
 
 // ------------------------------------------------------------------ stable scatter
 template <typename K, typename V = uint32_t>

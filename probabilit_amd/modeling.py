@@ -356,16 +356,33 @@ class Node(abc.ABC):
         return self._evaluate(src, correlator, gc_strategy, to_host=True)
 
     def sample_device(self, size=None, random_state=None, method=None, correlator="imanconover",
-                      gc_strategy=None):
-        """As sample(), but return the sink's device tensor (no D2H copy)."""
+                      gc_strategy=None, group=None):
+        """As sample(), but return the sink's device tensor (no D2H copy).
+
+        group: a torch.distributed process group (one process per GPU).  With more than one
+        rank the `size` rows are sharded: rank r evaluates every node on the rows
+        [size r / R, size (r + 1) / R) and returns its rows of the sink; generators are
+        counter-addressed by the global row, correlations run through the row-sharded
+        Iman-Conover of probabilit_amd.distributed."""
         size = 1 if size is None else size
         source = qmc.make_source(method, size, self.num_distribution_nodes(), random_state)
-        return self._evaluate(source, correlator, gc_strategy, to_host=False)
+        return self._evaluate(source, correlator, gc_strategy, to_host=False, group=group)
 
-    def _evaluate(self, source, correlator, gc_strategy, to_host):
+    def _evaluate(self, source, correlator, gc_strategy, to_host, group=None):
         assert nx.is_directed_acyclic_graph(self.to_graph())
-        size, n_dim = source.n, source.d
+        n_dim = source.d
         assert n_dim == self.num_distribution_nodes()
+        world, rank = 1, 0
+        if group is not None:
+            import torch.distributed as tdist
+
+            world, rank = tdist.get_world_size(group), tdist.get_rank(group)
+        if world > 1:
+            from .distributed import shard_bounds
+
+            rb = shard_bounds(source.n, world)
+            source.shard(rb[rank], rb[rank + 1] - rb[rank])
+        size = source.rows  # the rows this process evaluates
 
         if isinstance(correlator, str):
             correlator = {"imanconover": ImanConover, "cholesky": Cholesky}[correlator.lower()]
@@ -395,6 +412,9 @@ class Node(abc.ABC):
                      and set(all_variables) <= set(isns)
                      and all(type(v) is Distribution and v.distr in _DIST_SHAPES and v.is_leaf
                              for v in all_variables))
+        if world > 1 and correlations and not generated:
+            raise NotImplementedError("row-sharded evaluation correlates natively generated LHS columns of leaf "
+                                      "Distributions with Iman-Conover; evaluate this graph on one GPU")
         deferred = {}
         if correlations and set(all_variables) <= set(isns) and not generated:
             block = device.empty((len(all_variables), size))
@@ -425,10 +445,22 @@ class Node(abc.ABC):
             indexed = [(tuple(var_to_int[v] for v in vs), cm) for (vs, cm) in correlations]
             C = nearest_correlation_matrix(build_corrmat(indexed))
             inst = correlator().set_target(C)
-            if generated:
+            if generated and world > 1:
+                from .distributed import LHSColumn, iman_conover_lhs
+
                 cols = []
                 for var in all_variables:
-                    _, seed, n_total, col = deferred[var]
+                    _, seed, n_total, col, _ = deferred[var]
+                    cols.append(LHSColumn(seed, col, _lib.DIST_IDS[var.distr], [float(p) for p in var._params(size)]))
+                vflags = device.zeros(len(cols), "int32")
+                Y = iman_conover_lhs(cols, inst.P, source.n, group=group, flags=vflags)
+                for j, var in enumerate(all_variables):
+                    ev.flags[ev.slot[var]] += vflags[j]
+                    var._set_device(Y[j])
+            elif generated:
+                cols = []
+                for var in all_variables:
+                    _, seed, n_total, col, _ = deferred[var]
                     params = [float(p) for p in var._params(size)]
                     cols.append(_lib.ICColumn(seed, col, _lib.DIST_IDS[var.distr], (ctypes.c_double * 3)(*params),
                                               len(params), ev.flag_ptr(var)))
@@ -459,6 +491,10 @@ class Node(abc.ABC):
             gc.decrement_and_delete(node)
 
         # fused non-finite check (:600-606): first flagged node in topological order raises
+        if world > 1:  # every rank raises the same error
+            from .distributed import _all_reduce
+
+            _all_reduce(ev.flags, group, world)
         flags = device.to_host(ev.flags)
         if flags.any():
             for node in nx.topological_sort(G):
@@ -601,8 +637,8 @@ class Distribution(AbstractDistribution):
         lib = _lib.load()
         dist = _lib.DIST_IDS[self.distr]
         if column[0] == "lhs":
-            _, seed, n_total, col = column
-            _lib.check(lib.pbh_lhs_ppf(seed, n_total, 0, n, col, dist, arr, len(params), out.data_ptr(),
+            _, seed, n_total, col, row0 = column
+            _lib.check(lib.pbh_lhs_ppf(seed, n_total, row0, n, col, dist, arr, len(params), out.data_ptr(),
                                        ev.flag_ptr(self), device.stream()), f"{self}")
         else:
             _, q, stride = column

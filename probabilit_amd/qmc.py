@@ -142,6 +142,14 @@ class QuantileSource:
 
     def __init__(self, n, d):
         self.n, self.d, self._next = int(n), int(d), 0
+        self.row0, self.rows = 0, int(n)  # the rows this process evaluates (all, unless sharded)
+
+    def shard(self, row0, rows):
+        """Restrict generation to rows [row0, row0 + rows) of the n-row design (row-sharded
+        multi-GPU evaluation); generators are counter-addressed, so a shard is generated
+        without the others."""
+        self.row0, self.rows = int(row0), int(rows)
+        return self
 
     def next_column(self):
         if self._next >= self.d:
@@ -167,7 +175,7 @@ class DeviceMatrixSource(QuantileSource):
         self.q = q
 
     def column(self, c):
-        col = self.q[:, c]
+        col = self.q[self.row0:self.row0 + self.rows, c]
         return ("vector", col, col.stride(0))
 
 
@@ -177,9 +185,9 @@ class UniformSource(QuantileSource):
         self.seed = seed
 
     def column(self, c):
-        out = device.empty(self.n)
+        out = device.empty(self.rows)
         lib = _lib.load()
-        _lib.check(lib.pbh_fill_uniform(self.seed, 0, self.n, c, 1, out.data_ptr(), max(self.n, 1),
+        _lib.check(lib.pbh_fill_uniform(self.seed, self.row0, self.rows, c, 1, out.data_ptr(), max(self.rows, 1),
                                         device.stream()), "pbh_fill_uniform")
         return ("vector", out, 1)
 
@@ -190,13 +198,13 @@ class LHSSource(QuantileSource):
         self.seed = seed
 
     def column(self, c):
-        return ("lhs", self.seed, self.n, c)
+        return ("lhs", self.seed, self.n, c, self.row0)
 
     def materialize(self, c):
-        out = device.empty(self.n)
+        out = device.empty(self.rows)
         lib = _lib.load()
-        _lib.check(lib.pbh_fill_lhs(self.seed, self.n, 0, self.n, c, 1, out.data_ptr(), max(self.n, 1),
-                                    device.stream()), "pbh_fill_lhs")
+        _lib.check(lib.pbh_fill_lhs(self.seed, self.n, self.row0, self.rows, c, 1, out.data_ptr(),
+                                    max(self.rows, 1), device.stream()), "pbh_fill_lhs")
         return out
 
 
@@ -213,12 +221,12 @@ class SobolSource(QuantileSource):
         self.sv, self.shift = sobol_setup(d, rng, bits)
 
     def column(self, c):
-        out = device.empty(self.n)
+        out = device.empty(self.rows)
         lib = _lib.load()
         sv = np.ascontiguousarray(self.sv, dtype=np.uint32)
         sh = np.ascontiguousarray(self.shift, dtype=np.uint32)
-        _lib.check(lib.pbh_fill_sobol(_lib.np_ptr(sv), _lib.np_ptr(sh), self.d, self.bits, 0, self.n, c, 1,
-                                      out.data_ptr(), max(self.n, 1), device.stream()), "pbh_fill_sobol")
+        _lib.check(lib.pbh_fill_sobol(_lib.np_ptr(sv), _lib.np_ptr(sh), self.d, self.bits, self.row0, self.rows, c,
+                                      1, out.data_ptr(), max(self.rows, 1), device.stream()), "pbh_fill_sobol")
         return ("vector", out, 1)
 
 

@@ -1,0 +1,85 @@
+"""Row-sharded Iman-Conover (probabilit_amd/distributed.py) under the gloo
+backend with world size 1 and 2 on CPU: the exchange logic (run-head all-gather, sum and
+Gram all-reduces, the two all-to-alls) with numpy phases (tests/dist_cpu_phases.py), against
+the oracle's single-process ImanConover on the same LHS design.  The GPU phases of the same
+orchestrator are checked in test_gpu_distributed.py."""
+
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from oracle.ic import iman_conover
+from oracle.pipeline import cfg3_corr
+
+CASES = {
+    # (n, [(dist id, params)]): continuous + tied (poisson) columns, uneven shards
+    "mixed": (3001, [(0, [0.0, 1.0]), (6, [4.0, 0.0]), (5, [2.0, 0.0, 1.0]), (4, [0.3, 0.0, 1.0]),
+                     (6, [30.0, 0.0])]),
+    "two": (2048, [(0, [5.0, 2.0]), (5, [0.7, 0.0, 3.0])]),
+}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _columns(spec):
+    from probabilit_amd.distributed import LHSColumn
+
+    return [LHSColumn(0, c, d, p) for c, (d, p) in enumerate(spec)]
+
+
+def _worker(rank, world, port, case, outdir):
+    import torch
+    import torch.distributed as dist
+
+    from dist_cpu_phases import CpuPhases, design
+    from probabilit_amd.distributed import iman_conover_lhs
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, spec = CASES[case]
+        perms, us = design(n, len(spec), seed=3)
+        P = np.linalg.cholesky(cfg3_corr(len(spec)))
+        Y = iman_conover_lhs(_columns(spec), P, n, phases=CpuPhases(perms, us),
+                             flags=torch.zeros(len(spec), dtype=torch.int32))
+        np.save(os.path.join(outdir, f"y{rank}.npy"), Y.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_sharded_ic_matches_single_process_oracle(world, case):
+    from dist_cpu_phases import column_values, design
+    from probabilit_amd.distributed import shard_bounds
+
+    n, spec = CASES[case]
+    perms, us = design(n, len(spec), seed=3)
+    cols = _columns(spec)
+    X = np.column_stack([column_values(c, perms, us, n) for c in cols])
+    ref = iman_conover(X, cfg3_corr(len(spec)))["Y"]
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), case, d), nprocs=world, join=True,
+                           start_method="spawn")
+        parts = [np.load(os.path.join(d, f"y{r}.npy")) for r in range(world)]
+    b = shard_bounds(n, world)
+    for r, part in enumerate(parts):
+        assert part.shape == (len(spec), b[r + 1] - b[r])
+        np.testing.assert_array_equal(part.T, ref[b[r]:b[r + 1]])
+
+
+def test_shard_bounds_cover_rows():
+    from probabilit_amd.distributed import shard_bounds
+
+    for n in (1, 7, 4096, 100_000_001):
+        for w in (1, 2, 3, 8):
+            b = shard_bounds(n, w)
+            assert b[0] == 0 and b[-1] == n and all(b[i] <= b[i + 1] for i in range(w))

@@ -88,6 +88,22 @@ def test_ic_outputs_vs_oracle_placement_path(gpu, n, k):
     np.testing.assert_array_equal(Y, ref["Y"])
 
 
+def test_ic_exact_ties_in_correlated_scores(gpu):
+    """Duplicated rows of X give identical scores rows, so CS has exact ties: their 'average'
+    rank is shared (correlation.py:422), which the placement path must reproduce."""
+    from oracle import ic as oic
+    from oracle.pipeline import cfg3_corr
+    from probabilit_amd.correlation import ImanConover
+
+    rng = np.random.default_rng(4)
+    X = rng.normal(size=(20_000, 3))
+    X[100:140] = X[0:40]  # 40 duplicated rows -> 40 tie runs of length 2 in every CS column
+    X[7000:7003] = X[9000]  # and a run of 4
+    C = cfg3_corr(3)
+    ref = oic.iman_conover(X, C)
+    np.testing.assert_array_equal(ImanConover().set_target(C)(X), ref["Y"])
+
+
 def test_ic_properties_large(gpu):
     """N = 4M, K = 32: marginals preserved exactly, rank correlation near the target."""
     import torch
