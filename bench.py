@@ -6,7 +6,7 @@ through the public DAG API: native LHS fused into the 32 inverse-CDF kernels (no
 triang / poisson x 4, BASELINE config 2 set), then the Iman-Conover reorder of all 32 columns
 (rank + scores + Gram + decorrelate/correlate + rank + gather); outputs stay in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n ROWS] [--d COLS] [--cpu-n ROWS]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows ROWS] [--d COLS] [--cpu-n ROWS]
 
 With N > 1 (torch.distributed.run, one process per GPU, RCCL) the same N-row problem is
 row-sharded across the ranks (BASELINE config 4; strong scaling): rank r generates and
@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--d", type=int, default=32)
     ap.add_argument("--cpu-n", type=int, default=262_144)
     ap.add_argument("--no-cpu", action="store_true")
@@ -74,7 +74,7 @@ def main():
     from probabilit_amd.modeling import Distribution, NoOp
 
     dev = device.device()
-    n, d = args.n, args.d
+    n, d = args.rows, args.d
     base = [("norm", {"loc": 0.0, "scale": 1.0}), ("gamma", {"a": 2.0}), ("triang", {"c": 0.3}),
             ("poisson", {"mu": 4.0}), ("norm", {"loc": 5.0, "scale": 2.0}), ("gamma", {"a": 0.7, "scale": 3.0}),
             ("triang", {"c": 0.8, "loc": 1.0, "scale": 2.0}), ("poisson", {"mu": 30.0})]

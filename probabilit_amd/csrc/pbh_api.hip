@@ -56,6 +56,7 @@ struct IcLayout {
   double* tmp;                  // n doubles: fallback X column, or the run heads (u32) of a tied column
   unsigned long long* counts;   // ties, inversions of a generated sorted column
   void* heads_ws;
+  uint32_t* codes;              // K x n step-4 sort keys, written by the step-3 kernel
 };
 
 size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
@@ -73,7 +74,9 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* tmp = c.take((size_t)n * 8);
   void* counts = c.take(256);
   void* hws = c.take(run_heads_ws_bytes(n));
+  void* codes = c.take((size_t)n * k * 4);
   if (carve) {
+    L->codes = (uint32_t*)codes;
     L->S = (double*)S;
     L->sorted_x = (double*)sx;
     L->reorder_ws = rws;
@@ -252,7 +255,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   PBH_CHECK_HIP(hipMemcpyAsync(L.P, P.data(), (size_t)k * k * 8, hipMemcpyHostToDevice, s));
 
   // ---- step 3: CS = (S L^-T) P^T, in place
-  st = apply_decorrelate_correlate(L.S, n, k, n, L.L, L.inv_diag, L.P, s);
+  st = apply_decorrelate_correlate(L.S, n, k, n, L.L, L.inv_diag, L.P, s, L.codes, n, &rw.cm);
   if (st) return st;
   if (a->cscores_out)
     PBH_CHECK_HIP(hipMemcpyAsync(a->cscores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
@@ -260,7 +263,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   // ---- step 4: Y[:, c] = sort(X[:, c])[rankdata(CS[:, c]).astype(int) - 1]
   for (int c = 0; c < k; ++c) {
     st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
-                        a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s);
+                        a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n);
     if (st) return st;
   }
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // host vectors above were sources of async copies

@@ -51,15 +51,27 @@ struct CodeMap {
   const double* scale;   // m slopes (codes per unit x)
 };
 constexpr int kCodeSegments = 8192;
+__device__ __forceinline__ uint32_t code_of(double x, const CodeMap& c) {
+  double u = (x - c.x0) * c.inv_w;
+  if (!(u >= 0.0)) return 0u;
+  if (u >= (double)c.m) return 0xFFFFFFFFu;
+  int j = (int)u;
+  double lo = c.x0 + (double)j * c.w;
+  uint32_t b0 = c.base[j], cnt = c.base[j + 1] - b0;
+  double off = floor((x - lo) * c.scale[j]);
+  uint32_t o = off <= 0.0 ? 0u : (off >= (double)(cnt - 1) ? cnt - 1 : (uint32_t)off);
+  return b0 + o;
+}
 size_t code_map_bytes();
 // Host: fill base / scale for N(0, 1)-shaped data into the host buffers.
 void code_map_host(uint32_t* base, double* scale, double* x0, double* w);
 int make_codes(const double* x, int64_t n, const CodeMap& cm, uint32_t* codes, hipStream_t s);
 // rows_out = rows with every run of equal codes (length <= 16) ordered by the full value
-// x[row]; eqprev[i] = element i equals element i - 1.  *flags |= 1 when a run is longer
-// (the caller falls back to 64-bit keys), |= 2 when any exact tie exists.
+// x[row]; eqprev[i] = element i equals element i - 1.  flags[0] |= 1 when a run is longer
+// (the caller falls back to 64-bit keys), |= 2 when any exact tie exists; flags[1] is used as
+// the run counter.  starts: scratch for up to n / 2 run starts.
 int resolve_code_runs(const uint32_t* codes, const uint32_t* rows, uint32_t* rows_out, const double* x, int64_t n,
-                      uint8_t* eqprev, int32_t* flags, hipStream_t s);
+                      uint8_t* eqprev, int32_t* flags, uint32_t* starts, hipStream_t s);
 
 // dst = src, then dst[p] = src[s + (e - s) / 2] inside every tie run [s, e] flagged by eqprev:
 // the value every member of a tie run receives in step 4 (int of the 'average' rank).
@@ -76,8 +88,10 @@ int centered_gram(const double* S, int64_t n, int k, int64_t ld, const double* m
                   double* gram, hipStream_t s);
 // In place, per row r: d = forward-substitute(L, s_r) (d_j = (s_j - sum_{m<j} L_jm d_m) * inv_diag_j),
 // then cs_j = sum_{m<=j} P_jm d_m.   L, P: k x k row-major device, inv_diag: k.
+// With codes != NULL (and cm), also codes[c * ldc + r] = code_of(CS[r][c]) (step 4's keys).
 int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const double* L, const double* inv_diag,
-                                const double* P, hipStream_t s);
+                                const double* P, hipStream_t s, uint32_t* codes = nullptr, int64_t ldc = 0,
+                                const CodeMap* cm = nullptr);
 
 // ---------------------------------------------------------------- shared orchestration pieces
 // Host, step 2 (correlation.py:398-405): G = centered Gram (k x k, row-major) of scores over n
@@ -99,7 +113,8 @@ size_t reorder_ws_bytes(int64_t n);
 // Carves ws and uploads the code map (stream ordered).
 int reorder_carve(void* ws, int64_t n, ReorderWs& w, hipStream_t s);
 // y[r * y_rs] = sorted_src[rank(cs[r]) - 1]; idx[r] = rank - 1 when idx != NULL.
+// codes (optional): code_of(cs) already computed (by the step-3 kernel); not modified.
 int reorder_column(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx,
-                   ReorderWs& w, hipStream_t s);
+                   ReorderWs& w, hipStream_t s, const uint32_t* codes = nullptr);
 
 }  // namespace pbh

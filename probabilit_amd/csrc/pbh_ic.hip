@@ -447,7 +447,8 @@ __global__ void k_gram_rows_reduce(const double* __restrict__ partials, int nb, 
 template <int KMAX>
 __global__ __launch_bounds__(256) void k_apply(double* __restrict__ S, int64_t n, int k, int64_t ld,
                                               const double* __restrict__ L, const double* __restrict__ inv_diag,
-                                              const double* __restrict__ P) {
+                                              const double* __restrict__ P, uint32_t* __restrict__ codes,
+                                              int64_t ldc, CodeMap cm) {
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
     double v[KMAX];
 #pragma unroll
@@ -475,6 +476,11 @@ __global__ __launch_bounds__(256) void k_apply(double* __restrict__ S, int64_t n
 #pragma unroll
     for (int m = 0; m < KMAX; ++m)
       if (m < k) S[(int64_t)m * ld + r] = v[m];
+    if (codes) {  // step 4's sort keys, while the row is in registers
+#pragma unroll
+      for (int m = 0; m < KMAX; ++m)
+        if (m < k) codes[(int64_t)m * ldc + r] = code_of(v[m], cm);
+    }
   }
 }
 
@@ -589,18 +595,21 @@ int centered_gram(const double* S, int64_t n, int k, int64_t ld, const double* m
 }
 
 int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const double* L, const double* inv_diag,
-                                const double* P, hipStream_t s) {
+                                const double* P, hipStream_t s, uint32_t* codes, int64_t ldc, const CodeMap* cm) {
   dim3 g(grid_for(n, 256, 8192)), b(256);
+  CodeMap c = cm ? *cm : CodeMap{};
+  if (!cm) codes = nullptr;
   if (k <= 8)
-    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<8>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<8>, g, b, 0, s, S, n, k, ld, L, inv_diag, P, codes, ldc, c));
   else if (k <= 16)
-    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<16>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<16>, g, b, 0, s, S, n, k, ld, L, inv_diag, P, codes, ldc, c));
   else if (k <= 32)
-    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<32>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<32>, g, b, 0, s, S, n, k, ld, L, inv_diag, P, codes, ldc, c));
   else if (k <= 64)
-    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<64>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<64>, g, b, 0, s, S, n, k, ld, L, inv_diag, P, codes, ldc, c));
   else if (k <= 128)
-    PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<128>, g, b, 0, s, S, n, k, ld, L, inv_diag, P));
+    PBH_TIMED(kKApply, s,
+              hipLaunchKernelGGL(k_apply<128>, g, b, 0, s, S, n, k, ld, L, inv_diag, P, codes, ldc, c));
   else {
     set_error("Iman-Conover: K = %d exceeds the supported maximum of 128 variables", k);
     return PBH_ERR_UNSUPPORTED;
@@ -610,18 +619,6 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
 }
 
 // ---------------------------------------------------------------- 32-bit codes of the scores
-__device__ __forceinline__ uint32_t code_of(double x, const CodeMap& c) {
-  double u = (x - c.x0) * c.inv_w;
-  if (!(u >= 0.0)) return 0u;
-  if (u >= (double)c.m) return 0xFFFFFFFFu;
-  int j = (int)u;
-  double lo = c.x0 + (double)j * c.w;
-  uint32_t b0 = c.base[j], cnt = c.base[j + 1] - b0;
-  double off = floor((x - lo) * c.scale[j]);
-  uint32_t o = off <= 0.0 ? 0u : (off >= (double)(cnt - 1) ? cnt - 1 : (uint32_t)off);
-  return b0 + o;
-}
-
 static __global__ __launch_bounds__(256) void k_make_codes(const double* __restrict__ x, int64_t n, CodeMap cm,
                                                           uint32_t* __restrict__ codes) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
@@ -630,72 +627,91 @@ static __global__ __launch_bounds__(256) void k_make_codes(const double* __restr
 
 constexpr int kMaxRun = 16;
 
-// One thread per 4 sorted positions (16-byte loads and stores).  Outside runs of equal
-// codes (~98% of positions for N(0, 1) scores at N = 1e8) the rows are copied; inside a run
-// (length <= kMaxRun) each element counts the members that precede it in (value, position)
-// order, which is its place in the run, and flags a tie when an earlier member has the same
-// value.  eqprev must be zeroed by the caller; only tied positions are written.
-// flags: bit 0 = a run longer than kMaxRun, bit 1 = an exact tie.
-__device__ __forceinline__ void code_run_one(const uint32_t* __restrict__ code, const uint32_t* __restrict__ rows,
-                                             uint32_t* __restrict__ rows_out, const double* __restrict__ x, int64_t n,
-                                             uint8_t* __restrict__ eqprev, int32_t* flags, int64_t p) {
-  const uint32_t c = code[p];
-  const uint32_t r = rows[p];
-  const bool prev_same = p > 0 && code[p - 1] == c;
-  const bool next_same = p + 1 < n && code[p + 1] == c;
-  if (!prev_same && !next_same) {
-    rows_out[p] = r;
-    return;
-  }
-  int64_t s = p, e = p;
-  bool too_long = false;
-  while (s > 0 && code[s - 1] == c) {
-    if (--s <= p - kMaxRun) {
-      too_long = true;
-      break;
-    }
-  }
-  while (!too_long && e + 1 < n && code[e + 1] == c) {
-    if (++e - s + 1 > kMaxRun) too_long = true;
-  }
-  if (too_long) {
-    atomicOr(flags, 1);
-    return;
-  }
-  const double v = x[r];
-  int pos = 0;
-  bool tie = false;
-  for (int64_t j = s; j <= e; ++j) {
-    if (j == p) continue;
-    const double w = x[rows[j]];
-    pos += (w < v || (w == v && j < p)) ? 1 : 0;
-    tie |= (w == v && j < p);
-  }
-  rows_out[s + pos] = r;
-  if (tie) {
-    eqprev[s + pos] = 1;
-    atomicOr(flags, 2);
-  }
-}
-
-static __global__ __launch_bounds__(256) void k_code_runs(const uint32_t* __restrict__ code,
+// Runs of equal codes, two phases.  Phase 1 streams the sorted (code, row) pairs with 16-byte
+// accesses: rows are copied to rows_out and the start of every run of equal codes (~1% of
+// positions for N(0, 1) scores at N = 1e8) is appended to a list (one atomic per wave).
+// Phase 2 takes one run per thread: a member's place in its run is the number of members
+// before it in (value, position) order, ties with an earlier member are flagged in eqprev.
+// flags: bit 0 = a run longer than kMaxRun (caller falls back to 64-bit keys), bit 1 = a tie.
+static __global__ __launch_bounds__(256) void k_runs_copy(const uint32_t* __restrict__ code,
                                                          const uint32_t* __restrict__ rows,
-                                                         uint32_t* __restrict__ rows_out, const double* __restrict__ x,
-                                                         int64_t n, uint8_t* __restrict__ eqprev, int32_t* flags) {
+                                                         uint32_t* __restrict__ rows_out, int64_t n,
+                                                         uint32_t* __restrict__ starts, uint32_t* nstarts) {
   const int64_t nq = (n + 3) / 4;
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t q0 = (int64_t)blockIdx.x * 256; q0 < nq; q0 += (int64_t)gridDim.x * 256) {
+    const int64_t q = q0 + threadIdx.x;
     const int64_t p0 = q * 4;
+    uint32_t found = 0;  // bit i: position p0 + i starts a run
     if (p0 + 4 <= n) {
       const uint4 c = *(const uint4*)(code + p0);
       const uint32_t cprev = p0 > 0 ? code[p0 - 1] : ~c.x;
       const uint32_t cnext = p0 + 4 < n ? code[p0 + 4] : ~c.w;
-      const bool run = (cprev == c.x) | (c.x == c.y) | (c.y == c.z) | (c.z == c.w) | (c.w == cnext);
-      if (!run) {
-        *(uint4*)(rows_out + p0) = *(const uint4*)(rows + p0);
-        continue;
+      *(uint4*)(rows_out + p0) = *(const uint4*)(rows + p0);
+      found = (uint32_t)(c.x == c.y && cprev != c.x) | ((uint32_t)(c.y == c.z && c.x != c.y) << 1) |
+              ((uint32_t)(c.z == c.w && c.y != c.z) << 2) | ((uint32_t)(c.w == cnext && c.z != c.w) << 3);
+    } else if (p0 < n) {
+      for (int64_t p = p0; p < n; ++p) {
+        rows_out[p] = rows[p];
+        const bool start = p + 1 < n && code[p + 1] == code[p] && (p == 0 || code[p - 1] != code[p]);
+        found |= (uint32_t)start << (p - p0);
       }
     }
-    for (int64_t p = p0; p < p0 + 4 && p < n; ++p) code_run_one(code, rows, rows_out, x, n, eqprev, flags, p);
+    const int cnt = __popc(found);
+    // wave-aggregated append
+    int excl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(excl, o, 64);
+      if (lane >= o) excl += y;
+    }
+    const int total = __shfl(excl, 63, 64);
+    excl -= cnt;
+    uint32_t base = 0;
+    if (lane == 0 && total) base = atomicAdd(nstarts, (uint32_t)total);
+    base = __shfl(base, 0, 64);
+    uint32_t k = base + (uint32_t)excl;
+    for (int i = 0; i < 4; ++i)
+      if (found & (1u << i)) starts[k++] = (uint32_t)(p0 + i);
+  }
+}
+
+static __global__ __launch_bounds__(256) void k_runs_resolve(const uint32_t* __restrict__ code,
+                                                            const uint32_t* __restrict__ rows,
+                                                            uint32_t* __restrict__ rows_out,
+                                                            const double* __restrict__ x, int64_t n,
+                                                            const uint32_t* __restrict__ starts,
+                                                            const uint32_t* nstarts, uint8_t* __restrict__ eqprev,
+                                                            int32_t* flags) {
+  const uint32_t m = *nstarts;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < m; i += gridDim.x * 256) {
+    const int64_t s = starts[i];
+    const uint32_t c = code[s];
+    int64_t e = s + 1;
+    while (e + 1 < n && code[e + 1] == c && e - s + 1 <= kMaxRun) ++e;
+    if (e - s + 1 > kMaxRun) {
+      atomicOr(flags, 1);
+      continue;
+    }
+    bool any_tie = false;
+    for (int64_t p = s; p <= e; ++p) {
+      const uint32_t r = rows[p];
+      const double v = x[r];
+      int pos = 0;
+      bool tie = false;
+      for (int64_t j = s; j <= e; ++j) {
+        if (j == p) continue;
+        const double w = x[rows[j]];
+        pos += (w < v || (w == v && j < p)) ? 1 : 0;
+        tie |= (w == v && j < p);
+      }
+      rows_out[s + pos] = r;
+      if (tie) {
+        eqprev[s + pos] = 1;
+        any_tie = true;
+      }
+    }
+    if (any_tie) atomicOr(flags, 2);
   }
 }
 
@@ -757,11 +773,15 @@ int make_codes(const double* x, int64_t n, const CodeMap& cm, uint32_t* codes, h
 }
 
 int resolve_code_runs(const uint32_t* codes, const uint32_t* rows, uint32_t* rows_out, const double* x, int64_t n,
-                      uint8_t* eqprev, int32_t* flags, hipStream_t s) {
+                      uint8_t* eqprev, int32_t* flags, uint32_t* starts, hipStream_t s) {
+  uint32_t* nstarts = (uint32_t*)(flags + 1);
   PBH_TIMED(kKCodeRuns, s,
             hipMemsetAsync(eqprev, 0, (size_t)n, s);
-            hipLaunchKernelGGL(k_code_runs, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, s, codes, rows,
-                               rows_out, x, n, eqprev, flags));
+            hipMemsetAsync(nstarts, 0, sizeof(uint32_t), s);
+            hipLaunchKernelGGL(k_runs_copy, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, s, codes, rows,
+                               rows_out, n, starts, nstarts);
+            hipLaunchKernelGGL(k_runs_resolve, dim3(1024), dim3(256), 0, s, codes, rows, rows_out, x, n, starts,
+                               nstarts, eqprev, flags));
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }

@@ -107,7 +107,7 @@ int reorder_carve(void* ws, int64_t n, ReorderWs& w, hipStream_t s) {
 // rank - 1 of row r is its sorted position, and Y is written by the LDS row placement; exact
 // ties use the tie-aware gather, and a run longer than kMaxRun the 64-bit sort.
 int reorder_column(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx,
-                   ReorderWs& w, hipStream_t s) {
+                   ReorderWs& w, hipStream_t s, const uint32_t* codes) {
   SortBuffers& sb = w.sb;
   RankOut out = {};
   out.sorted_src = sorted_src;
@@ -115,12 +115,16 @@ int reorder_column(const double* cs, int64_t n, const double* sorted_src, double
   out.y_rs = y_rs;
   out.idx = idx;
   int buf = 0;
-  int st = make_codes(cs, n, w.cm, (uint32_t*)sb.keys[0], s);
-  if (st) return st;
-  st = radix_sort_keys32(sb, n, s, &buf);
+  int st;
+  if (!codes) {
+    st = make_codes(cs, n, w.cm, (uint32_t*)sb.keys[0], s);
+    if (st) return st;
+  }
+  st = radix_sort_keys32(sb, n, s, &buf, codes);
   if (st) return st;
   PBH_CHECK_HIP(hipMemsetAsync(w.flags, 0, sizeof(int32_t), s));
-  st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], sb.vals[buf ^ 1], cs, n, w.eqprev, w.flags, s);
+  st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], sb.vals[buf ^ 1], cs, n, w.eqprev, w.flags,
+                         (uint32_t*)sb.keys[buf ^ 1], s);
   if (st) return st;
   int32_t run_flags = 0;
   PBH_CHECK_HIP(hipMemcpyAsync(&run_flags, w.flags, sizeof(int32_t), hipMemcpyDeviceToHost, s));

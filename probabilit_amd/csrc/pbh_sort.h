@@ -44,8 +44,9 @@ void sort_carve(void* ws, int64_t n, SortBuffers& b);
 int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf);
 // In-place exclusive scan of m uint32 counts (partials: scan_partials_count(m) entries).
 int exclusive_scan_u32(uint32_t* a, int64_t m, uint32_t* partials, hipStream_t s);
-// The same on uint32 keys stored in b.keys[0] (reinterpreted): at most 4 passes.
-int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf);
+// The same on uint32 keys stored in b.keys[0] (reinterpreted), or read from `in` (left
+// unmodified): at most 4 passes.
+int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, const uint32_t* in = nullptr);
 
 // Y[rows[p] * y_rs] = v[p] for a permutation `rows` of [0, n): the inverse-permutation write
 // of Iman-Conover step 4 (correlation.py:423) without random 8-byte stores.  LSD bucket passes

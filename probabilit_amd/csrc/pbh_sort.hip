@@ -231,11 +231,13 @@ __global__ __launch_bounds__(T) void k_scatter(const K* __restrict__ kin, const 
 // that started before it: the look-back always terminates.
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62, kCountMask = (1ull << 62) - 1;
 
-template <typename K, typename V>
+template <typename K, typename V, int IPTT>
 __global__ __launch_bounds__(T) void k_onesweep(const K* __restrict__ kin, const V* __restrict__ vin,
                                                K* __restrict__ kout, V* __restrict__ vout, int64_t n, int shift,
                                                const uint32_t* __restrict__ digit_base, uint64_t* status,
                                                uint32_t* tile_counter) {
+  constexpr int IPT = IPTT;
+  constexpr int TILE = T * IPTT;
   __shared__ K skeys[TILE];
   __shared__ V svals[TILE];
   __shared__ uint32_t wcnt[4][256];
@@ -363,6 +365,29 @@ __global__ __launch_bounds__(256) void k_place_bases(int64_t n, int shift, uint3
   bases[d] = block_exclusive_scan_256((uint32_t)count, sh, nullptr);
 }
 
+// Items per thread of the one-sweep scatter (tile = 256 x items): PBH_OS_IPT = 16 or 32.
+int onesweep_items() {
+  static const int v = [] {
+    const char* e = getenv("PBH_OS_IPT");
+    return (e && atoi(e) == 32) ? 32 : 16;
+  }();
+  return v;
+}
+
+template <typename K, typename V>
+void launch_onesweep(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
+                     uint64_t* status, uint32_t* counter, hipStream_t s) {
+  if (onesweep_items() == 32) {
+    const int64_t nt = (n + T * 32 - 1) / (T * 32);
+    hipLaunchKernelGGL((k_onesweep<K, V, 32>), dim3((unsigned)nt), dim3(T), 0, s, kin, vin, kout, vout, n, shift,
+                       bases, status, counter);
+  } else {
+    const int64_t nt = (n + T * 16 - 1) / (T * 16);
+    hipLaunchKernelGGL((k_onesweep<K, V, 16>), dim3((unsigned)nt), dim3(T), 0, s, kin, vin, kout, vout, n, shift,
+                       bases, status, counter);
+  }
+}
+
 bool onesweep_enabled() {
   static const bool on = [] {
     const char* e = getenv("PBH_SORT");
@@ -406,9 +431,8 @@ int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, in
       PBH_CHECK_LAUNCH();
       PBH_CHECK_HIP(hipMemsetAsync(pb.status, 0, (size_t)nt * 256 * 8 + 256, s));  // words, counter, flag
       PBH_TIMED(kKPlaceScatter, s,
-                hipLaunchKernelGGL((k_onesweep<uint32_t, double>), dim3((unsigned)nt), dim3(T), 0, s, rin, vin,
-                                   pb.rows[cur], pb.vals[cur], n, shift, pb.bases, pb.status,
-                                   (uint32_t*)(pb.status + nt * 256)));
+                launch_onesweep<uint32_t, double>(rin, vin, pb.rows[cur], pb.vals[cur], n, shift, pb.bases, pb.status,
+                                                  (uint32_t*)(pb.status + nt * 256), s));
       PBH_CHECK_LAUNCH();
       rin = pb.rows[cur];
       vin = pb.vals[cur];
@@ -481,15 +505,16 @@ void sort_carve(void* ws, int64_t n, SortBuffers& sb) {
 }
 
 template <typename K>
-int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
+int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, const K* in = nullptr) {
   constexpr int NB = sizeof(K);
   PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "radix sort: n out of range");
   const int64_t nt = sort_tiles(n);
   K* keys[2] = {(K*)b.keys[0], (K*)b.keys[1]};
+  const K* first = in ? in : keys[0];  // pass 0 reads here and writes keys[1]
   // which byte positions vary?
   PBH_CHECK_HIP(hipMemsetAsync(b.hist, 0, 8 * 256 * 4, s));
   PBH_TIMED(NB == 8 ? kKSortDigitHist : kKSortDigitHist32, s,
-            hipLaunchKernelGGL(k_digit_hist<K>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, keys[0], n, b.hist));
+            hipLaunchKernelGGL(k_digit_hist<K>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, first, n, b.hist));
   PBH_CHECK_LAUNCH();
   PBH_CHECK_HIP(hipMemcpyAsync(b.hist_host, b.hist, NB * 256 * 4, hipMemcpyDeviceToHost, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));
@@ -509,9 +534,9 @@ int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
       const int shift = 8 * passes[ip];
       PBH_CHECK_HIP(hipMemsetAsync(b.status, 0, (size_t)nt * 256 * 8 + 4, s));  // words + tile counter
       PBH_TIMED(NB == 8 ? kKSortScatter : kKSortScatter32, s,
-                hipLaunchKernelGGL((k_onesweep<K, uint32_t>), dim3((unsigned)nt), dim3(T), 0, s, keys[cur],
-                                   ip == 0 ? nullptr : b.vals[cur], keys[cur ^ 1], b.vals[cur ^ 1], n, shift,
-                                   b.bases + passes[ip] * 256, b.status, (uint32_t*)(b.status + nt * 256)));
+                launch_onesweep<K, uint32_t>(ip == 0 ? first : keys[cur], ip == 0 ? nullptr : b.vals[cur],
+                                             keys[cur ^ 1], b.vals[cur ^ 1], n, shift, b.bases + passes[ip] * 256,
+                                             b.status, (uint32_t*)(b.status + nt * 256), s));
       PBH_CHECK_LAUNCH();
       cur ^= 1;
     }
@@ -528,12 +553,13 @@ int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
   for (int ip = 0; ip < npass; ++ip) {
     const int shift = 8 * passes[ip];
     PBH_TIMED(NB == 8 ? kKSortUpsweep : kKSortUpsweep32, s,
-              hipLaunchKernelGGL(k_upsweep<K>, dim3((unsigned)nt), dim3(T), 0, s, keys[cur], n, shift, b.counts, nt));
+              hipLaunchKernelGGL(k_upsweep<K>, dim3((unsigned)nt), dim3(T), 0, s, ip == 0 ? first : keys[cur], n,
+                                 shift, b.counts, nt));
     PBH_CHECK_LAUNCH();
     int st = exclusive_scan_u32(b.counts, 256 * nt, b.partials, s);
     if (st != PBH_OK) return st;
     PBH_TIMED(NB == 8 ? kKSortScatter : kKSortScatter32, s,
-              hipLaunchKernelGGL(k_scatter<K>, dim3((unsigned)nt), dim3(T), 0, s, keys[cur],
+              hipLaunchKernelGGL(k_scatter<K>, dim3((unsigned)nt), dim3(T), 0, s, ip == 0 ? first : keys[cur],
                                  ip == 0 ? nullptr : b.vals[cur], keys[cur ^ 1], b.vals[cur ^ 1], n, shift, b.counts,
                                  nt));
     PBH_CHECK_LAUNCH();
@@ -547,8 +573,8 @@ int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
   return radix_sort_impl<uint64_t>(b, n, s, out_buf);
 }
 
-int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
-  return radix_sort_impl<uint32_t>(b, n, s, out_buf);
+int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, const uint32_t* in) {
+  return radix_sort_impl<uint32_t>(b, n, s, out_buf, in);
 }
 
 }  // namespace pbh
