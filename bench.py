@@ -64,7 +64,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        # modulo: PBH_DIST_BACKEND=gloo rehearses several ranks on a one-GPU box
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
         # RCCL; PBH_DIST_BACKEND=gloo rehearses the sharded path with several ranks on one GPU
         dist.init_process_group(os.environ.get("PBH_DIST_BACKEND", "nccl"))
     else:

@@ -66,12 +66,12 @@ size_t code_map_bytes();
 // Host: fill base / scale for N(0, 1)-shaped data into the host buffers.
 void code_map_host(uint32_t* base, double* scale, double* x0, double* w);
 int make_codes(const double* x, int64_t n, const CodeMap& cm, uint32_t* codes, hipStream_t s);
-// rows_out = rows with every run of equal codes (length <= 16) ordered by the full value
-// x[row]; eqprev[i] = element i equals element i - 1.  flags[0] |= 1 when a run is longer
-// (the caller falls back to 64-bit keys), |= 2 when any exact tie exists; flags[1] is used as
-// the run counter.  starts: scratch for up to n / 2 run starts.
-int resolve_code_runs(const uint32_t* codes, const uint32_t* rows, uint32_t* rows_out, const double* x, int64_t n,
-                      uint8_t* eqprev, int32_t* flags, uint32_t* starts, hipStream_t s);
+// Reorders `rows` in place so that every run of equal codes (length <= 16) is ordered by the
+// full value x[row]; eqprev[i] = element i equals element i - 1.  flags[0] |= 1 when a run is
+// longer (the caller falls back to 64-bit keys), |= 2 when any exact tie exists.
+// starts: scratch for n / 2 + 2048 run starts; counts: 2048 per-block counters.
+int resolve_code_runs(const uint32_t* codes, uint32_t* rows, const double* x, int64_t n, uint8_t* eqprev,
+                      int32_t* flags, uint32_t* starts, uint32_t* counts, hipStream_t s);
 
 // dst = src, then dst[p] = src[s + (e - s) / 2] inside every tie run [s, e] flagged by eqprev:
 // the value every member of a tie run receives in step 4 (int of the 'average' rank).

@@ -627,38 +627,52 @@ static __global__ __launch_bounds__(256) void k_make_codes(const double* __restr
 
 constexpr int kMaxRun = 16;
 
-// Runs of equal codes, two phases.  Phase 1 streams the sorted (code, row) pairs with 16-byte
-// accesses: rows are copied to rows_out and the start of every run of equal codes (~1% of
-// positions for N(0, 1) scores at N = 1e8) is appended to a list (one atomic per wave).
-// Phase 2 takes one run per thread: a member's place in its run is the number of members
-// before it in (value, position) order, ties with an earlier member are flagged in eqprev.
+// Runs of equal codes, two phases.  Phase 1 streams the sorted codes with 16-byte loads:
+// block b owns the contiguous positions [b * chunk, (b + 1) * chunk) and appends the start of
+// every run of equal codes in it (~1% of positions for N(0, 1) scores at N = 1e8) to its own
+// region of `starts` (a run has >= 2 members, so <= chunk / 2 + 1 entries), one LDS atomic per
+// wave and no global atomics: the single global counter of a previous version serialised
+// ~4e5 atomics per column at N = 1e8 (4 ms).  Phase 2 takes one run per thread and reorders it
+// in place: a member's place in its run is the number of members before it in (value, position)
+// order; ties with an earlier member are flagged in eqprev.
 // flags: bit 0 = a run longer than kMaxRun (caller falls back to 64-bit keys), bit 1 = a tie.
-static __global__ __launch_bounds__(256) void k_runs_copy(const uint32_t* __restrict__ code,
-                                                         const uint32_t* __restrict__ rows,
-                                                         uint32_t* __restrict__ rows_out, int64_t n,
-                                                         uint32_t* __restrict__ starts, uint32_t* nstarts) {
-  const int64_t nq = (n + 3) / 4;
+constexpr int kRunBlocks = 2048;
+
+static inline int64_t run_chunk(int64_t n, int64_t* nb) {
+  int64_t c = (n + kRunBlocks - 1) / kRunBlocks;
+  c = (c + 1023) / 1024 * 1024;
+  *nb = (n + c - 1) / c;
+  return c;
+}
+// run starts a block can hold: a run has >= 2 members, so <= min(chunk, n) / 2 + 1
+PBH_HD inline int64_t run_stride(int64_t n, int64_t chunk) { return (chunk < n ? chunk : n) / 2 + 1; }
+
+static __global__ __launch_bounds__(256) void k_runs_scan(const uint32_t* __restrict__ code, int64_t n, int64_t chunk,
+                                                         uint32_t* __restrict__ starts,
+                                                         uint32_t* __restrict__ counts) {
+  __shared__ uint32_t cnt_sh;
   const int lane = threadIdx.x & 63;
-  for (int64_t q0 = (int64_t)blockIdx.x * 256; q0 < nq; q0 += (int64_t)gridDim.x * 256) {
-    const int64_t q = q0 + threadIdx.x;
-    const int64_t p0 = q * 4;
+  if (threadIdx.x == 0) cnt_sh = 0;
+  __syncthreads();
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  uint32_t* out = starts + (int64_t)blockIdx.x * run_stride(n, chunk);
+  for (int64_t q0 = lo; q0 < hi; q0 += 1024) {
+    const int64_t p0 = q0 + 4 * (int64_t)threadIdx.x;
     uint32_t found = 0;  // bit i: position p0 + i starts a run
-    if (p0 + 4 <= n) {
+    if (p0 + 4 <= hi) {
       const uint4 c = *(const uint4*)(code + p0);
       const uint32_t cprev = p0 > 0 ? code[p0 - 1] : ~c.x;
       const uint32_t cnext = p0 + 4 < n ? code[p0 + 4] : ~c.w;
-      *(uint4*)(rows_out + p0) = *(const uint4*)(rows + p0);
       found = (uint32_t)(c.x == c.y && cprev != c.x) | ((uint32_t)(c.y == c.z && c.x != c.y) << 1) |
               ((uint32_t)(c.z == c.w && c.y != c.z) << 2) | ((uint32_t)(c.w == cnext && c.z != c.w) << 3);
-    } else if (p0 < n) {
-      for (int64_t p = p0; p < n; ++p) {
-        rows_out[p] = rows[p];
+    } else {
+      for (int64_t p = p0; p < hi; ++p) {
         const bool start = p + 1 < n && code[p + 1] == code[p] && (p == 0 || code[p - 1] != code[p]);
         found |= (uint32_t)start << (p - p0);
       }
     }
     const int cnt = __popc(found);
-    // wave-aggregated append
     int excl = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -668,24 +682,26 @@ static __global__ __launch_bounds__(256) void k_runs_copy(const uint32_t* __rest
     const int total = __shfl(excl, 63, 64);
     excl -= cnt;
     uint32_t base = 0;
-    if (lane == 0 && total) base = atomicAdd(nstarts, (uint32_t)total);
+    if (lane == 0 && total) base = atomicAdd(&cnt_sh, (uint32_t)total);
     base = __shfl(base, 0, 64);
     uint32_t k = base + (uint32_t)excl;
     for (int i = 0; i < 4; ++i)
-      if (found & (1u << i)) starts[k++] = (uint32_t)(p0 + i);
+      if (found & (1u << i)) out[k++] = (uint32_t)(p0 + i);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = cnt_sh;
 }
 
 static __global__ __launch_bounds__(256) void k_runs_resolve(const uint32_t* __restrict__ code,
-                                                            const uint32_t* __restrict__ rows,
-                                                            uint32_t* __restrict__ rows_out,
-                                                            const double* __restrict__ x, int64_t n,
+                                                            uint32_t* __restrict__ rows,
+                                                            const double* __restrict__ x, int64_t n, int64_t chunk,
                                                             const uint32_t* __restrict__ starts,
-                                                            const uint32_t* nstarts, uint8_t* __restrict__ eqprev,
-                                                            int32_t* flags) {
-  const uint32_t m = *nstarts;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < m; i += gridDim.x * 256) {
-    const int64_t s = starts[i];
+                                                            const uint32_t* __restrict__ counts,
+                                                            uint8_t* __restrict__ eqprev, int32_t* flags) {
+  const uint32_t m = counts[blockIdx.x];
+  const uint32_t* st = starts + (int64_t)blockIdx.x * run_stride(n, chunk);
+  for (uint32_t i = threadIdx.x; i < m; i += 256) {
+    const int64_t s = st[i];
     const uint32_t c = code[s];
     int64_t e = s + 1;
     while (e + 1 < n && code[e + 1] == c && e - s + 1 <= kMaxRun) ++e;
@@ -693,19 +709,29 @@ static __global__ __launch_bounds__(256) void k_runs_resolve(const uint32_t* __r
       atomicOr(flags, 1);
       continue;
     }
+    const int len = (int)(e - s + 1);
+    // fully unrolled over kMaxRun with predicates: the run stays in registers (no scratch)
+    uint32_t r[kMaxRun];
+    double v[kMaxRun];
+#pragma unroll
+    for (int j = 0; j < kMaxRun; ++j) {
+      r[j] = j < len ? rows[s + j] : 0u;
+      v[j] = j < len ? x[r[j]] : 0.0;
+    }
     bool any_tie = false;
-    for (int64_t p = s; p <= e; ++p) {
-      const uint32_t r = rows[p];
-      const double v = x[r];
+#pragma unroll
+    for (int p = 0; p < kMaxRun; ++p) {
+      if (p >= len) break;
       int pos = 0;
       bool tie = false;
-      for (int64_t j = s; j <= e; ++j) {
+#pragma unroll
+      for (int j = 0; j < kMaxRun; ++j) {
+        if (j >= len) break;
         if (j == p) continue;
-        const double w = x[rows[j]];
-        pos += (w < v || (w == v && j < p)) ? 1 : 0;
-        tie |= (w == v && j < p);
+        pos += (v[j] < v[p] || (v[j] == v[p] && j < p)) ? 1 : 0;
+        tie |= (v[j] == v[p] && j < p);
       }
-      rows_out[s + pos] = r;
+      rows[s + pos] = r[p];
       if (tie) {
         eqprev[s + pos] = 1;
         any_tie = true;
@@ -772,16 +798,15 @@ int make_codes(const double* x, int64_t n, const CodeMap& cm, uint32_t* codes, h
   return PBH_OK;
 }
 
-int resolve_code_runs(const uint32_t* codes, const uint32_t* rows, uint32_t* rows_out, const double* x, int64_t n,
-                      uint8_t* eqprev, int32_t* flags, uint32_t* starts, hipStream_t s) {
-  uint32_t* nstarts = (uint32_t*)(flags + 1);
+int resolve_code_runs(const uint32_t* codes, uint32_t* rows, const double* x, int64_t n, uint8_t* eqprev,
+                      int32_t* flags, uint32_t* starts, uint32_t* counts, hipStream_t s) {
+  int64_t nb;
+  const int64_t chunk = run_chunk(n, &nb);
   PBH_TIMED(kKCodeRuns, s,
             hipMemsetAsync(eqprev, 0, (size_t)n, s);
-            hipMemsetAsync(nstarts, 0, sizeof(uint32_t), s);
-            hipLaunchKernelGGL(k_runs_copy, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, s, codes, rows,
-                               rows_out, n, starts, nstarts);
-            hipLaunchKernelGGL(k_runs_resolve, dim3(1024), dim3(256), 0, s, codes, rows, rows_out, x, n, starts,
-                               nstarts, eqprev, flags));
+            hipLaunchKernelGGL(k_runs_scan, dim3((unsigned)nb), dim3(256), 0, s, codes, n, chunk, starts, counts);
+            hipLaunchKernelGGL(k_runs_resolve, dim3((unsigned)nb), dim3(256), 0, s, codes, rows, x, n, chunk, starts,
+                               counts, eqprev, flags));
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }

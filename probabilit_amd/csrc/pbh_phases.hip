@@ -123,8 +123,8 @@ int reorder_column(const double* cs, int64_t n, const double* sorted_src, double
   st = radix_sort_keys32(sb, n, s, &buf, codes);
   if (st) return st;
   PBH_CHECK_HIP(hipMemsetAsync(w.flags, 0, sizeof(int32_t), s));
-  st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], sb.vals[buf ^ 1], cs, n, w.eqprev, w.flags,
-                         (uint32_t*)sb.keys[buf ^ 1], s);
+  st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], cs, n, w.eqprev, w.flags,
+                         (uint32_t*)sb.keys[buf ^ 1], sb.counts, s);
   if (st) return st;
   int32_t run_flags = 0;
   PBH_CHECK_HIP(hipMemcpyAsync(&run_flags, w.flags, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -137,18 +137,18 @@ int reorder_column(const double* cs, int64_t n, const double* sorted_src, double
       if (st) return st;
       vals = fixed;
     }
-    PlaceBuffers pb;
-    pb.rows[0] = sb.vals[buf];
+    PlaceBuffers pb;  // input rows: sb.vals[buf]; pass 1 -> [0], pass 2 -> [1]
+    pb.rows[0] = sb.vals[buf ^ 1];
     pb.vals[0] = (double*)sb.keys[buf ^ 1];
-    pb.rows[1] = sb.vals[buf ^ 1];
+    pb.rows[1] = sb.vals[buf];
     pb.vals[1] = (double*)sb.keys[buf];
     pb.counts = sb.counts;
     pb.partials = sb.partials;
     pb.status = sb.status;
     pb.bases = sb.bases;
-    return place_by_row(sb.vals[buf ^ 1], vals, n, y, y_rs, pb, s);
+    return place_by_row(sb.vals[buf], vals, n, y, y_rs, pb, s);
   }
-  if (!(run_flags & 1)) return rank_finish(kModeGather, nullptr, sb.vals[buf ^ 1], n, w.tb, out, s, w.eqprev);
+  if (!(run_flags & 1)) return rank_finish(kModeGather, nullptr, sb.vals[buf], n, w.tb, out, s, w.eqprev);
   st = load_keys(cs, 1, n, sb.keys[0], nullptr, s);
   if (st) return st;
   st = radix_sort_keys(sb, n, s, &buf);
