@@ -44,6 +44,30 @@ def kernel_bytes(name, n, k):
     return per_elem.get(name, 0) * n
 
 
+# bench (HIP-event) kernel names -> rocprofv3 kernel names in the committed PMC summaries
+PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 16>", "k_scatter<unsigned int>"],
+             "k_scatter<place>": ["k_onesweep<unsigned int, double, 16>", "k_scatter<unsigned int, double>"],
+             "k_code_runs": ["k_runs_scan", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
+             "k_apply": ["k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"]}
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/r*/pmc_traffic_*.json, written by tools/gpu/pmc.sh + tools/pmc_summary.py:
+    2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_*.json")), key=os.path.getmtime)
+    if not files:
+        return None, None
+    ks = json.load(open(files[-1]))["kernels"]
+    names = PMC_NAMES.get(kernel, [kernel])
+    hits = [ks[n]["hbm_bytes"] for n in names if n in ks]
+    if not hits:
+        return None, None
+    return int(sum(hits)), os.path.relpath(files[-1], ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,8 +154,10 @@ def main():
     dom = max(kernels, key=lambda k: kernels[k]["total_ms_per_step"])
     dk = kernels[dom]
     achieved = dk["GBps"] or 0.0
+    traffic, traffic_src = pmc_traffic(dom)
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": dom,
                 "avg_launch_ms": dk["avg_ms"], "bytes_per_launch": dk["bytes_per_launch"]}
 
     cpu = None

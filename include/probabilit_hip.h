@@ -72,6 +72,26 @@ int pbh_fill_lhs(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col0
 int pbh_fill_uniform(uint64_t seed, int64_t row0, int64_t nrows, int col0, int ncols, double* q, int64_t ldq,
                      void* stream);
 
+/* numpy's np.random.RandomState(...).random((N, d)) bit for bit (MT19937, legacy double
+ * a >> 5, b >> 6): what check_random_state(int | None | RandomState).random((size, d)) gives at
+ * modeling.py:484-486, rows [row0, row0 + nrows) of it.  key_host / pos: the generator's state
+ * (RandomState.get_state()[1:3]).  Workspace: pbh_mt19937_workspace_size (8 B per draw + the
+ * 107 KB jump table).  pbh_mt19937_advance returns numpy's state after nwords 32-bit draws (key
+ * block + pos), so that a caller-owned or the global RandomState advances exactly as in numpy. */
+int pbh_mt19937_workspace_size(int64_t nrows, int32_t d, size_t* bytes);
+int pbh_mt19937_random(const uint32_t* key_host, int32_t pos, int64_t row0, int64_t nrows, int32_t d, double* q,
+                       int64_t ldq, void* ws, size_t ws_bytes, void* stream);
+int pbh_mt19937_advance(const uint32_t* key_host, int32_t pos, int64_t nwords, uint32_t* key_out_host,
+                        int32_t* pos_out, void* ws, size_t ws_bytes, void* stream);
+
+/* numpy's Generator(PCG64).random((nrows, d)) bit for bit, starting at draw index draw0 of the
+ * stream whose 128-bit state / increment are state_host / inc_host ({low, high} words; numpy's
+ * bit_generator.state["state"]): random_state=Generator at modeling.py:484-486, and the
+ * rng.uniform(size=(n, d)) of scipy.stats.qmc.LatinHypercube._random_lhs. */
+int pbh_pcg64_workspace_size(size_t* bytes);
+int pbh_pcg64_random(const uint64_t* state_host, const uint64_t* inc_host, int64_t draw0, int64_t nrows, int32_t d,
+                     double* q, int64_t ldq, void* ws, size_t ws_bytes, void* stream);
+
 /* Scrambled Sobol' points, bit-exact with scipy.stats.qmc.Sobol (modeling.py:482,488):
  * x_r[c] = (shift[c] ^ XOR_{b in gray(r)} sv[c][b]) * 2^-bits.  sv_host is d x bits (row-major),
  * shift_host has d entries (both produced by the host-side engine setup). */

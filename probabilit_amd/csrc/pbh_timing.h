@@ -30,6 +30,7 @@ enum KernelId {
   kKPlaceUpsweep,
   kKPlaceScatter,
   kKPlace,
+  kKStreams,
   kKCount
 };
 

@@ -14,6 +14,8 @@ numpy's PCG64 / MT19937 bit streams.  Bit-level parity with the reference is def
 Node.sample_from_quantiles: identical quantiles in give identical samples out.
 """
 
+import ctypes
+import numbers
 import os
 import warnings
 
@@ -22,6 +24,40 @@ import numpy as np
 from . import _lib, device
 
 MASK63 = (1 << 63) - 1
+
+
+# ------------------------------------------------------------------ numpy bit-generator state
+PCG_MULT = 0x2360ED051FC65DA44385DF649FCCF645
+M128 = (1 << 128) - 1
+
+
+def check_random_state(seed):
+    """scipy._lib._util.check_random_state, which modeling.py:485 calls: None (or np.random) ->
+    numpy's global RandomState, int -> a new RandomState(seed), Generator / RandomState -> itself."""
+    if seed is None or seed is np.random:
+        return np.random.mtrand._rand
+    if isinstance(seed, (numbers.Integral, np.integer)):
+        return np.random.RandomState(seed)
+    if isinstance(seed, (np.random.RandomState, np.random.Generator)):
+        return seed
+    raise ValueError(f"{seed!r} cannot be used to seed a numpy.random.RandomState instance")
+
+
+def pcg64_advance(state, inc, k):
+    """PCG64's 128-bit LCG state after k steps (host bookkeeping of the caller's Generator)."""
+    acc_mult, acc_plus, cur_mult, cur_plus = 1, 0, PCG_MULT, inc
+    while k:
+        if k & 1:
+            acc_mult = acc_mult * cur_mult & M128
+            acc_plus = (acc_plus * cur_mult + cur_plus) & M128
+        cur_plus = (cur_mult + 1) * cur_plus & M128
+        cur_mult = cur_mult * cur_mult & M128
+        k >>= 1
+    return (acc_mult * state + acc_plus) & M128
+
+
+def _u128_words(v):
+    return np.array([v & ((1 << 64) - 1), v >> 64], dtype=np.uint64)
 
 
 # ------------------------------------------------------------------ seeds
@@ -192,6 +228,85 @@ class UniformSource(QuantileSource):
         return ("vector", out, 1)
 
 
+class MT19937Source(QuantileSource):
+    """RandomState.random((n, d)) bit for bit (modeling.py:484-486 with random_state None, an
+    int or a RandomState), generated on the device (pbh_mt19937_random) at the first column.
+    The RandomState itself advances exactly as numpy's random() would (pbh_mt19937_advance),
+    unless it is a throwaway instance made here from an int seed."""
+
+    def __init__(self, n, d, rs, advance=True):
+        super().__init__(n, d)
+        st = rs.get_state(legacy=False)
+        if st.get("bit_generator") != "MT19937":
+            raise NotImplementedError(f"RandomState over {st.get('bit_generator')!r}: only MT19937 has a native stream")
+        self.key = np.ascontiguousarray(st["state"]["key"], dtype=np.uint32)
+        self.pos = int(st["state"]["pos"])
+        self.q = None
+        if advance:
+            lib = _lib.load()
+            ws = _workspace(lib.pbh_mt19937_workspace_size, 0, 0)
+            key_out = np.empty(624, dtype=np.uint32)
+            pos_out = ctypes.c_int32()
+            _lib.check(lib.pbh_mt19937_advance(_lib.np_ptr(self.key), self.pos, 2 * self.n * self.d,
+                                               _lib.np_ptr(key_out), ctypes.byref(pos_out), ws.data_ptr(),
+                                               ws.numel(), device.stream()), "pbh_mt19937_advance")
+            st["state"] = {"key": key_out, "pos": int(pos_out.value)}
+            rs.set_state(st)
+
+    def column(self, c):
+        if self.q is None:
+            lib = _lib.load()
+            ws = _workspace(lib.pbh_mt19937_workspace_size, self.rows, self.d)
+            self.q = device.empty((self.d, self.rows))
+            _lib.check(lib.pbh_mt19937_random(_lib.np_ptr(self.key), self.pos, self.row0, self.rows, self.d,
+                                              self.q.data_ptr(), max(self.rows, 1), ws.data_ptr(), ws.numel(),
+                                              device.stream()), "pbh_mt19937_random")
+        return ("vector", self.q[c], 1)
+
+
+class PCG64Source(QuantileSource):
+    """Generator(PCG64).random((n, d)) bit for bit (modeling.py:484-486 with a Generator),
+    generated on the device (pbh_pcg64_random); the Generator advances by n * d draws."""
+
+    def __init__(self, n, d, gen, advance=True):
+        super().__init__(n, d)
+        bg = gen.bit_generator
+        if type(bg) is not np.random.PCG64:
+            raise NotImplementedError(f"Generator over {type(bg).__name__}: only PCG64 has a native stream")
+        st = bg.state
+        self.state, self.inc = int(st["state"]["state"]), int(st["state"]["inc"])
+        self.q = None
+        if advance:  # Generator.random leaves the buffered 32-bit half untouched
+            st["state"] = {"state": pcg64_advance(self.state, self.inc, self.n * self.d), "inc": self.inc}
+            bg.state = st
+
+    def column(self, c):
+        if self.q is None:
+            lib = _lib.load()
+            ws = _workspace(lib.pbh_pcg64_workspace_size)
+            self.q = device.empty((self.d, self.rows))
+            s, inc = _u128_words(self.state), _u128_words(self.inc)
+            _lib.check(lib.pbh_pcg64_random(_lib.np_ptr(s), _lib.np_ptr(inc), self.row0 * self.d, self.rows, self.d,
+                                            self.q.data_ptr(), max(self.rows, 1), ws.data_ptr(), ws.numel(),
+                                            device.stream()), "pbh_pcg64_random")
+        return ("vector", self.q[c], 1)
+
+
+def _workspace(size_fn, *args):
+    need = ctypes.c_size_t()
+    _lib.check(size_fn(*args, ctypes.byref(need)))
+    return device.empty(max(int(need.value), 1), "uint8")
+
+
+def pseudo_random_source(n, d, random_state):
+    """modeling.py:484-486: check_random_state(random_state).random((size, d))."""
+    rs = check_random_state(random_state)
+    if isinstance(rs, np.random.Generator):
+        return PCG64Source(n, d, rs)
+    fresh = isinstance(random_state, (numbers.Integral, np.integer))
+    return MT19937Source(n, d, rs, advance=not fresh)
+
+
 class LHSSource(QuantileSource):
     def __init__(self, n, d, seed):
         super().__init__(n, d)
@@ -232,7 +347,7 @@ class SobolSource(QuantileSource):
 
 def make_source(method, n, d, random_state):
     if method is None:
-        return UniformSource(n, d, seed_from(random_state))
+        return pseudo_random_source(n, d, random_state)
     m = method.lower().strip()
     if m == "lhs":
         return LHSSource(n, d, seed_from(random_state))
