@@ -92,6 +92,16 @@ int pbh_pcg64_workspace_size(size_t* bytes);
 int pbh_pcg64_random(const uint64_t* state_host, const uint64_t* inc_host, int64_t draw0, int64_t nrows, int32_t d,
                      double* q, int64_t ldq, void* ws, size_t ws_bytes, void* stream);
 
+/* Scrambled Halton points, bit-exact with scipy.stats.qmc.Halton(d, rng=...) (modeling.py:481,488):
+ * column c is the van der Corput sequence in base bases_host[c] with counts_host[c] digit
+ * permutations (perms_host: concatenated counts_host[c] x bases_host[c] tables, produced by the
+ * host-side engine setup from the engine's Generator).  Rows [row0, row0 + nrows) = sequence
+ * indices; columns [col0, col0 + ncols).  Workspace: pbh_halton_workspace_size. */
+int pbh_halton_workspace_size(const int32_t* bases_host, const int32_t* counts_host, int d, size_t* bytes);
+int pbh_fill_halton(const int32_t* bases_host, const int32_t* counts_host, const int32_t* perms_host, int d,
+                    int64_t row0, int64_t nrows, int col0, int ncols, double* q, int64_t ldq, void* ws,
+                    size_t ws_bytes, void* stream);
+
 /* Scrambled Sobol' points, bit-exact with scipy.stats.qmc.Sobol (modeling.py:482,488):
  * x_r[c] = (shift[c] ^ XOR_{b in gray(r)} sv[c][b]) * 2^-bits.  sv_host is d x bits (row-major),
  * shift_host has d entries (both produced by the host-side engine setup). */
@@ -252,6 +262,18 @@ int pbh_average(const double* const* parents_host, int m, int64_t n, double* out
 /* Column-major <-> row-major transpose of an (rows x cols) float64 matrix (LDS-tiled). */
 int pbh_transpose(const double* in, int64_t rows, int64_t cols, int64_t ld_in, double* out, int64_t ld_out,
                   void* stream);
+
+/* ---------------------------------------------------------------- affine row transform
+ * Y[r, j] = offset[j] + sum_i ((X[r, i] - shift[i]) / scale[i]) * M[i, j], rows r < n, k <= 128
+ * (X[r, i] at X[r * x_rs + i * x_cs], likewise Y; M row-major k x k; scale_host NULL = 1).
+ * The N-sized step of the Cholesky correlator (replaces correlation.py:271-285:
+ * mean + ((X - mean) / std) @ (solve_triangular(P_x^T, P^T) * std)) and of decorrelate
+ * (correlation.py:745-754: mean + (X - mean) @ inv(L)^T); the K x K factors come from
+ * pbh_column_sums / pbh_centered_gram.  Workspace: pbh_affine_workspace_size. */
+int pbh_affine_workspace_size(int32_t k, size_t* bytes);
+int pbh_affine_rows(const double* X, int64_t n, int32_t k, int64_t x_rs, int64_t x_cs, const double* shift_host,
+                    const double* scale_host, const double* offset_host, const double* M_host, double* Y,
+                    int64_t y_rs, int64_t y_cs, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- measurement
  * When enabled, every launch of the library's main kernels is bracketed by two HIP events

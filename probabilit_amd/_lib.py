@@ -39,14 +39,15 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_column_sums", "pbh_centered_gram", "pbh_ic_factor", "pbh_ic_apply", "pbh_ic_reorder_workspace_size",
            "pbh_ic_reorder", "pbh_mt19937_workspace_size", "pbh_mt19937_random", "pbh_mt19937_advance",
            "pbh_pcg64_workspace_size",
-           "pbh_pcg64_random"]
+           "pbh_pcg64_random", "pbh_halton_workspace_size", "pbh_fill_halton",
+           "pbh_affine_workspace_size", "pbh_affine_rows"]
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
            "k_rank_finish<gather>", "k_load_keys", "k_gram", "k_apply", "k_elementwise", "k_head_bounds", "k_scan",
            "k_lhs_sorted_ppf", "k_perm_scores", "k_code_runs",
            "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>",
-           "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams"]
+           "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine"]
 
 
 class Param(ctypes.Structure):
@@ -130,6 +131,10 @@ def load():
         "pbh_mt19937_advance": ([vp, ctypes.c_int32, i64, vp, ctypes.POINTER(ctypes.c_int32), vp, sz, vp], i32),
         "pbh_pcg64_workspace_size": ([ctypes.POINTER(sz)], i32),
         "pbh_pcg64_random": ([vp, vp, i64, i64, ctypes.c_int32, vp, i64, vp, sz, vp], i32),
+        "pbh_halton_workspace_size": ([vp, vp, i32, ctypes.POINTER(sz)], i32),
+        "pbh_fill_halton": ([vp, vp, vp, i32, i64, i64, i32, i32, vp, i64, vp, sz, vp], i32),
+        "pbh_affine_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
+        "pbh_affine_rows": ([vp, i64, ctypes.c_int32, i64, i64, vp, vp, vp, vp, vp, i64, i64, vp, sz, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -8,8 +8,9 @@
   SCS formulation (correlation.py:59-150: minimise ||H o (X - G)||_F subject to diag(X) = 1
   and X - (10 eps / n) I >= 0) with a host ADMM on the K x K matrix (cvxpy is not a
   dependency).  It returns the optimum to ~1e-10, where SCS stops at its `eps`.
-* `Cholesky` is the next correlator on the roadmap: it raises
-  NotImplementedError instead of silently running on the CPU.
+* `Cholesky` (correlation.py:205-285) and `decorrelate` (correlation.py:706-754): column
+  means and the centered Gram on the device (pbh_column_sums, pbh_centered_gram), the K x K
+  factors on the host, the N-sized row transform on the device (pbh_affine_rows).
 """
 
 import ctypes
@@ -142,12 +143,99 @@ class Correlator:
         return N, K
 
 
+def _as_block(X):
+    """(N, K) numpy array or device tensor -> (K, N) contiguous device block, plus whether the
+    caller passed a device tensor."""
+    import torch
+
+    on_device = isinstance(X, torch.Tensor)
+    Xd = X.to(device.device(), torch.float64) if on_device else device.to_device(np.asarray(X, dtype=np.float64))
+    return Xd.t().contiguous(), on_device
+
+
+def _block_stats(block):
+    """Column means (numpy's mean: sum / N) and centered Gram sum_r (x_r - m)(x_r - m)^T of a
+    (K, N) device block, both as host arrays."""
+    K, N = block.shape
+    lib = _lib.load()
+    nb = ctypes.c_size_t()
+    _lib.check(lib.pbh_gram_workspace_size(K, ctypes.byref(nb)))
+    ws = device.empty(max(int(nb.value), 1), "uint8")
+    sums = device.zeros(K)
+    _lib.check(lib.pbh_column_sums(block.data_ptr(), N, K, block.stride(0), sums.data_ptr(), ws.data_ptr(), nb.value,
+                                   device.stream()), "pbh_column_sums")
+    mean = device.to_host(sums) / N
+    G = device.zeros((K, K))
+    _lib.check(lib.pbh_centered_gram(block.data_ptr(), N, K, block.stride(0), device.to_device(mean).data_ptr(),
+                                     G.data_ptr(), ws.data_ptr(), nb.value, device.stream()), "pbh_centered_gram")
+    return mean, device.to_host(G)
+
+
+def _affine_block(block, shift, scale, offset, M):
+    """(K, N) device block -> Y (K, N): Y[:, r] = offset + ((X[:, r] - shift) / scale) @ M."""
+    K, N = block.shape
+    lib = _lib.load()
+    nb = ctypes.c_size_t()
+    _lib.check(lib.pbh_affine_workspace_size(K, ctypes.byref(nb)))
+    ws = device.empty(int(nb.value), "uint8")
+    Y = device.empty((K, N))
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (shift, scale, offset, M)]
+    _lib.check(lib.pbh_affine_rows(block.data_ptr(), N, K, 1, block.stride(0), *[_lib.np_ptr(a) for a in arrs],
+                                   Y.data_ptr(), 1, N, ws.data_ptr(), nb.value, device.stream()), "pbh_affine_rows")
+    return Y
+
+
 class Cholesky(Correlator):
-    """Cholesky correlator (correlation.py:205-285): next on the device roadmap."""
+    """Cholesky correlator (correlation.py:205-285): X_n = (X - mean) / std, remove the
+    correlation of X_n with its own Cholesky factor, impose P, restore mean and std.  Does not
+    preserve marginals (that is what ImanConover is for).
+
+    Floating-point parity: the reference's covariance and products are BLAS calls whose
+    summation order is library dependent, so the device result agrees to ~1e-12 relative,
+    not bit for bit."""
+
+    def set_target(self, correlation_matrix):
+        super().set_target(correlation_matrix)
+        return self
 
     def __call__(self, X):
-        raise NotImplementedError("correlator='cholesky' has no device implementation yet "
-                                  "(SURVEY.md §8f, next #1); use 'imanconover'")
+        """Transform X of shape (N, K); returns a new array (or device tensor)."""
+        self._validate_X(X)
+        block, on_device = _as_block(X)
+        Y = self._transform_device(block).t()
+        return Y.contiguous() if on_device else device.to_host(Y)
+
+    def _transform_device(self, block, ev=None):
+        import scipy.linalg
+
+        K, N = block.shape
+        self._validate_X(block.T)
+        mean, G = _block_stats(block)
+        std = np.sqrt(np.diag(G) / N)                        # np.std(X, axis=0)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            cov = G / N / np.outer(std, std)                 # np.cov(X_n, rowvar=False, ddof=0)
+        P = np.linalg.cholesky(cov)                          # :262
+        transform = scipy.linalg.solve_triangular(P.T, self.P.T, lower=False)  # :284
+        return _affine_block(block, mean, std, mean, transform * std)          # :285
+
+
+def decorrelate(X, remove_variance=True):
+    """Removes correlations (and optionally variances) from X of shape (N, K), keeping the
+    mean (correlation.py:706-754): mean + (X - mean) @ inv(L).T with L = cholesky(cov(X)),
+    or L / sqrt(var) when remove_variance is False."""
+    import scipy.linalg
+
+    block, on_device = _as_block(X)
+    K, N = block.shape
+    mean, G = _block_stats(block)
+    var = np.diag(G) / N                                     # np.var(X, axis=0, ddof=0)
+    cov = G / (N - 1)                                        # np.cov(X, rowvar=False)
+    L = np.linalg.cholesky(cov)
+    if not remove_variance:
+        L = L / np.sqrt(var)
+    M = scipy.linalg.solve_triangular(L, np.eye(K), lower=True).T  # inv(L).T
+    Y = _affine_block(block, mean, np.ones(K), mean, M).t()
+    return Y.contiguous() if on_device else device.to_host(Y)
 
 
 _NOT_PD_MSG = ("Rank data correlation not positive definite."

@@ -721,20 +721,20 @@ static __global__ __launch_bounds__(256) void k_runs_resolve(const uint32_t* __r
     bool any_tie = false;
 #pragma unroll
     for (int p = 0; p < kMaxRun; ++p) {
-      if (p >= len) break;
       int pos = 0;
       bool tie = false;
 #pragma unroll
       for (int j = 0; j < kMaxRun; ++j) {
-        if (j >= len) break;
-        if (j == p) continue;
-        pos += (v[j] < v[p] || (v[j] == v[p] && j < p)) ? 1 : 0;
-        tie |= (v[j] == v[p] && j < p);
+        const bool other = j < len && j != p;
+        pos += (other && (v[j] < v[p] || (v[j] == v[p] && j < p))) ? 1 : 0;
+        tie |= other && v[j] == v[p] && j < p;
       }
-      rows[s + pos] = r[p];
-      if (tie) {
-        eqprev[s + pos] = 1;
-        any_tie = true;
+      if (p < len) {
+        rows[s + pos] = r[p];
+        if (tie) {
+          eqprev[s + pos] = 1;
+          any_tie = true;
+        }
       }
     }
     if (any_tie) atomicOr(flags, 2);
@@ -803,7 +803,7 @@ int resolve_code_runs(const uint32_t* codes, uint32_t* rows, const double* x, in
   int64_t nb;
   const int64_t chunk = run_chunk(n, &nb);
   PBH_TIMED(kKCodeRuns, s,
-            hipMemsetAsync(eqprev, 0, (size_t)n, s);
+            (void)hipMemsetAsync(eqprev, 0, (size_t)n, s);
             hipLaunchKernelGGL(k_runs_scan, dim3((unsigned)nb), dim3(256), 0, s, codes, n, chunk, starts, counts);
             hipLaunchKernelGGL(k_runs_resolve, dim3((unsigned)nb), dim3(256), 0, s, codes, rows, x, n, chunk, starts,
                                counts, eqprev, flags));

@@ -160,6 +160,47 @@ __global__ __launch_bounds__(256) void k_pcg_random(const pcg::u128* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- scrambled Halton
+// scipy.stats.qmc.Halton._random -> van_der_corput(scramble=True) per dimension
+// (scipy:stats/_qmc.py; the loop of scipy:stats/_qmc_cy.pyx): for index i,
+//   s = 0; b2r = 1/base; repeat count times: s += perm[j][i % base] * b2r; b2r /= base; i /= base
+// with count = ceil(54 / log2(base)) - 1 (every digit permuted, zeros included).  b2r comes
+// from a host table built by the same repeated IEEE divisions; each += rounds separately
+// (-ffp-contract=off), so the points are bit-identical.
+struct HaltonDim {
+  int32_t base, count;
+  int64_t perm_off, b2r_off;
+};
+
+__global__ __launch_bounds__(256) void k_fill_halton(const HaltonDim* __restrict__ dims,
+                                                     const int32_t* __restrict__ perms,
+                                                     const double* __restrict__ b2r, int64_t row0, int64_t nrows,
+                                                     int col0, int ncols, double* __restrict__ q, int64_t ldq) {
+  const int c = blockIdx.y;
+  const HaltonDim hd = dims[col0 + c];
+  const int32_t* P = perms + hd.perm_off;
+  const double* B = b2r + hd.b2r_off;
+  const uint64_t base = (uint64_t)hd.base;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * 256) {
+    uint64_t idx = (uint64_t)(row0 + r);
+    double s = 0.0;
+    for (int j = 0; j < hd.count; ++j) {
+      uint64_t quo, rem;
+      if (idx <= 0xFFFFFFFFull) {
+        const uint32_t i32 = (uint32_t)idx;
+        quo = i32 / (uint32_t)base;
+        rem = i32 - (uint32_t)quo * (uint32_t)base;
+      } else {
+        quo = idx / base;
+        rem = idx - quo * base;
+      }
+      s = s + (double)P[j * hd.base + rem] * B[j];
+      idx = quo;
+    }
+    q[(int64_t)c * ldq + r] = s;
+  }
+}
+
 // ---------------------------------------------------------------- host
 struct JumpTable {
   std::vector<uint64_t> words;
@@ -298,5 +339,64 @@ extern "C" int pbh_pcg64_random(const uint64_t* state_host, const uint64_t* inc_
     PBH_CHECK_LAUNCH();
   }
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // `table` is pageable and goes out of scope
+  return PBH_OK;
+}
+
+extern "C" int pbh_halton_workspace_size(const int32_t* bases_host, const int32_t* counts_host, int d, size_t* bytes) {
+  PBH_REQUIRE(bases_host && counts_host && bytes && d >= 0, "pbh_halton_workspace_size: bad arguments");
+  size_t perm = 0, b2r = 0;
+  for (int c = 0; c < d; ++c) {
+    perm += (size_t)counts_host[c] * bases_host[c];
+    b2r += (size_t)counts_host[c];
+  }
+  *bytes = align256((size_t)d * sizeof(HaltonDim)) + align256(perm * 4) + align256(b2r * 8);
+  return PBH_OK;
+}
+
+extern "C" int pbh_fill_halton(const int32_t* bases_host, const int32_t* counts_host, const int32_t* perms_host, int d,
+                               int64_t row0, int64_t nrows, int col0, int ncols, double* q, int64_t ldq, void* ws,
+                               size_t ws_bytes, void* stream) {
+  PBH_REQUIRE(bases_host && counts_host && perms_host && ws && d >= 0 && row0 >= 0 && nrows >= 0,
+              "pbh_fill_halton: bad arguments");
+  PBH_REQUIRE(col0 >= 0 && ncols >= 0 && col0 + ncols <= d && (nrows * ncols == 0 || (q && ldq >= nrows)),
+              "pbh_fill_halton: bad output range");
+  size_t need = 0;
+  pbh_halton_workspace_size(bases_host, counts_host, d, &need);
+  if (ws_bytes < need) {
+    set_error("pbh_fill_halton: workspace %zu < %zu bytes", ws_bytes, need);
+    return PBH_ERR_WORKSPACE;
+  }
+  std::vector<HaltonDim> dims(d);
+  std::vector<double> b2r;
+  int64_t poff = 0;
+  for (int c = 0; c < d; ++c) {
+    PBH_REQUIRE(bases_host[c] >= 2 && counts_host[c] >= 1, "pbh_fill_halton: base < 2 or no permutation");
+    dims[c] = HaltonDim{bases_host[c], counts_host[c], poff, (int64_t)b2r.size()};
+    double v = 1.0 / (double)bases_host[c];
+    for (int j = 0; j < counts_host[c]; ++j) {
+      b2r.push_back(v);
+      v /= (double)bases_host[c];
+    }
+    poff += (int64_t)counts_host[c] * bases_host[c];
+  }
+  hipStream_t s = as_stream(stream);
+  char* p = (char*)ws;
+  HaltonDim* dims_dev = (HaltonDim*)p;
+  p += align256((size_t)d * sizeof(HaltonDim));
+  int32_t* perms_dev = (int32_t*)p;
+  p += align256((size_t)poff * 4);
+  double* b2r_dev = (double*)p;
+  if (d > 0) {
+    PBH_CHECK_HIP(hipMemcpyAsync(dims_dev, dims.data(), (size_t)d * sizeof(HaltonDim), hipMemcpyHostToDevice, s));
+    PBH_CHECK_HIP(hipMemcpyAsync(perms_dev, perms_host, (size_t)poff * 4, hipMemcpyHostToDevice, s));
+    PBH_CHECK_HIP(hipMemcpyAsync(b2r_dev, b2r.data(), b2r.size() * 8, hipMemcpyHostToDevice, s));
+  }
+  if (nrows > 0 && ncols > 0) {
+    PBH_TIMED(kKStreams, s,
+              hipLaunchKernelGGL(k_fill_halton, dim3(grid_for(nrows, 256, 16384), (unsigned)ncols), dim3(256), 0, s,
+                                 dims_dev, perms_dev, b2r_dev, row0, nrows, col0, ncols, q, ldq));
+    PBH_CHECK_LAUNCH();
+  }
+  PBH_CHECK_HIP(hipStreamSynchronize(s));  // host tables are pageable and go out of scope
   return PBH_OK;
 }

@@ -31,6 +31,7 @@ enum KernelId {
   kKPlaceScatter,
   kKPlace,
   kKStreams,
+  kKAffine,
   kKCount
 };
 

@@ -467,7 +467,7 @@ class Node(abc.ABC):
                 Y = inst._transform_generated(cols, size)
                 for j, var in enumerate(all_variables):
                     var._set_device(Y[j])
-            elif isinstance(inst, ImanConover):
+            elif isinstance(inst, (ImanConover, Cholesky)):
                 Y = inst._transform_device(block, ev)
                 for j, var in enumerate(all_variables):
                     var._set_device(Y[j])

@@ -345,6 +345,57 @@ class SobolSource(QuantileSource):
         return ("vector", out, 1)
 
 
+def first_primes(d):
+    """The first d primes (scipy.stats._qmc.n_primes: the Halton bases)."""
+    out, k = [], 2
+    while len(out) < d:
+        if all(k % p for p in out if p * p <= k):
+            out.append(k)
+        k += 1
+    return out
+
+
+def halton_setup(d, rng=None):
+    """(bases, counts, perms) of scipy.stats.qmc.Halton(d, rng=rng): per dimension
+    ceil(54 / log2(base)) - 1 shuffled copies of arange(base), drawn from the engine's owned
+    Generator in dimension order (scipy:stats/_qmc.py _van_der_corput_permutations)."""
+    import math
+
+    g = engine_rng(rng)
+    bases = first_primes(d)
+    counts, perms = [], []
+    for b in bases:
+        count = math.ceil(54 / math.log2(b)) - 1
+        p = np.repeat(np.arange(b)[None], count, axis=0)
+        for row in p:
+            g.shuffle(row)
+        counts.append(count)
+        perms.append(p.astype(np.int32).ravel())
+    return (np.asarray(bases, dtype=np.int32), np.asarray(counts, dtype=np.int32),
+            np.concatenate(perms) if perms else np.zeros(0, np.int32))
+
+
+class HaltonSource(QuantileSource):
+    """scipy.stats.qmc.Halton(d, rng=random_state).random(n) (modeling.py:481,488), bit-exact:
+    engine setup (primes, digit permutations) on the host, the points on the device."""
+
+    def __init__(self, n, d, rng):
+        super().__init__(n, d)
+        self.bases, self.counts, self.perms = halton_setup(d, rng)
+        self.q = None
+
+    def column(self, c):
+        if self.q is None:
+            lib = _lib.load()
+            b, k, p = self.bases, self.counts, np.ascontiguousarray(self.perms)
+            ws = _workspace(lib.pbh_halton_workspace_size, _lib.np_ptr(b), _lib.np_ptr(k), self.d)
+            self.q = device.empty((self.d, self.rows))
+            _lib.check(lib.pbh_fill_halton(_lib.np_ptr(b), _lib.np_ptr(k), _lib.np_ptr(p), self.d, self.row0, self.rows,
+                                           0, self.d, self.q.data_ptr(), max(self.rows, 1), ws.data_ptr(),
+                                           ws.numel(), device.stream()), "pbh_fill_halton")
+        return ("vector", self.q[c], 1)
+
+
 def make_source(method, n, d, random_state):
     if method is None:
         return pseudo_random_source(n, d, random_state)
@@ -354,5 +405,5 @@ def make_source(method, n, d, random_state):
     if m == "sobol":
         return SobolSource(n, d, random_state)
     if m == "halton":
-        raise NotImplementedError("method='halton' has no native generator yet (supported: None, 'lhs', 'sobol')")
+        return HaltonSource(n, d, random_state)
     raise KeyError(method)

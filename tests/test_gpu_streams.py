@@ -120,3 +120,43 @@ def test_cfg1_readme_norm(gpu):
     x = Distribution("norm", loc=176, scale=7.1).sample(999, random_state=0)
     ref = scipy.stats.norm(loc=176, scale=7.1).ppf(np.random.RandomState(0).random((999, 1))[:, 0])
     np.testing.assert_allclose(x, ref, rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("d,seed,n", [(1, 0, 10), (5, 0, 1000), (12, 3, 4097), (32, 123, 20_000)])
+def test_halton_matches_scipy(gpu, d, seed, n):
+    import scipy.stats
+
+    from probabilit_amd import qmc
+
+    src = qmc.make_source("halton", n, d, seed)
+    np.testing.assert_array_equal(_src_matrix(src), scipy.stats.qmc.Halton(d, rng=seed).random(n))
+
+
+def test_halton_row_shard_and_large_index(gpu):
+    """Shards regenerate any index range; indices past 2^32 take the 64-bit digit path."""
+    from scipy.stats._qmc import van_der_corput
+
+    from probabilit_amd import device, qmc
+
+    src = qmc.make_source("halton", 2**32 + 200, 3, 7).shard(2**32 + 5, 100)
+    q = _src_matrix(src)
+    perms = np.split(src.perms, np.cumsum(src.counts * src.bases)[:-1])
+    for c, b in enumerate(src.bases):
+        ref = van_der_corput(100, int(b), start_index=2**32 + 5, scramble=True,
+                             permutations=perms[c].reshape(src.counts[c], b))
+        np.testing.assert_array_equal(q[:, c], ref)
+    del device
+
+
+def test_halton_node_sample(gpu):
+    """Node.sample(method="halton") equals the reference's computation: scipy Halton quantiles
+    (modeling.py:481,488) through the ppf (modeling.py:807)."""
+    import scipy.stats
+
+    from probabilit_amd.modeling import Distribution
+
+    a, b = Distribution("norm", loc=1, scale=2), Distribution("expon", scale=3)
+    out = (a * b).sample(513, random_state=4, method="halton")
+    Q = scipy.stats.qmc.Halton(2, rng=4).random(513)
+    ref = scipy.stats.norm(1, 2).ppf(Q[:, 0]) * scipy.stats.expon(scale=3).ppf(Q[:, 1])
+    np.testing.assert_allclose(out, ref, rtol=1e-10)

@@ -95,3 +95,17 @@ def test_oracle_pipelines_reproduce_fixtures():
     np.testing.assert_array_equal(mutual_fund(z["fund_Q"]), z["fund_sink"])
     np.testing.assert_array_equal(mutual_fund(z["fund999_Q"]), z["fund999_sink"])
     np.testing.assert_array_equal(cfg3_corr(8), z["corr8_C"])
+
+
+def test_oracle_correlators_vs_reference():
+    """oracle/correlators.py restates Cholesky.__call__ / decorrelate on the same numpy calls:
+    identical to the reference's outputs (tests/golden/correlators.npz)."""
+    from oracle.correlators import cholesky_transform, decorrelate
+
+    z = golden("correlators.npz")
+    for tag in ("9x2", "500x3", "2000x8"):
+        X, C = z[f"chol_X_{tag}"], z[f"chol_C_{tag}"]
+        np.testing.assert_allclose(cholesky_transform(X, C), z[f"chol_Y_{tag}"], rtol=1e-14, atol=1e-14)
+        np.testing.assert_allclose(decorrelate(X), z[f"decor_Y_{tag}"], rtol=1e-14, atol=1e-14)
+        np.testing.assert_allclose(decorrelate(X, remove_variance=False), z[f"decor_keepvar_Y_{tag}"], rtol=1e-14,
+                                   atol=1e-14)
