@@ -263,6 +263,20 @@ int pbh_average(const double* const* parents_host, int m, int64_t n, double* out
 int pbh_transpose(const double* in, int64_t rows, int64_t cols, int64_t ld_in, double* out, int64_t ld_out,
                   void* stream);
 
+/* ---------------------------------------------------------------- table distributions
+ * Inverse CDF of the table-driven nodes (modeling.py:825-927): out[i] = f(q[i * q_stride]).
+ *   PBH_TABLE_INTERP   CumulativeDistribution: np.interp(q, xp = t0, fp = t1)     (float64 out)
+ *   PBH_TABLE_QUANTILE EmpiricalDistribution: np.quantile(t0 = sorted data, q, method)
+ *                      method 0 linear, 1 lower, 2 higher, 3 nearest, 4 midpoint (float64 out)
+ *   PBH_TABLE_SEARCH   DiscreteDistribution: t1[searchsorted(t0 = cumsum(p), q, 'right')],
+ *                      t1 = values (float64 / int64 per out_dtype) or NULL for the index itself
+ *                      (int64 out); an index past the table sets flag bit 2 (the reference
+ *                      raises IndexError there).
+ * Tables are device arrays of m entries; flag bit 0 = a non-finite float output. */
+typedef enum pbh_table_kind { PBH_TABLE_INTERP = 0, PBH_TABLE_QUANTILE = 1, PBH_TABLE_SEARCH = 2 } pbh_table_kind;
+int pbh_table_ppf(int kind, const double* q, int64_t q_stride, int64_t n, const double* t0, const void* t1, int64_t m,
+                  int method, int out_dtype, void* out, int32_t* flag, void* stream);
+
 /* ---------------------------------------------------------------- affine row transform
  * Y[r, j] = offset[j] + sum_i ((X[r, i] - shift[i]) / scale[i]) * M[i, j], rows r < n, k <= 128
  * (X[r, i] at X[r * x_rs + i * x_cs], likewise Y; M row-major k x k; scale_host NULL = 1).

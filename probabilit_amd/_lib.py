@@ -16,6 +16,9 @@ OK, ERR_INVALID, ERR_HIP, ERR_NOT_PD, ERR_NONFINITE, ERR_WORKSPACE, ERR_UNSUPPOR
 # pbh_dist
 DIST_IDS = {"norm": 0, "uniform": 1, "expon": 2, "lognorm": 3, "triang": 4, "gamma": 5, "poisson": 6}
 
+# pbh_table_kind
+TABLE_INTERP, TABLE_QUANTILE, TABLE_SEARCH = 0, 1, 2
+
 # pbh_dtype
 BOOL, INT64, FLOAT64 = 0, 1, 2
 
@@ -40,14 +43,14 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_ic_reorder", "pbh_mt19937_workspace_size", "pbh_mt19937_random", "pbh_mt19937_advance",
            "pbh_pcg64_workspace_size",
            "pbh_pcg64_random", "pbh_halton_workspace_size", "pbh_fill_halton",
-           "pbh_affine_workspace_size", "pbh_affine_rows"]
+           "pbh_affine_workspace_size", "pbh_affine_rows", "pbh_table_ppf"]
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
            "k_rank_finish<gather>", "k_load_keys", "k_gram", "k_apply", "k_elementwise", "k_head_bounds", "k_scan",
            "k_lhs_sorted_ppf", "k_perm_scores", "k_code_runs",
            "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>",
-           "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine"]
+           "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine", "k_table_ppf"]
 
 
 class Param(ctypes.Structure):
@@ -134,6 +137,7 @@ def load():
         "pbh_halton_workspace_size": ([vp, vp, i32, ctypes.POINTER(sz)], i32),
         "pbh_fill_halton": ([vp, vp, vp, i32, i64, i64, i32, i32, vp, i64, vp, sz, vp], i32),
         "pbh_affine_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
+        "pbh_table_ppf": ([i32, vp, i64, i64, vp, vp, i64, i32, i32, vp, vp, vp], i32),
         "pbh_affine_rows": ([vp, i64, ctypes.c_int32, i64, i64, vp, vp, vp, vp, vp, i64, i64, vp, sz, vp], i32),
     }
     for name, (args, res) in sig.items():

@@ -32,6 +32,7 @@ enum KernelId {
   kKPlace,
   kKStreams,
   kKAffine,
+  kKTable,
   kKCount
 };
 

@@ -498,6 +498,9 @@ class Node(abc.ABC):
         flags = device.to_host(ev.flags)
         if flags.any():
             for node in nx.topological_sort(G):
+                if flags[ev.slot[node]] & 4:  # DiscreteDistribution: q past the last cumulative
+                    m = len(node.probabilities)
+                    raise IndexError(f"index {m} is out of bounds for axis 0 with size {m}")
                 if flags[ev.slot[node]] & 2:  # numpy's integer power check
                     raise ValueError("Integers to negative integer powers are not allowed.")
                 if flags[ev.slot[node]]:
@@ -657,18 +660,75 @@ class Distribution(AbstractDistribution):
         return list(self.get_parents()) == []
 
 
+def _into(res, out):
+    """Write a node's samples into a preallocated float64 row (the correlated block) if given."""
+    if out is None:
+        return res
+    out.copy_(res)
+    return out
+
+
+_QUANTILE_METHODS = {"linear": 0, "lower": 1, "higher": 2, "nearest": 3, "midpoint": 4}
+
+
 class _TableDistribution(AbstractDistribution):
+    """Leaf distribution given by a host table; sampled on the device by pbh_table_ppf.  The
+    table (at most a few thousand entries, independent of the sample size) is prepared on the
+    host once and cached on the device."""
+
     is_leaf = True
 
     def get_parents(self):
         yield from []
 
-    def _sample_device(self, ev, column, out=None):
-        raise NotImplementedError(f"{type(self).__name__} has no native kernel yet (SURVEY.md §8f, next #3)")
+    @staticmethod
+    def _quantile_column(column, n):
+        """(device q vector, stride) of this node's quantile column; a fused native-LHS column
+        is materialised (pbh_fill_lhs)."""
+        if column[0] == "lhs":
+            _, seed, n_total, col, row0 = column
+            q = device.empty(n)
+            _lib.check(_lib.load().pbh_fill_lhs(seed, n_total, row0, n, col, 1, q.data_ptr(), max(n, 1),
+                                                device.stream()), "pbh_fill_lhs")
+            return q, 1
+        _, q, stride = column
+        return q, stride
+
+    def _sample(self, q):
+        """The reference's `_sample(q)` (inverse CDF of explicit quantiles), on the device."""
+        q = np.asarray(q, dtype=np.float64)
+        qd = device.to_device(np.ascontiguousarray(q.ravel()))
+        ev = _Evaluation(qd.shape[0], [self])
+        res = device.to_host(self._sample_device(ev, ("vector", qd, 1)))
+        flags = device.to_host(ev.flags)
+        if flags[0] & 4:
+            m = len(self.probabilities)
+            raise IndexError(f"index {m} is out of bounds for axis 0 with size {m}")
+        labels = self.__dict__.get("_labels")
+        res = res if labels is None else labels[res]
+        return res.reshape(q.shape)
+
+    def _tables(self):
+        cache = self.__dict__.get("_dev_tables")
+        if cache is None:
+            cache = self.__dict__["_dev_tables"] = self._build_tables()
+        return cache
+
+    def _launch(self, ev, column, kind, t0, t1, m, method, out_dt):
+        n = ev.size
+        q, stride = self._quantile_column(column, n)
+        out = device.empty(n, out_dt)
+        _lib.check(_lib.load().pbh_table_ppf(kind, q.data_ptr(), stride, n, t0.data_ptr(),
+                                             None if t1 is None else t1.data_ptr(), m, method,
+                                             _PBH_DTYPE[np.dtype(out_dt)], out.data_ptr(), ev.flag_ptr(self),
+                                             device.stream()), f"{self}")
+        return out
 
 
 class EmpiricalDistribution(_TableDistribution):
-    """np.quantile of data (modeling.py:825-844)."""
+    """np.quantile of data (modeling.py:825-844) on the device (pbh_table_ppf QUANTILE).
+    Supported np.quantile keywords: method in linear (default) / lower / higher / nearest /
+    midpoint; the data are flattened as np.quantile does with axis=None."""
 
     def __init__(self, data, **kwargs):
         self.data = np.array(data)
@@ -678,12 +738,37 @@ class EmpiricalDistribution(_TableDistribution):
     def __repr__(self):
         return f"{type(self).__name__}()"
 
-    def _sample(self, q):
-        return np.quantile(a=self.data, q=q, **self.kwargs)
+    def _method(self):
+        extra = set(self.kwargs) - {"method"}
+        if extra:
+            raise NotImplementedError(f"EmpiricalDistribution: np.quantile keywords {sorted(extra)} have no device path")
+        method = self.kwargs.get("method", "linear")
+        if method not in _QUANTILE_METHODS:
+            raise NotImplementedError(f"np.quantile method={method!r} has no device path; "
+                                      f"supported: {sorted(_QUANTILE_METHODS)}")
+        return method
+
+    def _build_tables(self):
+        data = np.sort(np.asarray(self.data).ravel()).astype(np.float64)
+        if data.size == 0:
+            raise IndexError("index -1 is out of bounds for axis 0 with size 0")
+        return (device.to_device(data),)
+
+    def _sample_device(self, ev, column, out=None):
+        return _into(self._sample_table(ev, column), out)
+
+    def _sample_table(self, ev, column):
+        method = self._method()
+        (t0,) = self._tables()
+        res = self._launch(ev, column, _lib.TABLE_QUANTILE, t0, None, t0.shape[0], _QUANTILE_METHODS[method],
+                           "float64")
+        if method in ("lower", "higher", "nearest") and np.issubdtype(self.data.dtype, np.integer):
+            res = _elementwise("cast", res, None, ev.size, np.dtype(np.int64), np.dtype(np.int64), None)
+        return res
 
 
 class CumulativeDistribution(_TableDistribution):
-    """Piecewise-linear inverse CDF (modeling.py:847-882)."""
+    """Piecewise-linear inverse CDF (modeling.py:847-882): np.interp on the device."""
 
     def __init__(self, quantiles, cumulatives):
         self.q = np.array(quantiles)
@@ -699,17 +784,29 @@ class CumulativeDistribution(_TableDistribution):
     def __repr__(self):
         return f"{type(self).__name__}(quantiles={repr(self.q)}, cumulatives={repr(self.cumulatives)})"
 
-    def _sample(self, q):
-        return np.interp(x=q, xp=self.q, fp=self.cumulatives)
+    def _build_tables(self):
+        return (device.to_device(np.asarray(self.q, dtype=np.float64)),
+                device.to_device(np.asarray(self.cumulatives, dtype=np.float64)))
+
+    def _sample_device(self, ev, column, out=None):
+        return _into(self._sample_table(ev, column), out)
+
+    def _sample_table(self, ev, column):
+        xp, fp = self._tables()
+        return self._launch(ev, column, _lib.TABLE_INTERP, xp, fp, xp.shape[0], 0, "float64")
 
 
 class DiscreteDistribution(_TableDistribution):
-    """Categorical values with probabilities (modeling.py:885-927)."""
+    """Categorical values with probabilities (modeling.py:885-927):
+    values[searchsorted(cumsum(p), q, side='right')] on the device.  Numeric values are
+    gathered on the device; other values (e.g. strings) are sampled as indices on the device
+    and mapped to the labels when `.samples_` is read (they cannot enter arithmetic)."""
 
     def __init__(self, values, probabilities=None):
         self.values = np.array(values)
         if probabilities is None:
-            self.probabilities = np.ones(len(self.values), dtype=float) / len(self.values)
+            self.probabilities = np.ones(len(self.values), dtype=float)
+            self.probabilities = self.probabilities / np.sum(self.probabilities)
         else:
             self.probabilities = np.array(probabilities)
         if not len(self.values) == len(self.probabilities):
@@ -723,8 +820,43 @@ class DiscreteDistribution(_TableDistribution):
     def __repr__(self):
         return f"{type(self).__name__}(values={repr(self.values)}, probabilities={repr(self.probabilities)})"
 
-    def _sample(self, q):
-        return self.values[np.searchsorted(np.cumsum(self.probabilities), v=q, side="right")]
+    def _kind(self):
+        dt = self.values.dtype
+        if dt == np.bool_ or np.issubdtype(dt, np.integer):
+            return "int64"
+        if np.issubdtype(dt, np.floating):
+            return "float64"
+        return None  # labels
+
+    def _build_tables(self):
+        cum = np.cumsum(self.probabilities).astype(np.float64)  # the reference's host cumsum, bit for bit
+        kind = self._kind()
+        vals = None if kind is None else device.to_device(self.values.astype(kind))
+        return device.to_device(cum), vals
+
+    def _sample_device(self, ev, column, out=None):
+        return _into(self._sample_table(ev, column), out)
+
+    def _sample_table(self, ev, column):
+        cum, vals = self._tables()
+        kind = self._kind() or "int64"
+        res = self._launch(ev, column, _lib.TABLE_SEARCH, cum, vals, cum.shape[0], 0, kind)
+        self.__dict__["_labels"] = self.values if self._kind() is None else None
+        if self.values.dtype == np.bool_:
+            res = _elementwise("cast", res, None, ev.size, np.dtype(bool), np.dtype(np.int64), None)
+        return res
+
+    def _samples_get(self):
+        v = Node.samples_.fget(self)
+        labels = self.__dict__.get("_labels")
+        return v if labels is None or v is None else labels[v]
+
+    samples_ = property(_samples_get, Node.samples_.fset, Node.samples_.fdel)
+
+    def _dev(self):
+        if self.__dict__.get("_labels") is not None:
+            raise TypeError(f"{self!r}: non-numeric values cannot enter device arithmetic")
+        return super()._dev()
 
 
 # =============================================================================
