@@ -41,7 +41,11 @@ typedef enum pbh_dist {
   PBH_DIST_LOGNORM = 3, /* params: s, loc, scale              exp(s * ndtri(q))              */
   PBH_DIST_TRIANG = 4,  /* params: c, loc, scale                                             */
   PBH_DIST_GAMMA = 5,   /* params: a, loc, scale              gammaincinv(a, q)              */
-  PBH_DIST_POISSON = 6  /* params: mu, loc  (discrete)        smallest k: pdtr(k, mu) >= q   */
+  PBH_DIST_POISSON = 6, /* params: mu, loc  (discrete)        smallest k: pdtr(k, mu) >= q   */
+  PBH_DIST_BETA = 7,    /* params: a, b, loc, scale           I_x(a, b) = q (Boost ibeta_inv) */
+  PBH_DIST_TRUNCNORM = 8, /* params: a, b, loc, scale         truncnorm._ppf (log space)     */
+  PBH_DIST_BINOM = 9,   /* params: n, p, loc (discrete)       smallest k: bdtr(k, n, p) >= q */
+  PBH_DIST_BERNOULLI = 10 /* params: p, loc (discrete)        binom with n = 1               */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(HERE, "libprobabilit_hip.so")
 OK, ERR_INVALID, ERR_HIP, ERR_NOT_PD, ERR_NONFINITE, ERR_WORKSPACE, ERR_UNSUPPORTED = range(7)
 
 # pbh_dist
-DIST_IDS = {"norm": 0, "uniform": 1, "expon": 2, "lognorm": 3, "triang": 4, "gamma": 5, "poisson": 6}
+DIST_IDS = {"norm": 0, "uniform": 1, "expon": 2, "lognorm": 3, "triang": 4, "gamma": 5, "poisson": 6, "beta": 7,
+            "truncnorm": 8, "binom": 9, "bernoulli": 10}
 
 # pbh_table_kind
 TABLE_INTERP, TABLE_QUANTILE, TABLE_SEARCH = 0, 1, 2

@@ -7,6 +7,7 @@
 #include <math.h>
 
 #include "pbh_error.h"
+#include "pbh_ppf_ext.h"
 #include "pbh_rng.h"
 #include "pbh_special.h"
 #include "pbh_sort.h"
@@ -546,6 +547,7 @@ extern "C" int pbh_ppf(int dist, const double* q, int64_t q_stride, int64_t n, c
   if (n == 0) return PBH_OK;
   PBH_REQUIRE(q != nullptr && out != nullptr, "pbh_ppf: q and out must be device pointers");
   hipStream_t s = as_stream(stream);
+  if (dist >= PBH_DIST_BETA) return ppf_ext(dist, q, q_stride, n, params, nparams, out, nonfinite_flag, s);
   Params prm;
   PoissonTable pt;
   double* table = nullptr;
@@ -563,6 +565,8 @@ extern "C" int pbh_lhs_ppf(uint64_t seed, int64_t n, int64_t row0, int64_t nrows
   PBH_REQUIRE(col >= 0, "pbh_lhs_ppf: bad column");
   if (nrows == 0) return PBH_OK;
   hipStream_t s = as_stream(stream);
+  if (dist >= PBH_DIST_BETA)
+    return lhs_ppf_ext(seed, n, row0, nrows, col, dist, params, nparams, out, nonfinite_flag, s);
   Params prm;
   PoissonTable pt;
   double* table = nullptr;

@@ -410,7 +410,7 @@ class Node(abc.ABC):
         generated = (bool(correlations) and isinstance(source, qmc.LHSSource)
                      and isinstance(correlator, type) and issubclass(correlator, ImanConover)
                      and set(all_variables) <= set(isns)
-                     and all(type(v) is Distribution and v.distr in _DIST_SHAPES and v.is_leaf
+                     and all(type(v) is Distribution and v.distr in _FUSED_LHS and v.is_leaf
                              for v in all_variables))
         if world > 1 and correlations and not generated:
             raise NotImplementedError("row-sharded evaluation correlates natively generated LHS columns of leaf "
@@ -568,8 +568,11 @@ class AbstractDistribution(Node, OverloadMixin, abc.ABC):
 # scipy.stats parameter layout of the distributions with native kernels: shape names,
 # then loc (and scale for continuous ones) -- scipy's rv_generic._parse_args.
 _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "triang": ("c",),
-                "gamma": ("a",), "poisson": ("mu",)}
-_DISCRETE = {"poisson"}
+                "gamma": ("a",), "poisson": ("mu",), "beta": ("a", "b"), "truncnorm": ("a", "b"),
+                "binom": ("n", "p"), "bernoulli": ("p",)}
+_DISCRETE = {"poisson", "binom", "bernoulli"}
+# distributions with a fused native-LHS + inverse-CDF kernel (and the Iman-Conover fast path)
+_FUSED_LHS = {"norm", "uniform", "expon", "lognorm", "triang", "gamma", "poisson"}
 
 
 def _parse_scipy_args(name, args, kwargs):

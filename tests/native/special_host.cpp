@@ -46,3 +46,27 @@ double sfh_guide_ok_fraction(double a) {
   return (double)ok / (m - 1);
 }
 }
+
+// ---- extended distributions (pbh_special_ext.h)
+#include "pbh_special_ext.h"
+
+extern "C" {
+void sfh_log_ndtr(const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::log_ndtr(x[i]);
+}
+void sfh_ndtri_exp(const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::ndtri_exp(x[i]);
+}
+void sfh_truncnorm_ppf(double a, double b, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::truncnorm_ppf01(q[i], a, b);
+}
+void sfh_incbet(double a, double b, const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::incbet(a, b, x[i]);
+}
+void sfh_beta_ppf(double a, double b, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::beta_ppf01(q[i], a, b);
+}
+void sfh_binom_ppf(double nn, double p, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::binom_ppf01(q[i], nn, p);
+}
+}

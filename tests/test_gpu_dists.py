@@ -1,0 +1,103 @@
+"""Distributions beyond the base set on the GPU (beta / PERT, truncnorm,
+binom, bernoulli and the distributions.py constructors) against scipy's ppf on the same
+quantiles (the reference's computation, modeling.py:807) and against outputs of the reference
+itself (tests/golden/dists.npz).  Gate: 1e-10 relative for floating point, exact for discrete."""
+
+import numpy as np
+import pytest
+
+from conftest import assert_close, golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _q(n, seed):
+    q = np.random.default_rng(seed).random(n)
+    return np.concatenate([q, [0.0, 2.0**-53 / 1e8, 1e-12, 0.5, 1 - 1e-12, 1 - 2.0**-53, 1.0]])
+
+
+@pytest.mark.parametrize("kw", [dict(a=0.5, b=0.5), dict(a=3.4, b=2.6, loc=0, scale=10), dict(a=7.0, b=5.0),
+                                dict(a=0.1, b=10.0), dict(a=50.0, b=80.0, loc=-1.0, scale=3.0), dict(a=1.0, b=1.0)])
+def test_beta_ppf(gpu, kw):
+    import scipy.stats
+
+    from probabilit_amd import native
+
+    q = _q(20_000, 1)
+    assert_close(native.ppf("beta", q, **kw), scipy.stats.beta(**kw).ppf(q), rtol=1e-10, atol=1e-300, what=f"{kw}")
+
+
+@pytest.mark.parametrize("kw", [dict(a=3.0, b=3.3), dict(a=-1.0, b=1.0, loc=2.0, scale=0.5), dict(a=-3.3, b=-3.0),
+                                dict(a=-0.5, b=2.0), dict(a=0.1, b=8.0), dict(a=-40.0, b=-39.5)])
+def test_truncnorm_ppf(gpu, kw):
+    import scipy.stats
+
+    from probabilit_amd import native
+
+    q = _q(20_000, 2)
+    ref = scipy.stats.truncnorm(**kw).ppf(q)
+    assert_close(native.ppf("truncnorm", q, **kw), ref, rtol=1e-10, atol=1e-13, what=f"{kw}")
+
+
+@pytest.mark.parametrize("name,kw", [("binom", dict(n=1, p=0.3)), ("binom", dict(n=20, p=0.3)),
+                                     ("binom", dict(n=1000, p=0.7, loc=2)), ("binom", dict(n=37, p=0.01)),
+                                     ("binom", dict(n=5, p=0.0)), ("binom", dict(n=5, p=1.0)),
+                                     ("binom", dict(n=2.5, p=0.5)), ("bernoulli", dict(p=0.25)),
+                                     ("bernoulli", dict(p=0.0))])
+def test_discrete_ppf_exact(gpu, name, kw):
+    import scipy.stats
+
+    from probabilit_amd import native
+
+    q = _q(50_000, 3)
+    np.testing.assert_array_equal(native.ppf(name, q, **kw), getattr(scipy.stats, name)(**kw).ppf(q))
+
+
+def test_composite_beta_parameters(gpu):
+    import scipy.stats
+
+    from probabilit_amd import native
+
+    n = 10_000
+    rng = np.random.default_rng(4)
+    q, a, b = rng.random(n), 1 + 3 * rng.random(n), 0.5 + rng.random(n)
+    assert_close(native.ppf("beta", q, a=a, b=b), scipy.stats.beta(a=a, b=b).ppf(q), rtol=1e-10, atol=1e-300)
+
+
+def test_distribution_constructors_vs_reference(gpu):
+    """distributions.py constructors sampled with method=None: the reference's own outputs."""
+    from probabilit_amd import distributions as dists
+    from probabilit_amd.modeling import Distribution as D
+
+    z = golden("dists.npz")
+    assert_close(dists.PERT(0, 6, 10).sample(2000, random_state=0), z["pert"], what="PERT")
+    assert_close(dists.TruncatedNormal(loc=0, scale=1, low=3, high=3.3).sample(2000, random_state=0), z["tnorm"],
+                 what="TruncatedNormal")
+    assert_close(dists.Lognormal(mean=2, std=1).sample(999, random_state=0), z["lognorm_ms"], what="Lognormal")
+    assert_close(dists.Lognormal(mean=D("expon", scale=1), std=1).sample(500, random_state=0), z["lognorm_comp"],
+                 what="Lognormal composite")
+    assert_close(dists.Triangular(low=1, mode=5, high=9).sample(1000, random_state=3), z["tri"], what="Triangular")
+    np.testing.assert_array_equal(D("binom", n=20, p=0.3).sample(3000, random_state=2), z["binom"])
+    np.testing.assert_array_equal(D("bernoulli", p=0.25).sample(3000, random_state=2), z["bern"])
+    assert_close(D("beta", 0.5, 0.5).sample(2000, random_state=5), z["beta_small"], what="beta(0.5, 0.5)")
+    assert_close(D("beta", a=D("uniform", loc=1, scale=3), b=2.0).sample(1500, random_state=7), z["composite"],
+                 what="composite beta")
+
+
+def test_distributions_docstring_pins(gpu):
+    """distributions.py:22-24, 40-55, 70-74, 84-88, 105-111."""
+    from probabilit_amd import distributions as dists
+    from probabilit_amd.modeling import Distribution as D
+
+    np.testing.assert_array_equal(dists.TruncatedNormal(loc=0, scale=1, low=3, high=3.3).sample(7, random_state=0)
+                                  .round(3), [3.13, 3.182, 3.146, 3.129, 3.095, 3.159, 3.099])
+    s = dists.Lognormal(mean=2, std=1).sample(999, random_state=0)
+    assert str(float(np.mean(s))).startswith("2.00173") and str(float(np.std(s))).startswith("1.02675")
+    np.testing.assert_allclose(dists.Lognormal(mean=D("expon", scale=1), std=1).sample(5, random_state=0),
+                               [0.86196529, 0.69165866, 0.41782557, 1.23340656, 2.90778578], rtol=0, atol=5e-9)
+    np.testing.assert_allclose(dists.Lognormal.from_log_params(mu=D("norm"), sigma=1).sample(5, random_state=0),
+                               [1.99625633, 1.45244764, 1.19926216, 2.94150961, 4.47459182], rtol=0, atol=5e-9)
+    assert repr(dists.PERT(0, 6, 10)) == 'Distribution("beta", a=3.4, b=2.6, loc=0, scale=10)'
+    assert repr(dists.PERT(0, 6, 10, gamma=10)) == 'Distribution("beta", a=7.0, b=5.0, loc=0, scale=10)'
+    assert repr(dists.Triangular(low=1, mode=5, high=9, low_perc=0, high_perc=1)) == \
+        'Distribution("triang", loc=1, scale=8, c=0.5)'

@@ -190,7 +190,7 @@ def test_unsupported_distribution_fails_loudly(gpu):
     from probabilit_amd.modeling import Distribution
 
     with pytest.raises(NotImplementedError):
-        Distribution("beta", a=2, b=3).sample(10, random_state=0)
+        Distribution("weibull_min", c=2).sample(10, random_state=0)
     with pytest.raises(AttributeError):
         Distribution("no_such_distribution").sample(10, random_state=0)
 

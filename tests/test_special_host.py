@@ -26,7 +26,7 @@ def sfh():
     hipcc = "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else shutil.which("hipcc")
     if hipcc is None:
         pytest.skip("hipcc not available")
-    deps = [SRC] + [os.path.join(ROOT, "probabilit_amd", "csrc", f) for f in ("pbh_special.h", "pbh_common.h",
+    deps = [SRC] + [os.path.join(ROOT, "probabilit_amd", "csrc", f) for f in ("pbh_special.h", "pbh_special_ext.h", "pbh_common.h",
                                                                             "pbh_tables.inc")]
     if not os.path.exists(OUT) or any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
@@ -99,3 +99,57 @@ def test_guide_table_mostly_interpolates(sfh, a, floor):
     which is deliberately left to igami."""
     sfh.sfh_guide_ok_fraction.restype = ctypes.c_double
     assert sfh.sfh_guide_ok_fraction(ctypes.c_double(a)) >= floor
+
+
+# ---------------------------------------------------------------- extended distributions
+def _arr(lib, fn, *scal, x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    f = getattr(lib, fn)
+    f.restype = None
+    cargs = [ctypes.c_double(v) for v in scal]
+    f(*cargs, x.ctypes.data_as(ctypes.c_void_p), ctypes.c_long(x.size), out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def _rel(a, e):
+    with np.errstate(all="ignore"):
+        return np.nanmax(np.abs(a - e) / np.maximum(np.abs(e), 1e-300))
+
+
+def test_log_ndtr_and_ndtri_exp(sfh):
+    x = np.concatenate([-np.logspace(-3, 2.5, 400), np.linspace(-5, 8, 400)])
+    assert _rel(_arr(sfh, "sfh_log_ndtr", x=x), sp.log_ndtr(x)) < 1e-13
+    y = np.concatenate([-np.logspace(-12, 4, 500), [-1e-300, -0.1454134578688591, -2.0, -2.0000001]])
+    assert _rel(_arr(sfh, "sfh_ndtri_exp", x=y), sp.ndtri_exp(y)) < 1e-13
+
+
+@pytest.mark.parametrize("a,b", [(-1.0, 1.0), (3.0, 3.3), (-3.3, -3.0), (-0.5, 2.0), (0.1, 8.0), (-40, -39.5)])
+def test_truncnorm_ppf(sfh, a, b):
+    import scipy.stats as st
+
+    q = np.concatenate([np.linspace(1e-6, 1 - 1e-6, 999), [1e-300, 0.5, 1 - 2**-53]])
+    got = _arr(sfh, "sfh_truncnorm_ppf", a, b, x=q)
+    ref = st.truncnorm(a, b).ppf(q)
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-13)
+
+
+@pytest.mark.parametrize("a,b", [(0.5, 0.5), (2.0, 3.0), (3.4, 2.6), (7.0, 5.0), (0.1, 10.0), (50.0, 80.0),
+                                 (1.0, 1.0), (200.0, 0.7)])
+def test_incbet_and_beta_ppf(sfh, a, b):
+    x = np.linspace(0, 1, 1001)
+    np.testing.assert_allclose(_arr(sfh, "sfh_incbet", a, b, x=x), sp.betainc(a, b, x), rtol=1e-12, atol=1e-300)
+    # q >= 2^-53 / n covers every generator here; Boost (scipy) gives NaN for some q ~ 1e-300
+    # where the root underflows its internal scaling, which no generated quantile reaches
+    q = np.concatenate([np.linspace(1e-9, 1 - 1e-9, 2001), [1e-30, 2.0**-53 / 1e8, 0.5, 1 - 2**-52]])
+    got = _arr(sfh, "sfh_beta_ppf", a, b, x=q)
+    np.testing.assert_allclose(got, sp.betaincinv(a, b, q), rtol=1e-10, atol=1e-300)
+
+
+@pytest.mark.parametrize("n,p", [(1, 0.3), (10, 0.5), (37, 0.01), (1000, 0.7), (20, 0.0), (20, 1.0)])
+def test_binom_ppf(sfh, n, p):
+    import scipy.stats as st
+
+    q = np.random.default_rng(n).random(5000)
+    got = _arr(sfh, "sfh_binom_ppf", n, p, x=q)
+    np.testing.assert_array_equal(got, st.binom(n, p).ppf(q))
