@@ -57,6 +57,7 @@ struct IcLayout {
   unsigned long long* counts;   // ties, inversions of a generated sorted column
   void* heads_ws;
   uint32_t* codes;              // K x n step-4 sort keys, written by the step-3 kernel
+  double* colpart;              // K x perm_scores_blocks(n) per-block score sums (step-2 means)
 };
 
 size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
@@ -75,7 +76,9 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* counts = c.take(256);
   void* hws = c.take(run_heads_ws_bytes(n));
   void* codes = c.take((size_t)n * k * 4);
+  void* colpart = c.take((size_t)k * perm_scores_blocks(n) * 8);
   if (carve) {
+    L->colpart = (double*)colpart;
     L->codes = (uint32_t*)codes;
     L->S = (double*)S;
     L->sorted_x = (double*)sx;
@@ -181,6 +184,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
 
   // ---- step 1: van der Waerden scores of every column (+ the sorted column for step 4)
   PBH_CHECK_HIP(hipMemsetAsync(L.flag, 0, sizeof(int32_t), s));
+  bool all_generated = true;  // every column's scores came from perm_scores (with partial sums)
   for (int c = 0; c < k; ++c) {
     double* S_c = L.S + (int64_t)c * n;
     double* sx_c = L.sorted_x + (int64_t)c * n;
@@ -191,9 +195,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       const pbh_ic_column& g = a->columns[c];
       pbh_param prm[3];
       for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
-      st = lhs_sorted_ppf(g.seed, n, 0, n, g.lhs_col, g.dist, prm, g.nparams, sx_c, g.nonfinite_flag, s);
-      if (st) return st;
-      st = check_sorted(sx_c, n, L.counts, s);
+      st = lhs_sorted_ppf(g.seed, n, 0, n, g.lhs_col, g.dist, prm, g.nparams, sx_c, g.nonfinite_flag, s, L.counts);
       if (st) return st;
       unsigned long long cnt[2];
       PBH_CHECK_HIP(hipMemcpyAsync(cnt, L.counts, sizeof(cnt), hipMemcpyDeviceToHost, s));
@@ -206,7 +208,8 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
           st = run_heads(sx_c, n, 0, false, heads, &nheads, L.heads_ws, s);
           if (st) return st;
         }
-        st = perm_scores(g.seed, n, g.lhs_col, 0, n, heads, nheads, S_c, s);
+        st = perm_scores(g.seed, n, g.lhs_col, 0, n, heads, nheads, S_c, s,
+                         L.colpart + (int64_t)c * perm_scores_blocks(n));
         if (st) return st;
         continue;
       }
@@ -216,6 +219,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       x_c = L.tmp;
       x_stride = 1;
     }
+    all_generated = false;
     st = load_keys(x_c, x_stride, n, sb.keys[0], L.flag, s);
     if (st) return st;
     int buf = 0;
@@ -233,7 +237,10 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     PBH_CHECK_HIP(hipMemcpyAsync(a->scores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
 
   // ---- step 2: E = corrcoef(S) on the host from the device Gram matrix
-  st = column_means(L.S, n, k, n, L.partials, L.means, s);
+  if (all_generated)  // the scores kernels left per-block sums behind
+    st = means_from_partials(L.colpart, (int)perm_scores_blocks(n), k, (double)n, L.means, s);
+  else
+    st = column_means(L.S, n, k, n, L.partials, L.means, s);
   if (st) return st;
   st = centered_gram(L.S, n, k, n, L.means, L.partials, L.gram, s);
   if (st) return st;

@@ -81,6 +81,8 @@ int tie_fix_values(const uint8_t* eqprev, int64_t n, const double* src, double* 
 int column_sums(const double* S, int64_t n, int k, int64_t ld, double* partial, double* out, double divisor,
                 hipStream_t s);
 // Column means (k columns of length n, column stride ld) into means[k] (device), fixed order.
+// means[c] = (sum_b partial[c * nb + b]) / divisor, in block order (k_means).
+int means_from_partials(const double* partial, int nb, int k, double divisor, double* means, hipStream_t s);
 int column_means(const double* S, int64_t n, int k, int64_t ld, double* partial, double* means, hipStream_t s);
 size_t gram_partials_bytes(int k);
 // Centered Gram matrix G = (S - m)^T (S - m), k x k row-major into gram (device), fixed order.

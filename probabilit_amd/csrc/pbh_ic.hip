@@ -563,6 +563,12 @@ int column_sums(const double* S, int64_t n, int k, int64_t ld, double* partial, 
   return PBH_OK;
 }
 
+int means_from_partials(const double* partial, int nb, int k, double divisor, double* means, hipStream_t s) {
+  hipLaunchKernelGGL(k_means, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, s, partial, nb, k, divisor, means);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
 int column_means(const double* S, int64_t n, int k, int64_t ld, double* partial, double* means, hipStream_t s) {
   return column_sums(S, n, k, ld, partial, means, (double)n, s);
 }

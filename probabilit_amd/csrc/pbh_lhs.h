@@ -7,15 +7,20 @@ namespace pbh {
 
 // out[t - t0] = ppf of the LHS point in stratum t of column `col`, t in [t0, t0 + nt)
 // (scalar parameters only).
+// counts != NULL: counts[0] = #ties x[t] == x[t+1], counts[1] = #inversions, inside the segment
+// (zeroed first; device counters).
 int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist, const pbh_param* params,
-                   int nparams, double* out, int32_t* flag, hipStream_t s);
+                   int nparams, double* out, int32_t* flag, hipStream_t s, unsigned long long* counts = nullptr);
 // counts[0] = #ties x[t] == x[t+1], counts[1] = #inversions x[t] > x[t+1] (device counters).
 int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStream_t s);
 // S[r - row0] = ndtri(rank(r) / (n + 1)) for rows [row0, row0 + nrows): rank(r) = pi(r) + 1, or
 // the 'average' rank of the run holding stratum pi(r) when heads != NULL (nheads sorted run
 // heads of the whole sorted column, heads[0] == 0).
+// partial != NULL: partial[b] = sum of the scores block b wrote (ppf_grid(nrows) blocks).
 int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, const uint32_t* heads,
-                int64_t nheads, double* S, hipStream_t s);
+                int64_t nheads, double* S, hipStream_t s, double* partial = nullptr);
+// number of partial sums perm_scores writes for nrows rows
+unsigned perm_scores_blocks(int64_t nrows);
 // Run heads of a sorted segment x[0..m) (see k_heads_write); *count = number written (syncs).
 size_t run_heads_ws_bytes(int64_t m);
 int run_heads(const double* x, int64_t m, int64_t t0, bool first_is_prev, uint32_t* heads, int64_t* count,

@@ -151,23 +151,74 @@ __global__ __launch_bounds__(kBlock) void k_lhs_ppf(uint64_t seed, int64_t n, in
 
 // The same LHS column in stratum order: out[t] = ppf(q) for the row pi^-1(t) that holds
 // stratum t.  Bit-identical to k_lhs_ppf's value for that row; non-decreasing in t whenever
-// the ppf is monotone, which k_check_sorted verifies before anything relies on it.
+// the ppf is monotone.  With counts != NULL the kernel also counts, over the pairs (t, t + 1)
+// inside the segment, counts[0] += #ties and counts[1] += #inversions (what k_check_sorted
+// would find, without re-reading the column): lane l compares with lane l + 1 through a wave
+// shuffle, the last lane of a wave evaluates stratum t + 1 itself; one atomic pair per block.
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt,
                                                            uint32_t col, Params prm, PoissonTable pt,
-                                                           double* __restrict__ out, int32_t* flag) {
+                                                           double* __restrict__ out, int32_t* flag,
+                                                           unsigned long long* counts) {
+  __shared__ unsigned long long sh[2][kBlock / 64];
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int64_t step = (int64_t)gridDim.x * kBlock;
-  for (; i < nt; i += step) {
-    const int64_t t = t0 + i;
-    uint64_t row = fp.inverse((uint64_t)t);
-    double u = ph.uniform(row, col, kPurposeLhsU);
-    double q = ((double)(t + 1) - u) / (double)n;
-    double x = ppf_one<D>(q, prm.val[0], prm.val[1], prm.val[2], pt);
-    out[i] = x;
-    flag_nonfinite(flag, !isfinite(x));
+  auto value = [&](int64_t t) {
+    const uint64_t row = fp.inverse((uint64_t)t);
+    const double u = ph.uniform(row, col, kPurposeLhsU);
+    const double q = ((double)(t + 1) - u) / (double)n;
+    return ppf_one<D>(q, prm.val[0], prm.val[1], prm.val[2], pt);
+  };
+  const int lane = threadIdx.x & 63;
+  unsigned long long ties = 0, inv = 0;
+  if (!counts) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nt; i += (int64_t)gridDim.x * kBlock) {
+      const double x = value(t0 + i);
+      out[i] = x;
+      flag_nonfinite(flag, !isfinite(x));
+    }
+  } else {
+    // waves advance by 63 strata and overlap by one: lane 63 evaluates the stratum the next
+    // wave writes from its lane 0, so every pair (t, t + 1) meets inside one wave (a divergent
+    // extra evaluation by one lane would cost the whole wave a second pass).
+    const int64_t waves = (int64_t)gridDim.x * (kBlock / 64);
+    const int64_t wid0 = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int64_t iters = (nt + 63 * waves - 1) / (63 * waves);  // uniform trip count
+    for (int64_t it = 0; it < iters; ++it) {
+      const int64_t i = (it * waves + wid0) * 63 + lane;
+      const bool valid = i < nt;
+      double x = 0.0;
+      if (valid) {
+        x = value(t0 + i);
+        if (lane < 63) out[i] = x;
+      }
+      flag_nonfinite(flag, valid && lane < 63 && !isfinite(x));
+      const double nx = __shfl_down(x, 1, 64);
+      const bool has_next = valid && lane < 63 && i + 1 < nt;
+      ties += has_next && x == nx;
+      inv += has_next && !(x <= nx);
+    }
+  }
+  if (counts) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      ties += __shfl_xor(ties, o, 64);
+      inv += __shfl_xor(inv, o, 64);
+    }
+    if (lane == 0) {
+      sh[0][threadIdx.x >> 6] = ties;
+      sh[1][threadIdx.x >> 6] = inv;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long a = 0, b = 0;
+      for (int w = 0; w < kBlock / 64; ++w) {
+        a += sh[0][w];
+        b += sh[1][w];
+      }
+      if (a) atomicAdd(&counts[0], a);
+      if (b) atomicAdd(&counts[1], b);
+    }
   }
 }
 
@@ -211,17 +262,35 @@ __device__ __forceinline__ double run_average_rank(const uint32_t* __restrict__ 
 
 // Van der Waerden scores of an LHS column, rows [row0, row0 + nrows), in row order: the rank
 // of row r is pi(r) + 1 (untied), or the run average of stratum pi(r) (heads != NULL), so
-// S[r] = ndtri(rank / (n + 1)) (correlation.py:394-395) without sorting anything.
+// S[r] = ndtri(rank / (n + 1)) (correlation.py:394-395) without sorting anything.  With
+// partial != NULL each block also writes the sum of its scores to partial[blockIdx.x] (the
+// column mean of step 2 without re-reading S; summed in a fixed order by k_means).
 __global__ __launch_bounds__(kBlock) void k_perm_scores(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
                                                         int64_t nrows, const uint32_t* __restrict__ heads,
-                                                        int64_t nheads, double* __restrict__ S) {
+                                                        int64_t nheads, double* __restrict__ S,
+                                                        double* __restrict__ partial) {
+  __shared__ double sh[kBlock / 64];
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
   const double np1 = (double)(n + 1);
+  double sum = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
     const uint64_t t = fp((uint64_t)(row0 + i));
     const double rank = heads ? run_average_rank(heads, nheads, n, (int64_t)t) : (double)(t + 1);
-    S[i] = sf::ndtri(rank / np1);
+    const double v = sf::ndtri(rank / np1);
+    S[i] = v;
+    sum += v;
+  }
+  if (partial) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double b = 0.0;
+      for (int w = 0; w < kBlock / 64; ++w) b += sh[w];
+      partial[blockIdx.x] = b;
+    }
   }
 }
 
@@ -454,7 +523,7 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
 }  // namespace
 
 int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist, const pbh_param* params,
-                   int nparams, double* out, int32_t* flag, hipStream_t s) {
+                   int nparams, double* out, int32_t* flag, hipStream_t s, unsigned long long* counts) {
   PBH_REQUIRE(t0 >= 0 && nt >= 0 && t0 + nt <= n, "lhs_sorted_ppf: strata [%lld, %lld) outside [0, %lld)",
               (long long)t0, (long long)(t0 + nt), (long long)n);
   if (nt == 0) return PBH_OK;
@@ -466,12 +535,13 @@ int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, in
   int st = with_params(dist, params, nparams, prm, pt, &table, s);
   if (st != PBH_OK) return st;
   dim3 g(ppf_grid(nt)), b(kBlock);
+  if (counts) PBH_CHECK_HIP(hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), s));
   switch (dist) {
 #define PBH_CASE(D)                                                                                         \
   case D:                                                                                                   \
     PBH_TIMED(kKLhsSorted, s,                                                                               \
               hipLaunchKernelGGL(k_lhs_sorted_ppf<D>, g, b, 0, s, seed, n, t0, nt, (uint32_t)col, prm, pt, \
-                                 out, flag));                                                               \
+                                 out, flag, counts));                                                       \
     break;
     PBH_CASE(PBH_DIST_NORM)
     PBH_CASE(PBH_DIST_UNIFORM)
@@ -497,13 +567,15 @@ int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStre
   return PBH_OK;
 }
 
+unsigned perm_scores_blocks(int64_t nrows) { return ppf_grid(nrows); }
+
 int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, const uint32_t* heads,
-                int64_t nheads, double* S, hipStream_t s) {
+                int64_t nheads, double* S, hipStream_t s, double* partial) {
   PBH_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "perm_scores: rows outside [0, n)");
   if (nrows == 0) return PBH_OK;
   PBH_TIMED(kKPermScores, s,
             hipLaunchKernelGGL(k_perm_scores, dim3(ppf_grid(nrows)), dim3(kBlock), 0, s, seed, n, (uint32_t)col, row0,
-                               nrows, heads, nheads, S));
+                               nrows, heads, nheads, S, partial));
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }

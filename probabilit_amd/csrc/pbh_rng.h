@@ -4,11 +4,13 @@
 // (row, column, purpose), so every (row, column) draw is independent of launch geometry
 // and of how rows are sharded across GPUs.
 //
-// The LHS permutation of column c is a keyed bijection of [0, n): a balanced Feistel
-// network on the smallest even bit width 2h with 2^(2h) >= n, restricted to [0, n) by
-// cycle walking (Black & Rogaway 2002).  Both directions are cheap, so a row's stratum and
-// a stratum's row are computed, never stored.
+// The LHS permutation of column c is a keyed bijection of [0, n): a mixed-radix Feistel
+// network on [0, A B) with A B just above n, restricted to [0, n) by cycle walking (Black &
+// Rogaway 2002).  Both directions are cheap, so a row's stratum and a stratum's row are
+// computed, never stored.
 #pragma once
+
+#include <math.h>
 
 #include "pbh_common.h"
 
@@ -67,24 +69,31 @@ PBH_HD inline uint32_t mix32(uint32_t x) {  // lowbias32 finalizer
   return x;
 }
 
-// Alternating (unbalanced) Feistel network on b = ceil(log2 n) bits: the high part L
-// (b - b/2 bits) and the low part R (b/2 bits) take turns being xored with a keyed round
-// function of the other part.  Every round is an involution on its half, so the network is
-// a bijection of [0, 2^b) for any split, and 2^b < 2n keeps cycle walking short (expected
-// < 2 walks; the wave-wide maximum, which is what a SIMD lane waits for, stays ~3-4).
+// Keyed bijection of [0, n): an alternating Feistel network over the mixed radix
+// Z_A x Z_B (A = ceil(sqrt(n)), B = ceil(n / A), so n <= A B < n + A), with modular addition
+// (Black & Rogaway 2002, the FE2 construction of format-preserving encryption): x = L B + R,
+// even rounds L <- (L + F(R)) mod A, odd rounds R <- (R + F(L)) mod B.  Every round is a
+// bijection of its half, so the network is a bijection of [0, A B); values >= n are cycle-
+// walked, which happens with probability < 1 / B (~1e-4 at n = 1e8), so a SIMD lane almost
+// never waits on a neighbour's walk -- unlike a power-of-two domain, where 2^b can be ~2n and
+// the wave-wide maximum walk count is ~4.  F = lowbias32 of the half, reduced to the radix by
+// a multiply-high (Lemire), 4 32-bit multiplies per round.
 struct FeistelPerm {
   static constexpr int kRounds = 6;
   uint64_t n;
-  uint32_t r_bits, mask_l, mask_r;
+  uint32_t A, B;
+  double inv_b;
   uint32_t rk[kRounds];
 
   PBH_HD FeistelPerm(const Philox& ph, uint64_t n_, uint32_t col) : n(n_) {
-    uint32_t bits = 0;
-    while (bits < 64 && (1ull << bits) < n_) ++bits;
-    r_bits = bits / 2;
-    uint32_t l_bits = bits - r_bits;
-    mask_r = (r_bits >= 32) ? 0xFFFFFFFFu : ((1u << r_bits) - 1u);
-    mask_l = (l_bits >= 32) ? 0xFFFFFFFFu : ((1u << l_bits) - 1u);
+    uint64_t a = (uint64_t)sqrt((double)n_);  // A = ceil(sqrt(n)): sqrt, then at most a step or two
+    if (a == 0) a = 1;
+    while (a * a < n_) ++a;
+    while (a > 1 && (a - 1) * (a - 1) >= n_) --a;
+    A = (uint32_t)a;
+    B = (uint32_t)((n_ + A - 1) / A);
+    if (B == 0) B = 1;
+    inv_b = 1.0 / (double)B;
     uint32_t c[4] = {col, 0u, 0u, kPurposeFeistel};
     ph(c);
     uint32_t d[4] = {col, 1u, 0u, kPurposeFeistel};
@@ -97,30 +106,47 @@ struct FeistelPerm {
     rk[5] = d[1];
   }
 
+  PBH_HD static inline uint32_t reduce(uint32_t h, uint32_t m) { return (uint32_t)(((uint64_t)h * m) >> 32); }
   PBH_HD inline uint32_t F(uint32_t v, uint32_t k) const { return mix32(v * 0x9E3779B1u ^ k); }
 
+  PBH_HD inline void split(uint64_t x, uint32_t& L, uint32_t& R) const {
+    uint64_t q = (uint64_t)((double)x * inv_b);
+    while (q * B > x) --q;
+    while (x - q * B >= B) ++q;
+    L = (uint32_t)q;
+    R = (uint32_t)(x - q * B);
+  }
+
   PBH_HD inline uint64_t round_trip(uint64_t x) const {
-    uint32_t L = (uint32_t)(x >> r_bits), R = (uint32_t)(x & mask_r);
+    uint32_t L, R;
+    split(x, L, R);
 #pragma unroll
     for (int i = 0; i < kRounds; ++i) {
-      if (i & 1)
-        R ^= F(L, rk[i]) & mask_r;
-      else
-        L ^= F(R, rk[i]) & mask_l;
+      if (i & 1) {
+        const uint32_t h = reduce(F(L, rk[i]), B);
+        R = R + h >= B ? R + h - B : R + h;
+      } else {
+        const uint32_t h = reduce(F(R, rk[i]), A);
+        L = L + h >= A ? L + h - A : L + h;
+      }
     }
-    return ((uint64_t)L << r_bits) | R;
+    return (uint64_t)L * B + R;
   }
 
   PBH_HD inline uint64_t round_trip_inv(uint64_t y) const {
-    uint32_t L = (uint32_t)(y >> r_bits), R = (uint32_t)(y & mask_r);
+    uint32_t L, R;
+    split(y, L, R);
 #pragma unroll
     for (int i = kRounds - 1; i >= 0; --i) {
-      if (i & 1)
-        R ^= F(L, rk[i]) & mask_r;
-      else
-        L ^= F(R, rk[i]) & mask_l;
+      if (i & 1) {
+        const uint32_t h = reduce(F(L, rk[i]), B);
+        R = R >= h ? R - h : R + B - h;
+      } else {
+        const uint32_t h = reduce(F(R, rk[i]), A);
+        L = L >= h ? L - h : L + A - h;
+      }
     }
-    return ((uint64_t)L << r_bits) | R;
+    return (uint64_t)L * B + R;
   }
 
   // Bijection of [0, n) by cycle walking.

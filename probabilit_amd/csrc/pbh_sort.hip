@@ -365,19 +365,24 @@ __global__ __launch_bounds__(256) void k_place_bases(int64_t n, int shift, uint3
   bases[d] = block_exclusive_scan_256((uint32_t)count, sh, nullptr);
 }
 
-// Items per thread of the one-sweep scatter (tile = 256 x items): PBH_OS_IPT = 16 or 32.
-int onesweep_items() {
-  static const int v = [] {
+// Items per thread of the one-sweep scatter (tile = 256 x items).  Measured on MI355X
+// (profiles/r01/bench_r14_*): 32-bit key + 32-bit payload passes are faster with 32 items
+// (8192-key tiles: ~32 keys per digit bucket, i.e. whole 128-byte lines per burst; 64 KB of LDS,
+// 2 tiles per CU), the 32-bit key + 64-bit value passes of the row placement with 16 (their
+// 96 KB tile would leave one tile per CU).  PBH_OS_IPT = 16 or 32 forces either.
+int onesweep_items(size_t value_bytes) {
+  static const int forced = [] {
     const char* e = getenv("PBH_OS_IPT");
-    return (e && atoi(e) == 32) ? 32 : 16;
+    return e ? atoi(e) : 0;
   }();
-  return v;
+  if (forced == 16 || forced == 32) return forced;
+  return value_bytes <= 4 ? 32 : 16;
 }
 
 template <typename K, typename V>
 void launch_onesweep(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
                      uint64_t* status, uint32_t* counter, hipStream_t s) {
-  if (onesweep_items() == 32) {
+  if (onesweep_items(sizeof(V)) == 32) {
     const int64_t nt = (n + T * 32 - 1) / (T * 32);
     hipLaunchKernelGGL((k_onesweep<K, V, 32>), dim3((unsigned)nt), dim3(T), 0, s, kin, vin, kout, vout, n, shift,
                        bases, status, counter);
