@@ -77,6 +77,7 @@ def main():
     ap.add_argument("--d", type=int, default=32)
     ap.add_argument("--cpu-n", type=int, default=262_144)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--ppf-rows", type=int, default=100_000_000, help="rows of the ppf-sweep side measurement (0: skip)")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
 
@@ -160,6 +161,8 @@ def main():
                 "kernel": dom,
                 "avg_launch_ms": dk["avg_ms"], "bytes_per_launch": dk["bytes_per_launch"]}
 
+    sweep = ppf_sweep(lib, base, args.ppf_rows, args.seed) if args.ppf_rows > 0 else None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_n, d)
@@ -175,10 +178,40 @@ def main():
                            "rows": n, "d": d,
                            "parallelism": f"row-sharded x{world} (RCCL all-reduce + all-to-all)" if world > 1
                            else "single"},
-                "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels}
+                "roofline": roofline, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels}
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def ppf_sweep(lib, dists, n, seed, reps=3):
+    """Side measurement for the north_star's "ppf sweep" roofline (16 B/draw, read
+    q 8 + write x 8, at the sample_from_quantiles boundary): pbh_ppf over one HBM-resident
+    quantile column of n rows for each cfg2 distribution, HIP-event time of k_ppf on the
+    launching stream.  Not part of `value` (the fused LHS path never stores q)."""
+    import ctypes
+
+    from probabilit_amd import _lib, native
+
+    q = native.fill_uniform(seed + 12345, n, 1, return_device=True)[0]
+    kid = _lib.KERNELS.index("k_ppf")
+    per, tot_ms, tot_b = {}, 0.0, 0
+    for name, kw in dists:
+        native.ppf(name, q, return_device=True, **kw)  # warm (and build the poisson / gamma tables once)
+        lib.pbh_timing_reset()
+        lib.pbh_timing_enable(1)
+        for _ in range(reps):
+            native.ppf(name, q, return_device=True, **kw)
+        lib.pbh_timing_enable(0)
+        t, c = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(lib.pbh_timing_read(kid, ctypes.byref(t), ctypes.byref(c)))
+        avg = t.value / max(c.value, 1)
+        per[f"{name}{kw}"] = {"ms": round(avg, 4), "GBps": round(16 * n / (avg / 1e3) / 1e9, 1)}
+        tot_ms += avg
+        tot_b += 16 * n
+    gbps = tot_b / (tot_ms / 1e3) / 1e9
+    return {"kernel": "k_ppf", "rows": n, "bytes_per_draw": 16, "achieved": round(gbps, 1), "unit": "GB/s",
+            "frac": round(gbps / HBM_PEAK_GBS, 4), "per_dist": per}
 
 
 def cpu_baseline(n, d):

@@ -293,6 +293,24 @@ int pbh_affine_rows(const double* X, int64_t n, int32_t k, int64_t x_rs, int64_t
                     const double* scale_host, const double* offset_host, const double* M_host, double* Y,
                     int64_t y_rs, int64_t y_cs, void* ws, size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------- permutation correlator
+ * The hill-climbing loop of PermutationCorrelator.__call__ (replaces correlation.py:650-700 with
+ * CorrelationMatrix.update_column / commit, :875-921, and _error, :582-586) as one persistent
+ * workgroup.  xs: the measured columns X_ (k columns of n rows, column c at xs + c * ldx), swapped
+ * in place; xo: the original X when it differs from X_ (spearman), swapped alongside, else NULL.
+ * corr: device k x k row-major correlation matrix, updated in place.  den_host (k), target_host
+ * and weights_host (k x k row-major, weights already divided by their sum): host, copied into
+ * the workspace.  Step t (0 <= t < nsteps, nsteps a multiple of k) treats variable t % k with
+ * swap rows swaps[offsets[t] .. offsets[t] + s) against the next s entries, s = (offsets[t + 1] -
+ * offsets[t]) / 2 (device int64 arrays, the SwapIndexGenerator stream).  After each variable-0
+ * step errlog[t / k] = the weighted RMS error; the loop stops after the first one below tol.
+ * state[0] = steps run, state[1] = 1 when stopped by tol (device int64[2]).  1 <= k <= 128. */
+int pbh_permcorr_workspace_size(int32_t k, size_t* bytes);
+int pbh_permcorr_climb(double* xs, double* xo, int64_t n, int32_t k, int64_t ldx, double* corr, const double* den_host,
+                       const double* target_host, const double* weights_host, const int64_t* swaps,
+                       const int64_t* offsets, int64_t nsteps, double tol, double* errlog, int64_t* state, void* ws,
+                       size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------- measurement
  * When enabled, every launch of the library's main kernels is bracketed by two HIP events
  * recorded on the launching stream; pbh_timing_read returns the summed device time and the

@@ -44,14 +44,16 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_ic_reorder", "pbh_mt19937_workspace_size", "pbh_mt19937_random", "pbh_mt19937_advance",
            "pbh_pcg64_workspace_size",
            "pbh_pcg64_random", "pbh_halton_workspace_size", "pbh_fill_halton",
-           "pbh_affine_workspace_size", "pbh_affine_rows", "pbh_table_ppf"]
+           "pbh_affine_workspace_size", "pbh_affine_rows", "pbh_table_ppf", "pbh_permcorr_workspace_size",
+           "pbh_permcorr_climb"]
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
            "k_rank_finish<gather>", "k_load_keys", "k_gram", "k_apply", "k_elementwise", "k_head_bounds", "k_scan",
            "k_lhs_sorted_ppf", "k_perm_scores", "k_code_runs",
            "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>",
-           "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine", "k_table_ppf"]
+           "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine", "k_table_ppf",
+           "k_permcorr"]
 
 
 class Param(ctypes.Structure):
@@ -140,6 +142,9 @@ def load():
         "pbh_affine_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
         "pbh_table_ppf": ([i32, vp, i64, i64, vp, vp, i64, i32, i32, vp, vp, vp], i32),
         "pbh_affine_rows": ([vp, i64, ctypes.c_int32, i64, i64, vp, vp, vp, vp, vp, i64, i64, vp, sz, vp], i32),
+        "pbh_permcorr_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
+        "pbh_permcorr_climb": ([vp, vp, i64, ctypes.c_int32, i64, vp, vp, vp, vp, vp, vp, i64, dbl, vp, vp, vp, sz, vp],
+                               i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

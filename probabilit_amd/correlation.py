@@ -343,3 +343,278 @@ def rankdata(x):
     _lib.check(lib.pbh_rankdata_average(xd.data_ptr(), xd.stride(0), n, out.data_ptr(), ws.data_ptr(), wsb.value,
                                         device.stream()), "rankdata")
     return out if on_device else device.to_host(out)
+
+
+# ------------------------------------------------------------------ permutation correlator
+class SwapIndexGenerator:
+    """Disjoint index sets (indices1, indices2) of length `size` from range(n)
+    (correlation.py:428-470): each call takes the next 2 * size entries of a running
+    permutation drawn from `rng`; when fewer remain they are dropped and a fresh permutation is
+    drawn.  The stream is host state of the caller's numpy Generator, consumed exactly as the
+    reference consumes it (the rng continues identically after the call)."""
+
+    def __init__(self, rng, n: int):
+        assert n >= 2
+        self.rng = rng
+        self.indices = np.arange(n)
+        self.permutation = self.rng.permutation(self.indices)
+
+    def __call__(self, size: int):
+        assert size >= 1
+        flat, offs = self._take_many(np.array([size]))
+        s = (offs[1] - offs[0]) // 2
+        return flat[:s], flat[s:2 * s]
+
+    def _take_many(self, sizes):
+        """The concatenated (i, j) lists of len(sizes) consecutive calls, step t occupying
+        flat[offsets[t]:offsets[t + 1]] (i first, then j), without a Python call per step."""
+        need = 2 * np.minimum(np.asarray(sizes, dtype=np.int64), len(self.indices) // 2)
+        offs = np.zeros(len(need) + 1, dtype=np.int64)
+        pieces, t = [], 0
+        while t < len(need):
+            window = need[t:t + len(self.permutation) // 2 + 1]  # every step takes >= 2 entries
+            cum = np.cumsum(window)
+            fit = int(np.searchsorted(cum, len(self.permutation), side="right"))
+            if fit:
+                used = int(cum[fit - 1])
+                pieces.append(self.permutation[:used])
+                self.permutation = self.permutation[used:]
+                offs[t + 1:t + fit + 1] = offs[t] + cum[:fit]
+                t += fit
+            if t < len(need) and need[t] > len(self.permutation):
+                self.permutation = self.rng.permutation(self.indices)  # the short rest is dropped
+        flat = np.concatenate(pieces).astype(np.int64) if pieces else np.zeros(0, dtype=np.int64)
+        return flat, offs
+
+
+def _rank_block(block):
+    """Column-wise rankdata('average') of a (K, N) device block (spearman space)."""
+    out = device.empty(tuple(block.shape))
+    for c in range(block.shape[0]):
+        out[c] = rankdata(block[c])
+    return out
+
+
+def _private_block(X):
+    """(N, K) input -> a (K, N) device block this module may modify, and whether X was a
+    device tensor."""
+    block, on_device = _as_block(X)
+    if on_device and block.data_ptr() == X.data_ptr():
+        block = block.clone()
+    return block, on_device
+
+
+class CorrelationMatrix:
+    """Incrementally updated correlation matrix of X under row swaps within one column
+    (correlation.py:757-921): swapping rows i and j of column k changes only row and column k
+    of the matrix, by sum_s (X_[i_s] - X_[j_s]) (X_[j_s, k] - X_[i_s, k]) / (m std std_k).
+
+    The data live on the device as a (K, N) block; the initial Gram matrix is computed there
+    (pbh_centered_gram); a swap reads 2 s rows of K values back for the K-vector update, so the
+    numerics of update_column / commit are the reference's numpy expressions on the same
+    values.  The initial numerator comes from the device Gram (a different summation order
+    than numpy's BLAS matmul), so it agrees with the reference to ~1e-15 relative."""
+
+    def __init__(self, X, correlation_type="pearson", check=True):
+        valid_corrs = ("pearson", "spearman")
+        assert correlation_type in valid_corrs
+        assert X.ndim == 2
+        self.correlation_type = correlation_type
+        self.check = check
+        self._Xd, self._on_device = _private_block(X)
+        self._Xsd = self._Xd if correlation_type == "pearson" else _rank_block(self._Xd)
+        self.n, self.m = self._Xsd.shape
+        _, G = _block_stats(self._Xsd)
+        self.numerator = G / self.m
+        self.denominator = np.sqrt(np.diag(G) / self.m)
+        if np.any(np.isclose(self.denominator, 0)):
+            raise ValueError("X has one or several constant columns")
+        self.corr_mat = (self.numerator / self.denominator[None, :]) / self.denominator[:, None]
+
+    @property
+    def X(self):
+        """The (permuted) data, (N, K): numpy, or a device tensor when X was one."""
+        Y = self._Xd.t().contiguous()
+        return Y if self._on_device else device.to_host(Y)
+
+    @property
+    def X_(self):
+        Y = self._Xsd.t().contiguous()
+        return Y if self._on_device else device.to_host(Y)
+
+    def __repr__(self):
+        return repr(self.corr_mat)
+
+    def __getitem__(self, *args, **kwargs):
+        return self.corr_mat.__getitem__(*args, **kwargs)
+
+    def _rows(self, idx):
+        import torch
+
+        t = torch.as_tensor(np.asarray(idx, dtype=np.int64), device=self._Xsd.device)
+        return device.to_host(self._Xsd.index_select(1, t).t())  # (len(idx), K)
+
+    def _delta_numerator(self, col, i, j):
+        if self.check:
+            assert isinstance(col, int)
+            assert 0 <= col < self.n
+            if isinstance(i, int):
+                i = [i]
+            if isinstance(j, int):
+                j = [j]
+            assert len(i) == len(j)
+            if set(i).intersection(set(j)):
+                raise ValueError(f"Swaps must be two disjoint sets, got {i} and {j}")
+        i, j = np.atleast_1d(i), np.atleast_1d(j)
+        row_i, row_j = self._rows(i), self._rows(j)
+        d = np.sum((row_i - row_j) * (row_j[:, col] - row_i[:, col])[:, None], axis=0)
+        d[col] = 0.0
+        return d
+
+    def delta_column(self, col, i, j):
+        return self._delta_numerator(col, i, j) / (self.m * self.denominator * self.denominator[col])
+
+    def update_column(self, col, i, j):
+        return self.corr_mat[:, col] + self.delta_column(col, i, j)
+
+    def commit(self, col, i, j):
+        import torch
+
+        dnum = self._delta_numerator(col, i, j)
+        dcol = dnum / (self.m * self.denominator * self.denominator[col])
+        self.corr_mat[:, col] += dcol
+        self.corr_mat[col, :] += dcol
+        self.numerator[:, col] += dnum
+        self.numerator[col, :] += dnum
+        ii = torch.as_tensor(np.atleast_1d(i).astype(np.int64), device=self._Xd.device)
+        jj = torch.as_tensor(np.atleast_1d(j).astype(np.int64), device=self._Xd.device)
+        for blk in {id(self._Xsd): self._Xsd, id(self._Xd): self._Xd}.values():
+            vi, vj = blk[col, ii].clone(), blk[col, jj].clone()
+            blk[col, ii] = vj
+            blk[col, jj] = vi
+        return self
+
+
+class PermutationCorrelator(Correlator):
+    """Induces the target correlation by swapping rows within columns, keeping a swap when it
+    lowers the weighted error of that variable's correlation column (randomized hill climbing,
+    correlation.py:473-703).  Same constructor, validation, printed progress and rng stream as
+    the reference; the loop runs on the device (pbh_permcorr_climb, one persistent workgroup)
+    in chunks of whole cycles through the variables, with the swap lists of a chunk drawn up
+    front from the correlator's numpy Generator (they do not depend on the accept decisions;
+    after an early stop the rng is rewound and advanced by exactly the steps the reference
+    takes).  Decisions are bit-exact given the initial correlation matrix, which is computed
+    from the device Gram (~1e-15 relative to the reference's BLAS matmul)."""
+
+    def __init__(self, *, weights=None, iterations=1000, tol=0.01, correlation_type="pearson", seed=None,
+                 verbose=False):
+        if not (weights is None or np.all(weights > 0)):
+            raise ValueError("`weights` must have positive entries.")
+        if not (isinstance(iterations, int) and iterations >= 0):
+            raise ValueError("`iterations` must be non-negative integer.")
+        if not isinstance(tol, float) and tol > 0:  # sic (correlation.py:561)
+            raise ValueError("`tol` must be a positive float.")
+        if not (seed is None or isinstance(seed, int)):
+            raise TypeError("`seed` must be None or an integer")
+        if not isinstance(verbose, bool):
+            raise TypeError("`verbose` must be boolean")
+        self.iters = iterations
+        self.tol = tol
+        self.rng = np.random.default_rng(seed)
+        self.verbose = verbose
+        self.correlation_type = correlation_type
+
+    def set_target(self, correlation_matrix, *, weights=None):
+        super().set_target(correlation_matrix)
+        weights = np.ones_like(self.C) if weights is None else weights
+        self.weights = weights / np.sum(weights)
+        self.triu_indices = np.triu_indices(self.C.shape[0], k=1)
+        return self
+
+    def _error(self, observed, target):
+        """Weighted RMSE over the strict upper triangle of corr(X) - target (:582-586)."""
+        idx = self.triu_indices
+        return float(np.sqrt(np.sum(self.weights[idx] * (observed[idx] - target[idx]) ** 2.0)))
+
+    @staticmethod
+    def subiters(n, i):
+        """Swaps per step in iteration i of n: ceil((log2 n + 1) ** (1 - 2 i / n)) (:588-608)."""
+        C = np.log2(n) + 1
+        return int(np.ceil(C ** (1 - (2 * i / n))))
+
+    def __call__(self, X):
+        """A copy of X (N, K) with rows shuffled within columns (numpy in, numpy out; a device
+        tensor in, a device tensor out)."""
+        self._validate_X(X, check_rows_cols=False)
+        block, on_device = _private_block(X)
+        Y = self._transform_device(block, copy=False).t().contiguous()
+        return Y if on_device else device.to_host(Y)
+
+    def _transform_device(self, block, ev=None, copy=True):
+        """(K, N) device block -> the permuted (K, N) block (a new one unless copy=False)."""
+        K, N = block.shape
+        if self.P.shape[0] != K:
+            raise ValueError("Number of variables in `X` does not match `correlation_matrix`.")
+        xo = block.clone() if copy else block
+        if self.verbose:
+            print(f"Running permutation correlator for {self.iters if self.iters else 'inf'} iterations.")
+        gen = SwapIndexGenerator(rng=self.rng, n=N)
+        assert self.correlation_type in ("pearson", "spearman")  # CorrelationMatrix.__init__ (:821)
+        xs = xo if self.correlation_type == "pearson" else _rank_block(xo)
+        _, G = _block_stats(xs)
+        den = np.sqrt(np.diag(G) / N)
+        if np.any(np.isclose(den, 0)):
+            raise ValueError("X has one or several constant columns")
+        corr = ((G / N) / den[None, :]) / den[:, None]
+        if 0 < self.iters < 10:  # iteration % (iters // 10) at the first step (:660)
+            raise ZeroDivisionError("integer modulo by zero")
+        self._climb(xs, None if xs is xo else xo, corr, den, gen)
+        return xo
+
+    def _climb(self, xs, xo, corr, den, gen):
+        import torch
+
+        K, N = xs.shape
+        lib = _lib.load()
+        nb = ctypes.c_size_t()
+        _lib.check(lib.pbh_permcorr_workspace_size(K, ctypes.byref(nb)), "pbh_permcorr_workspace_size")
+        ws = device.empty(int(nb.value), "uint8")
+        C = np.ascontiguousarray(self.C, dtype=np.float64)
+        Wn = np.ascontiguousarray(self.weights, dtype=np.float64)
+        den = np.ascontiguousarray(den, dtype=np.float64)
+        corr_d = device.to_device(np.ascontiguousarray(corr, dtype=np.float64))
+        chunk = max(1, 16384 // K)  # iterations per launch
+        errlog = device.empty(chunk)
+        state = device.zeros(2, "int64")
+        n_sched = self.iters if self.iters else 10_000
+        every = self.iters // 10 if self.iters else 0  # iterations == 0 never prints per iteration
+        err = self._error(corr, C)
+        it0 = 1
+        while self.iters == 0 or it0 <= self.iters:
+            n_it = chunk if self.iters == 0 else min(chunk, self.iters - it0 + 1)
+            per_it = [self.subiters(n_sched, it) for it in range(it0, it0 + n_it)]
+            sizes = np.repeat(np.array(per_it, dtype=np.int64), K)
+            snap = (self.rng.bit_generator.state, gen.permutation)
+            flat, offs = gen._take_many(sizes)
+            sw = torch.as_tensor(flat, device=xs.device)
+            of = torch.as_tensor(offs, device=xs.device)
+            _lib.check(lib.pbh_permcorr_climb(xs.data_ptr(), device.ptr(xo), N, K, N, corr_d.data_ptr(),
+                                              _lib.np_ptr(den), _lib.np_ptr(C), _lib.np_ptr(Wn), sw.data_ptr(),
+                                              of.data_ptr(), n_it * K, float(self.tol), errlog.data_ptr(),
+                                              state.data_ptr(), ws.data_ptr(), nb.value, device.stream()),
+                       "pbh_permcorr_climb")
+            steps, stopped = (int(v) for v in device.to_host(state))
+            errs = device.to_host(errlog)
+            reached = (steps + K - 1) // K  # iterations whose variable-0 step ran
+            for q in range(reached):
+                if self.verbose and every and (it0 + q) % every == 0:
+                    print(f" Iter {it0 + q:>6}  Error: {err:.6f} Swaps: {per_it[q]:>2}")
+                err = float(errs[q])
+            if stopped:
+                self.rng.bit_generator.state = snap[0]  # rewind: the reference stops drawing here
+                gen.permutation = snap[1]
+                gen._take_many(sizes[:steps])
+                if self.verbose:
+                    print(f""" Terminating at iteration {it0 + reached - 1} due to tolerance. Error: {err:.6f}""")
+                return
+            it0 += n_it

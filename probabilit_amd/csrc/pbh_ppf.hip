@@ -27,8 +27,11 @@ struct Params {
 };
 
 // Per-launch constants of the distribution (scalar parameters only).
+constexpr int kPoissonGuideBits = 11;  // 2048 guide buckets
+
 struct PoissonTable {
   const double* cdf;  // poisson: cdf[j] = pdtr(k_lo + j, mu) for scalar mu, else NULL
+  const int32_t* cdf_guide;  // cdf_guide[b] = first j with cdf[j] >= b / 2^kPoissonGuideBits
   int64_t k_lo;
   int64_t len;
   int has_gamma;      // gamma with scalar a: hoisted GammaAux + z-grid guide
@@ -54,21 +57,21 @@ PBH_DI double poisson_search(double q, double mu) {
   return k;
 }
 
+// First j with cdf[j] >= q, by the guide table (Chen & Asau 1974): q lies in bucket
+// b = floor(q 2^bits) (exact: a power-of-two scale), whose guide entry is the answer for
+// q = b / 2^bits <= q, so a short forward scan from it ends at the answer -- the same j as a
+// binary search over the table, in ~1 probe instead of log2(len) dependent ones.
 PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
-  int64_t lo = 0, hi = t.len;  // first j with cdf[j] >= q
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (t.cdf[mid] >= q)
-      hi = mid;
-    else
-      lo = mid + 1;
-  }
+  int64_t lo = t.cdf_guide[(int)(q * (double)(1 << kPoissonGuideBits))];
+  while (lo < t.len && t.cdf[lo] < q) ++lo;
   if (lo == t.len || (lo == 0 && t.k_lo > 0)) return poisson_search(q, mu);  // outside coverage
   return (double)(t.k_lo + lo);
 }
 
 // ppf of one element for distribution D; p = (shape..., loc, scale) already resolved.
-template <int D>
+// PART selects ndtri's branch for norm / lognorm (0: ndtri, 1: ndtri_centre, 2: ndtri_tail),
+// for the compacted kernels that know which one an element takes.
+template <int D, int PART = 0>
 PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTable& pt) {
   if constexpr (D == PBH_DIST_POISSON) {
     double mu = p0, loc = p1;
@@ -103,13 +106,13 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
     if (!(q > 0.0 && q < 1.0)) return kNaN;
     double x;
     if constexpr (D == PBH_DIST_NORM) {
-      x = sf::ndtri(q);
+      x = PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q);
     } else if constexpr (D == PBH_DIST_UNIFORM) {
       x = q;
     } else if constexpr (D == PBH_DIST_EXPON) {
       x = -sf::log1p_(-q);  // scipy expon._ppf: -sc.log1p(-q), the Cephes log1p
     } else if constexpr (D == PBH_DIST_LOGNORM) {
-      x = exp(shape * sf::ndtri(q));
+      x = exp(shape * (PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q)));
     } else if constexpr (D == PBH_DIST_TRIANG) {
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
@@ -118,6 +121,97 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
     }
     return x * scale + loc;
   }
+}
+
+// ---------------------------------------------------------------- tail compaction
+// ndtri (norm / lognorm ppf, the van der Waerden scores) is one rational function for
+// min(q, 1 - q) > e^-2 (73% of uniform q) and an expensive tail (two logs, a sqrt, three
+// divisions) otherwise.  With q in random order nearly every wave holds both kinds, and a wave
+// executes every branch one of its lanes takes, so a plain grid-stride kernel pays centre + tail
+// for every element.  The compacted kernels give each thread kCIpt items of a block tile: centre
+// items are evaluated at once, tail items are queued in LDS (one LDS atomic per wave) and then
+// drained by all lanes of the block together, so the tail costs its 27% share.  Every value is
+// computed by the same inline function either way (bit-identical to the plain kernels); the
+// results pass through LDS so that the global stores stay coalesced.
+constexpr int kCIpt = 8;
+constexpr int kCTile = kBlock * kCIpt;
+
+struct TailQueue {
+  double arg[kCTile];
+  uint16_t pos[kCTile];
+  int count;
+};
+
+PBH_DI void tail_push(TailQueue& tq, bool take, double a, int p) {
+  const uint64_t m = __ballot(take);
+  if (m == 0ull) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const int leader = __builtin_ctzll(m);
+  int base = 0;
+  if (lane == leader) base = atomicAdd(&tq.count, (int)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (take) {
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int slot = base + (int)__popcll(m & lt);
+    tq.arg[slot] = a;
+    tq.pos[slot] = (uint16_t)p;
+  }
+}
+
+unsigned compact_grid(int64_t n) { return grid_for(n, kCTile, 256 * 8); }
+
+bool compaction_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PBH_COMPACT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// k_ppf / k_lhs_ppf for D in {norm, lognorm} with tail compaction.  Q(i) gives the quantile of
+// tile item i (a strided load, or the fused LHS generator).
+template <int D, class Q>
+PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm, const PoissonTable& pt, double* __restrict__ out,
+                          int32_t* flag, TailQueue& tq, double* res) {
+  for (int64_t base = (int64_t)blockIdx.x * kCTile; base < n; base += (int64_t)gridDim.x * kCTile) {
+    if (threadIdx.x == 0) tq.count = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kCIpt; ++j) {
+      const int p = j * kBlock + threadIdx.x;
+      const int64_t i = base + p;
+      const bool valid = i < n;
+      const double qv = valid ? qof(i) : 0.5;
+      const bool tail = valid && sf::ndtri_takes_tail(qv);
+      if (valid && !tail) res[p] = ppf_one<D, 1>(qv, prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
+      tail_push(tq, tail, qv, p);
+    }
+    __syncthreads();
+    const int T = tq.count;
+    for (int t = threadIdx.x; t < T; t += kBlock) {
+      const int p = tq.pos[t];
+      const int64_t i = base + p;
+      res[p] = ppf_one<D, 2>(tq.arg[t], prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kCIpt; ++j) {
+      const int p = j * kBlock + threadIdx.x;
+      const int64_t i = base + p;
+      const double x = i < n ? res[p] : 0.0;
+      if (i < n) out[i] = x;
+      flag_nonfinite(flag, !isfinite(x));
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_ppf_c(const double* __restrict__ q, int64_t q_stride, int64_t n,
+                                                  Params prm, PoissonTable pt, double* __restrict__ out,
+                                                  int32_t* flag) {
+  __shared__ TailQueue tq;
+  __shared__ double res[kCTile];
+  ppf_compacted<D>(n, [&](int64_t i) { return q[i * q_stride]; }, prm, pt, out, flag, tq, res);
 }
 
 template <int D>
@@ -147,6 +241,18 @@ __global__ __launch_bounds__(kBlock) void k_lhs_ppf(uint64_t seed, int64_t n, in
     out[i] = x;
     flag_nonfinite(flag, !isfinite(x));
   }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_lhs_ppf_c(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
+                                                      uint32_t col, Params prm, PoissonTable pt,
+                                                      double* __restrict__ out, int32_t* flag) {
+  __shared__ TailQueue tq;
+  __shared__ double res[kCTile];
+  Philox ph(seed);
+  FeistelPerm fp(ph, (uint64_t)n, col);
+  ppf_compacted<D>(nrows, [&](int64_t i) { return lhs_quantile(ph, fp, (uint64_t)(row0 + i), col); }, prm, pt, out,
+                   flag, tq, res);
 }
 
 // The same LHS column in stratum order: out[t] = ppf(q) for the row pi^-1(t) that holds
@@ -262,24 +368,53 @@ __device__ __forceinline__ double run_average_rank(const uint32_t* __restrict__ 
 
 // Van der Waerden scores of an LHS column, rows [row0, row0 + nrows), in row order: the rank
 // of row r is pi(r) + 1 (untied), or the run average of stratum pi(r) (heads != NULL), so
-// S[r] = ndtri(rank / (n + 1)) (correlation.py:394-395) without sorting anything.  With
+// S[r] = ndtri(rank / (n + 1)) (correlation.py:394-395) without sorting anything.  Ranks of
+// consecutive rows are random, so ndtri's tail is compacted (see TailQueue).  With
 // partial != NULL each block also writes the sum of its scores to partial[blockIdx.x] (the
 // column mean of step 2 without re-reading S; summed in a fixed order by k_means).
 __global__ __launch_bounds__(kBlock) void k_perm_scores(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
                                                         int64_t nrows, const uint32_t* __restrict__ heads,
                                                         int64_t nheads, double* __restrict__ S,
                                                         double* __restrict__ partial) {
+  __shared__ TailQueue tq;
+  __shared__ double res[kCTile];
   __shared__ double sh[kBlock / 64];
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
   const double np1 = (double)(n + 1);
   double sum = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
-    const uint64_t t = fp((uint64_t)(row0 + i));
-    const double rank = heads ? run_average_rank(heads, nheads, n, (int64_t)t) : (double)(t + 1);
-    const double v = sf::ndtri(rank / np1);
-    S[i] = v;
-    sum += v;
+  for (int64_t base = (int64_t)blockIdx.x * kCTile; base < nrows; base += (int64_t)gridDim.x * kCTile) {
+    if (threadIdx.x == 0) tq.count = 0;
+    __syncthreads();
+#pragma unroll 2
+    for (int j = 0; j < kCIpt; ++j) {
+      const int p = j * kBlock + threadIdx.x;
+      const int64_t i = base + p;
+      const bool valid = i < nrows;
+      double y = 0.5;
+      if (valid) {
+        const uint64_t t = fp((uint64_t)(row0 + i));
+        const double rank = heads ? run_average_rank(heads, nheads, n, (int64_t)t) : (double)(t + 1);
+        y = rank / np1;
+      }
+      const bool tail = valid && sf::ndtri_takes_tail(y);
+      if (valid && !tail) res[p] = sf::ndtri_centre(y);
+      tail_push(tq, tail, y, p);
+    }
+    __syncthreads();
+    const int T = tq.count;
+    for (int t = threadIdx.x; t < T; t += kBlock) res[tq.pos[t]] = sf::ndtri_tail(tq.arg[t]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kCIpt; ++j) {
+      const int p = j * kBlock + threadIdx.x;
+      const int64_t i = base + p;
+      if (i < nrows) {
+        const double v = res[p];
+        S[i] = v;
+        sum += v;
+      }
+    }
   }
   if (partial) {
 #pragma unroll
@@ -359,6 +494,22 @@ __global__ void k_poisson_table(double mu, int64_t k_lo, int64_t len, double* cd
   if (j < len) cdf[j] = sf::pdtr((double)(k_lo + j), mu);
 }
 
+// guide[b] = first j with cdf[j] >= b / 2^kPoissonGuideBits (len when none)
+__global__ void k_poisson_guide(const double* __restrict__ cdf, int64_t len, int32_t* __restrict__ guide) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= (1 << kPoissonGuideBits)) return;
+  const double v = (double)b / (double)(1 << kPoissonGuideBits);
+  int64_t lo = 0, hi = len;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (cdf[mid] >= v)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  guide[b] = (int32_t)lo;
+}
+
 // ---------------------------------------------------------------- generators
 __global__ __launch_bounds__(kBlock) void k_fill_lhs(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
                                                      int col0, double* __restrict__ q, int64_t ldq) {
@@ -409,7 +560,12 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
   switch (dist) {
 #define PBH_CASE(D) \
   case D:           \
-    PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf<D>, g, b, 0, s, q, qs, n, prm, pt, out, flag)); break;
+    if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
+      PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_c<D>, dim3(compact_grid(n)), b, 0, s, q, qs, n, prm, pt, out,  \
+                                             flag));                                                            \
+    else                                                                                                        \
+      PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf<D>, g, b, 0, s, q, qs, n, prm, pt, out, flag));              \
+    break;
     PBH_CASE(PBH_DIST_NORM)
     PBH_CASE(PBH_DIST_UNIFORM)
     PBH_CASE(PBH_DIST_EXPON)
@@ -432,8 +588,13 @@ int launch_lhs_ppf(int dist, uint64_t seed, int64_t n, int64_t row0, int64_t nro
   switch (dist) {
 #define PBH_CASE(D) \
   case D:           \
-    PBH_TIMED(kKLhsPpf, s,                                                                         \
-              hipLaunchKernelGGL(k_lhs_ppf<D>, g, b, 0, s, seed, n, row0, nrows, col, prm, pt, out, flag)); \
+    if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
+      PBH_TIMED(kKLhsPpf, s,                                                                                    \
+                hipLaunchKernelGGL(k_lhs_ppf_c<D>, dim3(compact_grid(nrows)), b, 0, s, seed, n, row0, nrows, col, \
+                                   prm, pt, out, flag));                                                        \
+    else                                                                                                        \
+      PBH_TIMED(kKLhsPpf, s,                                                                                    \
+                hipLaunchKernelGGL(k_lhs_ppf<D>, g, b, 0, s, seed, n, row0, nrows, col, prm, pt, out, flag));   \
     break;
     PBH_CASE(PBH_DIST_NORM)
     PBH_CASE(PBH_DIST_UNIFORM)
@@ -508,11 +669,16 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
       int64_t k_lo = lo > 0.0 ? (int64_t)lo : 0;
       int64_t k_hi = (int64_t)ceil(mu + 20.0 * sd + 40.0);
       int64_t len = k_hi - k_lo + 1;
-      PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)len * sizeof(double), s));
+      const int nb = 1 << kPoissonGuideBits;
+      PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)len * sizeof(double) + (size_t)nb * 4, s));
       hipLaunchKernelGGL(k_poisson_table, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, mu, k_lo, len,
                          *table);
       PBH_CHECK_LAUNCH();
+      int32_t* guide = (int32_t*)(*table + len);
+      hipLaunchKernelGGL(k_poisson_guide, dim3((unsigned)(nb / 256)), dim3(256), 0, s, *table, len, guide);
+      PBH_CHECK_LAUNCH();
       pt.cdf = *table;
+      pt.cdf_guide = guide;
       pt.k_lo = k_lo;
       pt.len = len;
     }
@@ -567,14 +733,14 @@ int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStre
   return PBH_OK;
 }
 
-unsigned perm_scores_blocks(int64_t nrows) { return ppf_grid(nrows); }
+unsigned perm_scores_blocks(int64_t nrows) { return compact_grid(nrows); }
 
 int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, const uint32_t* heads,
                 int64_t nheads, double* S, hipStream_t s, double* partial) {
   PBH_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "perm_scores: rows outside [0, n)");
   if (nrows == 0) return PBH_OK;
   PBH_TIMED(kKPermScores, s,
-            hipLaunchKernelGGL(k_perm_scores, dim3(ppf_grid(nrows)), dim3(kBlock), 0, s, seed, n, (uint32_t)col, row0,
+            hipLaunchKernelGGL(k_perm_scores, dim3(compact_grid(nrows)), dim3(kBlock), 0, s, seed, n, (uint32_t)col, row0,
                                nrows, heads, nheads, S, partial));
   PBH_CHECK_LAUNCH();
   return PBH_OK;

@@ -54,13 +54,36 @@ PBH_HD inline double p1evl(double x, const double* c, int n) {
 }
 
 // ---------------------------------------------------------------- inverse normal CDF
-PBH_HD inline double ndtri(double y0) {
+constexpr double kNdtriExpM2 = 0.13533528323661269189;  // exp(-2): ndtri's centre / tail split
+
+// True when ndtri(y0) takes the tail branch (two logs, a sqrt, three divisions): y0 in (0, 1)
+// with min(y0, 1 - y0) <= exp(-2), decided exactly as ndtri decides it.  Lets the compacted
+// kernels (pbh_ppf.hip) defer those elements and drain them with full waves.
+PBH_HD inline bool ndtri_takes_tail(double y0) {
+  if (!(y0 > 0.0 && y0 < 1.0)) return false;
+  double y = y0;
+  if (y > (1.0 - kNdtriExpM2)) y = 1.0 - y;
+  return !(y > kNdtriExpM2);
+}
+
+// ndtri's two branches as separate functions, so that a kernel evaluating only one of them
+// carries (and if-converts) no code of the other.  Same operations, same order as ndtri.
+// Centre: y0 in (exp(-2), 1 - exp(-2)].
+PBH_HD inline double ndtri_centre(double y0) {
   // |y - 0.5| <= 3/8 rational approximation
   const double P0[5] = {-5.99633501014107895267e1, 9.80010754185999661536e1, -5.66762857469070293439e1,
                         1.39312609387279679503e1, -1.23916583867381258016e0};
   const double Q0[8] = {1.95448858338141759834e0, 4.67627912898881538453e0, 8.63602421390890590575e1,
                         -2.25462687854119370527e2, 2.00260212380060660359e2, -8.20372256168333339912e1,
                         1.59056225126211695515e1, -1.18331621121330003142e0};
+  const double y = y0 - 0.5;
+  const double y2 = y * y;
+  const double x = y + y * (y2 * polevl(y2, P0, 4) / p1evl(y2, Q0, 8));
+  return x * kSqrt2Pi;
+}
+
+// Tail: ndtri_takes_tail(y0).
+PBH_HD inline double ndtri_tail(double y0) {
   // z = sqrt(-2 log y) in [2, 8)
   const double P1[9] = {4.05544892305962419923e0, 3.15251094599893866154e1, 5.71628192246421288162e1,
                         4.40805073893200834700e1, 1.46849561928858024014e1, 2.18663306850790267539e0,
@@ -75,28 +98,31 @@ PBH_HD inline double ndtri(double y0) {
   const double Q2[8] = {6.02427039364742014255e0, 3.67983563856160859403e0, 1.37702099489081330271e0,
                         2.16236993594496635890e-1, 1.34204006088543189037e-2, 3.28014464682127739104e-4,
                         2.89247864745380683936e-6, 6.79019408009981274425e-9};
-  const double kExpM2 = 0.13533528323661269189;  // exp(-2)
-  if (y0 == 0.0) return -kInf;
-  if (y0 == 1.0) return kInf;
-  if (y0 < 0.0 || y0 > 1.0) return kNaN;
   bool negate = true;
   double y = y0;
-  if (y > (1.0 - kExpM2)) {
+  if (y > (1.0 - kNdtriExpM2)) {
     y = 1.0 - y;
     negate = false;
   }
-  if (y > kExpM2) {
-    y = y - 0.5;
-    double y2 = y * y;
-    double x = y + y * (y2 * polevl(y2, P0, 4) / p1evl(y2, Q0, 8));
-    return x * kSqrt2Pi;
-  }
   double x = sqrt(-2.0 * log(y));
-  double x0 = x - log(x) / x;
-  double z = 1.0 / x;
-  double x1 = (x < 8.0) ? z * polevl(z, P1, 8) / p1evl(z, Q1, 8) : z * polevl(z, P2, 8) / p1evl(z, Q2, 8);
+  const double x0 = x - log(x) / x;
+  const double z = 1.0 / x;
+  double x1;
+  if (x < 8.0)
+    x1 = z * polevl(z, P1, 8) / p1evl(z, Q1, 8);
+  else
+    x1 = z * polevl(z, P2, 8) / p1evl(z, Q2, 8);
   x = x0 - x1;
   return negate ? -x : x;
+}
+
+// Cephes ndtri (scipy.special.ndtri): Phi^-1(y0).
+PBH_HD inline double ndtri(double y0) {
+  if (y0 == 0.0) return -kInf;
+  if (y0 == 1.0) return kInf;
+  if (y0 < 0.0 || y0 > 1.0) return kNaN;
+  if (ndtri_takes_tail(y0)) return ndtri_tail(y0);
+  return ndtri_centre(y0);
 }
 
 // ---------------------------------------------------------------- erf / erfc (for Temme)
@@ -701,24 +727,29 @@ PBH_HD inline double igamci(double a, double q) {  // x with Q(a, x) = q
 }
 
 // ---------------------------------------------------------------- table-guided gammaincinv
-// For a scalar shape `a`, y(z) = log(igami(a, Phi(z))) is tabulated on a uniform z grid with
-// its first two z-derivatives (x = e^y, f = igam_fac(a, x) = x^a e^-x / Gamma(a)):
-//     y'  = phi(z) / f,        y'' = -z y' - (a - x) y'^2,
-// and an element's value is the quintic Hermite interpolant at z = ndtri(p) (relative error
-// <= ~1e-12 over a in [0.05, 1e5]; checked per interval when the table is built, at the
-// interval midpoint against igami itself).  An interval that fails the check, elements
-// outside the grid and results near the subnormal range keep igami's own iteration (one
-// Halley step from the interpolant, or the full DiDonato-Morris + 3 Halley steps).
-constexpr double kGammaGuideZ0 = -12.0;       // grid start (Phi(z0) ~ 1.8e-33)
-constexpr double kGammaGuideH = 1.0 / 64.0;   // grid step
-constexpr int kGammaGuideM = 1289;            // entries: z0 .. z0 + (m - 1) h = 8.125 (1 - Phi ~ 2.2e-16)
+// For a scalar shape `a`, y(w) = log(igami(a, p)) is tabulated on a uniform grid of the log-odds
+// w = log(p / (1 - p)) with its first two w-derivatives (x = e^y, f = igam_fac(a, x) =
+// x^a e^-x / Gamma(a), g = dp/dw = p (1 - p)):
+//     y'  = g / f,        y'' = g (1 - 2 p) / f - (a - x) y'^2,
+// and an element's value is the quintic Hermite interpolant at w (relative error <= ~1e-12
+// over a in [0.05, 1e5]; checked per interval when the table is built, at the interval
+// midpoint against igami itself).  The log-odds costs one log and one division per element
+// (no branches: the earlier z = ndtri(p) grid paid ndtri's divergent tail in most waves), and
+// y is nearly linear in w in both tails (log x ~ (w + log Gamma(a + 1)) / a for p -> 0,
+// log x ~ log(w) for p -> 1), so a uniform grid spans p in [1.8e-35, 1 - 4e-18].  An interval
+// that fails the check, elements outside the grid and results near the subnormal range keep
+// igami's own iteration (one Halley step from the interpolant, or the full DiDonato-Morris +
+// 3 Halley steps).
+constexpr double kGammaGuideZ0 = -80.0;       // grid start (p ~ 1.8e-35)
+constexpr double kGammaGuideH = 1.0 / 32.0;   // grid step in w
+constexpr int kGammaGuideM = 3841;            // entries: w0 .. w0 + (m - 1) h = 40 (1 - p ~ 4.2e-18)
 constexpr double kGammaGuideTol = 1e-12;      // accepted |interpolant - log igami| at interval midpoints
 
 struct GammaGuide {
-  const double* y;   // log x at z_j = z0 + j h
-  const double* d1;  // dy/dz at z_j
-  const double* d2;  // d2y/dz2 at z_j
-  const double* ok;  // 1.0 when interval [z_j, z_j+1] passed the midpoint check
+  const double* y;   // log x at w_j = z0 + j h
+  const double* d1;  // dy/dw at w_j
+  const double* d2;  // d2y/dw2 at w_j
+  const double* ok;  // 1.0 when interval [w_j, w_j+1] passed the midpoint check
   int m;
   double z0, h, inv_h;
 };
@@ -755,8 +786,8 @@ PBH_HD inline double guide_interp(const GammaGuide& T, int j, double t) {
 
 PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const GammaGuide& T) {
   if (!(p > 0.0 && p < 1.0)) return igami(a, p);
-  double z = ndtri(p);
-  double u = (z - T.z0) * T.inv_h;
+  const double w = log(p / (1.0 - p));
+  double u = (w - T.z0) * T.inv_h;
   if (!(u >= 0.0 && u < (double)(T.m - 1))) return igami(a, p);
   int j = (int)u;
   double y = guide_interp(T, j, u - (double)j);
@@ -765,30 +796,34 @@ PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const G
   return T.ok[j] != 0.0 ? x : gamma_halley(a, p, x, g);
 }
 
-// log igami(a, Phi(z)); the upper half goes through the complement Q = Phi(-z), which keeps
-// every entry consistent with its z (Phi(z) itself rounds to 1 - k ulp for z >~ 5).
-PBH_HD inline double gamma_guide_x(double a, double z, double* tail_out) {
-  double tail, x;
-  if (z > 0.0) {
-    tail = ndtr(-z);
-    x = igamci(a, tail);
+// igami(a, p(w)), p(w) = 1 / (1 + e^-w); the upper half goes through the complement
+// Q = 1 / (1 + e^w) (igamci), which keeps every entry consistent with its w.  *p_out, *q_out:
+// p and 1 - p.
+PBH_HD inline double gamma_guide_x(double a, double w, double* p_out, double* q_out) {
+  double p, q, x;
+  if (w > 0.0) {
+    q = 1.0 / (1.0 + exp(w));
+    p = 1.0 - q;
+    x = igamci(a, q);
   } else {
-    tail = ndtr(z);
-    x = igami(a, tail);
+    p = 1.0 / (1.0 + exp(-w));
+    q = 1.0 - p;
+    x = igami(a, p);
   }
-  *tail_out = tail;
+  *p_out = p;
+  *q_out = q;
   return x;
 }
 
 // Table entry j (NaN when unusable).
-PBH_HD inline void gamma_guide_entry(double a, double z, double* y, double* d1, double* d2) {
-  double tail;
-  double x = gamma_guide_x(a, z, &tail);
+PBH_HD inline void gamma_guide_entry(double a, double w, double* y, double* d1, double* d2) {
+  double p, q;
+  double x = gamma_guide_x(a, w, &p, &q);
   double fac = igam_fac(a, x);
-  double phi = exp(-0.5 * z * z) / kSqrt2Pi;
-  double ly = log(x), d = phi / fac;
-  double e = -z * d - (a - x) * d * d;
-  bool ok = tail > 0.0 && tail < 1.0 && x > 0.0 && isfinite(ly) && isfinite(d) && isfinite(e) && fac > 0.0;
+  double g = p * q;
+  double ly = log(x), d = g / fac;
+  double e = g * (q - p) / fac - (a - x) * d * d;
+  bool ok = p > 0.0 && q > 0.0 && x > 0.0 && isfinite(ly) && isfinite(d) && isfinite(e) && fac > 0.0;
   *y = ok ? ly : kNaN;
   *d1 = ok ? d : kNaN;
   *d2 = ok ? e : kNaN;
@@ -796,8 +831,8 @@ PBH_HD inline void gamma_guide_entry(double a, double z, double* y, double* d1, 
 
 // Midpoint check of interval j (entries j, j + 1 already built): 1.0 when accepted.
 PBH_HD inline double gamma_guide_check(double a, const GammaGuide& T, int j) {
-  double tail;
-  double x = gamma_guide_x(a, T.z0 + ((double)j + 0.5) * T.h, &tail);
+  double p, q;
+  double x = gamma_guide_x(a, T.z0 + ((double)j + 0.5) * T.h, &p, &q);
   double y = guide_interp(T, j, 0.5);
   double ly = log(x);
   return (isfinite(y) && isfinite(ly) && x > 1e-290 && fabs(y - ly) <= kGammaGuideTol) ? 1.0 : 0.0;

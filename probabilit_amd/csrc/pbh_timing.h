@@ -33,6 +33,7 @@ enum KernelId {
   kKStreams,
   kKAffine,
   kKTable,
+  kKPermCorr,
   kKCount
 };
 

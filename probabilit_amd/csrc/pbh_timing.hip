@@ -18,7 +18,8 @@ const char* kNames[kKCount] = {"k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "
                                "k_rank_finish<gather>", "k_load_keys", "k_gram", "k_apply", "k_elementwise",
                                "k_head_bounds", "k_scan", "k_lhs_sorted_ppf", "k_perm_scores", "k_code_runs",
                                "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>",
-                               "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine", "k_table_ppf"};
+                               "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine", "k_table_ppf",
+                               "k_permcorr"};
 
 hipEvent_t take_event() {
   if (!g_pool.empty()) {

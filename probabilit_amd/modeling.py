@@ -32,7 +32,7 @@ import numpy as np
 import scipy.stats
 
 from . import _lib, device, qmc
-from .correlation import Cholesky, ImanConover, nearest_correlation_matrix
+from .correlation import Cholesky, ImanConover, PermutationCorrelator, nearest_correlation_matrix
 from .garbage_collector import GarbageCollector
 from .utils import build_corrmat
 
@@ -467,7 +467,7 @@ class Node(abc.ABC):
                 Y = inst._transform_generated(cols, size)
                 for j, var in enumerate(all_variables):
                     var._set_device(Y[j])
-            elif isinstance(inst, (ImanConover, Cholesky)):
+            elif isinstance(inst, (ImanConover, Cholesky, PermutationCorrelator)):
                 Y = inst._transform_device(block, ev)
                 for j, var in enumerate(all_variables):
                     var._set_device(Y[j])
