@@ -17,6 +17,11 @@ namespace pbh {
 namespace {
 
 constexpr int kBlock = 256;
+// Register cap of the ppf kernels: gamma / poisson carry their rarely taken fallbacks (igami's
+// full iteration, the per-element poisson search) inline, which would otherwise size the
+// register allocation of every wave (~256 VGPRs, one wave per SIMD) for code the hot path never
+// runs.  Capping at 4 waves per SIMD (128 VGPRs) spills inside those fallbacks instead.
+#define PBH_OCC __attribute__((amdgpu_waves_per_eu(4)))
 constexpr double kInf = sf::kInf;
 constexpr double kNaN = sf::kNaN;
 
@@ -206,7 +211,7 @@ PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm, const Pois
 }
 
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_ppf_c(const double* __restrict__ q, int64_t q_stride, int64_t n,
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_c(const double* __restrict__ q, int64_t q_stride, int64_t n,
                                                   Params prm, PoissonTable pt, double* __restrict__ out,
                                                   int32_t* flag) {
   __shared__ TailQueue tq;
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(kBlock) void k_ppf_c(const double* __restrict__ q, 
 }
 
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_ppf(const double* __restrict__ q, int64_t q_stride, int64_t n,
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf(const double* __restrict__ q, int64_t q_stride, int64_t n,
                                                 Params prm, PoissonTable pt, double* __restrict__ out,
                                                 int32_t* flag) {
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(kBlock) void k_ppf(const double* __restrict__ q, in
 }
 
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_lhs_ppf(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
                                                     uint32_t col, Params prm, PoissonTable pt,
                                                     double* __restrict__ out, int32_t* flag) {
   Philox ph(seed);
@@ -244,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void k_lhs_ppf(uint64_t seed, int64_t n, in
 }
 
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_lhs_ppf_c(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_c(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
                                                       uint32_t col, Params prm, PoissonTable pt,
                                                       double* __restrict__ out, int32_t* flag) {
   __shared__ TailQueue tq;
@@ -262,7 +267,7 @@ __global__ __launch_bounds__(kBlock) void k_lhs_ppf_c(uint64_t seed, int64_t n, 
 // would find, without re-reading the column): lane l compares with lane l + 1 through a wave
 // shuffle, the last lane of a wave evaluates stratum t + 1 itself; one atomic pair per block.
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt,
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt,
                                                            uint32_t col, Params prm, PoissonTable pt,
                                                            double* __restrict__ out, int32_t* flag,
                                                            unsigned long long* counts) {
@@ -372,7 +377,7 @@ __device__ __forceinline__ double run_average_rank(const uint32_t* __restrict__ 
 // consecutive rows are random, so ndtri's tail is compacted (see TailQueue).  With
 // partial != NULL each block also writes the sum of its scores to partial[blockIdx.x] (the
 // column mean of step 2 without re-reading S; summed in a fixed order by k_means).
-__global__ __launch_bounds__(kBlock) void k_perm_scores(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
                                                         int64_t nrows, const uint32_t* __restrict__ heads,
                                                         int64_t nheads, double* __restrict__ S,
                                                         double* __restrict__ partial) {
