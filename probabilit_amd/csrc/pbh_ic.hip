@@ -7,6 +7,9 @@
 //                   solve_triangular of :409-411) and the multiply by P^T (:414)
 #include <math.h>
 
+#include <stdlib.h>
+#include <string.h>
+
 #include "pbh_error.h"
 #include "pbh_ic.h"
 #include "pbh_special.h"
@@ -484,6 +487,97 @@ __global__ __launch_bounds__(256) void k_apply(double* __restrict__ S, int64_t n
   }
 }
 
+// ---------------------------------------------------------------- step 3 on the matrix cores
+// For K <= 32 the two triangular factors fold into one 32 x 32 matrix M = L^-T P^T (zero padded),
+// CS = S M, and the N x 32 by 32 x 32 product runs on v_mfma_f64_16x16x4_f64.  The vector
+// kernel above is latency bound (one row per lane: 32 loads, ~1000 dependent FMAs, 64 stores,
+// 150 VGPRs); here a wave multiplies 64-row tiles with the whole of M held as B operands in
+// registers, and the result goes through LDS so that every column store is 512 contiguous
+// bytes.  M is computed on the device from L by column-wise forward substitution (f64); the
+// product differs from substitution-then-multiply in the last bits only, as the reference's
+// own dtrsm + dgemm order does from either.
+__global__ void k_transform_matrix(const double* __restrict__ L, const double* __restrict__ inv_diag,
+                                   const double* __restrict__ P, int k, double* __restrict__ M) {
+  __shared__ double Linv[32][33];  // Linv[i][c] = (L^-1)[i][c]
+  const int c = threadIdx.x;  // column c of L^-1: solve L x = e_c
+  if (c < 32) {
+    for (int i = 0; i < 32; ++i) {
+      double v = 0.0;
+      if (i < k && c < k && i >= c) {
+        double acc = (i == c) ? 1.0 : 0.0;
+        for (int m = c; m < i; ++m) acc = __builtin_fma(-L[i * k + m], Linv[m][c], acc);
+        v = acc * inv_diag[i];
+      }
+      Linv[i][c] = v;
+    }
+  }
+  __syncthreads();
+  // M[m][j] = sum_q Linv[q][m] P[j][q]  (q in [m, j]: both triangular)
+  for (int e = threadIdx.x; e < 32 * 32; e += blockDim.x) {
+    const int m = e >> 5, j = e & 31;
+    double acc = 0.0;
+    if (m < k && j < k)
+      for (int q = m; q <= j; ++q) acc = __builtin_fma(Linv[q][m], P[j * k + q], acc);
+    M[e] = acc;
+  }
+}
+
+constexpr int AM_ROWS = 64;  // rows per wave tile
+
+__global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int64_t n, int k, int64_t ld,
+                                                   const double* __restrict__ M, uint32_t* __restrict__ codes,
+                                                   int64_t ldc, CodeMap cm) {
+  __shared__ double tile[4][AM_ROWS * 33];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* tl = tile[w];
+  const int q = lane >> 4, m16 = lane & 15;
+  double b[8][2];  // B operands: M[4 s + q][16 J + m16]
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int J = 0; J < 2; ++J) b[s][J] = M[(4 * s + q) * 32 + 16 * J + m16];
+  const int64_t tiles = (n + AM_ROWS - 1) / AM_ROWS;
+  for (int64_t bt = blockIdx.x; bt * 4 < tiles; bt += gridDim.x) {  // uniform trip count per block
+    const int64_t tw = bt * 4 + w;
+    const int64_t r0 = tw * AM_ROWS;
+    if (tw < tiles) {
+#pragma unroll
+      for (int rb = 0; rb < AM_ROWS / 16; ++rb) {
+        const int64_t r = r0 + rb * 16 + m16;
+        double a[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int c = 4 * s + q;
+          a[s] = (c < k && r < n) ? S[(int64_t)c * ld + r] : 0.0;
+        }
+        f64x4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s][0], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s][1], c1, 0, 0, 0);
+        }
+        // C[i][j]: register g of lane l holds row i = (l >> 4) + 4 g, column j = l & 15
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = rb * 16 + q + 4 * g;
+          tl[row * 33 + m16] = c0[g];
+          tl[row * 33 + 16 + m16] = c1[g];
+        }
+      }
+    }
+    __syncthreads();
+    const int64_t r = r0 + lane;
+    if (tw < tiles && r < n) {
+      for (int c = 0; c < k; ++c) {
+        const double v = tl[lane * 33 + c];
+        S[(int64_t)c * ld + r] = v;
+        if (codes) codes[(int64_t)c * ldc + r] = code_of(v, cm);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 size_t tie_workspace_bytes(int64_t n) {
@@ -605,6 +699,23 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
   dim3 g(grid_for(n, 256, 8192)), b(256);
   CodeMap c = cm ? *cm : CodeMap{};
   if (!cm) codes = nullptr;
+  static const bool vector_only = [] {
+    const char* e = getenv("PBH_APPLY");
+    return e && strcmp(e, "vector") == 0;
+  }();
+  if (k <= 32 && !vector_only) {
+    double* M = nullptr;
+    PBH_CHECK_HIP(hipMallocAsync((void**)&M, 32 * 32 * sizeof(double), s));
+    hipLaunchKernelGGL(k_transform_matrix, dim3(1), dim3(64), 0, s, L, inv_diag, P, k, M);
+    PBH_CHECK_LAUNCH();
+    const int64_t tiles = (n + AM_ROWS - 1) / AM_ROWS;
+    const unsigned gb = (unsigned)((tiles + 3) / 4 < 8192 ? (tiles + 3) / 4 : 8192);
+    PBH_TIMED(kKApply, s,
+              hipLaunchKernelGGL(k_apply_mfma, dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc, c));
+    PBH_CHECK_LAUNCH();
+    PBH_CHECK_HIP(hipFreeAsync(M, s));
+    return PBH_OK;
+  }
   if (k <= 8)
     PBH_TIMED(kKApply, s, hipLaunchKernelGGL(k_apply<8>, g, b, 0, s, S, n, k, ld, L, inv_diag, P, codes, ldc, c));
   else if (k <= 16)
