@@ -45,10 +45,12 @@ def kernel_bytes(name, n, k):
 
 
 # bench (HIP-event) kernel names -> rocprofv3 kernel names in the committed PMC summaries
-PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 16>", "k_scatter<unsigned int>"],
+PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 32>", "k_onesweep<unsigned int, unsigned int, 16>",
+                                "k_scatter<unsigned int>"],
              "k_scatter<place>": ["k_onesweep<unsigned int, double, 16>", "k_scatter<unsigned int, double>"],
              "k_code_runs": ["k_runs_scan", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
-             "k_apply": ["k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"]}
+             "k_apply": ["k_apply_mfma", "k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"],
+             "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"]}
 
 
 def pmc_traffic(kernel):
@@ -62,10 +64,11 @@ def pmc_traffic(kernel):
         return None, None
     ks = json.load(open(files[-1]))["kernels"]
     names = PMC_NAMES.get(kernel, [kernel])
-    hits = [ks[n]["hbm_bytes"] for n in names if n in ks]
-    if not hits:
-        return None, None
-    return int(sum(hits)), os.path.relpath(files[-1], ROOT)
+    for name in names:  # alternatives (the kernel variant that ran), first match wins
+        if name in ks:
+            k = ks[name]
+            return int(k["hbm_bytes"]), os.path.relpath(files[-1], ROOT)  # per dispatch (pmc_summary.py)
+    return None, None
 
 
 def main():
