@@ -120,12 +120,19 @@ int reorder_column(const double* cs, int64_t n, const double* sorted_src, double
     st = make_codes(cs, n, w.cm, (uint32_t*)sb.keys[0], s);
     if (st) return st;
   }
-  st = radix_sort_keys32(sb, n, s, &buf, codes);
-  if (st) return st;
   PBH_CHECK_HIP(hipMemsetAsync(w.flags, 0, sizeof(int32_t), s));
-  st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], cs, n, w.eqprev, w.flags,
-                         (uint32_t*)sb.keys[buf ^ 1], sb.counts, s);
-  if (st) return st;
+  buf = -1;
+  if (code_buckets_enabled(n)) {  // 2 one-sweep passes + per-bucket LDS finish (runs included)
+    st = code_sort_buckets(sb, n, codes ? codes : (const uint32_t*)sb.keys[0], cs, w.eqprev, w.flags, s, &buf);
+    if (st) return st;
+  }
+  if (buf < 0) {  // four one-sweep passes + the run fix-up
+    st = radix_sort_keys32(sb, n, s, &buf, codes);
+    if (st) return st;
+    st = resolve_code_runs((const uint32_t*)sb.keys[buf], sb.vals[buf], cs, n, w.eqprev, w.flags,
+                           (uint32_t*)sb.keys[buf ^ 1], sb.counts, s);
+    if (st) return st;
+  }
   int32_t run_flags = 0;
   PBH_CHECK_HIP(hipMemcpyAsync(&run_flags, w.flags, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));

@@ -47,6 +47,12 @@ int exclusive_scan_u32(uint32_t* a, int64_t m, uint32_t* partials, hipStream_t s
 // The same on uint32 keys stored in b.keys[0] (reinterpreted), or read from `in` (left
 // unmodified): at most 4 passes.
 int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, const uint32_t* in = nullptr);
+// Step 4's code sort for 2^22 <= n <= 2^27 (see k_code_buckets): codes -> rows in final rank
+// order in b.vals[*out_buf] plus eqprev / flags exactly as resolve_code_runs leaves them (flags
+// bit 0: fall back to 64-bit keys; bit 1: exact ties).  flags must be zeroed by the caller.
+bool code_buckets_enabled(int64_t n);
+int code_sort_buckets(SortBuffers& b, int64_t n, const uint32_t* codes, const double* x, uint8_t* eqprev,
+                      int32_t* flags, hipStream_t s, int* out_buf);
 
 // Y[rows[p] * y_rs] = v[p] for a permutation `rows` of [0, n): the inverse-permutation write
 // of Iman-Conover step 4 (correlation.py:423) without random 8-byte stores.  LSD bucket passes

@@ -419,6 +419,225 @@ __global__ __launch_bounds__(T) void k_place(const uint32_t* __restrict__ rows, 
   }
 }
 
+// ------------------------------------------------------------------ top-16-bit code buckets
+// Step 4's 32-bit code sort in three launches instead of four one-sweep passes plus the run
+// fix-up: two one-sweep passes on bytes 2 and 3 leave the (code, row) pairs sorted by the top
+// 16 code bits, stable in row order; every top-16 bucket (~n / 65536 pairs: the codes are
+// Phi-uniformised, so ~1500 at n = 1e8) is then finished by one wave in LDS -- two stable
+// counting passes on bytes 0 and 1, and the ordering of equal-code runs by the full value with
+// the exact-tie flags, as resolve_code_runs does (equal codes share their bucket).
+// A bucket larger than kBucketCap, or a run longer than kBucketMaxRun, sets flags bit 0 and the
+// caller falls back to the 64-bit sort, exactly like a long run of the four-pass path.
+constexpr int kBucketCap = 2048;  // pairs per bucket (one wave)
+constexpr int kBucketMaxRun = 16;
+constexpr uint32_t kNoStart = 0xFFFFFFFFu;
+
+// start[b] = first position of bucket b (keys sorted by their top 16 bits); untouched (kNoStart)
+// for empty buckets.
+__global__ __launch_bounds__(256) void k_bucket_starts(const uint32_t* __restrict__ keys, int64_t n,
+                                                      uint32_t* __restrict__ start) {
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+    const uint32_t b = keys[p] >> 16;
+    if (p == 0 || (keys[p - 1] >> 16) != b) start[b] = (uint32_t)p;
+  }
+}
+
+// Every wave finishes one bucket on its own (no block barriers): the bucket's low 16 code bits
+// and rows sit in registers (32 items per lane, position order j * 64 + lane), and each of the
+// two stable counting passes ranks them with ballot peer matching against LDS digit counters,
+// scans the 256 counters across the wave, and scatters into the wave's LDS arrays, which are
+// read back in position order for the next pass.  ~15 KB of LDS per wave.  (Measured
+// alternatives, profiles/r01/: one block-wide bucket per workgroup was 2x slower; a non-stable
+// atomic grouping + per-group insertion sort was slower on columns with equal-code runs, its
+// insertion chains being LDS-latency bound.)
+constexpr int kWBItems = kBucketCap / 64;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct WaveBucket {
+  uint16_t key[kBucketCap];
+  uint32_t row[kBucketCap];
+  uint8_t eq[kBucketCap];
+  uint32_t cnt[256];
+  uint16_t runs[256];
+};
+
+// one stable pass on the byte of k at `shift` (0 or 8); k / r: this lane's items in position order
+__device__ __forceinline__ void wave_radix_pass(uint32_t (&k)[kWBItems], uint32_t (&r)[kWBItems], int len,
+                                                int shift, WaveBucket& B) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) B.cnt[lane * 4 + q] = 0;
+  wave_sync();
+  uint32_t rank[kWBItems];
+#pragma unroll
+  for (int j = 0; j < kWBItems; ++j) {
+    const bool valid = j * 64 + lane < len;
+    const uint32_t d = (k[j] >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bb = __ballot(valid && ((d >> b) & 1u));
+      peers &= ((d >> b) & 1u) ? bb : ~bb;
+    }
+    const uint32_t below = (uint32_t)__popcll(peers & lt);
+    const uint32_t c = valid ? B.cnt[d] : 0u;  // LDS is in order within a wave
+    rank[j] = c + below;
+    if (valid && below == 0) B.cnt[d] = c + (uint32_t)__popcll(peers);
+  }
+  wave_sync();
+  // exclusive scan of the 256 counters: lane l owns digits 4 l .. 4 l + 3
+  uint32_t v[4], sum = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = B.cnt[lane * 4 + q];
+    sum += v[q];
+  }
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  uint32_t run = incl - sum;
+  wave_sync();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    B.cnt[lane * 4 + q] = run;
+    run += v[q];
+  }
+  wave_sync();
+#pragma unroll
+  for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 + lane < len) {
+      const uint32_t lp = B.cnt[(k[j] >> shift) & 255u] + rank[j];
+      B.key[lp] = (uint16_t)k[j];
+      B.row[lp] = r[j];
+    }
+  }
+  wave_sync();
+}
+
+constexpr int kCBWaves = 2;  // waves (buckets) per block: ~31 KB of LDS
+
+__global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* __restrict__ keys,
+                                                               uint32_t* __restrict__ rows,
+                                                               const double* __restrict__ x, int64_t n,
+                                                               const uint32_t* __restrict__ start,
+                                                               uint8_t* __restrict__ eqprev, int32_t* flags) {
+  __shared__ WaveBucket wb[kCBWaves];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  WaveBucket& B = wb[w];
+  const int bkt = blockIdx.x * kCBWaves + w;
+  if (bkt >= 65536) return;
+  const uint32_t s0 = start[bkt];
+  if (s0 == kNoStart) return;  // empty bucket (wave-uniform)
+  // end: the first non-empty bucket after this one, 64 candidates per probe
+  int64_t e = n;
+  for (int c0 = bkt + 1; c0 < 65536; c0 += 64) {
+    const int c = c0 + lane;
+    const uint32_t v = c < 65536 ? start[c] : kNoStart;
+    const uint64_t m = __ballot(v != kNoStart);
+    if (m) {
+      e = __shfl(v, __builtin_ctzll(m), 64);
+      break;
+    }
+  }
+  const int64_t s = s0;
+  if (e - s > kBucketCap) {
+    if (lane == 0) atomicOr(flags, 1);
+    return;
+  }
+  const int len = (int)(e - s);
+  uint32_t k[kWBItems], r[kWBItems];
+#pragma unroll
+  for (int j = 0; j < kWBItems; ++j) {
+    const int p = j * 64 + lane;
+    k[j] = p < len ? (keys[s + p] & 0xFFFFu) : 0u;
+    r[j] = p < len ? rows[s + p] : 0u;
+  }
+  wave_radix_pass(k, r, len, 0, B);
+#pragma unroll
+  for (int j = 0; j < kWBItems; ++j) {
+    const int p = j * 64 + lane;
+    k[j] = p < len ? B.key[p] : 0u;
+    r[j] = p < len ? B.row[p] : 0u;
+  }
+  wave_sync();
+  wave_radix_pass(k, r, len, 8, B);
+  // runs of equal codes (equal low 16 bits inside a bucket), compacted into B.runs
+  int nrun = 0;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll 4
+  for (int j = 0; j < kWBItems; ++j) {
+    const int p = j * 64 + lane;
+    bool st = false;
+    if (p < len) {
+      const uint16_t c = B.key[p];
+      st = p + 1 < len && B.key[p + 1] == c && (p == 0 || B.key[p - 1] != c);
+      B.eq[p] = 0;
+    }
+    const uint64_t m = __ballot(st);
+    const int slot = nrun + (int)__popcll(m & lt);
+    if (st && slot < 256) B.runs[slot] = (uint16_t)p;
+    nrun += (int)__popcll(m);
+  }
+  wave_sync();
+  if (nrun > 256) {
+    if (lane == 0) atomicOr(flags, 1);
+    return;
+  }
+  bool any_tie = false;
+  for (int i = lane; i < nrun; i += 64) {  // as k_runs_resolve: stable order by value, ties flagged
+    const int p = B.runs[i];
+    const uint16_t c = B.key[p];
+    int L = 2;
+    while (p + L < len && B.key[p + L] == c && L <= kBucketMaxRun) ++L;
+    if (L > kBucketMaxRun) {
+      atomicOr(flags, 1);
+      continue;
+    }
+    uint32_t rr[kBucketMaxRun];
+    double v[kBucketMaxRun];
+#pragma unroll
+    for (int j = 0; j < kBucketMaxRun; ++j) {
+      rr[j] = j < L ? B.row[p + j] : 0u;
+      v[j] = j < L ? x[rr[j]] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kBucketMaxRun; ++q) {
+      int pos = 0;
+      bool tie = false;
+#pragma unroll
+      for (int j = 0; j < kBucketMaxRun; ++j) {
+        const bool other = j < L && j != q;
+        pos += (other && (v[j] < v[q] || (v[j] == v[q] && j < q))) ? 1 : 0;
+        tie |= other && v[j] == v[q] && j < q;
+      }
+      if (q < L) {
+        B.row[p + pos] = rr[q];
+        B.eq[p + pos] = tie ? 1 : 0;
+        any_tie |= tie;
+      }
+    }
+  }
+  if (__ballot(any_tie) && lane == 0) atomicOr(flags, 2);
+  wave_sync();
+#pragma unroll 4
+  for (int j = 0; j < kWBItems; ++j) {
+    const int p = j * 64 + lane;
+    if (p < len) {
+      rows[s + p] = B.row[p];
+      eqprev[s + p] = B.eq[p];
+    }
+  }
+}
+
 }  // namespace
 
 int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, int64_t y_rs, const PlaceBuffers& pb,
@@ -469,6 +688,64 @@ int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, in
       return PBH_ERR_HIP;
     }
   }
+  return PBH_OK;
+}
+
+bool code_buckets_enabled(int64_t n) {
+  const char* e = getenv("PBH_STEP4");  // read per call: "buckets" forces, "lsd" disables
+  if (e && strcmp(e, "buckets") == 0) return n >= 2 && n < ((int64_t)1 << 32);
+  if (e && strcmp(e, "lsd") == 0) return false;
+  if (!onesweep_enabled()) return false;
+  return n >= ((int64_t)1 << 22) && n <= (int64_t)110000000;  // mean bucket <= ~1700 of the 2048 cap
+}
+
+int code_sort_buckets(SortBuffers& b, int64_t n, const uint32_t* codes, const double* x, uint8_t* eqprev,
+                      int32_t* flags, hipStream_t s, int* out_buf) {
+  PBH_REQUIRE(n >= 2 && n < ((int64_t)1 << 32), "code_sort_buckets: n out of range");
+  const int64_t nt = sort_tiles(n);
+  uint32_t* keys[2] = {(uint32_t*)b.keys[0], (uint32_t*)b.keys[1]};
+  PBH_CHECK_HIP(hipMemsetAsync(b.hist, 0, 4 * 256 * 4, s));
+  PBH_TIMED(kKSortDigitHist32, s,
+            hipLaunchKernelGGL(k_digit_hist<uint32_t>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, codes, n, b.hist));
+  hipLaunchKernelGGL(k_digit_bases, dim3(4), dim3(256), 0, s, b.hist, b.bases);
+  PBH_CHECK_LAUNCH();
+  // A column whose top-byte histogram is far from flat (a mixture with discrete spikes, e.g. a
+  // poisson-dominated correlated score) would overflow top-16 buckets: leave it to the four
+  // passes (*out_buf = -1).  The kernel's overflow flag stays the safety net.
+  PBH_CHECK_HIP(hipMemcpyAsync(b.hist_host, b.hist, 4 * 256 * 4, hipMemcpyDeviceToHost, s));
+  PBH_CHECK_HIP(hipStreamSynchronize(s));
+  uint32_t top_max = 0;
+  for (int d = 0; d < 256; ++d) top_max = b.hist_host[3 * 256 + d] > top_max ? b.hist_host[3 * 256 + d] : top_max;
+  const char* force = getenv("PBH_STEP4");
+  const bool forced = force && strcmp(force, "buckets") == 0;  // tests: exercise the kernel and its safety net
+  if (!forced && (double)top_max > 1.5 * (double)n / 256.0 + 64.0) {
+    *out_buf = -1;
+    return PBH_OK;
+  }
+  PBH_CHECK_HIP(hipMemsetAsync(b.status + nt * 256, 0, 256, s));
+  int cur = 0;
+  for (int ip = 0; ip < 2; ++ip) {
+    const int byte = 2 + ip;
+    PBH_CHECK_HIP(hipMemsetAsync(b.status, 0, (size_t)nt * 256 * 8 + 4, s));
+    PBH_TIMED(kKSortScatter32, s,
+              launch_onesweep<uint32_t, uint32_t>(ip == 0 ? codes : keys[cur], ip == 0 ? nullptr : b.vals[cur],
+                                                  keys[cur ^ 1], b.vals[cur ^ 1], n, 8 * byte, b.bases + byte * 256,
+                                                  b.status, (uint32_t*)(b.status + nt * 256), s));
+    PBH_CHECK_LAUNCH();
+    cur ^= 1;
+  }
+  // 65536 bucket starts: in `counts` (256 * sort_tiles(n) words) when it is large enough
+  uint32_t* start = b.counts;
+  const bool own = (int64_t)256 * nt < 65536;
+  if (own) PBH_CHECK_HIP(hipMallocAsync((void**)&start, 65536 * 4, s));
+  PBH_CHECK_HIP(hipMemsetAsync(start, 0xFF, 65536 * 4, s));
+  PBH_TIMED(kKCodeRuns, s,
+            hipLaunchKernelGGL(k_bucket_starts, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, keys[cur], n, start);
+            hipLaunchKernelGGL(k_code_buckets, dim3(65536 / kCBWaves), dim3(64 * kCBWaves), 0, s, keys[cur], b.vals[cur], x, n, start,
+                               eqprev, flags));
+  PBH_CHECK_LAUNCH();
+  if (own) PBH_CHECK_HIP(hipFreeAsync(start, s));
+  *out_buf = cur;
   return PBH_OK;
 }
 

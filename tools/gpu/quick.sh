@@ -5,7 +5,7 @@ TAG=${1:-rX}; ARGS=$2; BENCH=$3
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
-timeout -k 10 600 python -u -m pytest $ARGS -x -q -rf --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest $ARGS ${XFLAG--x} -q -rf --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/${TAG}_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 if [ -n "$BENCH" ]; then
