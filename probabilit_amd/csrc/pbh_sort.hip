@@ -443,8 +443,9 @@ __global__ __launch_bounds__(256) void k_bucket_starts(const uint32_t* __restric
 }
 
 // Every wave finishes one bucket on its own (no block barriers): the bucket's low 16 code bits
-// and rows sit in registers (32 items per lane, position order j * 64 + lane), and each of the
-// two stable counting passes ranks them with ballot peer matching against LDS digit counters,
+// and rows sit in registers (32 items per lane, position order j * 64 + lane); the low byte pass
+// ranks with LDS atomics (see wave_count_pass), the stable high byte pass with ballot peer
+// matching against LDS digit counters; each pass
 // scans the 256 counters across the wave, and scatters into the wave's LDS arrays, which are
 // read back in position order for the next pass.  ~15 KB of LDS per wave.  (Measured
 // alternatives, profiles/r01/: one block-wide bucket per workgroup was 2x slower; a non-stable
@@ -523,6 +524,51 @@ __device__ __forceinline__ void wave_radix_pass(uint32_t (&k)[kWBItems], uint32_
   wave_sync();
 }
 
+// The first (low byte) pass need not be stable: pairs that tie on the low byte and then on the
+// high byte have equal codes, i.e. they form a run, which is put in value order afterwards.  So
+// it ranks with one LDS atomic per item instead of the ballot matching.
+__device__ __forceinline__ void wave_count_pass(uint32_t (&k)[kWBItems], uint32_t (&r)[kWBItems], int len,
+                                                WaveBucket& B) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) B.cnt[lane * 4 + q] = 0;
+  wave_sync();
+  uint32_t rank[kWBItems];
+#pragma unroll
+  for (int j = 0; j < kWBItems; ++j)
+    rank[j] = (j * 64 + lane < len) ? atomicAdd(&B.cnt[k[j] & 255u], 1u) : 0u;
+  wave_sync();
+  uint32_t v[4], sum = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = B.cnt[lane * 4 + q];
+    sum += v[q];
+  }
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  uint32_t run = incl - sum;
+  wave_sync();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    B.cnt[lane * 4 + q] = run;
+    run += v[q];
+  }
+  wave_sync();
+#pragma unroll
+  for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 + lane < len) {
+      const uint32_t lp = B.cnt[k[j] & 255u] + rank[j];
+      B.key[lp] = (uint16_t)k[j];
+      B.row[lp] = r[j];
+    }
+  }
+  wave_sync();
+}
+
 constexpr int kCBWaves = 2;  // waves (buckets) per block: ~31 KB of LDS
 
 __global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* __restrict__ keys,
@@ -561,7 +607,7 @@ __global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* 
     k[j] = p < len ? (keys[s + p] & 0xFFFFu) : 0u;
     r[j] = p < len ? rows[s + p] : 0u;
   }
-  wave_radix_pass(k, r, len, 0, B);
+  wave_count_pass(k, r, len, B);
 #pragma unroll
   for (int j = 0; j < kWBItems; ++j) {
     const int p = j * 64 + lane;
