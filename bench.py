@@ -35,7 +35,12 @@ def kernel_bytes(name, n, k):
                 "k_scatter<u32>": 16, "k_upsweep<u32>": 4, "k_digit_hist<u32>": 4,  # u32 code + u32 row
                 "k_rank_finish<scores>": 28,  # read key 8 + row 4, write score 8 + sorted x 8
                 "k_rank_finish<gather>": 21,  # read eqprev 1 + row 4 + sorted x 8, write y 8 (idx only in debug calls)
-                "k_load_keys": 16, "k_make_codes": 12, "k_code_runs": 13,  # runs: codes 4 + row 4 + out 4 + eqprev 1
+                "k_load_keys": 16, "k_make_codes": 12,
+                # step-4 bucket finish (k_bucket_starts: codes 4; k_code_buckets: codes 4 + rows 4 in,
+                # rows 4 + eqprev 1 out) -- the four-pass fallback's run fix-up moves 13
+                "k_code_runs": 17,
+                "k_scatter<place>": 24,  # row u32 + value f64, read and written
+                "k_place": 20,  # row 4 + value 8 in, y 8 out
                 "k_elementwise": 24, "k_head_bounds": 8, "k_scan": 0}
     if name == "k_gram":
         return 8 * n * k
@@ -48,7 +53,7 @@ def kernel_bytes(name, n, k):
 PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 32>", "k_onesweep<unsigned int, unsigned int, 16>",
                                 "k_scatter<unsigned int>"],
              "k_scatter<place>": ["k_onesweep<unsigned int, double, 16>", "k_scatter<unsigned int, double>"],
-             "k_code_runs": ["k_runs_scan", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
+             "k_code_runs": ["k_code_buckets", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
              "k_apply": ["k_apply_mfma", "k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"],
              "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"]}
 

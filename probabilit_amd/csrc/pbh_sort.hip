@@ -366,30 +366,43 @@ __global__ __launch_bounds__(256) void k_place_bases(int64_t n, int shift, uint3
 }
 
 // Items per thread of the one-sweep scatter (tile = 256 x items).  Measured on MI355X
-// (profiles/r01/bench_r14_*): 32-bit key + 32-bit payload passes are faster with 32 items
-// (8192-key tiles: ~32 keys per digit bucket, i.e. whole 128-byte lines per burst; 64 KB of LDS,
-// 2 tiles per CU), the 32-bit key + 64-bit value passes of the row placement with 16 (their
-// 96 KB tile would leave one tile per CU).  PBH_OS_IPT = 16 or 32 forces either.
+// (profiles/r01/bench_r14_*, bench_r40_*, bench_r41_*): 32-bit key + 32-bit payload passes take 36
+// items (9216-key tiles: ~36 keys per digit bucket, whole 128-byte lines per burst; 72 KB of LDS,
+// 2 tiles per CU; 0.59 ms per 1e8-key pass against 0.62 with 32, 0.69 with 24); the 32-bit key +
+// 64-bit value passes of the row placement with 24
+// (72 KB, still 2 tiles per CU: 0.75 ms per 1e8-row pass against 0.91 with 16).  PBH_OS_IPT
+// (16 / 24 / 32 / 36) and PBH_PLACE_IPT (16 / 20 / 24) force either.
 int onesweep_items(size_t value_bytes) {
   static const int forced = [] {
     const char* e = getenv("PBH_OS_IPT");
     return e ? atoi(e) : 0;
   }();
-  if (forced == 16 || forced == 32) return forced;
-  return value_bytes <= 4 ? 32 : 16;
+  static const int forced_place = [] {
+    const char* e = getenv("PBH_PLACE_IPT");
+    return e ? atoi(e) : 0;
+  }();
+  if (value_bytes > 4 && (forced_place == 16 || forced_place == 20 || forced_place == 24)) return forced_place;
+  if (value_bytes <= 4 && (forced == 16 || forced == 24 || forced == 32 || forced == 36)) return forced;
+  return value_bytes <= 4 ? 36 : 24;
+}
+
+template <typename K, typename V, int IPT_>
+void launch_onesweep_ipt(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
+                         uint64_t* status, uint32_t* counter, hipStream_t s) {
+  const int64_t nt = (n + T * IPT_ - 1) / (T * IPT_);
+  hipLaunchKernelGGL((k_onesweep<K, V, IPT_>), dim3((unsigned)nt), dim3(T), 0, s, kin, vin, kout, vout, n, shift,
+                     bases, status, counter);
 }
 
 template <typename K, typename V>
 void launch_onesweep(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
                      uint64_t* status, uint32_t* counter, hipStream_t s) {
-  if (onesweep_items(sizeof(V)) == 32) {
-    const int64_t nt = (n + T * 32 - 1) / (T * 32);
-    hipLaunchKernelGGL((k_onesweep<K, V, 32>), dim3((unsigned)nt), dim3(T), 0, s, kin, vin, kout, vout, n, shift,
-                       bases, status, counter);
-  } else {
-    const int64_t nt = (n + T * 16 - 1) / (T * 16);
-    hipLaunchKernelGGL((k_onesweep<K, V, 16>), dim3((unsigned)nt), dim3(T), 0, s, kin, vin, kout, vout, n, shift,
-                       bases, status, counter);
+  switch (onesweep_items(sizeof(V))) {
+    case 36: launch_onesweep_ipt<K, V, 36>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
+    case 32: launch_onesweep_ipt<K, V, 32>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
+    case 24: launch_onesweep_ipt<K, V, 24>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
+    case 20: launch_onesweep_ipt<K, V, 20>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
+    default: launch_onesweep_ipt<K, V, 16>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
   }
 }
 
