@@ -50,9 +50,10 @@ def kernel_bytes(name, n, k):
 
 
 # bench (HIP-event) kernel names -> rocprofv3 kernel names in the committed PMC summaries
-PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 32>", "k_onesweep<unsigned int, unsigned int, 16>",
-                                "k_scatter<unsigned int>"],
-             "k_scatter<place>": ["k_onesweep<unsigned int, double, 16>", "k_scatter<unsigned int, double>"],
+PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k_onesweep<unsigned int, unsigned int, 32>",
+                                "k_onesweep<unsigned int, unsigned int, 16>", "k_scatter<unsigned int>"],
+             "k_scatter<place>": ["k_onesweep<unsigned int, double, 24>", "k_onesweep<unsigned int, double, 16>",
+                                  "k_scatter<unsigned int, double>"],
              "k_code_runs": ["k_code_buckets", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
              "k_apply": ["k_apply_mfma", "k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"],
              "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"]}
