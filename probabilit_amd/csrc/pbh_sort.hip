@@ -372,7 +372,8 @@ __global__ __launch_bounds__(256) void k_place_bases(int64_t n, int shift, uint3
 // 64-bit value passes of the row placement with 24
 // (72 KB, still 2 tiles per CU: 0.75 ms per 1e8-row pass against 0.91 with 16).  PBH_OS_IPT
 // (16 / 24 / 32 / 36) and PBH_PLACE_IPT (16 / 20 / 24) force either.
-int onesweep_items(size_t value_bytes) {
+int onesweep_items(size_t item_bytes_minus_key4) {
+  const size_t value_bytes = item_bytes_minus_key4;
   static const int forced = [] {
     const char* e = getenv("PBH_OS_IPT");
     return e ? atoi(e) : 0;
@@ -383,7 +384,7 @@ int onesweep_items(size_t value_bytes) {
   }();
   if (value_bytes > 4 && (forced_place == 16 || forced_place == 20 || forced_place == 24)) return forced_place;
   if (value_bytes <= 4 && (forced == 16 || forced == 24 || forced == 32 || forced == 36)) return forced;
-  return value_bytes <= 4 ? 36 : 24;
+  return value_bytes <= 4 ? 36 : 24;  // item_bytes (key + value) 8 -> 36, 12 -> 24: ~79 KB of LDS either way
 }
 
 template <typename K, typename V, int IPT_>
@@ -397,7 +398,7 @@ void launch_onesweep_ipt(const K* kin, const V* vin, K* kout, V* vout, int64_t n
 template <typename K, typename V>
 void launch_onesweep(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
                      uint64_t* status, uint32_t* counter, hipStream_t s) {
-  switch (onesweep_items(sizeof(V))) {
+  switch (onesweep_items(sizeof(K) + sizeof(V) - 4)) {  // u64 key + u32 row sizes like u32 + f64
     case 36: launch_onesweep_ipt<K, V, 36>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
     case 32: launch_onesweep_ipt<K, V, 32>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
     case 24: launch_onesweep_ipt<K, V, 24>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
