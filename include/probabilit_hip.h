@@ -112,6 +112,15 @@ int pbh_fill_halton(const int32_t* bases_host, const int32_t* counts_host, const
 int pbh_fill_sobol(const uint32_t* sv_host, const uint32_t* shift_host, int d, int bits, int64_t row0,
                    int64_t nrows, int col0, int ncols, double* q, int64_t ldq, void* stream);
 
+/* One scrambled Sobol' column (as pbh_fill_sobol: column `col` of d, `bits`, rows [row0, row0 +
+ * nrows)) pushed through the inverse CDF of `dist` in one kernel, the quantile never stored:
+ * out[r] = ppf(q(row0 + r)) (replaces the "sobol" branch of Node.sample, modeling.py:482,488,
+ * followed by Distribution._sample, :795-807).  dist < PBH_DIST_BETA; others return
+ * PBH_ERR_UNSUPPORTED (materialise with pbh_fill_sobol + pbh_ppf). */
+int pbh_sobol_ppf(const uint32_t* sv_host, const uint32_t* shift_host, int d, int bits, int64_t row0, int64_t nrows,
+                  int col, int dist, const pbh_param* params, int nparams, double* out, int32_t* nonfinite_flag,
+                  void* stream);
+
 /* ---------------------------------------------------------------- inverse CDF sweep
  * Distribution._sample (modeling.py:795-807) -> scipy rv_continuous.ppf / rv_discrete.ppf:
  * out[i] = ppf(q[i * q_stride]; params) with scipy's argument checks, support bounds at

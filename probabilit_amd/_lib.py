@@ -45,7 +45,7 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_pcg64_workspace_size",
            "pbh_pcg64_random", "pbh_halton_workspace_size", "pbh_fill_halton",
            "pbh_affine_workspace_size", "pbh_affine_rows", "pbh_table_ppf", "pbh_permcorr_workspace_size",
-           "pbh_permcorr_climb"]
+           "pbh_permcorr_climb", "pbh_sobol_ppf"]
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
@@ -142,6 +142,7 @@ def load():
         "pbh_affine_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
         "pbh_table_ppf": ([i32, vp, i64, i64, vp, vp, i64, i32, i32, vp, vp, vp], i32),
         "pbh_affine_rows": ([vp, i64, ctypes.c_int32, i64, i64, vp, vp, vp, vp, vp, i64, i64, vp, sz, vp], i32),
+        "pbh_sobol_ppf": ([vp, vp, i32, i32, i64, i64, i32, i32, ctypes.POINTER(Param), i32, vp, vp, vp], i32),
         "pbh_permcorr_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
         "pbh_permcorr_climb": ([vp, vp, i64, ctypes.c_int32, i64, vp, vp, vp, vp, vp, vp, i64, dbl, vp, vp, vp, sz, vp],
                                i32),

@@ -541,19 +541,73 @@ struct SobolArgs {
   uint32_t shift[kSobolColsPerLaunch];
 };
 
+// x(r) = shift XOR (the direction numbers of the set bits of gray(r) = r ^ (r >> 1)), by four
+// 256-entry tables of the XORs over each byte of gray(r) (built in LDS per block): 4 lookups per
+// point instead of a loop over ~15 set bits.  Identical values (XOR is associative).
+PBH_DI void build_sobol_tables(const uint32_t* sv, uint32_t* T) {
+  for (int t = threadIdx.x; t < 256; t += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+        if ((t >> b) & 1) v ^= sv[8 * k + b];
+      T[k * 256 + t] = v;
+    }
+  }
+}
+
+PBH_DI uint32_t sobol_point(const uint32_t* T, uint32_t shift, uint64_t r) {
+  const uint32_t g = (uint32_t)(r ^ (r >> 1));  // r < 2^bits <= 2^32
+  return shift ^ T[g & 255u] ^ T[256 + ((g >> 8) & 255u)] ^ T[512 + ((g >> 16) & 255u)] ^ T[768 + (g >> 24)];
+}
+
 __global__ __launch_bounds__(kBlock) void k_fill_sobol(SobolArgs a, double scale, int64_t row0, int64_t nrows,
                                                        double* __restrict__ q, int64_t ldq) {
+  __shared__ uint32_t T[1024];
   const int c = blockIdx.y;
+  build_sobol_tables(a.sv[c], T);
+  __syncthreads();
   double* qc = q + (int64_t)c * ldq;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
-    uint64_t r = (uint64_t)(row0 + i);
-    uint64_t g = r ^ (r >> 1);
-    uint32_t x = a.shift[c];
-    while (g) {
-      x ^= a.sv[c][__builtin_ctzll(g)];
-      g &= g - 1;
-    }
+    const uint32_t x = sobol_point(T, a.shift[c], (uint64_t)(row0 + i));
     qc[i] = (double)x * scale;
+  }
+}
+
+// One scrambled Sobol' column fused into the inverse CDF (the "sobol" method of Node.sample,
+// modeling.py:482,488): the quantile never goes through HBM.  norm / lognorm take the tail-
+// compacted form.  Same points as k_fill_sobol, same values as pbh_ppf on them.
+struct SobolCol {
+  uint32_t sv[32];
+  uint32_t shift;
+  double scale;
+};
+
+template <int D>
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_sobol_ppf_c(SobolCol sc, int64_t row0, int64_t nrows, Params prm,
+                                                               PoissonTable pt, double* __restrict__ out,
+                                                               int32_t* flag) {
+  __shared__ TailQueue tq;
+  __shared__ double res[kCTile];
+  __shared__ uint32_t T[1024];
+  build_sobol_tables(sc.sv, T);
+  __syncthreads();
+  ppf_compacted<D>(nrows, [&](int64_t i) { return (double)sobol_point(T, sc.shift, (uint64_t)(row0 + i)) * sc.scale; },
+                   prm, pt, out, flag, tq, res);
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_sobol_ppf(SobolCol sc, int64_t row0, int64_t nrows, Params prm,
+                                                             PoissonTable pt, double* __restrict__ out, int32_t* flag) {
+  __shared__ uint32_t T[1024];
+  build_sobol_tables(sc.sv, T);
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
+    const double q = (double)sobol_point(T, sc.shift, (uint64_t)(row0 + i)) * sc.scale;
+    const double x = ppf_one<D>(q, prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
+    out[i] = x;
+    flag_nonfinite(flag, !isfinite(x));
   }
 }
 
@@ -866,5 +920,55 @@ extern "C" int pbh_fill_sobol(const uint32_t* sv_host, const uint32_t* shift_hos
                        q + (int64_t)c0 * ldq, ldq);
     PBH_CHECK_LAUNCH();
   }
+  return PBH_OK;
+}
+
+extern "C" int pbh_sobol_ppf(const uint32_t* sv_host, const uint32_t* shift_host, int d, int bits, int64_t row0,
+                             int64_t nrows, int col, int dist, const pbh_param* params, int nparams, double* out,
+                             int32_t* nonfinite_flag, void* stream) {
+  PBH_REQUIRE(sv_host && shift_host && out, "pbh_sobol_ppf: null pointer");
+  PBH_REQUIRE(bits >= 1 && bits <= 32, "pbh_sobol_ppf: bits must be in [1, 32]");
+  PBH_REQUIRE(col >= 0 && col < d, "pbh_sobol_ppf: bad column");
+  PBH_REQUIRE(row0 >= 0 && nrows >= 0 && (row0 + nrows) <= (int64_t)1 << bits, "pbh_sobol_ppf: rows exceed 2^bits");
+  if (nrows == 0) return PBH_OK;
+  if (dist < 0 || dist >= PBH_DIST_BETA) {
+    set_error("pbh_sobol_ppf: distribution %d has no fused Sobol' kernel (use pbh_fill_sobol + pbh_ppf)", dist);
+    return PBH_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = as_stream(stream);
+  SobolCol sc = {};
+  for (int b = 0; b < bits; ++b) sc.sv[b] = sv_host[(int64_t)col * bits + b];
+  sc.shift = shift_host[col];
+  sc.scale = 1.0 / (double)((uint64_t)1 << bits);
+  Params prm;
+  PoissonTable pt;
+  double* table = nullptr;
+  int st = with_params(dist, params, nparams, prm, pt, &table, s);
+  if (st != PBH_OK) return st;
+  dim3 g(ppf_grid(nrows)), b(kBlock);
+  switch (dist) {
+#define PBH_CASE(D)                                                                                               \
+  case D:                                                                                                         \
+    if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                                    \
+      PBH_TIMED(kKPpf, s,                                                                                         \
+                hipLaunchKernelGGL(k_sobol_ppf_c<D>, dim3(compact_grid(nrows)), b, 0, s, sc, row0, nrows, prm, pt, \
+                                   out, nonfinite_flag));                                                         \
+    else                                                                                                          \
+      PBH_TIMED(kKPpf, s,                                                                                         \
+                hipLaunchKernelGGL(k_sobol_ppf<D>, g, b, 0, s, sc, row0, nrows, prm, pt, out, nonfinite_flag));  \
+    break;
+    PBH_CASE(PBH_DIST_NORM)
+    PBH_CASE(PBH_DIST_UNIFORM)
+    PBH_CASE(PBH_DIST_EXPON)
+    PBH_CASE(PBH_DIST_LOGNORM)
+    PBH_CASE(PBH_DIST_TRIANG)
+    PBH_CASE(PBH_DIST_GAMMA)
+    PBH_CASE(PBH_DIST_POISSON)
+#undef PBH_CASE
+    default:
+      break;
+  }
+  PBH_CHECK_LAUNCH();
+  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));
   return PBH_OK;
 }

@@ -646,7 +646,15 @@ class Distribution(AbstractDistribution):
             _, seed, n_total, col, row0 = column
             _lib.check(lib.pbh_lhs_ppf(seed, n_total, row0, n, col, dist, arr, len(params), out.data_ptr(),
                                        ev.flag_ptr(self), device.stream()), f"{self}")
+        elif column[0] == "sobol" and dist < _lib.DIST_IDS["beta"]:  # generator fused into the ppf kernel
+            _, src, col = column
+            sv = np.ascontiguousarray(src.sv, dtype=np.uint32)
+            sh = np.ascontiguousarray(src.shift, dtype=np.uint32)
+            _lib.check(lib.pbh_sobol_ppf(_lib.np_ptr(sv), _lib.np_ptr(sh), src.d, src.bits, src.row0, n, col, dist, arr,
+                                         len(params), out.data_ptr(), ev.flag_ptr(self), device.stream()), f"{self}")
         else:
+            if column[0] == "sobol":
+                column = ("vector", column[1].materialize(column[2]), 1)
             _, q, stride = column
             _lib.check(lib.pbh_ppf(dist, q.data_ptr(), stride, n, arr, len(params), out.data_ptr(),
                                    ev.flag_ptr(self), device.stream()), f"{self}")
@@ -694,6 +702,8 @@ class _TableDistribution(AbstractDistribution):
             _lib.check(_lib.load().pbh_fill_lhs(seed, n_total, row0, n, col, 1, q.data_ptr(), max(n, 1),
                                                 device.stream()), "pbh_fill_lhs")
             return q, 1
+        if column[0] == "sobol":
+            return column[1].materialize(column[2]), 1
         _, q, stride = column
         return q, stride
 

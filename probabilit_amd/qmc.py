@@ -336,13 +336,18 @@ class SobolSource(QuantileSource):
         self.sv, self.shift = sobol_setup(d, rng, bits)
 
     def column(self, c):
+        """A lazy column: inverse-CDF nodes fuse the point generation into their kernel
+        (pbh_sobol_ppf); other consumers call materialize(c)."""
+        return ("sobol", self, c)
+
+    def materialize(self, c):
         out = device.empty(self.rows)
         lib = _lib.load()
         sv = np.ascontiguousarray(self.sv, dtype=np.uint32)
         sh = np.ascontiguousarray(self.shift, dtype=np.uint32)
         _lib.check(lib.pbh_fill_sobol(_lib.np_ptr(sv), _lib.np_ptr(sh), self.d, self.bits, self.row0, self.rows, c,
                                       1, out.data_ptr(), max(self.rows, 1), device.stream()), "pbh_fill_sobol")
-        return ("vector", out, 1)
+        return out
 
 
 def first_primes(d):

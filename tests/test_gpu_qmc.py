@@ -65,3 +65,47 @@ def test_native_uniform(gpu):
     assert np.all((q >= 0) & (q < 1))
     assert abs(q.mean() - 0.5) < 2e-3
     assert abs(np.corrcoef(q.T)[0, 1]) < 5e-3
+
+
+@pytest.mark.parametrize("name,kw", [("norm", {"loc": 1.11, "scale": 0.15}), ("lognorm", {"s": 0.5}),
+                                     ("gamma", {"a": 2.0}), ("triang", {"c": 0.3}), ("poisson", {"mu": 4.0}),
+                                     ("expon", {}), ("uniform", {"loc": -1.0, "scale": 3.0})])
+def test_sobol_fused_ppf_equals_fill_then_ppf(gpu, name, kw):
+    """pbh_sobol_ppf (the generator inside the inverse-CDF kernel, tail-compacted for norm /
+    lognorm) gives exactly pbh_fill_sobol followed by pbh_ppf, for any row range."""
+    import ctypes
+
+    from probabilit_amd import _lib, device, native, qmc
+    from probabilit_amd.modeling import _parse_scipy_args
+
+    d, bits, col = 6, 30, 4
+    sv, shift = qmc.sobol_setup(d, 5)
+    svc, shc = np.ascontiguousarray(sv, np.uint32), np.ascontiguousarray(shift, np.uint32)
+    for row0, n in [(0, 100_000), (12_345, 77_777)]:
+        q = native.fill_sobol(sv, shift, n, row0=row0)[:, col]
+        ref = native.ppf(name, q, **kw)
+        params = [float(p) for p in _parse_scipy_args(name, (), kw)]
+        arr = (_lib.Param * len(params))(*[_lib.Param(None, p) for p in params])
+        out = device.empty(n)
+        _lib.check(_lib.load().pbh_sobol_ppf(_lib.np_ptr(svc), _lib.np_ptr(shc), d, bits, row0, n, col,
+                                             _lib.DIST_IDS[name], arr, len(params), out.data_ptr(), None,
+                                             device.stream()), "pbh_sobol_ppf")
+        np.testing.assert_array_equal(device.to_host(out), ref)
+
+
+def test_sobol_dag_matches_materialised_quantiles(gpu):
+    """A Sobol DAG (fused columns) equals sample_from_quantiles on the materialised points."""
+    from probabilit_amd import native, qmc
+    from probabilit_amd.modeling import Distribution
+
+    def model():
+        a = Distribution("norm", loc=1.0, scale=2.0)
+        b = Distribution("gamma", a=2.0)
+        c = Distribution("beta", a=2.0, b=3.0)  # no fused kernel: materialised column
+        return a * b + c
+
+    n = 4096
+    y = model().sample(n, random_state=3, method="sobol")
+    sv, shift = qmc.sobol_setup(3, 3)
+    Q = native.fill_sobol(sv, shift, n)
+    np.testing.assert_array_equal(y, model().sample_from_quantiles(Q))
