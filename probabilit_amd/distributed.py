@@ -187,17 +187,27 @@ def _all_reduce(t, group, world, op="sum"):
     return t
 
 
-def _all_to_all(out, inp, out_splits, in_splits, group, world):
+class _Done:
+    def wait(self):
+        return None
+
+
+def _all_to_all(out, inp, out_splits, in_splits, group, world, async_op=False):
+    """all_to_all_single; with async_op the returned handle's wait() orders the caller's stream
+    after the exchange (RCCL runs it on its own stream meanwhile).  gloo (host staging) and
+    world == 1 complete before returning."""
     import torch.distributed as dist
 
     if world == 1:
         out.copy_(inp)
-        return out
+        return _Done() if async_op else out
     if _staged(group) and out.device.type != "cpu":
         h = out.cpu()
         dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
         out.copy_(h)
-        return out
+        return _Done() if async_op else out
+    if async_op:
+        return dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=True)
     dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
     return out
 
@@ -261,34 +271,65 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
     # ---- step 3: correlated scores of the local rows ------------------------------------
     phases.apply(S, L, np.asarray(P, dtype=np.float64))
 
-    # ---- step 4: column owners rank their full columns ----------------------------------
-    k_own = cb[rank + 1] - cb[rank]
-    send = S.reshape(-1)
-    in_splits = [(cb[o + 1] - cb[o]) * nrows for o in range(world)]
-    out_splits = [k_own * (rb[s + 1] - rb[s]) for s in range(world)]
-    recv = phases.empty(sum(out_splits))
-    _all_to_all(recv, send, out_splits, in_splits, group, world)
-    del S, send
-    pieces, off = [], 0
-    for s in range(world):
-        ns = rb[s + 1] - rb[s]
-        pieces.append(recv[off:off + k_own * ns].view(k_own, ns))
-        off += k_own * ns
-    cs_own = torch.cat(pieces, dim=1) if k_own else None
-    del recv, pieces
-    Y_own = phases.empty((k_own, n))
-    for j in range(k_own):
-        col = columns[cb[rank] + j]
-        sorted_full = phases.sorted_segment(col, n, 0, n, flags[cb[rank] + j:cb[rank] + j + 1])
-        phases.reorder(cs_own[j].contiguous(), sorted_full, Y_own[j])
-    del cs_own
-
-    # ---- back to row shards ---------------------------------------------------------------
-    send = torch.cat([Y_own[:, rb[s]:rb[s + 1]].reshape(-1) for s in range(world)])
-    in_splits = [k_own * (rb[s + 1] - rb[s]) for s in range(world)]
-    out_splits = [(cb[o + 1] - cb[o]) * nrows for o in range(world)]
+    # ---- step 4: column owners rank their full columns, pipelined -----------------------------
+    # Exchange i (i < max k_own) moves the i-th owned column of every owner: its rows from all
+    # ranks to the owner (all-to-all), the owner ranks it, and its result rows go back (a second
+    # all-to-all).  On RCCL the exchanges run asynchronously on the communicator's stream, so
+    # column i + 1's CS arrives and column i - 1's Y leaves while column i is being ranked.
+    own = [cb[o + 1] - cb[o] for o in range(world)]
+    k_own, m = own[rank], max(own)
     Y = phases.empty((K, nrows))
-    _all_to_all(Y.view(-1), send, out_splits, in_splits, group, world)
+    rows_of = [rb[s + 1] - rb[s] for s in range(world)]
+
+    def cs_exchange(i):
+        owners = [o for o in range(world) if i < own[o]]
+        send = torch.cat([S[cb[o] + i] for o in owners]) if owners else phases.empty(0)
+        in_splits = [nrows if i < own[o] else 0 for o in range(world)]
+        out_splits = [rows_of[s] if i < k_own else 0 for s in range(world)]
+        recv = phases.empty(sum(out_splits))
+        work = _all_to_all(recv, send, out_splits, in_splits, group, world, async_op=True)
+        return recv, work, send
+
+    def y_exchange(i, y_col):
+        in_splits = [rows_of[s] if i < k_own else 0 for s in range(world)]
+        out_splits = [nrows if i < own[o] else 0 for o in range(world)]
+        send = y_col if i < k_own else phases.empty(0)
+        recv = phases.empty(sum(out_splits))
+        work = _all_to_all(recv, send, out_splits, in_splits, group, world, async_op=True)
+        return recv, work, send
+
+    def y_scatter(i, recv):
+        off = 0
+        for o in range(world):
+            if i < own[o]:
+                Y[cb[o] + i].copy_(recv[off:off + nrows])
+                off += nrows
+
+    pending_cs = cs_exchange(0) if m else None
+    pending_y = []
+    for i in range(m):
+        cur = pending_cs  # (recv, work, send): the send buffer stays referenced until the wait
+        pending_cs = cs_exchange(i + 1) if i + 1 < m else None
+        recv_cs, work_cs, _ = cur
+        work_cs.wait()
+        del cur
+        y_col = None
+        if i < k_own:
+            col = columns[cb[rank] + i]
+            sorted_full = phases.sorted_segment(col, n, 0, n, flags[cb[rank] + i:cb[rank] + i + 1])
+            y_col = phases.empty(n)
+            phases.reorder(recv_cs, sorted_full, y_col)
+            del sorted_full
+        del recv_cs
+        pending_y.append((i,) + y_exchange(i, y_col))
+        while len(pending_y) > 2:  # bound the buffers in flight
+            j, recv_y, work_y, _ = pending_y.pop(0)
+            work_y.wait()
+            y_scatter(j, recv_y)
+    for j, recv_y, work_y, _ in pending_y:
+        work_y.wait()
+        y_scatter(j, recv_y)
+    del S
     _all_reduce(flags, group, world)
     return Y
 

@@ -1,5 +1,5 @@
 """Row-sharded Iman-Conover (probabilit_amd/distributed.py) under the gloo
-backend with world size 1 and 2 on CPU: the exchange logic (run-head all-gather, sum and
+backend with world sizes 1 to 4 on CPU (uneven row shards, ranks owning 2, 1 or no column): the exchange logic (run-head all-gather, sum and
 Gram all-reduces, the two all-to-alls) with numpy phases (tests/dist_cpu_phases.py), against
 the oracle's single-process ImanConover on the same LHS design.  The GPU phases of the same
 orchestrator are checked in test_gpu_distributed.py."""
@@ -55,7 +55,7 @@ def _worker(rank, world, port, case, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_sharded_ic_matches_single_process_oracle(world, case):
     from dist_cpu_phases import column_values, design
