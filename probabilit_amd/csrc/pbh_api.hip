@@ -73,7 +73,7 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* P = c.take((size_t)k * k * 8);
   void* flag = c.take(256);
   void* tmp = c.take((size_t)n * 8);
-  void* counts = c.take(256);
+  void* counts = c.take(16 * 128);  // ties, inversions per generated column (k <= 128)
   void* hws = c.take(run_heads_ws_bytes(n));
   void* codes = c.take((size_t)n * k * 4);
   void* colpart = c.take((size_t)k * perm_scores_blocks(n) * 8);
@@ -185,6 +185,21 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   // ---- step 1: van der Waerden scores of every column (+ the sorted column for step 4)
   PBH_CHECK_HIP(hipMemsetAsync(L.flag, 0, sizeof(int32_t), s));
   bool all_generated = true;  // every column's scores came from perm_scores (with partial sums)
+  // Generated columns: every sorted column first, with its tie / inversion counts, then one
+  // readback for all of them (instead of a stream sync per column).
+  std::vector<unsigned long long> cnt_host(2 * (size_t)k, 0);
+  if (a->columns) {
+    for (int c = 0; c < k; ++c) {
+      const pbh_ic_column& g = a->columns[c];
+      pbh_param prm[3];
+      for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
+      st = lhs_sorted_ppf(g.seed, n, 0, n, g.lhs_col, g.dist, prm, g.nparams, L.sorted_x + (int64_t)c * n,
+                          g.nonfinite_flag, s, L.counts + 2 * c);
+      if (st) return st;
+    }
+    PBH_CHECK_HIP(hipMemcpyAsync(cnt_host.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+  }
   for (int c = 0; c < k; ++c) {
     double* S_c = L.S + (int64_t)c * n;
     double* sx_c = L.sorted_x + (int64_t)c * n;
@@ -195,11 +210,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       const pbh_ic_column& g = a->columns[c];
       pbh_param prm[3];
       for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
-      st = lhs_sorted_ppf(g.seed, n, 0, n, g.lhs_col, g.dist, prm, g.nparams, sx_c, g.nonfinite_flag, s, L.counts);
-      if (st) return st;
-      unsigned long long cnt[2];
-      PBH_CHECK_HIP(hipMemcpyAsync(cnt, L.counts, sizeof(cnt), hipMemcpyDeviceToHost, s));
-      PBH_CHECK_HIP(hipStreamSynchronize(s));
+      const unsigned long long* cnt = cnt_host.data() + 2 * c;
       if (cnt[1] == 0) {
         uint32_t* heads = nullptr;
         int64_t nheads = 0;
@@ -268,11 +279,27 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     PBH_CHECK_HIP(hipMemcpyAsync(a->cscores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
 
   // ---- step 4: Y[:, c] = sort(X[:, c])[rankdata(CS[:, c]).astype(int) - 1]
+  // The code histograms of all columns up front, one readback for the bucket-path decisions.
+  uint32_t* hists = nullptr;
+  std::vector<uint32_t> hists_host;
+  if (code_buckets_enabled(n)) {
+    PBH_CHECK_HIP(hipMallocAsync((void**)&hists, (size_t)k * 1024 * 4, s));
+    for (int c = 0; c < k; ++c) {
+      st = code_hist(L.codes + (int64_t)c * n, n, hists + (size_t)c * 1024, s);
+      if (st) return st;
+    }
+    hists_host.resize((size_t)k * 1024);
+    PBH_CHECK_HIP(hipMemcpyAsync(hists_host.data(), hists, (size_t)k * 1024 * 4, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+  }
   for (int c = 0; c < k; ++c) {
+    const uint32_t* hc = hists ? hists + (size_t)c * 1024 : nullptr;
+    const int flat = hists ? (code_hist_flat(hists_host.data() + (size_t)c * 1024, n) ? 1 : 0) : 1;
     st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
-                        a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n);
+                        a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n, hc, flat);
     if (st) return st;
   }
+  if (hists) PBH_CHECK_HIP(hipFreeAsync(hists, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // host vectors above were sources of async copies
   return PBH_OK;
 }

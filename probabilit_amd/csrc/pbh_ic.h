@@ -116,7 +116,10 @@ size_t reorder_ws_bytes(int64_t n);
 int reorder_carve(void* ws, int64_t n, ReorderWs& w, hipStream_t s);
 // y[r * y_rs] = sorted_src[rank(cs[r]) - 1]; idx[r] = rank - 1 when idx != NULL.
 // codes (optional): code_of(cs) already computed (by the step-3 kernel); not modified.
+// code_hist (optional): the codes' byte histograms on the device with the host's decision
+// `code_flat` (code_hist_flat), so that the bucket path needs no sync of its own.
 int reorder_column(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx,
-                   ReorderWs& w, hipStream_t s, const uint32_t* codes = nullptr);
+                   ReorderWs& w, hipStream_t s, const uint32_t* codes = nullptr, const uint32_t* code_hist = nullptr,
+                   int code_flat = 1);
 
 }  // namespace pbh

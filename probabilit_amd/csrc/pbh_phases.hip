@@ -107,7 +107,7 @@ int reorder_carve(void* ws, int64_t n, ReorderWs& w, hipStream_t s) {
 // rank - 1 of row r is its sorted position, and Y is written by the LDS row placement; exact
 // ties use the tie-aware gather, and a run longer than kMaxRun the 64-bit sort.
 int reorder_column(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx,
-                   ReorderWs& w, hipStream_t s, const uint32_t* codes) {
+                   ReorderWs& w, hipStream_t s, const uint32_t* codes, const uint32_t* code_hist, int code_flat) {
   SortBuffers& sb = w.sb;
   RankOut out = {};
   out.sorted_src = sorted_src;
@@ -123,7 +123,8 @@ int reorder_column(const double* cs, int64_t n, const double* sorted_src, double
   PBH_CHECK_HIP(hipMemsetAsync(w.flags, 0, sizeof(int32_t), s));
   buf = -1;
   if (code_buckets_enabled(n)) {  // 2 one-sweep passes + per-bucket LDS finish (runs included)
-    st = code_sort_buckets(sb, n, codes ? codes : (const uint32_t*)sb.keys[0], cs, w.eqprev, w.flags, s, &buf);
+    st = code_sort_buckets(sb, n, codes ? codes : (const uint32_t*)sb.keys[0], cs, w.eqprev, w.flags, s, &buf,
+                           codes ? code_hist : nullptr, code_flat);
     if (st) return st;
   }
   if (buf < 0) {  // four one-sweep passes + the run fix-up

@@ -50,9 +50,14 @@ int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, co
 // Step 4's code sort for 2^22 <= n <= 2^27 (see k_code_buckets): codes -> rows in final rank
 // order in b.vals[*out_buf] plus eqprev / flags exactly as resolve_code_runs leaves them (flags
 // bit 0: fall back to 64-bit keys; bit 1: exact ties).  flags must be zeroed by the caller.
+// hist_dev (optional): the four byte histograms of `codes` already on the device (code_hist),
+// with `flat` the host's code_hist_flat decision for them; without it the function computes
+// both (one stream sync).
 bool code_buckets_enabled(int64_t n);
+bool code_hist_flat(const uint32_t* hist4_host, int64_t n);
+int code_hist(const uint32_t* codes, int64_t n, uint32_t* hist4, hipStream_t s);
 int code_sort_buckets(SortBuffers& b, int64_t n, const uint32_t* codes, const double* x, uint8_t* eqprev,
-                      int32_t* flags, hipStream_t s, int* out_buf);
+                      int32_t* flags, hipStream_t s, int* out_buf, const uint32_t* hist_dev = nullptr, int flat = 1);
 
 // Y[rows[p] * y_rs] = v[p] for a permutation `rows` of [0, n): the inverse-permutation write
 // of Iman-Conover step 4 (correlation.py:423) without random 8-byte stores.  LSD bucket passes

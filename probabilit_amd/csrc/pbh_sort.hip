@@ -759,29 +759,44 @@ bool code_buckets_enabled(int64_t n) {
   return n >= ((int64_t)1 << 22) && n <= (int64_t)110000000;  // mean bucket <= ~1700 of the 2048 cap
 }
 
+bool code_hist_flat(const uint32_t* hist4, int64_t n) {
+  const char* force = getenv("PBH_STEP4");
+  if (force && strcmp(force, "buckets") == 0) return true;  // tests: exercise the kernel and its safety net
+  uint32_t top_max = 0;
+  for (int d = 0; d < 256; ++d) top_max = hist4[3 * 256 + d] > top_max ? hist4[3 * 256 + d] : top_max;
+  return (double)top_max <= 1.5 * (double)n / 256.0 + 64.0;
+}
+
+int code_hist(const uint32_t* codes, int64_t n, uint32_t* hist4, hipStream_t s) {
+  PBH_CHECK_HIP(hipMemsetAsync(hist4, 0, 4 * 256 * 4, s));
+  PBH_TIMED(kKSortDigitHist32, s,
+            hipLaunchKernelGGL(k_digit_hist<uint32_t>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, codes, n, hist4));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
 int code_sort_buckets(SortBuffers& b, int64_t n, const uint32_t* codes, const double* x, uint8_t* eqprev,
-                      int32_t* flags, hipStream_t s, int* out_buf) {
+                      int32_t* flags, hipStream_t s, int* out_buf, const uint32_t* hist_dev, int flat) {
   PBH_REQUIRE(n >= 2 && n < ((int64_t)1 << 32), "code_sort_buckets: n out of range");
   const int64_t nt = sort_tiles(n);
   uint32_t* keys[2] = {(uint32_t*)b.keys[0], (uint32_t*)b.keys[1]};
-  PBH_CHECK_HIP(hipMemsetAsync(b.hist, 0, 4 * 256 * 4, s));
-  PBH_TIMED(kKSortDigitHist32, s,
-            hipLaunchKernelGGL(k_digit_hist<uint32_t>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, codes, n, b.hist));
-  hipLaunchKernelGGL(k_digit_bases, dim3(4), dim3(256), 0, s, b.hist, b.bases);
-  PBH_CHECK_LAUNCH();
-  // A column whose top-byte histogram is far from flat (a mixture with discrete spikes, e.g. a
-  // poisson-dominated correlated score) would overflow top-16 buckets: leave it to the four
-  // passes (*out_buf = -1).  The kernel's overflow flag stays the safety net.
-  PBH_CHECK_HIP(hipMemcpyAsync(b.hist_host, b.hist, 4 * 256 * 4, hipMemcpyDeviceToHost, s));
-  PBH_CHECK_HIP(hipStreamSynchronize(s));
-  uint32_t top_max = 0;
-  for (int d = 0; d < 256; ++d) top_max = b.hist_host[3 * 256 + d] > top_max ? b.hist_host[3 * 256 + d] : top_max;
-  const char* force = getenv("PBH_STEP4");
-  const bool forced = force && strcmp(force, "buckets") == 0;  // tests: exercise the kernel and its safety net
-  if (!forced && (double)top_max > 1.5 * (double)n / 256.0 + 64.0) {
+  if (!hist_dev) {
+    int st = code_hist(codes, n, b.hist, s);
+    if (st) return st;
+    hist_dev = b.hist;
+    // A column whose top-byte histogram is far from flat (a mixture with discrete spikes, e.g.
+    // a poisson-dominated correlated score) would overflow top-16 buckets: leave it to the four
+    // passes (*out_buf = -1).  The kernel's overflow flag stays the safety net.
+    PBH_CHECK_HIP(hipMemcpyAsync(b.hist_host, b.hist, 4 * 256 * 4, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+    flat = code_hist_flat(b.hist_host, n) ? 1 : 0;
+  }
+  if (!flat) {
     *out_buf = -1;
     return PBH_OK;
   }
+  hipLaunchKernelGGL(k_digit_bases, dim3(4), dim3(256), 0, s, hist_dev, b.bases);
+  PBH_CHECK_LAUNCH();
   PBH_CHECK_HIP(hipMemsetAsync(b.status + nt * 256, 0, 256, s));
   int cur = 0;
   for (int ip = 0; ip < 2; ++ip) {
