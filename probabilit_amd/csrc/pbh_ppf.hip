@@ -273,11 +273,8 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_sorted_ppf(uint64_t seed
                                                            unsigned long long* counts) {
   __shared__ unsigned long long sh[2][kBlock / 64];
   Philox ph(seed);
-  FeistelPerm fp(ph, (uint64_t)n, col);
-  auto value = [&](int64_t t) {
-    const uint64_t row = fp.inverse((uint64_t)t);
-    const double u = ph.uniform(row, col, kPurposeLhsU);
-    const double q = ((double)(t + 1) - u) / (double)n;
+  auto value = [&](int64_t t) {  // stratum t's point: no permutation needed (lhs_sorted_quantile)
+    const double q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
     return ppf_one<D>(q, prm.val[0], prm.val[1], prm.val[2], pt);
   };
   const int lane = threadIdx.x & 63;

@@ -167,11 +167,17 @@ struct FeistelPerm {
 };
 
 // q = (perm + 1 - u) / n: scipy's `(perms - samples) / n` with perms in 1..n
-// (scipy:stats/_qmc.py LatinHypercube._random_lhs).
+// (scipy:stats/_qmc.py LatinHypercube._random_lhs).  The jitter u is keyed by the stratum
+// perm (not the row): the point of row r is stratum pi(r) with that stratum's jitter, which
+// is as random as a per-row jitter (pi is a random bijection) and lets the stratum-ordered
+// (sorted) column be generated without evaluating pi^-1 at all (lhs_sorted_quantile).
+PBH_HD inline double lhs_sorted_quantile(const Philox& ph, uint64_t t, uint32_t col, uint64_t n) {
+  const double u = ph.uniform(t, col, kPurposeLhsU);
+  return ((double)(t + 1) - u) / (double)n;
+}
+
 PBH_HD inline double lhs_quantile(const Philox& ph, const FeistelPerm& fp, uint64_t row, uint32_t col) {
-  uint64_t p = fp(row);
-  double u = ph.uniform(row, col, kPurposeLhsU);
-  return ((double)(p + 1) - u) / (double)fp.n;
+  return lhs_sorted_quantile(ph, fp(row), col, fp.n);
 }
 
 }  // namespace pbh
