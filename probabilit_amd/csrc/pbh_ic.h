@@ -50,7 +50,7 @@ struct CodeMap {
   const uint32_t* base;  // m + 1 strictly increasing code bases
   const double* scale;   // m slopes (codes per unit x)
 };
-constexpr int kCodeSegments = 8192;
+constexpr int kCodeSegments = 1024;  // 12 KB: small enough to sit in the LDS of the step-3 kernel
 __device__ __forceinline__ uint32_t code_of(double x, const CodeMap& c) {
   double u = (x - c.x0) * c.inv_w;
   if (!(u >= 0.0)) return 0u;

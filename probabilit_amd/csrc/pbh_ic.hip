@@ -528,8 +528,17 @@ __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int6
                                                    const double* __restrict__ M, uint32_t* __restrict__ codes,
                                                    int64_t ldc, CodeMap cm) {
   __shared__ double tile[4][AM_ROWS * 33];
+  __shared__ uint32_t cbase[kCodeSegments + 1];  // the code map in LDS: two lookups per code
+  __shared__ double cscale[kCodeSegments];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double* tl = tile[w];
+  if (codes) {
+    for (int j = threadIdx.x; j <= cm.m; j += 256) cbase[j] = cm.base[j];
+    for (int j = threadIdx.x; j < cm.m; j += 256) cscale[j] = cm.scale[j];
+    cm.base = cbase;
+    cm.scale = cscale;
+  }
+  __syncthreads();
   const int q = lane >> 4, m16 = lane & 15;
   double b[8][2];  // B operands: M[4 s + q][16 J + m16]
 #pragma unroll
