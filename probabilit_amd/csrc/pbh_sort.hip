@@ -583,6 +583,37 @@ __device__ __forceinline__ void wave_count_pass(uint32_t (&k)[kWBItems], uint32_
   wave_sync();
 }
 
+// Stable value order of the run [p, p + L) of equal codes (L <= R), with the exact-tie flags:
+// member q lands after every member of smaller value and every earlier member of equal value.
+template <int R>
+__device__ __forceinline__ bool resolve_run(WaveBucket& B, int p, int L, const double* __restrict__ x) {
+  uint32_t rr[R];
+  double v[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    rr[j] = j < L ? B.row[p + j] : 0u;
+    v[j] = j < L ? x[rr[j]] : 0.0;
+  }
+  bool any_tie = false;
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    int pos = 0;
+    bool tie = false;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const bool other = j < L && j != q;
+      pos += (other && (v[j] < v[q] || (v[j] == v[q] && j < q))) ? 1 : 0;
+      tie |= other && v[j] == v[q] && j < q;
+    }
+    if (q < L) {
+      B.row[p + pos] = rr[q];
+      B.eq[p + pos] = tie ? 1 : 0;
+      any_tie |= tie;
+    }
+  }
+  return any_tie;
+}
+
 constexpr int kCBWaves = 2;  // waves (buckets) per block: ~31 KB of LDS
 
 __global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* __restrict__ keys,
@@ -662,29 +693,10 @@ __global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* 
       atomicOr(flags, 1);
       continue;
     }
-    uint32_t rr[kBucketMaxRun];
-    double v[kBucketMaxRun];
-#pragma unroll
-    for (int j = 0; j < kBucketMaxRun; ++j) {
-      rr[j] = j < L ? B.row[p + j] : 0u;
-      v[j] = j < L ? x[rr[j]] : 0.0;
-    }
-#pragma unroll
-    for (int q = 0; q < kBucketMaxRun; ++q) {
-      int pos = 0;
-      bool tie = false;
-#pragma unroll
-      for (int j = 0; j < kBucketMaxRun; ++j) {
-        const bool other = j < L && j != q;
-        pos += (other && (v[j] < v[q] || (v[j] == v[q] && j < q))) ? 1 : 0;
-        tie |= other && v[j] == v[q] && j < q;
-      }
-      if (q < L) {
-        B.row[p + pos] = rr[q];
-        B.eq[p + pos] = tie ? 1 : 0;
-        any_tie |= tie;
-      }
-    }
+    if (L <= 4)  // nearly every run: a 4-wide register version; 16-wide only when some lane needs it
+      any_tie |= resolve_run<4>(B, p, L, x);
+    else
+      any_tie |= resolve_run<kBucketMaxRun>(B, p, L, x);
   }
   if (__ballot(any_tie) && lane == 0) atomicOr(flags, 2);
   wave_sync();
