@@ -388,6 +388,17 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
   for (int64_t base = (int64_t)blockIdx.x * kCTile; base < nrows; base += (int64_t)gridDim.x * kCTile) {
     if (threadIdx.x == 0) tq.count = 0;
     __syncthreads();
+    // the strata of all kCIpt items first: independent Feistel chains the compiler interleaves
+    // (one straight-line block; the rare cycle walks are finished afterwards)
+    uint64_t tt[kCIpt];
+#pragma unroll
+    for (int j = 0; j < kCIpt; ++j) {
+      const int64_t i = base + j * kBlock + threadIdx.x;
+      tt[j] = n > 1 && i < nrows ? fp.round_trip((uint64_t)(row0 + i)) : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kCIpt; ++j)
+      while (tt[j] >= (uint64_t)n) tt[j] = fp.round_trip(tt[j]);
 #pragma unroll 2
     for (int j = 0; j < kCIpt; ++j) {
       const int p = j * kBlock + threadIdx.x;
@@ -395,7 +406,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
       const bool valid = i < nrows;
       double y = 0.5;
       if (valid) {
-        const uint64_t t = fp((uint64_t)(row0 + i));
+        const uint64_t t = tt[j];
         const double rank = heads ? run_average_rank(heads, nheads, n, (int64_t)t) : (double)(t + 1);
         y = rank / np1;
       }
