@@ -177,7 +177,8 @@ def main():
         cpu = cpu_baseline(args.cpu_n, d)
 
     if rank == 0:
-        line = {"metric": "Msamples/s (N x d draws), LHS + ImanConover d=32", "value": round(value, 2),
+        line = {"metric": "Msamples/s (N\u00d7d draws) + achieved HBM GB/s, LHS+ImanConover d=32",  # BASELINE.json
+                "value": round(value, 2),
                 "unit": "Msamples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
                 "scaling": "strong" if world > 1 else "weak",
