@@ -272,7 +272,7 @@ __global__ void k_means(const double* __restrict__ partial, int nb, int k, doubl
 // ---------------------------------------------------------------- centered Gram
 constexpr int GT = 32;     // Gram tile (columns)
 constexpr int GROWS = 64;  // rows staged per step
-constexpr int kGramBlocksMax = 1024;
+constexpr int kGramBlocksMax = 768;  // 3 blocks per CU: the register prefetch of k_gram_mfma allows 3 waves per SIMD
 
 __global__ __launch_bounds__(256) void k_gram(const double* __restrict__ S, int64_t n, int k, int64_t ld,
                                              const double* __restrict__ means, int64_t chunk,
@@ -386,6 +386,20 @@ __global__ __launch_bounds__(256) void k_gram_mfma(const double* __restrict__ S,
 #pragma unroll
   for (int j = 0; j < 8; ++j) mu[j] = (w * 8 + j) < k ? means[w * 8 + j] : 0.0;
   f64x4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c11 = c00;
+  // the next chunk's loads are issued before this chunk's MFMAs (register prefetch)
+  double pre[GM_ROWS / 64][8];
+  auto load = [&](int64_t rb) {
+#pragma unroll
+    for (int h = 0; h < GM_ROWS / 64; ++h) {
+      const int64_t r = rb + h * 64 + lane;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = w * 8 + j;
+        pre[h][j] = (c < k && r < r1) ? S[(int64_t)c * ld + r] : 0.0;
+      }
+    }
+  };
+  if (r0 < r1) load(r0);
   for (int64_t rb = r0; rb < r1; rb += GM_ROWS) {
 #pragma unroll
     for (int h = 0; h < GM_ROWS / 64; ++h) {
@@ -394,10 +408,11 @@ __global__ __launch_bounds__(256) void k_gram_mfma(const double* __restrict__ S,
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int c = w * 8 + j;
-        smem[row * 33 + c] = (c < k && r < r1) ? S[(int64_t)c * ld + r] - mu[j] : 0.0;
+        smem[row * 33 + c] = (c < k && r < r1) ? pre[h][j] - mu[j] : 0.0;
       }
     }
     __syncthreads();
+    if (rb + GM_ROWS < r1) load(rb + GM_ROWS);
 #pragma unroll
     for (int qi = 0; qi < GM_ROWS / 16; ++qi) {
       const int row = (w + 4 * qi) * 4 + (lane >> 4);
