@@ -17,6 +17,7 @@ Prints ONE JSON line on rank 0.
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -65,7 +66,11 @@ def pmc_traffic(kernel):
     2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_*.json")), key=os.path.getmtime)
+    def tag(path):  # newest = highest pass number in pmc_traffic_r<NN>.json (mtimes do not survive a checkout)
+        m = re.search(r"_r(\d+)", os.path.basename(path))
+        return int(m.group(1)) if m else -1
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_*.json")), key=tag)
     if not files:
         return None, None
     ks = json.load(open(files[-1]))["kernels"]
