@@ -47,7 +47,7 @@ struct PoissonTable {
 // smallest k >= 0 with pdtr(k, mu) >= q, by stepping from a Cornish-Fisher guess.
 PBH_DI double poisson_search(double q, double mu) {
   if (mu == 0.0) return 0.0;
-  double z = sf::ndtri(q);
+  double z = sf::ndtri(q);  // a starting guess only (the search decides k)
   double g = floor(mu + sqrt(mu) * z + (z * z - 1.0) / 6.0);
   if (!(g >= 0.0)) g = 0.0;
   if (g > 9.0e15) g = 9.0e15;
@@ -74,7 +74,8 @@ PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
 }
 
 // ppf of one element for distribution D; p = (shape..., loc, scale) already resolved.
-// PART selects ndtri's branch for norm / lognorm (0: ndtri, 1: ndtri_centre, 2: ndtri_tail),
+// PART selects the inverse normal's branch for norm / lognorm (0: ndtri_fast, 1: its centre,
+// 2: its tail; PPND16, pbh_special.h),
 // for the compacted kernels that know which one an element takes.
 template <int D, int PART = 0>
 PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTable& pt) {
@@ -111,13 +112,13 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
     if (!(q > 0.0 && q < 1.0)) return kNaN;
     double x;
     if constexpr (D == PBH_DIST_NORM) {
-      x = PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q);
+      x = PART == 1 ? sf::ndtri_fast_centre(q) : PART == 2 ? sf::ndtri_fast_tail(q) : sf::ndtri_fast(q);
     } else if constexpr (D == PBH_DIST_UNIFORM) {
       x = q;
     } else if constexpr (D == PBH_DIST_EXPON) {
       x = -sf::log1p_(-q);  // scipy expon._ppf: -sc.log1p(-q), the Cephes log1p
     } else if constexpr (D == PBH_DIST_LOGNORM) {
-      x = exp(shape * (PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q)));
+      x = exp(shape * (PART == 1 ? sf::ndtri_fast_centre(q) : PART == 2 ? sf::ndtri_fast_tail(q) : sf::ndtri_fast(q)));
     } else if constexpr (D == PBH_DIST_TRIANG) {
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
@@ -129,13 +130,14 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
 }
 
 // ---------------------------------------------------------------- tail compaction
-// ndtri (norm / lognorm ppf, the van der Waerden scores) is one rational function for
-// min(q, 1 - q) > e^-2 (73% of uniform q) and an expensive tail (two logs, a sqrt, three
-// divisions) otherwise.  With q in random order nearly every wave holds both kinds, and a wave
+// The inverse normal CDF is one rational function in its centre and an expensive tail otherwise:
+// Cephes' ndtri (the van der Waerden scores) for min(q, 1 - q) > e^-2 (73% of uniform q, tail:
+// two logs, a sqrt, three divisions), PPND16 (norm / lognorm ppf outputs) for
+// |q - 0.5| <= 0.425 (85%, tail: one log, a sqrt, a division).  With q in random order nearly every wave holds both kinds, and a wave
 // executes every branch one of its lanes takes, so a plain grid-stride kernel pays centre + tail
 // for every element.  The compacted kernels give each thread kCIpt items of a block tile: centre
 // items are evaluated at once, tail items are queued in LDS (one LDS atomic per wave) and then
-// drained by all lanes of the block together, so the tail costs its 27% share.  Every value is
+// drained by all lanes of the block together, so the tail costs its 27% / 15% share.  Every value is
 // computed by the same inline function either way (bit-identical to the plain kernels); the
 // results pass through LDS so that the global stores stay coalesced.
 constexpr int kCIpt = 8;
@@ -163,6 +165,14 @@ PBH_DI void tail_push(TailQueue& tq, bool take, double a, int p) {
   }
 }
 
+bool stream_enabled() {  // PBH_PPF_STREAM=0 selects the plain grid-stride k_ppf (A/B measurements)
+  static const bool on = [] {
+    const char* e = getenv("PBH_PPF_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 unsigned compact_grid(int64_t n) { return grid_for(n, kCTile, 256 * 8); }
 
 bool compaction_enabled() {
@@ -181,13 +191,15 @@ PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm, const Pois
   for (int64_t base = (int64_t)blockIdx.x * kCTile; base < n; base += (int64_t)gridDim.x * kCTile) {
     if (threadIdx.x == 0) tq.count = 0;
     __syncthreads();
-#pragma unroll
+    // two items at a time: PPND16's 30 coefficients live in VGPR pairs (no 64-bit literal
+    // operands), and eight interleaved evaluations would spill under the 128-VGPR cap
+#pragma unroll 2
     for (int j = 0; j < kCIpt; ++j) {
       const int p = j * kBlock + threadIdx.x;
       const int64_t i = base + p;
       const bool valid = i < n;
       const double qv = valid ? qof(i) : 0.5;
-      const bool tail = valid && sf::ndtri_takes_tail(qv);
+      const bool tail = valid && sf::ndtri_fast_takes_tail(qv);
       if (valid && !tail) res[p] = ppf_one<D, 1>(qv, prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
       tail_push(tq, tail, qv, p);
     }
@@ -230,6 +242,48 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf(const double* __restrict
     out[i] = x;
     flag_nonfinite(flag, !isfinite(x));
   }
+}
+
+// Streaming form of k_ppf for the common case at the sample_from_quantiles boundary: a
+// contiguous, 16-byte-aligned q column and scalar parameters.  One wave's 64 lanes can keep
+// only one 512-B load in flight per grid-stride step in k_ppf, and with 16 waves per CU that is
+// ~2 MB in flight chip-wide, short of the ~12 MB that HBM latency x 6.3 TB/s needs.  Here every
+// lane issues kVU independent 16-byte loads (two draws each) before any arithmetic, and writes
+// back with non-temporal 16-byte stores (x is written once and not re-read by this launch).
+constexpr int kVU = 4;
+constexpr int kVTile = kBlock * kVU * 2;  // draws per block step
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+template <int D>
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_v(const double* __restrict__ q, int64_t n, Params prm,
+                                                  PoissonTable pt, double* __restrict__ out, int32_t* flag) {
+  const double p0 = prm.val[0], p1 = prm.val[1], p2 = prm.val[2];
+  const int64_t full = n / kVTile;
+  bool bad = false;
+  for (int64_t t = blockIdx.x; t < full; t += gridDim.x) {
+    const f64x2* qv = reinterpret_cast<const f64x2*>(q + t * kVTile);
+    f64x2* ov = reinterpret_cast<f64x2*>(out + t * kVTile);
+    f64x2 v[kVU];
+#pragma unroll
+    for (int u = 0; u < kVU; ++u) v[u] = __builtin_nontemporal_load(qv + u * kBlock + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < kVU; ++u) {
+      f64x2 r;
+      r.x = ppf_one<D>(v[u].x, p0, p1, p2, pt);
+      r.y = ppf_one<D>(v[u].y, p0, p1, p2, pt);
+      bad |= !isfinite(r.x) || !isfinite(r.y);
+      __builtin_nontemporal_store(r, ov + u * kBlock + threadIdx.x);
+    }
+  }
+  // ragged end (< kVTile draws): one block, scalar accesses
+  if (blockIdx.x == gridDim.x - 1) {
+    for (int64_t i = full * kVTile + threadIdx.x; i < n; i += kBlock) {
+      const double x = ppf_one<D>(q[i], p0, p1, p2, pt);
+      out[i] = x;
+      bad |= !isfinite(x);
+    }
+  }
+  flag_nonfinite(flag, bad);
 }
 
 template <int D>
@@ -624,12 +678,21 @@ unsigned ppf_grid(int64_t n) { return grid_for(n, kBlock, 256 * 16); }
 int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& prm, const PoissonTable& pt,
                double* out, int32_t* flag, hipStream_t s) {
   dim3 g(ppf_grid(n)), b(kBlock);
+  // k_ppf_v: contiguous 16-byte-aligned q and x, scalar parameters
+  // (uniform / triang / expon: the draws whose arithmetic is light enough for HBM to bound them;
+  // unrolling gamma's / poisson's code kVU x 2 times measured 1.7x / 1.25x slower)
+  const bool light = dist == PBH_DIST_UNIFORM || dist == PBH_DIST_TRIANG || dist == PBH_DIST_EXPON;
+  const bool streamable = light && qs == 1 && !prm.ptr[0] && !prm.ptr[1] && !prm.ptr[2] &&
+                          ((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0 && stream_enabled();
+  dim3 gv(grid_for(n, kVTile, 256 * 8));
   switch (dist) {
 #define PBH_CASE(D) \
   case D:           \
     if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
       PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_c<D>, dim3(compact_grid(n)), b, 0, s, q, qs, n, prm, pt, out,  \
                                              flag));                                                            \
+    else if (streamable)                                                                                        \
+      PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_v<D>, gv, b, 0, s, q, n, prm, pt, out, flag));               \
     else                                                                                                        \
       PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf<D>, g, b, 0, s, q, qs, n, prm, pt, out, flag));              \
     break;

@@ -1,0 +1,31 @@
+"""The bench's ppf-sweep side measurement on its own (pbh_ppf over an HBM-resident q column,
+16 B per draw, HIP-event time of k_ppf on the launching stream), for A/B runs of the kernels:
+
+    python tools/ppf_sweep.py [--rows 100000000]
+"""
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    a = ap.parse_args()
+    import bench
+    from probabilit_amd import _lib, device
+
+    device.device()
+    base = [("norm", {"loc": 0.0, "scale": 1.0}), ("gamma", {"a": 2.0}), ("triang", {"c": 0.3}),
+            ("poisson", {"mu": 4.0}), ("norm", {"loc": 5.0, "scale": 2.0}), ("gamma", {"a": 0.7, "scale": 3.0}),
+            ("triang", {"c": 0.8, "loc": 1.0, "scale": 2.0}), ("poisson", {"mu": 30.0}),
+            ("uniform", {}), ("expon", {}), ("lognorm", {"s": 0.5})]
+    print(json.dumps(bench.ppf_sweep(_lib.load(), base, a.rows, 0), indent=1))
+
+
+if __name__ == "__main__":
+    main()
