@@ -314,6 +314,68 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_c(uint64_t seed, int
                    flag, tq, res);
 }
 
+// ---------------------------------------------------------------- gamma: guide table in LDS
+// igami_guided reads 7 table values (y, d1, d2 at nodes j and j + 1, ok[j]) at a node chosen by
+// the draw.  With q in random order every lane of a wave hits a different cache line, so each of
+// those 7 loads costs the texture path ~64 line lookups per wave instruction -- the gamma sweep
+// measured 1.3 ms per 1e8 draws, gather-bound.  The whole table (4 x 3841 doubles = 120 KiB)
+// fits in a CU's 160 KiB LDS: one 1024-thread workgroup per CU stages it once and then gathers
+// from LDS.  The arithmetic and the table values are the same, so results are bit-identical to
+// k_ppf / k_lhs_ppf's.
+constexpr int kGBlock = 1024;
+constexpr int kGTable = 4 * sf::kGammaGuideM;  // y, d1, d2, ok
+
+PBH_DI sf::GammaGuide stage_guide(const sf::GammaGuide& T, double* lds) {
+  for (int k = threadIdx.x; k < kGTable; k += kGBlock) lds[k] = T.y[k];  // the four arrays are contiguous
+  __syncthreads();
+  const int m = sf::kGammaGuideM;
+  return sf::GammaGuide{lds, lds + m, lds + 2 * m, lds + 3 * m, m, T.z0, T.h, T.inv_h};
+}
+
+PBH_DI double gamma_ppf_lds(double q, const Params& prm, const PoissonTable& pt, const sf::GammaGuide& T) {
+  PoissonTable local = pt;  // ppf_one reads the guide through pt
+  local.guide = T;
+  return ppf_one<PBH_DIST_GAMMA>(q, prm.val[0], prm.val[1], prm.val[2], local);
+}
+
+__global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restrict__ q, int64_t q_stride, int64_t n,
+                                                           Params prm, PoissonTable pt, double* __restrict__ out,
+                                                           int32_t* flag) {
+  __shared__ double lds[kGTable];
+  const sf::GammaGuide T = stage_guide(pt.guide, lds);
+  for (int64_t i = (int64_t)blockIdx.x * kGBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kGBlock) {
+    const double x = gamma_ppf_lds(q[i * q_stride], prm, pt, T);
+    out[i] = x;
+    flag_nonfinite(flag, !isfinite(x));
+  }
+}
+
+__global__ __launch_bounds__(kGBlock) void k_lhs_ppf_gamma_lds(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
+                                                               uint32_t col, Params prm, PoissonTable pt,
+                                                               double* __restrict__ out, int32_t* flag) {
+  __shared__ double lds[kGTable];
+  const sf::GammaGuide T = stage_guide(pt.guide, lds);
+  Philox ph(seed);
+  FeistelPerm fp(ph, (uint64_t)n, col);
+  for (int64_t i = (int64_t)blockIdx.x * kGBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kGBlock) {
+    const double x = gamma_ppf_lds(lhs_quantile(ph, fp, (uint64_t)(row0 + i), col), prm, pt, T);
+    out[i] = x;
+    flag_nonfinite(flag, !isfinite(x));
+  }
+}
+
+// scalar shape with a built guide, scalar loc / scale
+bool gamma_lds_ok(int dist, const Params& prm, const PoissonTable& pt) {
+  static const bool on = [] {
+    const char* e = getenv("PBH_GAMMA_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return on && dist == PBH_DIST_GAMMA && pt.has_gamma && pt.guide.m == sf::kGammaGuideM && !prm.ptr[0] &&
+         !prm.ptr[1] && !prm.ptr[2];
+}
+
+unsigned gamma_lds_grid(int64_t n) { return grid_for(n, kGBlock, 256); }  // one workgroup per CU
+
 // The same LHS column in stratum order: out[t] = ppf(q) for the row pi^-1(t) that holds
 // stratum t.  Bit-identical to k_lhs_ppf's value for that row; non-decreasing in t whenever
 // the ppf is monotone.  With counts != NULL the kernel also counts, over the pairs (t, t + 1)
@@ -685,6 +747,12 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
   const bool streamable = light && qs == 1 && !prm.ptr[0] && !prm.ptr[1] && !prm.ptr[2] &&
                           ((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0 && stream_enabled();
   dim3 gv(grid_for(n, kVTile, 256 * 8));
+  if (gamma_lds_ok(dist, prm, pt)) {
+    PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_gamma_lds, dim3(gamma_lds_grid(n)), dim3(kGBlock), 0, s, q, qs, n,
+                                           prm, pt, out, flag));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
   switch (dist) {
 #define PBH_CASE(D) \
   case D:           \
@@ -715,6 +783,12 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
 int launch_lhs_ppf(int dist, uint64_t seed, int64_t n, int64_t row0, int64_t nrows, uint32_t col,
                    const Params& prm, const PoissonTable& pt, double* out, int32_t* flag, hipStream_t s) {
   dim3 g(ppf_grid(nrows)), b(kBlock);
+  if (gamma_lds_ok(dist, prm, pt)) {
+    PBH_TIMED(kKLhsPpf, s, hipLaunchKernelGGL(k_lhs_ppf_gamma_lds, dim3(gamma_lds_grid(nrows)), dim3(kGBlock), 0, s,
+                                              seed, n, row0, nrows, col, prm, pt, out, flag));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
   switch (dist) {
 #define PBH_CASE(D) \
   case D:           \

@@ -144,3 +144,27 @@ def test_ppf_streaming_ragged_and_misaligned(gpu, name, kw):
             _check_poisson(qh[:n], aligned, exp, kw["mu"])
         else:
             assert_close(aligned, exp, rtol=RTOL, what=f"{name}{kw} n={n}")
+
+
+@pytest.mark.parametrize("kw", [{"a": 2.0}, {"a": 0.7, "scale": 3.0}, {"a": 0.05}, {"a": 45.0, "loc": 1.0}])
+def test_gamma_lds_table_bit_identical(gpu, kw):
+    """k_ppf_gamma_lds / k_lhs_ppf_gamma_lds (guide table staged in LDS; scalar parameters) give
+    the same bits as k_ppf / k_lhs_ppf reading the table from global memory (taken when loc is
+    a per-row vector, here all equal to the scalar) and as the stratum-ordered generator."""
+    import ctypes
+
+    from probabilit_amd import _lib, device, native
+
+    n = 200_003
+    lds = native.lhs_ppf("gamma", 99, n, 3, **kw)
+    vec = dict(kw, loc=np.full(n, kw.get("loc", 0.0)))
+    glob = native.lhs_ppf("gamma", 99, n, 3, **vec)
+    np.testing.assert_array_equal(lds, glob)
+    q = native.fill_lhs(99, n, 4)[:, 3]
+    np.testing.assert_array_equal(native.ppf("gamma", q, **kw), native.ppf("gamma", q, **vec))
+    np.testing.assert_array_equal(native.ppf("gamma", q, **kw), lds)
+    out, flag = device.empty(n), device.zeros(1, "int32")
+    prm = (ctypes.c_double * 3)(kw["a"], kw.get("loc", 0.0), kw.get("scale", 1.0))
+    _lib.check(_lib.load().pbh_lhs_sorted_ppf(99, n, 0, n, 3, _lib.DIST_IDS["gamma"], prm, 3, out.data_ptr(),
+                                              flag.data_ptr(), device.stream()), "pbh_lhs_sorted_ppf")
+    np.testing.assert_array_equal(np.sort(lds), np.sort(device.to_host(out)))
