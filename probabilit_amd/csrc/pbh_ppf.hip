@@ -376,6 +376,65 @@ bool gamma_lds_ok(int dist, const Params& prm, const PoissonTable& pt) {
 
 unsigned gamma_lds_grid(int64_t n) { return grid_for(n, kGBlock, 256); }  // one workgroup per CU
 
+// ---------------------------------------------------------------- poisson: CDF table in LDS
+// The same gather pattern: poisson_from_table reads guide[floor(q 2^11)] and then cdf[lo..]
+// at random positions, two dependent gathers per draw.  The CDF table (32 sd + 53 entries) and
+// the 2048-entry guide are staged in LDS (dynamic, <= 56 KiB) when the table is short enough;
+// same table, same search, same result.
+constexpr int64_t kPoissonLdsMaxLen = 6144;
+
+PBH_DI PoissonTable stage_poisson(const PoissonTable& pt, double* lds) {
+  const int nb = 1 << kPoissonGuideBits;
+  int32_t* g = reinterpret_cast<int32_t*>(lds + pt.len);
+  for (int k = threadIdx.x; k < (int)pt.len; k += kBlock) lds[k] = pt.cdf[k];
+  for (int k = threadIdx.x; k < nb; k += kBlock) g[k] = pt.cdf_guide[k];
+  __syncthreads();
+  PoissonTable local = pt;
+  local.cdf = lds;
+  local.cdf_guide = g;
+  return local;
+}
+
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_poisson_lds(const double* __restrict__ q, int64_t q_stride,
+                                                            int64_t n, Params prm, PoissonTable pt,
+                                                            double* __restrict__ out, int32_t* flag) {
+  extern __shared__ double plds[];
+  const PoissonTable T = stage_poisson(pt, plds);
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const double x = ppf_one<PBH_DIST_POISSON>(q[i * q_stride], prm.val[0], prm.val[1], prm.val[2], T);
+    out[i] = x;
+    flag_nonfinite(flag, !isfinite(x));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_poisson_lds(uint64_t seed, int64_t n, int64_t row0,
+                                                                int64_t nrows, uint32_t col, Params prm,
+                                                                PoissonTable pt, double* __restrict__ out,
+                                                                int32_t* flag) {
+  extern __shared__ double plds[];
+  const PoissonTable T = stage_poisson(pt, plds);
+  Philox ph(seed);
+  FeistelPerm fp(ph, (uint64_t)n, col);
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
+    const double q = lhs_quantile(ph, fp, (uint64_t)(row0 + i), col);
+    const double x = ppf_one<PBH_DIST_POISSON>(q, prm.val[0], prm.val[1], prm.val[2], T);
+    out[i] = x;
+    flag_nonfinite(flag, !isfinite(x));
+  }
+}
+
+// dynamic LDS bytes of the poisson LDS kernels, or 0 when they do not apply
+size_t poisson_lds_bytes(int dist, const Params& prm, const PoissonTable& pt) {
+  static const bool on = [] {
+    const char* e = getenv("PBH_POISSON_LDS");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || dist != PBH_DIST_POISSON || !pt.cdf || !pt.cdf_guide || pt.len <= 0 || pt.len > kPoissonLdsMaxLen ||
+      prm.ptr[0] || prm.ptr[1])
+    return 0;
+  return (size_t)pt.len * sizeof(double) + ((size_t)1 << kPoissonGuideBits) * sizeof(int32_t);
+}
+
 // The same LHS column in stratum order: out[t] = ppf(q) for the row pi^-1(t) that holds
 // stratum t.  Bit-identical to k_lhs_ppf's value for that row; non-decreasing in t whenever
 // the ppf is monotone.  With counts != NULL the kernel also counts, over the pairs (t, t + 1)
@@ -753,6 +812,12 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
     PBH_CHECK_LAUNCH();
     return PBH_OK;
   }
+  if (const size_t pl = poisson_lds_bytes(dist, prm, pt)) {
+    PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_poisson_lds, dim3(grid_for(n, kBlock, 256 * 8)), b, pl, s, q, qs,
+                                           n, prm, pt, out, flag));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
   switch (dist) {
 #define PBH_CASE(D) \
   case D:           \
@@ -786,6 +851,12 @@ int launch_lhs_ppf(int dist, uint64_t seed, int64_t n, int64_t row0, int64_t nro
   if (gamma_lds_ok(dist, prm, pt)) {
     PBH_TIMED(kKLhsPpf, s, hipLaunchKernelGGL(k_lhs_ppf_gamma_lds, dim3(gamma_lds_grid(nrows)), dim3(kGBlock), 0, s,
                                               seed, n, row0, nrows, col, prm, pt, out, flag));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
+  if (const size_t pl = poisson_lds_bytes(dist, prm, pt)) {
+    PBH_TIMED(kKLhsPpf, s, hipLaunchKernelGGL(k_lhs_ppf_poisson_lds, dim3(grid_for(nrows, kBlock, 256 * 8)), b, pl,
+                                              s, seed, n, row0, nrows, col, prm, pt, out, flag));
     PBH_CHECK_LAUNCH();
     return PBH_OK;
   }

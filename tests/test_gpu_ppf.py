@@ -168,3 +168,22 @@ def test_gamma_lds_table_bit_identical(gpu, kw):
     _lib.check(_lib.load().pbh_lhs_sorted_ppf(99, n, 0, n, 3, _lib.DIST_IDS["gamma"], prm, 3, out.data_ptr(),
                                               flag.data_ptr(), device.stream()), "pbh_lhs_sorted_ppf")
     np.testing.assert_array_equal(np.sort(lds), np.sort(device.to_host(out)))
+
+
+@pytest.mark.parametrize("kw", [{"mu": 4.0}, {"mu": 30.0}, {"mu": 0.3, "loc": 2.0}, {"mu": 2500.0}, {"mu": 1e5}])
+def test_poisson_lds_table_bit_identical(gpu, kw):
+    """k_ppf_poisson_lds / k_lhs_ppf_poisson_lds (CDF table + guide staged in LDS; scalar mu and
+    loc, tables up to 6144 entries -- mu = 1e5 takes the global-table kernel) agree exactly with
+    the global-table kernels (taken for a per-row loc) and with scipy inside its domain."""
+    from oracle.ppf import ppf as ref_ppf
+    from probabilit_amd import native
+
+    n = 200_003
+    vec = dict(kw, loc=np.full(n, kw.get("loc", 0.0)))
+    lds = native.lhs_ppf("poisson", 5, n, 1, **kw)
+    np.testing.assert_array_equal(lds, native.lhs_ppf("poisson", 5, n, 1, **vec))
+    q = native.fill_lhs(5, n, 2)[:, 1]
+    out = native.ppf("poisson", q, **kw)
+    np.testing.assert_array_equal(out, native.ppf("poisson", q, **vec))
+    np.testing.assert_array_equal(out, lds)
+    _check_poisson(q[:20000], out[:20000], ref_ppf("poisson", q[:20000], **kw), kw["mu"], kw.get("loc", 0.0))
