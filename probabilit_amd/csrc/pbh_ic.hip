@@ -561,24 +561,34 @@ __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int6
 #pragma unroll
     for (int J = 0; J < 2; ++J) b[s][J] = M[(4 * s + q) * 32 + 16 * J + m16];
   const int64_t tiles = (n + AM_ROWS - 1) / AM_ROWS;
+  // A operands of the wave's next 64-row tile, loaded while the current tile's columns are
+  // stored (register prefetch: the loads of tile t + 1 overlap the LDS transpose and the stores
+  // of tile t; rows of different tiles never alias, so the in-place update is unaffected)
+  double pa[AM_ROWS / 16][8];
+  auto load = [&](int64_t bt) {
+    const int64_t tw = bt * 4 + w;
+#pragma unroll
+    for (int rb = 0; rb < AM_ROWS / 16; ++rb) {
+      const int64_t r = tw * AM_ROWS + rb * 16 + m16;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int c = 4 * s + q;
+        pa[rb][s] = (tw < tiles && c < k && r < n) ? S[(int64_t)c * ld + r] : 0.0;
+      }
+    }
+  };
+  if ((int64_t)blockIdx.x * 4 < tiles) load(blockIdx.x);
   for (int64_t bt = blockIdx.x; bt * 4 < tiles; bt += gridDim.x) {  // uniform trip count per block
     const int64_t tw = bt * 4 + w;
     const int64_t r0 = tw * AM_ROWS;
     if (tw < tiles) {
 #pragma unroll
       for (int rb = 0; rb < AM_ROWS / 16; ++rb) {
-        const int64_t r = r0 + rb * 16 + m16;
-        double a[8];
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const int c = 4 * s + q;
-          a[s] = (c < k && r < n) ? S[(int64_t)c * ld + r] : 0.0;
-        }
         f64x4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-          c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s][0], c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s][1], c1, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[rb][s], b[s][0], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[rb][s], b[s][1], c1, 0, 0, 0);
         }
         // C[i][j]: register g of lane l holds row i = (l >> 4) + 4 g, column j = l & 15
 #pragma unroll
@@ -589,6 +599,7 @@ __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int6
         }
       }
     }
+    if ((bt + gridDim.x) * 4 < tiles) load(bt + gridDim.x);
     __syncthreads();
     const int64_t r = r0 + lane;
     if (tw < tiles && r < n) {
