@@ -74,8 +74,7 @@ PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
 }
 
 // ppf of one element for distribution D; p = (shape..., loc, scale) already resolved.
-// PART selects the inverse normal's branch for norm / lognorm (0: ndtri_fast, 1: its centre,
-// 2: its tail; PPND16, pbh_special.h),
+// PART selects ndtri's branch for norm / lognorm (0: ndtri, 1: ndtri_centre, 2: ndtri_tail),
 // for the compacted kernels that know which one an element takes.
 template <int D, int PART = 0>
 PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTable& pt) {
@@ -112,13 +111,13 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
     if (!(q > 0.0 && q < 1.0)) return kNaN;
     double x;
     if constexpr (D == PBH_DIST_NORM) {
-      x = PART == 1 ? sf::ndtri_fast_centre(q) : PART == 2 ? sf::ndtri_fast_tail(q) : sf::ndtri_fast(q);
+      x = PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q);
     } else if constexpr (D == PBH_DIST_UNIFORM) {
       x = q;
     } else if constexpr (D == PBH_DIST_EXPON) {
       x = -sf::log1p_(-q);  // scipy expon._ppf: -sc.log1p(-q), the Cephes log1p
     } else if constexpr (D == PBH_DIST_LOGNORM) {
-      x = exp(shape * (PART == 1 ? sf::ndtri_fast_centre(q) : PART == 2 ? sf::ndtri_fast_tail(q) : sf::ndtri_fast(q)));
+      x = exp(shape * (PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q)));
     } else if constexpr (D == PBH_DIST_TRIANG) {
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
@@ -130,14 +129,13 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
 }
 
 // ---------------------------------------------------------------- tail compaction
-// The inverse normal CDF is one rational function in its centre and an expensive tail otherwise:
-// Cephes' ndtri (the van der Waerden scores) for min(q, 1 - q) > e^-2 (73% of uniform q, tail:
-// two logs, a sqrt, three divisions), PPND16 (norm / lognorm ppf outputs) for
-// |q - 0.5| <= 0.425 (85%, tail: one log, a sqrt, a division).  With q in random order nearly every wave holds both kinds, and a wave
+// ndtri (norm / lognorm ppf, the van der Waerden scores) is one rational function for
+// min(q, 1 - q) > e^-2 (73% of uniform q) and an expensive tail (two logs, a sqrt, three
+// divisions) otherwise.  With q in random order nearly every wave holds both kinds, and a wave
 // executes every branch one of its lanes takes, so a plain grid-stride kernel pays centre + tail
 // for every element.  The compacted kernels give each thread kCIpt items of a block tile: centre
 // items are evaluated at once, tail items are queued in LDS (one LDS atomic per wave) and then
-// drained by all lanes of the block together, so the tail costs its 27% / 15% share.  Every value is
+// drained by all lanes of the block together, so the tail costs its 27% share.  Every value is
 // computed by the same inline function either way (bit-identical to the plain kernels); the
 // results pass through LDS so that the global stores stay coalesced.
 constexpr int kCIpt = 8;
@@ -191,15 +189,13 @@ PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm, const Pois
   for (int64_t base = (int64_t)blockIdx.x * kCTile; base < n; base += (int64_t)gridDim.x * kCTile) {
     if (threadIdx.x == 0) tq.count = 0;
     __syncthreads();
-    // two items at a time: PPND16's 30 coefficients live in VGPR pairs (no 64-bit literal
-    // operands), and eight interleaved evaluations would spill under the 128-VGPR cap
-#pragma unroll 2
+#pragma unroll
     for (int j = 0; j < kCIpt; ++j) {
       const int p = j * kBlock + threadIdx.x;
       const int64_t i = base + p;
       const bool valid = i < n;
       const double qv = valid ? qof(i) : 0.5;
-      const bool tail = valid && sf::ndtri_fast_takes_tail(qv);
+      const bool tail = valid && sf::ndtri_takes_tail(qv);
       if (valid && !tail) res[p] = ppf_one<D, 1>(qv, prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
       tail_push(tq, tail, qv, p);
     }

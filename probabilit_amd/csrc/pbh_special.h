@@ -125,84 +125,6 @@ PBH_HD inline double ndtri(double y0) {
   return ndtri_centre(y0);
 }
 
-// ---------------------------------------------------------------- inverse normal CDF, ppf outputs
-// Wichura's PPND16 (Applied Statistics algorithm AS 241, 1988): the norm / lognorm ppf
-// OUTPUTS only, whose parity gate is 1e-10 relative to scipy's ndtri (north_star).  Measured
-// against scipy.special.ndtri on 7e6 points from 5e-324 to 1 - 2^-53 the largest relative
-// difference is 1.2e-15 (tests/test_gpu_ppf.py checks the 1e-10 gate on the device).  The
-// Iman-Conover van der Waerden scores keep Cephes' ndtri above: their exact bits decide ranks.
-//
-// Why a second algorithm: Cephes' tail (min(y, 1 - y) <= e^-2, 27% of uniform draws) costs two
-// logs, a sqrt and three divisions (~400 instructions); PPND16's centre covers |p - 0.5| <= 0.425
-// (85% of draws) with one 8/8 rational function, and its tail needs one log, one sqrt and one
-// division.  The Horner steps use fused multiply-adds (the gate is a tolerance, not bits).
-PBH_HD inline bool ndtri_fast_takes_tail(double p) { return p > 0.0 && p < 1.0 && !(fabs(p - 0.5) <= 0.425); }
-
-PBH_HD inline double ppnd16_horner(const double* c, double r) {
-  double x = c[7];
-#pragma unroll
-  for (int i = 6; i >= 0; --i) x = __builtin_fma(x, r, c[i]);
-  return x;
-}
-
-// |p - 0.5| <= 0.425
-PBH_HD inline double ndtri_fast_centre(double p) {
-  const double A[8] = {3.3871328727963666080e0, 1.3314166789178437745e+2, 1.9715909503065514427e+3,
-                       1.3731693765509461125e+4, 4.5921953931549871457e+4, 6.7265770927008700853e+4,
-                       3.3430575583588128105e+4, 2.5090809287301226727e+3};
-  const double B[8] = {1.0, 4.2313330701600911252e+1, 6.8718700749205790830e+2, 5.3941960214247511077e+3,
-                       2.1213794301586595867e+4, 3.9307895800092710610e+4, 2.8729085735721942674e+4,
-                       5.2264952788528545610e+3};
-  const double q = p - 0.5;
-  const double r = __builtin_fma(-q, q, 0.180625);
-  return q * ppnd16_horner(A, r) / ppnd16_horner(B, r);
-}
-
-// r = sqrt(-log(min(p, 1 - p))) > 5, i.e. min(p, 1 - p) < exp(-25) = 1.4e-11: out of line, so that
-// its 15 coefficients are not held in registers by every kernel that inlines the ppf.
-#if defined(__HIP_DEVICE_COMPILE__)
-static __device__ __attribute__((noinline))
-#else
-inline
-#endif
-double ndtri_fast_far_tail(double r) {
-  const double E[8] = {6.65790464350110377720e0, 5.46378491116411436990e0, 1.78482653991729133580e0,
-                       2.96560571828504891230e-1, 2.65321895265761230930e-2, 1.24266094738807843860e-3,
-                       2.71155556874348757815e-5, 2.01033439929228813265e-7};
-  const double F[8] = {1.0, 5.99832206555887937690e-1, 1.36929880922735805310e-1, 1.48753612908506148525e-2,
-                       7.86869131145613259100e-4, 1.84631831751005468180e-5, 1.42151175831644588870e-7,
-                       2.04426310338993978564e-15};
-  r -= 5.0;
-  return ppnd16_horner(E, r) / ppnd16_horner(F, r);
-}
-
-// ndtri_fast_takes_tail(p)
-PBH_HD inline double ndtri_fast_tail(double p) {
-  const double C[8] = {1.42343711074968357734e0, 4.63033784615654529590e0, 5.76949722146069140550e0,
-                       3.64784832476320460504e0, 1.27045825245236838258e0, 2.41780725177450611770e-1,
-                       2.27238449892691845833e-2, 7.74545014278341407640e-4};
-  const double D[8] = {1.0, 2.05319162663775882187e0, 1.67638483018380384940e0, 6.89767334985100004550e-1,
-                       1.48103976427480074590e-1, 1.51986665636164571966e-2, 5.47593808499534494600e-4,
-                       1.05075007164441684324e-9};
-  const bool lower = p < 0.5;
-  double r = sqrt(-log(lower ? p : 1.0 - p));
-  double x;
-  if (r <= 5.0) {
-    r -= 1.6;
-    x = ppnd16_horner(C, r) / ppnd16_horner(D, r);
-  } else {
-    x = ndtri_fast_far_tail(r);
-  }
-  return lower ? -x : x;
-}
-
-PBH_HD inline double ndtri_fast(double p) {
-  if (p == 0.0) return -kInf;
-  if (p == 1.0) return kInf;
-  if (!(p > 0.0 && p < 1.0)) return kNaN;
-  return ndtri_fast_takes_tail(p) ? ndtri_fast_tail(p) : ndtri_fast_centre(p);
-}
-
 // ---------------------------------------------------------------- erf / erfc (for Temme)
 PBH_HD inline double erfc_(double a);
 PBH_HD inline double erf_(double x) {
@@ -848,18 +770,23 @@ PBH_HD inline double gamma_halley(double a, double p, double x, const GammaAux* 
   return isinf(fpp_fp) ? x - f_fp : x - f_fp / (1.0 - 0.5 * f_fp * fpp_fp);
 }
 
-// Quintic Hermite interpolant of y on interval j at fraction t.
+// Quintic Hermite interpolant of y on interval j at fraction t, in monomial form:
+// p(t) = y0 + a1 t + a2/2 t^2 + c3 t^3 + c4 t^4 + c5 t^5 with p, p', p'' matching
+// (y0, a1 = h y0', a2 = h^2 y0'') at t = 0 and (y1, b1, b2) at t = 1; c3..c5 solve the three
+// end conditions.  ~26 operations (fused) against ~55 for the six Hermite basis polynomials.
 PBH_HD inline double guide_interp(const GammaGuide& T, int j, double t) {
   const double h = T.h, hh = h * h;
-  const double t2 = t * t, t3 = t2 * t, t4 = t3 * t, t5 = t4 * t;
-  const double h0 = 1.0 - 10.0 * t3 + 15.0 * t4 - 6.0 * t5;
-  const double h1 = t - 6.0 * t3 + 8.0 * t4 - 3.0 * t5;
-  const double h2 = 0.5 * (t2 - 3.0 * t3 + 3.0 * t4 - t5);
-  const double h3 = 0.5 * (t3 - 2.0 * t4 + t5);
-  const double h4 = -4.0 * t3 + 7.0 * t4 - 3.0 * t5;
-  const double h5 = 10.0 * t3 - 15.0 * t4 + 6.0 * t5;
-  return T.y[j] * h0 + T.d1[j] * h * h1 + T.d2[j] * hh * h2 + T.d2[j + 1] * hh * h3 + T.d1[j + 1] * h * h4 +
-         T.y[j + 1] * h5;
+  const double y0 = T.y[j], dy = T.y[j + 1] - y0;
+  const double a1 = T.d1[j] * h, b1 = T.d1[j + 1] * h;
+  const double a2 = T.d2[j] * hh, b2 = T.d2[j + 1] * hh;
+  const double c3 = __builtin_fma(10.0, dy, __builtin_fma(-6.0, a1, __builtin_fma(-4.0, b1, __builtin_fma(-1.5, a2, 0.5 * b2))));
+  const double c4 = __builtin_fma(-15.0, dy, __builtin_fma(8.0, a1, __builtin_fma(7.0, b1, __builtin_fma(1.5, a2, -b2))));
+  const double c5 = __builtin_fma(6.0, dy, __builtin_fma(-3.0, a1, __builtin_fma(-3.0, b1, __builtin_fma(-0.5, a2, 0.5 * b2))));
+  double p = __builtin_fma(t, c5, c4);
+  p = __builtin_fma(t, p, c3);
+  p = __builtin_fma(t, p, 0.5 * a2);
+  p = __builtin_fma(t, p, a1);
+  return __builtin_fma(t, p, y0);
 }
 
 PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const GammaGuide& T) {

@@ -13,9 +13,6 @@ extern "C" {
 void sfh_ndtri(const double* q, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = sf::ndtri(q[i]);
 }
-void sfh_ndtri_fast(const double* q, long n, double* out) {
-  for (long i = 0; i < n; ++i) out[i] = sf::ndtri_fast(q[i]);
-}
 
 void sfh_igami(double a, const double* p, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = sf::igami(a, p[i]);
