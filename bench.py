@@ -89,8 +89,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--d", type=int, default=32)
-    ap.add_argument("--cpu-n", type=int, default=262_144)
+    ap.add_argument("--cpu-n", type=int, default=1_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (D2H included) side measurement")
     ap.add_argument("--ppf-rows", type=int, default=100_000_000, help="rows of the ppf-sweep side measurement (0: skip)")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
@@ -175,6 +176,17 @@ def main():
                 "kernel": dom,
                 "avg_launch_ms": dk["avg_ms"], "bytes_per_launch": dk["bytes_per_launch"]}
 
+    # whole-step roofline: SURVEY.md §8(d)'s 96 algorithmic bytes per draw over the step time
+    pipeline = {"bytes_per_draw": 96, "achieved": round(96 * n * d * world / (ms_per_step / 1e3) / 1e9, 1),
+                "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                "frac": round(96 * n * d * world / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "kernel_time_ms_per_step": round(sum(k["total_ms_per_step"] for k in kernels.values()), 3)}
+    copy_peak = hbm_copy_peak(lib) if rank == 0 else None
+    if copy_peak:
+        pipeline["frac_of_measured_copy"] = round(pipeline["achieved"] / copy_peak["GBps"], 4)
+        roofline["frac_of_measured_copy"] = round(achieved / copy_peak["GBps"], 4)
+    e2e = end_to_end(step, ds, n, d, args.warmup + args.steps, barrier) if (world == 1 and not args.no_e2e) else None
+
     sweep = ppf_sweep(lib, base, args.ppf_rows, args.seed) if args.ppf_rows > 0 else None
 
     cpu = None
@@ -193,7 +205,8 @@ def main():
                            "rows": n, "d": d,
                            "parallelism": f"row-sharded x{world} (RCCL all-reduce + all-to-all)" if world > 1
                            else "single"},
-                "roofline": roofline, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels}
+                "roofline": roofline, "pipeline_roofline": pipeline, "hbm_copy_peak": copy_peak,
+                "end_to_end": e2e, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels}
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
@@ -229,9 +242,59 @@ def ppf_sweep(lib, dists, n, seed, reps=3):
             "frac": round(gbps / HBM_PEAK_GBS, 4), "per_dist": per}
 
 
+def hbm_copy_peak(lib, nbytes=4 << 30, reps=5):
+    """The box's HBM copy ceiling (re-measure with a copy kernel and report it
+    next to the 8 TB/s spec): pbh_hbm_copy over nbytes, read + write bytes / mean launch time."""
+    import ctypes
+
+    import torch
+
+    from probabilit_amd import _lib, device
+
+    src = torch.empty(nbytes, dtype=torch.uint8, device=device.device())
+    dst = torch.empty_like(src)
+    src.fill_(1)
+    kid = _lib.KERNELS.index("k_hbm_copy")
+    _lib.check(lib.pbh_hbm_copy(src.data_ptr(), dst.data_ptr(), nbytes, device.stream()))
+    lib.pbh_timing_reset()
+    lib.pbh_timing_enable(1)
+    for _ in range(reps):
+        _lib.check(lib.pbh_hbm_copy(src.data_ptr(), dst.data_ptr(), nbytes, device.stream()))
+    lib.pbh_timing_enable(0)
+    t, c = ctypes.c_double(), ctypes.c_int64()
+    _lib.check(lib.pbh_timing_read(kid, ctypes.byref(t), ctypes.byref(c)))
+    avg = t.value / max(c.value, 1)
+    del src, dst
+    return {"kernel": "k_hbm_copy", "bytes_moved": 2 * nbytes, "avg_ms": round(avg, 4),
+            "GBps": round(2 * nbytes / (avg / 1e3) / 1e9, 1), "frac_of_spec": round(2 * nbytes / (avg / 1e3) / 1e9 /
+                                                                                   HBM_PEAK_GBS, 4)}
+
+
+def end_to_end(step, ds, n, d, i, barrier):
+    """One more step with every output column handed back as numpy (the reference returns host
+    arrays, modeling.py:582-583,614): the device step plus the D2H of all d columns through
+    `.samples_` (pageable copies), timed together.  A side figure, never `value`."""
+    barrier()
+    t0 = time.perf_counter()
+    step(i)
+    barrier()
+    t1 = time.perf_counter()
+    host = [x.samples_ for x in ds]
+    t2 = time.perf_counter()
+    nbytes = sum(h.nbytes for h in host)
+    del host
+    return {"value": round(n * d / (t2 - t0) / 1e6, 2), "unit": "Msamples/s", "ms": round((t2 - t0) * 1e3, 1),
+            "device_ms": round((t1 - t0) * 1e3, 1), "d2h_ms": round((t2 - t1) * 1e3, 1),
+            "d2h_GBps": round(nbytes / (t2 - t1) / 1e9, 2), "bytes": nbytes,
+            "what": "one step + .samples_ of all columns (numpy, pageable D2H)"}
+
+
 def cpu_baseline(n, d):
     """The reference's CPU path (oracle.pipeline: scipy LatinHypercube -> scipy ppf ->
-    Iman-Conover restated in numpy with the reference's calls) on this host."""
+    Iman-Conover restated in numpy with the reference's calls) on this host, at N = n rows
+    (default 1e6: the size BASELINE.md quotes, 0.90 Msamples/s on the survey's 8-core Xeon)."""
+    import math
+
     from threadpoolctl import threadpool_info
 
     from oracle.pipeline import lhs_ic
@@ -240,9 +303,17 @@ def cpu_baseline(n, d):
     lhs_ic(n, d, 0)
     dt = time.perf_counter() - t0
     threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
-    return {"value": round(n * d / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+    rate = n * d / dt / 1e6
+    # the work per draw grows like log N (two sorts per column), so the rate at 1e8 is labelled
+    # an N log N extrapolation from the measured N, not a measurement
+    extrap = rate * math.log(n) / math.log(1e8)
+    return {"value": round(rate, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "openblas_num_threads": os.environ.get("OPENBLAS_NUM_THREADS"),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "survey_value_at_1e6": 0.90,
+            "extrapolated_1e8": {"value": round(extrap, 4), "method": f"N log N from N={n}: rate x ln({n}) / ln(1e8)"},
             "sample": f"cfg3 at N={n}, d={d} ({dt:.1f} s): scipy LHS + scipy ppf + numpy/scipy Iman-Conover; "
-                      f"ppf/sort single-threaded, BLAS on {threads} threads"}
+                      f"ppf/sort single-threaded, BLAS pool of {threads} threads (cores = that pool)"}
 
 
 if __name__ == "__main__":

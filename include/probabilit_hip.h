@@ -96,6 +96,24 @@ int pbh_pcg64_workspace_size(size_t* bytes);
 int pbh_pcg64_random(const uint64_t* state_host, const uint64_t* inc_host, int64_t draw0, int64_t nrows, int32_t d,
                      double* q, int64_t ldq, void* ws, size_t ws_bytes, void* stream);
 
+/* The reference's own Latin hypercube stream, opt-in parity mode (the default "lhs" path is the
+ * native design of pbh_fill_lhs): scipy.stats.qmc.LatinHypercube(d, rng).random(n) bit for bit
+ * (modeling.py:480,488 -> scipy:stats/_qmc.py LatinHypercube._random_lhs).  state_host / inc_host /
+ * has32 / buf32: the engine Generator's PCG64 state before the call ({low, high} words and numpy's
+ * buffered 32-bit half).  u = rng.uniform(size=(n, d)) is drawn on the device, the d Fisher-Yates
+ * shuffles of arange(1, n + 1) (numpy Generator.shuffle: random_interval with masked rejection
+ * on buffered 32-bit draws) run on the host -- one sequential stream, replayed per column in
+ * parallel threads after a counting pass -- and q = (perm - u) / n is combined on the device into
+ * q (column-major, column c at q + c * ldq).  n < 2^31.  Workspace: pbh_lhs_reference_workspace_size.
+ * pbh_lhs_reference_perms is the host half alone: the d permutations (d x n int32, row c = the
+ * shuffled column c) from the stream state at the first shuffle draw; state_out_host (optional,
+ * 4 words) receives the state after the last one (state low, high, has32, buf32). */
+int pbh_lhs_reference_workspace_size(int64_t n, int32_t d, size_t* bytes);
+int pbh_lhs_reference(const uint64_t* state_host, const uint64_t* inc_host, int32_t has32, uint32_t buf32, int64_t n,
+                      int32_t d, double* q, int64_t ldq, void* ws, size_t ws_bytes, void* stream);
+int pbh_lhs_reference_perms(const uint64_t* state_host, const uint64_t* inc_host, int32_t has32, uint32_t buf32,
+                            int64_t n, int32_t d, int32_t* perms_host, uint64_t* state_out_host);
+
 /* Scrambled Halton points, bit-exact with scipy.stats.qmc.Halton(d, rng=...) (modeling.py:481,488):
  * column c is the van der Corput sequence in base bases_host[c] with counts_host[c] digit
  * permutations (perms_host: concatenated counts_host[c] x bases_host[c] tables, produced by the
@@ -328,6 +346,9 @@ int pbh_timing_enable(int on);
 int pbh_timing_reset(void);
 const char* pbh_kernel_name(int id);
 int pbh_timing_read(int id, double* total_ms, int64_t* launches);
+/* The box's HBM copy ceiling for bench.py (the measured peak reported beside the 8 TB/s spec):
+ * dst = src over `bytes` (16-byte aligned), timed as kernel "k_hbm_copy". */
+int pbh_hbm_copy(const void* src, void* dst, size_t bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -37,8 +37,26 @@ def lhs_quantiles(n, d, seed):
     return scipy.stats.qmc.LatinHypercube(d=d, rng=seed).random(n)
 
 
-def ppf_columns(Q, dists):
-    return np.column_stack([ppf(name, Q[:, j], **kw) for j, (name, kw) in enumerate(dists)])
+def ppf_columns(Q, dists, threads=None, chunk=1 << 20):
+    """Column j = scipy.stats.<dist_j>(**kw).ppf(Q[:, j]) (modeling.py:807).  With `threads`,
+    each column is cut into row chunks evaluated on a thread pool (the same elementwise
+    scipy call per chunk, so identical values)."""
+    if not threads or threads <= 1:
+        return np.column_stack([ppf(name, Q[:, j], **kw) for j, (name, kw) in enumerate(dists)])
+    from concurrent.futures import ThreadPoolExecutor
+
+    n = Q.shape[0]
+    out = np.empty((n, len(dists)))
+    tasks = [(j, r0) for j in range(len(dists)) for r0 in range(0, n, chunk)]
+
+    def run(t):
+        j, r0 = t
+        name, kw = dists[j]
+        out[r0:r0 + chunk, j] = ppf(name, np.ascontiguousarray(Q[r0:r0 + chunk, j]), **kw)
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(run, tasks))
+    return out
 
 
 def lhs_ic(n, d, seed, C=None):

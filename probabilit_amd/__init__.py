@@ -18,7 +18,17 @@ from .modeling import (  # noqa: F401
     MultivariateDistribution,
     scalar_transform,
 )
+from .distributions import PERT  # noqa: F401  (probabilit/__init__.py:11)
+
+
+def plot(*variables, **kwargs):
+    """probabilit.inspection.plot (a seaborn pairplot of sampled nodes) is UI, outside the
+    sampling hot path this package accelerates: use the reference's plot
+    on the `.samples_` arrays, which are plain numpy."""
+    raise NotImplementedError("probabilit_amd does not provide plotting; call probabilit.inspection.plot "
+                              "(seaborn) on the sampled nodes' .samples_ arrays")
+
 
 __all__ = ["Distribution", "Constant", "EmpiricalDistribution", "CumulativeDistribution", "DiscreteDistribution",
-           "Equal", "scalar_transform", "MultivariateDistribution"]
+           "Equal", "scalar_transform", "MultivariateDistribution", "PERT", "plot"]
 __version__ = "0.1.0"

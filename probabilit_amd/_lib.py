@@ -45,7 +45,8 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_pcg64_workspace_size",
            "pbh_pcg64_random", "pbh_halton_workspace_size", "pbh_fill_halton",
            "pbh_affine_workspace_size", "pbh_affine_rows", "pbh_table_ppf", "pbh_permcorr_workspace_size",
-           "pbh_permcorr_climb", "pbh_sobol_ppf"]
+           "pbh_permcorr_climb", "pbh_sobol_ppf", "pbh_lhs_reference_workspace_size",
+           "pbh_lhs_reference", "pbh_lhs_reference_perms", "pbh_hbm_copy"]
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
@@ -53,7 +54,7 @@ KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_ra
            "k_lhs_sorted_ppf", "k_perm_scores", "k_code_runs",
            "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>",
            "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine", "k_table_ppf",
-           "k_permcorr"]
+           "k_permcorr", "k_hbm_copy"]
 
 
 class Param(ctypes.Structure):
@@ -144,6 +145,10 @@ def load():
         "pbh_affine_rows": ([vp, i64, ctypes.c_int32, i64, i64, vp, vp, vp, vp, vp, i64, i64, vp, sz, vp], i32),
         "pbh_sobol_ppf": ([vp, vp, i32, i32, i64, i64, i32, i32, ctypes.POINTER(Param), i32, vp, vp, vp], i32),
         "pbh_permcorr_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
+        "pbh_lhs_reference_workspace_size": ([i64, ctypes.c_int32, ctypes.POINTER(sz)], i32),
+        "pbh_lhs_reference": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, i64, vp, sz, vp], i32),
+        "pbh_hbm_copy": ([vp, vp, sz, vp], i32),
+        "pbh_lhs_reference_perms": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, vp], i32),
         "pbh_permcorr_climb": ([vp, vp, i64, ctypes.c_int32, i64, vp, vp, vp, vp, vp, vp, i64, dbl, vp, vp, vp, sz, vp],
                                i32),
     }

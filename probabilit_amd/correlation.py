@@ -269,11 +269,15 @@ class ImanConover(Correlator):
         args.target_chol_host = P.ctypes.data
         args.Y, args.y_rs, args.y_cs = Y.data_ptr(), y_rs, y_cs
         args.ws, args.ws_bytes = ws.data_ptr(), ws_bytes.value
-        if debug is not None:
-            args.scores_out = debug["S"].data_ptr()
-            args.cscores_out = debug["CS"].data_ptr()
-            args.idx_out = debug["idx"].data_ptr()
-            args.corr_host_out = debug["E"].ctypes.data
+        if debug is not None:  # intermediates for parity tests; "idx" selects the gather form of step 4
+            if "S" in debug:
+                args.scores_out = debug["S"].data_ptr()
+            if "CS" in debug:
+                args.cscores_out = debug["CS"].data_ptr()
+            if "idx" in debug:
+                args.idx_out = debug["idx"].data_ptr()
+            if "E" in debug:
+                args.corr_host_out = debug["E"].ctypes.data
         status = lib.pbh_iman_conover(ctypes.byref(args), device.stream())
         if status in (_lib.ERR_NOT_PD, _lib.ERR_NONFINITE):
             raise ValueError(_NOT_PD_MSG)
@@ -300,10 +304,12 @@ class ImanConover(Correlator):
         self._run(block, N, K, 1, N, Y, 1, N)
         return Y
 
-    def _transform_generated(self, columns, n):
+    def _transform_generated(self, columns, n, debug=None):
         """DAG fast path: K natively generated LHS columns (list of _lib.ICColumn) are
         generated, correlated and returned as a (K, N) device block without ever
-        materialising the uncorrelated samples (see pbh_ic_column)."""
+        materialising the uncorrelated samples (see pbh_ic_column).  debug: optional dict of
+        buffers for the intermediates (device (K, N) "S" / "CS", host (K, K) "E"), for the
+        parity tests of the production step 4 (no "idx": that would select the gather form)."""
         K = len(columns)
         if not (hasattr(self, "C") and hasattr(self, "P")):
             raise CorrelatorError("User must call `set_target` first.")
@@ -312,7 +318,7 @@ class ImanConover(Correlator):
         if n <= K:
             raise ValueError(f"The matrix X must have rows > columns. Got shape: {(n, K)}")
         Y = device.empty((K, n))
-        self._run(None, n, K, 1, n, Y, 1, n, columns=columns)
+        self._run(None, n, K, 1, n, Y, 1, n, columns=columns, debug=debug)
         return Y
 
     def _call_debug(self, X):

@@ -34,6 +34,7 @@ enum KernelId {
   kKAffine,
   kKTable,
   kKPermCorr,
+  kKHbmCopy,
   kKCount
 };
 

@@ -19,7 +19,7 @@ const char* kNames[kKCount] = {"k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "
                                "k_head_bounds", "k_scan", "k_lhs_sorted_ppf", "k_perm_scores", "k_code_runs",
                                "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>",
                                "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine", "k_table_ppf",
-                               "k_permcorr"};
+                               "k_permcorr", "k_hbm_copy"};
 
 hipEvent_t take_event() {
   if (!g_pool.empty()) {
@@ -45,9 +45,38 @@ void timing_after(int id, hipStream_t s) {
   g_slots[id].stop.push_back(e);
 }
 
+// HBM copy ceiling of the box (bench.py's measured peak next to the 8 TB/s spec): 16-byte
+// non-temporal loads and stores, four in flight per lane, grid-stride over the buffer.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_hbm_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = __builtin_nontemporal_load(src + i + j * stride);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(v[j], dst + i + j * stride);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 }  // namespace pbh
 
 using namespace pbh;
+
+extern "C" int pbh_hbm_copy(const void* src, void* dst, size_t bytes, void* stream) {
+  PBH_REQUIRE(src && dst && bytes % 16 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0,
+              "pbh_hbm_copy: 16-byte aligned buffers and size required");
+  hipStream_t s = as_stream(stream);
+  const int64_t n16 = (int64_t)(bytes / 16);
+  PBH_TIMED(kKHbmCopy, s,
+            hipLaunchKernelGGL(k_hbm_copy, dim3(grid_for(n16, 256, 256 * 16)), dim3(256), 0, s, (const u32x4*)src,
+                               (u32x4*)dst, n16));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
 
 extern "C" int pbh_timing_enable(int on) {
   g_timing_on = on != 0;

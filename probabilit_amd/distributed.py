@@ -187,6 +187,21 @@ def _all_reduce(t, group, world, op="sum"):
     return t
 
 
+def _all_reduce_flags(t, group, world, bits=3):
+    """Combine per-node non-finite flag words (bitmasks: bit 0 non-finite value, bit 1 the
+    integer-power error, bit 2 a DiscreteDistribution index past its table) across ranks
+    without changing their bits: each bit plane is all-reduced with MAX (a bitwise OR;
+    torch.distributed has no OR that RCCL supports) and the planes are recombined."""
+    import torch
+
+    if world <= 1:
+        return t
+    planes = torch.stack([(t >> b) & 1 for b in range(bits)])
+    _all_reduce(planes, group, world, op="max")
+    t.copy_(sum(planes[b] << b for b in range(bits)).to(t.dtype))
+    return t
+
+
 class _Done:
     def wait(self):
         return None
@@ -217,7 +232,7 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
     factor is P (K x K), returning this rank's rows of the result, shape (K, rows).
 
     columns: list of LHSColumn (same on every rank); flags: optional int32 tensor of K
-    non-finite flags (summed over ranks on return).  Raises ValueError exactly where
+    non-finite flag words (OR-combined over ranks on return, bits unchanged).  Raises ValueError exactly where
     ImanConover.__call__ does (rank-correlation matrix not positive definite)."""
     import torch
 
@@ -330,7 +345,7 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
         work_y.wait()
         y_scatter(j, recv_y)
     del S
-    _all_reduce(flags, group, world)
+    _all_reduce_flags(flags, group, world)
     return Y
 
 

@@ -338,16 +338,23 @@ class Node(abc.ABC):
         return self
 
     # ---- sampling ----------------------------------------------------------------
-    def sample(self, size=None, random_state=None, method=None, correlator="imanconover", gc_strategy=None):
+    def sample(self, size=None, random_state=None, method=None, correlator="imanconover", gc_strategy=None,
+               stream=None):
         """Sample this node and assign `.samples_` on every ancestor (modeling.py:431-493).
 
         The quantile matrix is generated on the GPU (see probabilit_amd.qmc) and never
-        materialised for method="lhs" (generator fused into the inverse-CDF kernels)."""
+        materialised for method="lhs" (generator fused into the inverse-CDF kernels).
+
+        stream (extra, keyword): for method="lhs", "native" (default: the counter-based
+        design) or "reference" (scipy's LatinHypercube(d, rng=random_state).random(size) bit
+        for bit, so results equal the reference's on the same seed); None takes the module
+        default (probabilit_amd.qmc.set_default_stream, env PBH_LHS_STREAM).  method=None,
+        "sobol" and "halton" always reproduce the reference's streams."""
         size = 1 if size is None else size
         d = self.num_distribution_nodes()
         if method is not None and method.lower().strip() not in ("lhs", "halton", "sobol"):
             raise KeyError(method.lower().strip())
-        source = qmc.make_source(method, size, d, random_state)
+        source = qmc.make_source(method, size, d, random_state, stream=stream)
         return self._evaluate(source, correlator, gc_strategy, to_host=True)
 
     def sample_from_quantiles(self, quantiles, correlator="imanconover", gc_strategy=None):
@@ -356,7 +363,7 @@ class Node(abc.ABC):
         return self._evaluate(src, correlator, gc_strategy, to_host=True)
 
     def sample_device(self, size=None, random_state=None, method=None, correlator="imanconover",
-                      gc_strategy=None, group=None):
+                      gc_strategy=None, group=None, stream=None):
         """As sample(), but return the sink's device tensor (no D2H copy).
 
         group: a torch.distributed process group (one process per GPU).  With more than one
@@ -365,7 +372,7 @@ class Node(abc.ABC):
         counter-addressed by the global row, correlations run through the row-sharded
         Iman-Conover of probabilit_amd.distributed."""
         size = 1 if size is None else size
-        source = qmc.make_source(method, size, self.num_distribution_nodes(), random_state)
+        source = qmc.make_source(method, size, self.num_distribution_nodes(), random_state, stream=stream)
         return self._evaluate(source, correlator, gc_strategy, to_host=False, group=group)
 
     def _evaluate(self, source, correlator, gc_strategy, to_host, group=None):
@@ -455,7 +462,7 @@ class Node(abc.ABC):
                 vflags = device.zeros(len(cols), "int32")
                 Y = iman_conover_lhs(cols, inst.P, source.n, group=group, flags=vflags)
                 for j, var in enumerate(all_variables):
-                    ev.flags[ev.slot[var]] += vflags[j]
+                    ev.flags[ev.slot[var]] |= vflags[j]  # bitmask words: OR, never add
                     var._set_device(Y[j])
             elif generated:
                 cols = []
@@ -491,10 +498,10 @@ class Node(abc.ABC):
             gc.decrement_and_delete(node)
 
         # fused non-finite check (:600-606): first flagged node in topological order raises
-        if world > 1:  # every rank raises the same error
-            from .distributed import _all_reduce
+        if world > 1:  # every rank raises the same error (flag words OR-combined, bits unchanged)
+            from .distributed import _all_reduce_flags
 
-            _all_reduce(ev.flags, group, world)
+            _all_reduce_flags(ev.flags, group, world)
         flags = device.to_host(ev.flags)
         if flags.any():
             for node in nx.topological_sort(G):

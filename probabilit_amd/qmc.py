@@ -1,17 +1,25 @@
 """Quantile sources for Node.sample (modeling.py:478-489), generated on the GPU.
 
-    method=None     native Philox4x32-10 uniforms            (pbh_fill_uniform)
-    method="lhs"    native Latin hypercube: per column a keyed Feistel bijection of the
-                    strata plus a Philox jitter, fused into the ppf kernel (pbh_lhs_ppf)
+    method=None     numpy's own streams bit for bit: RandomState (MT19937) for None / an int /
+                    a RandomState, Generator (PCG64) for a Generator, as check_random_state
+                    gives at modeling.py:484-486 (pbh_mt19937_random, pbh_pcg64_random:
+                    device jump-ahead, the caller's generator advanced exactly as numpy does)
+    method="lhs"    native Latin hypercube (default): per column a keyed Feistel bijection of
+                    the strata plus a Philox jitter, fused into the ppf kernel (pbh_lhs_ppf);
+                    with stream="reference": scipy's LatinHypercube stream bit for bit
+                    (pbh_lhs_reference: device PCG64 uniforms + host Fisher-Yates shuffles)
     method="sobol"  scrambled Sobol', bit-exact with scipy.stats.qmc.Sobol (pbh_fill_sobol);
                     only the O(d * bits^2) engine setup (direction numbers, LMS scramble,
                     digital shift) runs on the host, consuming the numpy Generator exactly
                     as scipy does.
+    method="halton" scrambled Halton, bit-exact with scipy.stats.qmc.Halton (pbh_fill_halton).
 
-"Native" streams are statistically the same designs as scipy's but are counter-based, so
-any row range can be generated independently (row-sharding across GPUs) — they are not
-numpy's PCG64 / MT19937 bit streams.  Bit-level parity with the reference is defined at
-Node.sample_from_quantiles: identical quantiles in give identical samples out.
+The native LHS design is statistically the same as scipy's but counter-based, so any row
+range can be generated independently (row-sharding across GPUs, generator fused into the
+inverse CDF); it is not scipy's PCG64 Fisher-Yates stream, which is sequential by
+construction.  For that method bit-level parity with the reference holds at
+Node.sample_from_quantiles (identical quantiles in give identical samples out), or end to end
+with stream="reference".
 """
 
 import ctypes
@@ -215,19 +223,6 @@ class DeviceMatrixSource(QuantileSource):
         return ("vector", col, col.stride(0))
 
 
-class UniformSource(QuantileSource):
-    def __init__(self, n, d, seed):
-        super().__init__(n, d)
-        self.seed = seed
-
-    def column(self, c):
-        out = device.empty(self.rows)
-        lib = _lib.load()
-        _lib.check(lib.pbh_fill_uniform(self.seed, self.row0, self.rows, c, 1, out.data_ptr(), max(self.rows, 1),
-                                        device.stream()), "pbh_fill_uniform")
-        return ("vector", out, 1)
-
-
 class MT19937Source(QuantileSource):
     """RandomState.random((n, d)) bit for bit (modeling.py:484-486 with random_state None, an
     int or a RandomState), generated on the device (pbh_mt19937_random) at the first column.
@@ -323,6 +318,59 @@ class LHSSource(QuantileSource):
         return out
 
 
+class ReferenceLHSSource(QuantileSource):
+    """scipy.stats.qmc.LatinHypercube(d, rng=random_state).random(n) bit for bit: the
+    reference's own LHS stream (modeling.py:480,488), opt-in with stream="reference".
+
+    The engine's owned Generator is set up exactly as scipy does (engine_rng: a spawned child,
+    which also advances a caller Generator's seed sequence as scipy would); the n x d uniforms
+    come from the device PCG64 (pbh_pcg64_random) and the d Fisher-Yates shuffles, one
+    sequential stream by construction, from host threads inside pbh_lhs_reference.  The whole
+    matrix is generated at the first column (no row sharding: the shuffles are global)."""
+
+    def __init__(self, n, d, rng):
+        super().__init__(n, d)
+        if n >= 2 ** 31:
+            raise NotImplementedError("the reference LHS stream is supported for n < 2**31")
+        st = engine_rng(rng).bit_generator.state
+        self.state, self.inc = int(st["state"]["state"]), int(st["state"]["inc"])
+        self.has32, self.buf32 = int(st["has_uint32"]), int(st["uinteger"])
+        self.q = None
+
+    def shard(self, row0, rows):
+        if (row0, rows) != (0, self.n):
+            raise NotImplementedError("the reference LHS stream is sequential: it cannot be row-sharded")
+        return self
+
+    def matrix(self):
+        if self.q is None and self.n > 0 and self.d > 0:
+            lib = _lib.load()
+            ws = _workspace(lib.pbh_lhs_reference_workspace_size, self.n, self.d)
+            self.q = device.empty((self.d, self.n))
+            s, inc = _u128_words(self.state), _u128_words(self.inc)
+            _lib.check(lib.pbh_lhs_reference(_lib.np_ptr(s), _lib.np_ptr(inc), self.has32, self.buf32, self.n, self.d,
+                                             self.q.data_ptr(), self.n, ws.data_ptr(), ws.numel(), device.stream()),
+                       "pbh_lhs_reference")
+        return self.q
+
+    def column(self, c):
+        return ("vector", self.matrix()[c], 1)
+
+
+_DEFAULT_STREAM = os.environ.get("PBH_LHS_STREAM", "native")
+
+
+def set_default_stream(stream):
+    """Module default for Node.sample(method="lhs", stream=None): "native" (the counter-based
+    design, fused into the inverse-CDF kernels; the default) or "reference" (scipy's
+    LatinHypercube stream bit for bit).  The environment variable PBH_LHS_STREAM sets the
+    initial value."""
+    global _DEFAULT_STREAM
+    if stream not in ("native", "reference"):
+        raise ValueError(f"stream must be 'native' or 'reference', got {stream!r}")
+    _DEFAULT_STREAM = stream
+
+
 class SobolSource(QuantileSource):
     def __init__(self, n, d, rng, bits=30):
         super().__init__(n, d)
@@ -401,11 +449,18 @@ class HaltonSource(QuantileSource):
         return ("vector", self.q[c], 1)
 
 
-def make_source(method, n, d, random_state):
+def make_source(method, n, d, random_state, stream=None):
+    """The quantile source of Node.sample (modeling.py:478-489).  `stream` only matters for
+    method="lhs": "native" (default) or "reference" (see set_default_stream)."""
+    stream = _DEFAULT_STREAM if stream is None else stream
+    if stream not in ("native", "reference"):
+        raise ValueError(f"stream must be 'native' or 'reference', got {stream!r}")
     if method is None:
         return pseudo_random_source(n, d, random_state)
     m = method.lower().strip()
     if m == "lhs":
+        if stream == "reference":
+            return ReferenceLHSSource(n, d, random_state)
         return LHSSource(n, d, seed_from(random_state))
     if m == "sobol":
         return SobolSource(n, d, random_state)

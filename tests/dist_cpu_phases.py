@@ -59,7 +59,7 @@ class CpuPhases:
         q = (t + 1 - self.us[col.lhs_col][rows]) / n
         x = _ppf(col, q)
         if not np.isfinite(x).all():
-            flag += 1
+            flag |= 1  # the kernels' atomicOr of bit 0
         return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64))
 
     def sorted_check(self, x):

@@ -20,7 +20,10 @@ CASES = {
     "mixed": (3001, [(0, [0.0, 1.0]), (6, [4.0, 0.0]), (5, [2.0, 0.0, 1.0]), (4, [0.3, 0.0, 1.0]),
                      (6, [30.0, 0.0])]),
     "two": (2048, [(0, [5.0, 2.0]), (5, [0.7, 0.0, 3.0])]),
+    # lognorm(s=1000) overflows to inf above q ~ 0.76 (and to 0 below ~ 0.23): flag bit 0
+    "nonfinite": (2001, [(0, [0.0, 1.0]), (3, [1000.0, 0.0, 1.0]), (5, [2.0, 0.0, 1.0])]),
 }
+EXPECTED_FLAGS = {"mixed": [0, 0, 0, 0, 0], "two": [0, 0], "nonfinite": [0, 1, 0]}
 
 
 def _free_port():
@@ -48,9 +51,10 @@ def _worker(rank, world, port, case, outdir):
         n, spec = CASES[case]
         perms, us = design(n, len(spec), seed=3)
         P = np.linalg.cholesky(cfg3_corr(len(spec)))
-        Y = iman_conover_lhs(_columns(spec), P, n, phases=CpuPhases(perms, us),
-                             flags=torch.zeros(len(spec), dtype=torch.int32))
+        flags = torch.zeros(len(spec), dtype=torch.int32)
+        Y = iman_conover_lhs(_columns(spec), P, n, phases=CpuPhases(perms, us), flags=flags)
         np.save(os.path.join(outdir, f"y{rank}.npy"), Y.numpy())
+        np.save(os.path.join(outdir, f"f{rank}.npy"), flags.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -70,6 +74,9 @@ def test_sharded_ic_matches_single_process_oracle(world, case):
         mp.start_processes(_worker, args=(world, _free_port(), case, d), nprocs=world, join=True,
                            start_method="spawn")
         parts = [np.load(os.path.join(d, f"y{r}.npy")) for r in range(world)]
+        flags = [np.load(os.path.join(d, f"f{r}.npy")).tolist() for r in range(world)]
+    # flag words are OR-combined across ranks (bits unchanged), identical on every rank
+    assert flags == [EXPECTED_FLAGS[case]] * world
     b = shard_bounds(n, world)
     for r, part in enumerate(parts):
         assert part.shape == (len(spec), b[r + 1] - b[r])

@@ -160,3 +160,90 @@ def test_halton_node_sample(gpu):
     Q = scipy.stats.qmc.Halton(2, rng=4).random(513)
     ref = scipy.stats.norm(1, 2).ppf(Q[:, 0]) * scipy.stats.expon(scale=3).ppf(Q[:, 1])
     np.testing.assert_allclose(out, ref, rtol=1e-10)
+
+
+# ---------------------------------------------------------------- reference LHS stream (row a2)
+@pytest.mark.parametrize("key,d,seed,n", [("lhs_d8_s0_n4096", 8, 0, 4096), ("lhs_d3_s123_n1000", 3, 123, 1000)])
+def test_reference_lhs_matches_golden(gpu, key, d, seed, n):
+    """stream="reference": LatinHypercube(d, rng=seed).random(n) bit for bit, against the
+    vectors the reference's scipy produced (tests/golden/make_golden.py)."""
+    from probabilit_amd import qmc
+
+    src = qmc.make_source("lhs", n, d, seed, stream="reference")
+    np.testing.assert_array_equal(_src_matrix(src), golden("streams.npz")[key])
+
+
+@pytest.mark.parametrize("n,d,seed", [(1, 1, 0), (2, 3, 5), (50_000, 32, 9), (1_000_003, 4, 2)])
+def test_reference_lhs_matches_scipy(gpu, n, d, seed):
+    import scipy.stats
+
+    from probabilit_amd import qmc
+
+    src = qmc.make_source("lhs", n, d, seed, stream="reference")
+    np.testing.assert_array_equal(_src_matrix(src), scipy.stats.qmc.LatinHypercube(d=d, rng=seed).random(n))
+
+
+def test_reference_lhs_generator_spawn(gpu):
+    """A Generator passed as random_state is used the way scipy uses it (an owned child is
+    spawned from it), so the caller's generator ends in the same state as under scipy."""
+    import scipy.stats
+
+    from probabilit_amd import qmc
+
+    g, ref = np.random.default_rng(21), np.random.default_rng(21)
+    q = _src_matrix(qmc.make_source("lhs", 777, 5, g, stream="reference"))
+    np.testing.assert_array_equal(q, scipy.stats.qmc.LatinHypercube(d=5, rng=ref).random(777))
+    np.testing.assert_array_equal(g.random(4), ref.random(4))
+
+
+def test_docstring_pin_lhs_reference_stream(gpu):
+    """modeling.py:448-449: result.sample(size=5, random_state=0, method="lhs")."""
+    from probabilit_amd.modeling import Distribution
+
+    result = 2 * Distribution("expon", scale=1 / 3)
+    out = result.sample(size=5, random_state=0, method="lhs", stream="reference")
+    # the doctest shows numpy's 8-decimal repr: agreement to half a unit in the 8th decimal
+    np.testing.assert_allclose(out, [1.11212876, 0.273718, 0.03808862, 0.5702549, 0.83779147], rtol=0, atol=5e-9)
+    # and the exact value: scipy's LatinHypercube quantiles through scipy's expon ppf, times 2
+    import scipy.stats
+
+    q = scipy.stats.qmc.LatinHypercube(d=1, rng=0).random(5)[:, 0]
+    np.testing.assert_allclose(out, 2 * scipy.stats.expon(scale=1 / 3).ppf(q), rtol=1e-10, atol=0)
+
+
+def test_reference_lhs_module_default(gpu):
+    from probabilit_amd import qmc
+    from probabilit_amd.modeling import Distribution
+
+    x = Distribution("norm")
+    native = x.sample(100, random_state=3, method="lhs").copy()
+    qmc.set_default_stream("reference")
+    try:
+        ref = x.sample(100, random_state=3, method="lhs")
+    finally:
+        qmc.set_default_stream("native")
+    import scipy.stats
+
+    q = scipy.stats.qmc.LatinHypercube(d=1, rng=3).random(100)[:, 0]
+    np.testing.assert_allclose(ref, scipy.stats.norm.ppf(q), rtol=1e-10, atol=0)
+    assert not np.array_equal(native, ref)
+    np.testing.assert_array_equal(x.sample(100, random_state=3, method="lhs"), native)
+
+
+def test_reference_lhs_correlated_dag_matches_reference_pipeline(gpu):
+    """The cfg3 graph (d=32) on the reference stream: the whole reference computation
+    (scipy LHS -> scipy ppf -> Iman-Conover, oracle.pipeline) on the same seed, values
+    within 1e-10 and identical ranks (a rank difference moves a value by a whole spacing)."""
+    from oracle import ic as oic
+    from oracle.pipeline import cfg3_corr, cfg_dists, lhs_quantiles, ppf_columns
+    from probabilit_amd.modeling import Distribution, NoOp
+
+    from conftest import assert_close
+
+    n, d, seed = 20_000, 32, 11
+    ds = [Distribution(nm, **kw) for nm, kw in cfg_dists(d)]
+    C = cfg3_corr(d)
+    NoOp(*ds).correlate(*ds, corr_mat=C).sample(n, random_state=seed, method="lhs", stream="reference")
+    Y = np.column_stack([x.samples_ for x in ds])
+    ref = oic.iman_conover(ppf_columns(lhs_quantiles(n, d, seed), cfg_dists(d)), C)["Y"]
+    assert_close(Y, ref, rtol=1e-10, what="reference-stream cfg3 DAG vs the reference pipeline")

@@ -263,3 +263,14 @@ def test_set_target_validation():
         ImanConover().set_target(np.array([[2.0, 0], [0, 1]]))
     t = ImanConover().set_target(np.array([[1, 0.5], [0.5, 1]]))
     np.testing.assert_allclose(t.P @ t.P.T, t.C)
+
+
+def test_top_level_names_match_reference():
+    """probabilit/__init__.py:16-27 exports these names; the drop-in has every one of them."""
+    import probabilit_amd
+
+    ref_all = ["Distribution", "Constant", "EmpiricalDistribution", "CumulativeDistribution",
+               "DiscreteDistribution", "Equal", "scalar_transform", "MultivariateDistribution", "PERT", "plot"]
+    assert probabilit_amd.__all__ == ref_all
+    for name in ref_all:
+        assert callable(getattr(probabilit_amd, name))

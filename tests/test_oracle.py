@@ -181,3 +181,19 @@ def test_permutation_correlator_validation():
     pc = PermutationCorrelator().set_target(np.array([[1.0, 0.5], [0.5, 1.0]]), weights=np.array([[1, 2], [2, 1]]))
     assert np.allclose(pc.weights, np.array([[1, 2], [2, 1]]) / 6)
     assert pc._error(np.eye(2), pc.C) == pytest.approx(np.sqrt(2 / 6 * 0.25))
+
+
+def test_threaded_oracle_is_bit_identical():
+    """The thread-pooled forms used by the large parity tests (oracle.ic threads=,
+    oracle.pipeline.ppf_columns threads=) give exactly the sequential results."""
+    from oracle import ic
+    from oracle.pipeline import cfg3_corr, cfg_dists, lhs_quantiles, ppf_columns
+
+    n, d = 30_000, 16
+    Q = lhs_quantiles(n, d, 5)
+    X1 = ppf_columns(Q, cfg_dists(d))
+    X4 = ppf_columns(Q, cfg_dists(d), threads=4, chunk=7_001)
+    np.testing.assert_array_equal(X1, X4)
+    a, b = ic.iman_conover(X1, cfg3_corr(d)), ic.iman_conover(X1, cfg3_corr(d), threads=4)
+    for key in ("Y", "S", "E", "CS", "idx"):
+        np.testing.assert_array_equal(a[key], b[key], err_msg=key)

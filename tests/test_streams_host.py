@@ -107,3 +107,50 @@ def test_check_random_state_semantics():
     assert check_random_state(g) is g
     with pytest.raises(ValueError):
         check_random_state("x")
+
+
+# ---------------------------------------------------------------- reference LHS shuffles (host half)
+@pytest.mark.parametrize("n,d,seed,draws", [(1, 1, 0, 0), (7, 5, 9, 0), (4096, 8, 0, 0), (100_000, 32, 3, 5),
+                                            (20_001, 1, 4, 1)])
+def test_lhs_reference_perms_match_numpy_shuffle(n, d, seed, draws):
+    """pbh_lhs_reference_perms (host C++, the sequential half of the reference LHS stream)
+    against numpy's Generator.shuffle on the same PCG64 state, LatinHypercube._random_lhs's
+    d shuffles of arange(1, n + 1) after rng.uniform(size=(n, d)); the final state (with the
+    buffered 32-bit half) must match too.  `draws` 32-bit draws first leave a buffered half."""
+    from probabilit_amd import _lib, qmc
+
+    lib = _lib.load()  # host-only entry point: no GPU is touched
+    g = np.random.default_rng(seed)
+    g.integers(0, 2, size=draws, dtype=np.uint32)
+    g.uniform(size=(n, d))
+    st = g.bit_generator.state
+    ref = np.tile(np.arange(1, n + 1), (d, 1))
+    for i in range(d):
+        g.shuffle(ref[i])
+    out = np.empty((d, n), dtype=np.int32)
+    so = np.zeros(4, dtype=np.uint64)
+    sw, iw = qmc._u128_words(st["state"]["state"]), qmc._u128_words(st["state"]["inc"])
+    _lib.check(lib.pbh_lhs_reference_perms(_lib.np_ptr(sw), _lib.np_ptr(iw), st["has_uint32"], st["uinteger"], n, d,
+                                           _lib.np_ptr(out), _lib.np_ptr(so)))
+    np.testing.assert_array_equal(out, ref)
+    end = g.bit_generator.state
+    assert (int(so[0]) | (int(so[1]) << 64)) == end["state"]["state"]
+    assert (int(so[2]), int(so[3])) == (end["has_uint32"], end["uinteger"])
+
+
+def test_lhs_reference_perms_vs_oracle_restatement():
+    """The same host half against the oracle's pure-Python restatement of _random_lhs
+    (oracle/streams.py lhs_reference), which tests/test_oracle.py pins to the golden LHS."""
+    from oracle import streams
+    from probabilit_amd import _lib, qmc
+
+    lib = _lib.load()
+    n, d = 300, 4
+    eng = qmc.engine_rng(5)
+    st = eng.bit_generator.state
+    s, inc = int(st["state"]["state"]), int(st["state"]["inc"])
+    q = streams.lhs_reference((s, inc), n, d)
+    out = np.empty((d, n), dtype=np.int32)
+    sw, iw = qmc._u128_words(qmc.pcg64_advance(s, inc, n * d)), qmc._u128_words(inc)
+    _lib.check(lib.pbh_lhs_reference_perms(_lib.np_ptr(sw), _lib.np_ptr(iw), 0, 0, n, d, _lib.np_ptr(out), None))
+    np.testing.assert_array_equal(out.T, np.ceil(q * n).astype(np.int64))
