@@ -28,26 +28,30 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
 
 
+# Algorithmic HBM bytes per row of ONE launch of each timed kernel (SURVEY.md §8(d) unit
+# figures, restated for the kernels this build runs; step 4 = the generated-column path of
+# pbh_step4.hip).  A launch covers one column, except the kernels in ALL_COLUMNS (k columns).
+LAUNCH_BYTES = {
+    "k_lhs_sorted_ppf": 8,       # write sort(X) 8 (stratum-ordered generation, fused tie/inversion counts)
+    "k_perm_scores": 8,          # write S 8 (ranks from the LHS permutation: no sort of X)
+    "k_gram": 8,                 # read S 8                                   (all columns)
+    "k_apply": 20,               # read S 8, write CS 8 + code 4              (all columns)
+    "k_hist16": 4,               # read code 4                                (all columns)
+    "k_msd1": 12,                # read code 4, write code 4 + row 4
+    "k_msd2": 14,                # read code 4 + row 4, write low16 2 + row 4
+    "k_finish": 14,              # bucket finish: read low16 2 + row 4, write (row, p) 8
+    "k_place_msd": 16,           # one row-placement MSD pass: read 8 + write 8
+    "k_place_gen": 16,           # read (row, p) 8, write Y 8 (sort(X)[p] regenerated, not read)
+    # the general path (columns whose codes are not flat, or with runs beyond the finish)
+    "k_digit_hist<u32>": 4, "k_scatter<u32>": 16, "k_code_runs": 17, "k_scatter<place>": 24, "k_place": 20,
+    "k_lhs_ppf": 8, "k_ppf": 16, "k_elementwise": 24,
+}
+ALL_COLUMNS = {"k_gram", "k_apply", "k_hist16"}
+
+
 def kernel_bytes(name, n, k):
-    """Algorithmic HBM bytes of ONE launch of `name` over n rows (k = columns where a launch
-    covers all of them).  SURVEY.md §8(d) per-unit figures."""
-    per_elem = {"k_lhs_ppf": 8, "k_ppf": 16, "k_lhs_sorted_ppf": 8, "k_perm_scores": 8,
-                "k_scatter": 24, "k_upsweep": 8, "k_digit_hist": 8,               # u64 key + u32 row
-                "k_scatter<u32>": 16, "k_upsweep<u32>": 4, "k_digit_hist<u32>": 4,  # u32 code + u32 row
-                "k_rank_finish<scores>": 28,  # read key 8 + row 4, write score 8 + sorted x 8
-                "k_rank_finish<gather>": 21,  # read eqprev 1 + row 4 + sorted x 8, write y 8 (idx only in debug calls)
-                "k_load_keys": 16, "k_make_codes": 12,
-                # step-4 bucket finish (k_bucket_starts: codes 4; k_code_buckets: codes 4 + rows 4 in,
-                # rows 4 + eqprev 1 out) -- the four-pass fallback's run fix-up moves 13
-                "k_code_runs": 17,
-                "k_scatter<place>": 24,  # row u32 + value f64, read and written
-                "k_place": 20,  # row 4 + value 8 in, y 8 out
-                "k_elementwise": 24, "k_head_bounds": 8, "k_scan": 0}
-    if name == "k_gram":
-        return 8 * n * k
-    if name == "k_apply":
-        return 16 * n * k
-    return per_elem.get(name, 0) * n
+    """Algorithmic bytes of ONE launch of `name` over n rows (k columns for ALL_COLUMNS)."""
+    return LAUNCH_BYTES.get(name, 0) * n * (k if name in ALL_COLUMNS else 1)
 
 
 # bench (HIP-event) kernel names -> rocprofv3 kernel names in the committed PMC summaries

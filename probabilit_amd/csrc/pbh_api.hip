@@ -13,6 +13,7 @@
 #include "pbh_ic.h"
 #include "pbh_lhs.h"
 #include "pbh_sort.h"
+#include "pbh_step4.h"
 
 namespace pbh {
 
@@ -58,6 +59,8 @@ struct IcLayout {
   void* heads_ws;
   uint32_t* codes;              // K x n step-4 sort keys, written by the step-3 kernel
   double* colpart;              // K x perm_scores_blocks(n) per-block score sums (step-2 means)
+  void* s4shared;               // step 4 of generated columns: per-column histograms, cursors
+  void* s4column;               //   and one column's staging (pbh_step4.hip)
 };
 
 size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
@@ -77,7 +80,11 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* hws = c.take(run_heads_ws_bytes(n));
   void* codes = c.take((size_t)n * k * 4);
   void* colpart = c.take((size_t)k * perm_scores_blocks(n) * 8);
+  void* s4s = c.take(step4_gen_shared_bytes(k));
+  void* s4c = c.take(step4_gen_column_bytes(n) * step4_streams());
   if (carve) {
+    L->s4shared = s4s;
+    L->s4column = s4c;
     L->colpart = (double*)colpart;
     L->codes = (uint32_t*)codes;
     L->S = (double*)S;
@@ -176,6 +183,22 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     return PBH_ERR_WORKSPACE;
   }
   hipStream_t s = as_stream(stream);
+  // host buffers that asynchronous copies read or write: declared before the guard, whose
+  // destructor synchronises the stream on every return (error returns included), so that no
+  // copy outlives them
+  std::vector<unsigned long long> cnt_host(2 * (size_t)k, 0);
+  std::vector<double> G((size_t)k * k), Lc((size_t)k * k), invd(k), P((size_t)k * k);
+  std::vector<int32_t> state(k), flags(k);
+  std::vector<uint32_t> hists_host;
+  int32_t flag_host = 0;
+  struct SyncOnExit {
+    hipStream_t s;
+    bool side = false;
+    ~SyncOnExit() {
+      if (side) step4_sync_side_streams();  // step 4's side streams too (an error return mid-loop)
+      (void)hipStreamSynchronize(s);
+    }
+  } sync_on_exit{s};
   ReorderWs rw;
   int st = reorder_carve(L.reorder_ws, n, rw, s);
   if (st) return st;
@@ -185,16 +208,25 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   // ---- step 1: van der Waerden scores of every column (+ the sorted column for step 4)
   PBH_CHECK_HIP(hipMemsetAsync(L.flag, 0, sizeof(int32_t), s));
   bool all_generated = true;  // every column's scores came from perm_scores (with partial sums)
+  std::vector<char> regenerable(k, 0);  // step 4 may regenerate sort(X[:, c])[p] from p (gen_place)
   // Generated columns: every sorted column first, with its tie / inversion counts, then one
   // readback for all of them (instead of a stream sync per column).
-  std::vector<unsigned long long> cnt_host(2 * (size_t)k, 0);
+  // the generated columns' inverse-CDF setups (tables built once, for step 1 and step 4)
+  struct Gens {
+    std::vector<GenColumn*> g;
+    hipStream_t s;
+    ~Gens() {
+      for (GenColumn* x : g) gen_destroy(x, s);
+    }
+  } gens{std::vector<GenColumn*>(a->columns ? k : 0, nullptr), s};
   if (a->columns) {
     for (int c = 0; c < k; ++c) {
       const pbh_ic_column& g = a->columns[c];
       pbh_param prm[3];
       for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
-      st = lhs_sorted_ppf(g.seed, n, 0, n, g.lhs_col, g.dist, prm, g.nparams, L.sorted_x + (int64_t)c * n,
-                          g.nonfinite_flag, s, L.counts + 2 * c);
+      st = gen_create(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, &gens.g[c], s);
+      if (st) return st;
+      st = gen_sorted(gens.g[c], 0, n, L.sorted_x + (int64_t)c * n, g.nonfinite_flag, L.counts + 2 * c, s);
       if (st) return st;
     }
     PBH_CHECK_HIP(hipMemcpyAsync(cnt_host.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
@@ -222,6 +254,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
         st = perm_scores(g.seed, n, g.lhs_col, 0, n, heads, nheads, S_c, s,
                          L.colpart + (int64_t)c * perm_scores_blocks(n));
         if (st) return st;
+        regenerable[c] = 1;
         continue;
       }
       // not monotone on this grid: materialise the column in row order and sort it
@@ -242,7 +275,6 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
     if (st) return st;
   }
-  int32_t flag_host = 0;
   PBH_CHECK_HIP(hipMemcpyAsync(&flag_host, L.flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   if (a->scores_out)
     PBH_CHECK_HIP(hipMemcpyAsync(a->scores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
@@ -255,7 +287,6 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   if (st) return st;
   st = centered_gram(L.S, n, k, n, L.means, L.partials, L.gram, s);
   if (st) return st;
-  std::vector<double> G((size_t)k * k), Lc((size_t)k * k);
   PBH_CHECK_HIP(hipMemcpyAsync(G.data(), L.gram, (size_t)k * k * 8, hipMemcpyDeviceToHost, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));
   if (flag_host) {
@@ -264,7 +295,6 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   }
   st = ic_factor(G.data(), n, k, a->corr_host_out, Lc.data());
   if (st) return st;
-  std::vector<double> invd(k), P((size_t)k * k);
   for (int j = 0; j < k; ++j) invd[j] = 1.0 / Lc[(size_t)j * k + j];
   for (int i = 0; i < k; ++i)
     for (int j = 0; j < k; ++j) P[(size_t)i * k + j] = j <= i ? a->target_chol_host[(size_t)i * k + j] : 0.0;
@@ -279,27 +309,82 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     PBH_CHECK_HIP(hipMemcpyAsync(a->cscores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
 
   // ---- step 4: Y[:, c] = sort(X[:, c])[rankdata(CS[:, c]).astype(int) - 1]
-  // The code histograms of all columns up front, one readback for the bucket-path decisions.
-  uint32_t* hists = nullptr;
-  std::vector<uint32_t> hists_host;
-  if (code_buckets_enabled(n)) {
-    PBH_CHECK_HIP(hipMallocAsync((void**)&hists, (size_t)k * 1024 * 4, s));
+  auto general = [&](int c) {  // the general path (sorted X read from the workspace)
+    return reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
+                          a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n);
+  };
+  bool any_regen = false;
+  for (int c = 0; c < k; ++c) any_regen |= regenerable[c] != 0;
+  if (a->columns && any_regen && step4_gen_enabled(n)) {
+    // generated columns: MSD code passes + bucket finish + row placement, sort(X)[p]
+    // regenerated (pbh_step4.hip); one readback for all columns' flatness before, one for
+    // over-long runs after
+    Step4Shared sh;
+    step4_gen_carve_shared(L.s4shared, k, sh);
+    const int ns = step4_streams();
+    sync_on_exit.side = ns > 1;
+    Step4Column cbs[kStep4MaxStreams];
+    hipStream_t ss[kStep4MaxStreams];
+    for (int i = 0; i < ns; ++i) {
+      step4_gen_carve_column((char*)L.s4column + (size_t)i * step4_gen_column_bytes(n), n, cbs[i]);
+      ss[i] = ns > 1 ? step4_side_stream(i) : s;
+      if (!ss[i]) ss[i] = s;
+    }
+    st = step4_gen_hist(L.codes, n, n, sh, s);
+    if (st) return st;
+    PBH_CHECK_HIP(hipMemcpyAsync(state.data(), sh.state, (size_t)k * 4, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));  // everything before is complete: the side streams may start
+    int next = 0;
     for (int c = 0; c < k; ++c) {
-      st = code_hist(L.codes + (int64_t)c * n, n, hists + (size_t)c * 1024, s);
+      if (state[c] != 0 || !regenerable[c]) continue;
+      const int i = next++ % ns;
+      hipStream_t cs_ = ss[i];
+      st = step4_gen_column(c, L.codes + (int64_t)c * n, L.S + (int64_t)c * n, n, sh, cbs[i], cs_);
+      if (st) return st;
+      int buf = 0;
+      st = step4_gen_place_passes(n, cbs[i], sh.flags + c, cs_, &buf);
+      if (st) return st;
+      st = gen_place(gens.g[c], cbs[i].pairs[buf], n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
+                     a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, sh.flags + c, cs_);
       if (st) return st;
     }
-    hists_host.resize((size_t)k * 1024);
-    PBH_CHECK_HIP(hipMemcpyAsync(hists_host.data(), hists, (size_t)k * 1024 * 4, hipMemcpyDeviceToHost, s));
+    for (int i = 0; i < ns; ++i) {  // the caller's stream continues after every side stream
+      if (ss[i] == s) continue;
+      PBH_CHECK_HIP(hipStreamSynchronize(ss[i]));
+    }
+    PBH_CHECK_HIP(hipMemcpyAsync(flags.data(), sh.flags, (size_t)k * 4, hipMemcpyDeviceToHost, s));
     PBH_CHECK_HIP(hipStreamSynchronize(s));
-  }
-  for (int c = 0; c < k; ++c) {
-    const uint32_t* hc = hists ? hists + (size_t)c * 1024 : nullptr;
-    const int flat = hists ? (code_hist_flat(hists_host.data() + (size_t)c * 1024, n) ? 1 : 0) : 1;
-    st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
-                        a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n, hc, flat);
+    for (int c = 0; c < k; ++c) {
+      if (state[c] == 0 && regenerable[c] && flags[c] == 0) continue;
+      st = general(c);  // not flat, not regenerable, or a run of equal codes beyond the finish
+      if (st) return st;
+    }
+  } else {
+    // The code histograms of all columns up front, one readback for the bucket-path decisions.
+    uint32_t* hists = nullptr;
+    if (code_buckets_enabled(n)) {
+      PBH_CHECK_HIP(hipMallocAsync((void**)&hists, (size_t)k * 1024 * 4, s));
+      for (int c = 0; c < k; ++c) {
+        st = code_hist(L.codes + (int64_t)c * n, n, hists + (size_t)c * 1024, s);
+        if (st) {
+          (void)hipFreeAsync(hists, s);
+          return st;
+        }
+      }
+      hists_host.resize((size_t)k * 1024);
+      PBH_CHECK_HIP(hipMemcpyAsync(hists_host.data(), hists, (size_t)k * 1024 * 4, hipMemcpyDeviceToHost, s));
+      PBH_CHECK_HIP(hipStreamSynchronize(s));
+    }
+    for (int c = 0; c < k && st == PBH_OK; ++c) {
+      const uint32_t* hc = hists ? hists + (size_t)c * 1024 : nullptr;
+      const int flat = hists ? (code_hist_flat(hists_host.data() + (size_t)c * 1024, n) ? 1 : 0) : 1;
+      st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
+                          a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n, hc,
+                          flat);
+    }
+    if (hists) PBH_CHECK_HIP(hipFreeAsync(hists, s));
     if (st) return st;
   }
-  if (hists) PBH_CHECK_HIP(hipFreeAsync(hists, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // host vectors above were sources of async copies
   return PBH_OK;
 }

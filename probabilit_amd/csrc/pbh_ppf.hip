@@ -11,6 +11,7 @@
 #include "pbh_rng.h"
 #include "pbh_special.h"
 #include "pbh_sort.h"
+#include "pbh_step4.h"
 #include "pbh_timing.h"
 
 namespace pbh {
@@ -501,6 +502,137 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_sorted_ppf(uint64_t seed
   }
 }
 
+// ---------------------------------------------------------------- step-4 placement, generated columns
+// The last pass of Iman-Conover step 4 for a generated column (pbh_step4.hip): the pairs
+// (row << 32 | p) of every block of 4096 consecutive rows are together, and Y[row] = sort(X)[p]
+// is this column's value in stratum p, regenerated here (lhs_sorted_quantile + ppf_one: the
+// same function k_lhs_sorted_ppf evaluates, so bit-identical to the stored sorted column)
+// instead of being carried through the placement passes.  The block is assembled in LDS and
+// written out contiguously.  norm / lognorm compact ndtri's tail (TailQueue, positions = row
+// offsets in the block); gamma / poisson stage their tables in LDS (random p: table gathers).
+constexpr int kGenRows = 1 << kGenPlaceShift;
+
+template <int D>
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __restrict__ pairs, int64_t n,
+                                                      uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
+                                                      double* __restrict__ y, int64_t y_rs, int32_t* __restrict__ idx,
+                                                      const int32_t* __restrict__ state) {
+  if (state && *state) return;
+  constexpr bool kCompact = D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM;
+  __shared__ double buf[kGenRows];
+  __shared__ TailQueue tq;
+  Philox ph(seed);
+  const double p0 = prm.val[0], p1 = prm.val[1], p2 = prm.val[2];
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
+    for (int h = 0; h < kGenRows; h += kCTile) {
+      if (kCompact) {
+        if (threadIdx.x == 0) tq.count = 0;
+        __syncthreads();
+      }
+#pragma unroll
+      for (int j = 0; j < kCIpt; ++j) {
+        const int p = h + j * kBlock + threadIdx.x;
+        const bool valid = p < cnt;
+        double q = 0.5;
+        int off = 0;
+        if (valid) {
+          const uint64_t pr = pairs[r0 + p];
+          const uint32_t t = (uint32_t)pr;
+          const int64_t row = (int64_t)(pr >> 32);
+          if (idx) idx[row] = (int32_t)t;
+          off = (int)(row - r0);
+          q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
+        }
+        if constexpr (kCompact) {
+          const bool tail = valid && sf::ndtri_takes_tail(q);
+          if (valid && !tail) buf[off] = ppf_one<D, 1>(q, p0, p1, p2, pt);
+          tail_push(tq, tail, q, off);
+        } else {
+          if (valid) buf[off] = ppf_one<D>(q, p0, p1, p2, pt);
+        }
+      }
+      if (kCompact) {
+        __syncthreads();
+        const int T = tq.count;
+        for (int i = threadIdx.x; i < T; i += kBlock) buf[tq.pos[i]] = ppf_one<D, 2>(tq.arg[i], p0, p1, p2, pt);
+      }
+    }
+    __syncthreads();
+    if (y_rs == 1) {
+      for (int p = threadIdx.x; p < cnt; p += kBlock) y[r0 + p] = buf[p];
+    } else {
+      for (int p = threadIdx.x; p < cnt; p += kBlock) y[(r0 + p) * y_rs] = buf[p];
+    }
+    __syncthreads();
+  }
+}
+
+// gamma with the guide table in LDS (120 KiB) next to the block (32 KiB): one 1024-thread
+// workgroup per CU
+__global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __restrict__ pairs, int64_t n,
+                                                             uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
+                                                             double* __restrict__ y, int64_t y_rs,
+                                                             int32_t* __restrict__ idx,
+                                                             const int32_t* __restrict__ state) {
+  if (state && *state) return;
+  __shared__ double lds[kGTable];
+  __shared__ double buf[kGenRows];
+  const sf::GammaGuide T = stage_guide(pt.guide, lds);
+  Philox ph(seed);
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
+    for (int p = threadIdx.x; p < cnt; p += kGBlock) {
+      const uint64_t pr = pairs[r0 + p];
+      const uint32_t t = (uint32_t)pr;
+      const int64_t row = (int64_t)(pr >> 32);
+      if (idx) idx[row] = (int32_t)t;
+      buf[row - r0] = gamma_ppf_lds(lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n), prm, pt, T);
+    }
+    __syncthreads();
+    if (y_rs == 1) {
+      for (int p = threadIdx.x; p < cnt; p += kGBlock) y[r0 + p] = buf[p];
+    } else {
+      for (int p = threadIdx.x; p < cnt; p += kGBlock) y[(r0 + p) * y_rs] = buf[p];
+    }
+    __syncthreads();
+  }
+}
+
+// poisson with the CDF table + guide in (dynamic) LDS
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_poisson(const uint64_t* __restrict__ pairs, int64_t n,
+                                                              uint64_t seed, uint32_t col, Params prm,
+                                                              PoissonTable pt, double* __restrict__ y, int64_t y_rs,
+                                                              int32_t* __restrict__ idx,
+                                                              const int32_t* __restrict__ state) {
+  if (state && *state) return;
+  extern __shared__ double plds[];
+  __shared__ double buf[kGenRows];
+  const PoissonTable T = stage_poisson(pt, plds);
+  Philox ph(seed);
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
+    for (int p = threadIdx.x; p < cnt; p += kBlock) {
+      const uint64_t pr = pairs[r0 + p];
+      const uint32_t t = (uint32_t)pr;
+      const int64_t row = (int64_t)(pr >> 32);
+      if (idx) idx[row] = (int32_t)t;
+      const double q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
+      buf[row - r0] = ppf_one<PBH_DIST_POISSON>(q, prm.val[0], prm.val[1], prm.val[2], T);
+    }
+    __syncthreads();
+    if (y_rs == 1) {
+      for (int p = threadIdx.x; p < cnt; p += kBlock) y[r0 + p] = buf[p];
+    } else {
+      for (int p = threadIdx.x; p < cnt; p += kBlock) y[(r0 + p) * y_rs] = buf[p];
+    }
+    __syncthreads();
+  }
+}
+
 // counts[0] += #(x[t] == x[t+1]), counts[1] += #(x[t] > x[t+1] or unordered)
 __global__ __launch_bounds__(kBlock) void k_check_sorted(const double* __restrict__ x, int64_t n,
                                                          unsigned long long* counts) {
@@ -959,26 +1091,54 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
 
 }  // namespace
 
-int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist, const pbh_param* params,
-                   int nparams, double* out, int32_t* flag, hipStream_t s, unsigned long long* counts) {
-  PBH_REQUIRE(t0 >= 0 && nt >= 0 && t0 + nt <= n, "lhs_sorted_ppf: strata [%lld, %lld) outside [0, %lld)",
-              (long long)t0, (long long)(t0 + nt), (long long)n);
-  if (nt == 0) return PBH_OK;
-  for (int j = 0; j < nparams; ++j)
-    PBH_REQUIRE(params[j].ptr == nullptr, "stratum-ordered LHS generation needs scalar parameters");
+struct GenColumn {
+  uint64_t seed;
+  int64_t n;
+  uint32_t col;
+  int dist;
   Params prm;
   PoissonTable pt;
-  double* table = nullptr;
-  int st = with_params(dist, params, nparams, prm, pt, &table, s);
-  if (st != PBH_OK) return st;
-  dim3 g(ppf_grid(nt)), b(kBlock);
+  double* table;
+};
+
+int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* params, int nparams, GenColumn** out,
+               hipStream_t s) {
+  for (int j = 0; j < nparams; ++j)
+    PBH_REQUIRE(params[j].ptr == nullptr, "stratum-ordered LHS generation needs scalar parameters");
+  GenColumn* g = new GenColumn{};
+  g->seed = seed;
+  g->n = n;
+  g->col = (uint32_t)col;
+  g->dist = dist;
+  int st = with_params(dist, params, nparams, g->prm, g->pt, &g->table, s);
+  if (st != PBH_OK) {
+    delete g;
+    return st;
+  }
+  *out = g;
+  return PBH_OK;
+}
+
+void gen_destroy(GenColumn* g, hipStream_t s) {
+  if (!g) return;
+  if (g->table) (void)hipFreeAsync(g->table, s);
+  delete g;
+}
+
+int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t* flag, unsigned long long* counts,
+               hipStream_t s) {
+  const int64_t n = g->n;
+  PBH_REQUIRE(t0 >= 0 && nt >= 0 && t0 + nt <= n, "lhs_sorted_ppf: strata [%lld, %lld) outside [0, %lld)",
+              (long long)t0, (long long)(t0 + nt), (long long)n);
   if (counts) PBH_CHECK_HIP(hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), s));
-  switch (dist) {
-#define PBH_CASE(D)                                                                                         \
-  case D:                                                                                                   \
-    PBH_TIMED(kKLhsSorted, s,                                                                               \
-              hipLaunchKernelGGL(k_lhs_sorted_ppf<D>, g, b, 0, s, seed, n, t0, nt, (uint32_t)col, prm, pt, \
-                                 out, flag, counts));                                                       \
+  if (nt == 0) return PBH_OK;
+  dim3 gr(ppf_grid(nt)), b(kBlock);
+  switch (g->dist) {
+#define PBH_CASE(D)                                                                                            \
+  case D:                                                                                                      \
+    PBH_TIMED(kKLhsSorted, s,                                                                                  \
+              hipLaunchKernelGGL(k_lhs_sorted_ppf<D>, gr, b, 0, s, g->seed, n, t0, nt, g->col, g->prm, g->pt, out, \
+                                 flag, counts));                                                               \
     break;
     PBH_CASE(PBH_DIST_NORM)
     PBH_CASE(PBH_DIST_UNIFORM)
@@ -989,12 +1149,66 @@ int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, in
     PBH_CASE(PBH_DIST_POISSON)
 #undef PBH_CASE
     default:
-      set_error("unsupported distribution id %d", dist);
+      set_error("unsupported distribution id %d", g->dist);
       return PBH_ERR_UNSUPPORTED;
   }
   PBH_CHECK_LAUNCH();
-  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));
   return PBH_OK;
+}
+
+int gen_place(const GenColumn* g, const uint64_t* pairs, int64_t n, double* y, int64_t y_rs, int32_t* idx,
+              const int32_t* state, hipStream_t s) {
+  PBH_REQUIRE(n == g->n, "gen_place: %lld rows for a column of %lld", (long long)n, (long long)g->n);
+  const int64_t blocks = (n + kGenRows - 1) / kGenRows;
+  if (gamma_lds_ok(g->dist, g->prm, g->pt)) {
+    PBH_TIMED(kKPlaceGen, s,
+              hipLaunchKernelGGL(k_place_gen_gamma, dim3((unsigned)(blocks < 256 ? blocks : 256)), dim3(kGBlock), 0, s,
+                                 pairs, n, g->seed, g->col, g->prm, g->pt, y, y_rs, idx, state));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
+  const unsigned gr = (unsigned)(blocks < 256 * 8 ? blocks : 256 * 8);
+  if (const size_t pl = poisson_lds_bytes(g->dist, g->prm, g->pt)) {
+    PBH_TIMED(kKPlaceGen, s,
+              hipLaunchKernelGGL(k_place_gen_poisson, dim3(gr), dim3(kBlock), pl, s, pairs, n, g->seed, g->col, g->prm,
+                                 g->pt, y, y_rs, idx, state));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
+  switch (g->dist) {
+#define PBH_CASE(D)                                                                                           \
+  case D:                                                                                                     \
+    PBH_TIMED(kKPlaceGen, s,                                                                                     \
+              hipLaunchKernelGGL(k_place_gen<D>, dim3(gr), dim3(kBlock), 0, s, pairs, n, g->seed, g->col, g->prm, \
+                                 g->pt, y, y_rs, idx, state));                                                \
+    break;
+    PBH_CASE(PBH_DIST_NORM)
+    PBH_CASE(PBH_DIST_UNIFORM)
+    PBH_CASE(PBH_DIST_EXPON)
+    PBH_CASE(PBH_DIST_LOGNORM)
+    PBH_CASE(PBH_DIST_TRIANG)
+    PBH_CASE(PBH_DIST_GAMMA)
+    PBH_CASE(PBH_DIST_POISSON)
+#undef PBH_CASE
+    default:
+      set_error("unsupported distribution id %d", g->dist);
+      return PBH_ERR_UNSUPPORTED;
+  }
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist, const pbh_param* params,
+                   int nparams, double* out, int32_t* flag, hipStream_t s, unsigned long long* counts) {
+  PBH_REQUIRE(t0 >= 0 && nt >= 0 && t0 + nt <= n, "lhs_sorted_ppf: strata [%lld, %lld) outside [0, %lld)",
+              (long long)t0, (long long)(t0 + nt), (long long)n);
+  if (nt == 0) return PBH_OK;
+  GenColumn* g = nullptr;
+  int st = gen_create(seed, n, col, dist, params, nparams, &g, s);
+  if (st != PBH_OK) return st;
+  st = gen_sorted(g, t0, nt, out, flag, counts, s);
+  gen_destroy(g, s);
+  return st;
 }
 
 int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStream_t s) {

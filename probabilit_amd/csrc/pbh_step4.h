@@ -1,0 +1,71 @@
+// Iman-Conover step 4 for generated LHS columns (pbh_step4.hip): MSD code passes with atomic
+// cursors, a per-bucket LDS finish that emits (row, sorted position) pairs, MSD row-placement
+// passes and the final assembly (gen_place, pbh_ppf.hip) that regenerates sort(X)[p].
+#pragma once
+
+#include "pbh_common.h"
+
+namespace pbh {
+
+constexpr int kGenPlaceShift = 12;  // final placement blocks of 4096 rows (32 KB of LDS)
+
+// per-call state of all k columns (device): histograms, bucket starts, cursors, tile maps,
+// state[c] (bit 0 counter overflow, bit 1 bucket above the finish capacity: the column takes
+// the general path) and flags[c] (bit 0: a run of equal codes too long for the finish: the
+// column is redone by the general path after the others)
+struct Step4Shared {
+  int k;
+  uint32_t* hist;
+  uint32_t* start;
+  uint32_t* cur1;
+  uint32_t* cur2;
+  uint32_t* tpre;
+  int32_t* state;
+  int32_t* flags;
+};
+// one column's staging (reused column after column)
+struct Step4Column {
+  uint32_t* keys32;
+  uint32_t* rows1;
+  uint16_t* keys16;
+  uint32_t* rows2;
+  uint64_t* pairs[2];
+  uint32_t* pcur[2];
+};
+
+size_t step4_gen_shared_bytes(int k);
+size_t step4_gen_column_bytes(int64_t n);
+void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh);
+void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb);
+bool step4_gen_enabled(int64_t n);
+// columns of step 4 run concurrently on this many streams (PBH_STEP4_STREAMS, default 2, at
+// most kStep4MaxStreams), each with its own Step4Column staging, so that one column's VALU- or
+// latency-bound kernels (bucket finish, gen_place) overlap another's bandwidth-bound passes
+constexpr int kStep4MaxStreams = 4;
+int step4_streams();
+hipStream_t step4_side_stream(int i);
+void step4_sync_side_streams();
+// top-16 histograms, bucket starts and flatness of all k code columns (codes + c * ldc)
+int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Shared& sh, hipStream_t s);
+// code passes and bucket finish of column c: (row << 32 | p') pairs in position order in cb.pairs[0]
+int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, const Step4Shared& sh,
+                     const Step4Column& cb, hipStream_t s);
+// row-placement MSD passes on cb.pairs[0]; *out_buf = the pairs buffer grouped by 4096-row block
+int step4_gen_place_passes(int64_t n, const Step4Column& cb, const int32_t* state, hipStream_t s, int* out_buf);
+
+// A generated LHS column's inverse-CDF setup (scalar parameters; gamma guide / poisson CDF
+// tables built once), shared by the stratum-ordered generator and the final placement.
+struct GenColumn;
+int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* params, int nparams, GenColumn** out,
+               hipStream_t s);
+void gen_destroy(GenColumn* g, hipStream_t s);
+// out[t - t0] = the column's value in stratum t (see lhs_sorted_ppf)
+int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t* flag, unsigned long long* counts,
+               hipStream_t s);
+// y[row * y_rs] = value of stratum p for every pair (row << 32 | p) of `pairs`, grouped by
+// 4096-row block (block b = positions [b << 12, ...)); idx[row] = p when idx != NULL.
+// state (optional device word): skip when non-zero.
+int gen_place(const GenColumn* g, const uint64_t* pairs, int64_t n, double* y, int64_t y_rs, int32_t* idx,
+              const int32_t* state, hipStream_t s);
+
+}  // namespace pbh

@@ -1,0 +1,691 @@
+// Iman-Conover step 4 for GENERATED columns (correlation.py:418-423):
+//     idx = rankdata(CS[:, k]).astype(int) - 1;  Y[:, k] = sort(X[:, k])[idx]
+// where sort(X[:, k]) is the stratum-ordered native LHS column, so its value at sorted
+// position p is regenerated from p (pbh_ppf.hip gen_place) and only the permutation moves:
+//
+//   hist16   top-16-bit histogram of the 32-bit codes (written by step 3), its prefix = the
+//            start of every top-16 bucket, a per-column flatness check        (read 4 B)
+//   msd1     (code, row) scattered by the top code byte                       (read 4, write 8)
+//   msd2     (low 16 code bits, row) scattered into the top-16 buckets        (read 8, write 6)
+//   finish   one wave per bucket (~1500 items): sort by the low 16 bits in LDS, order runs of
+//            equal codes by the full CS value (exact ties flagged), emit (row, p') packed in a
+//            u64 with p' = the sorted position, or the tie group's 'average' position  (read 6, write 8)
+//   place    MSD passes on the row of (row, p') until every 4096-row block is together (read 8,
+//            write 8 per pass; 2 passes at N = 1e8), then gen_place assembles each block in
+//            LDS, regenerating sort(X)[p'] (write 8)
+//
+// Every scatter is an MSD pass with per-destination cursors advanced by one global atomic per
+// (tile, digit): no decoupled look-back, no status words, no host round trip.  Stability is not
+// needed anywhere: the bucket finish orders every bucket completely, and the row placement
+// writes each value at its own row.  Host decisions are batched: one readback after hist16 for
+// all columns (flatness), one at the end (buckets that met a run longer than kRunCap), whose
+// columns are redone by the general path (pbh_phases.hip reorder_column).
+#include <stdlib.h>
+#include <string.h>
+
+#include "pbh_error.h"
+#include "pbh_step4.h"
+#include "pbh_timing.h"
+
+namespace pbh {
+namespace {
+
+constexpr int kT = 256;
+constexpr int kIpt1 = 32;
+constexpr int kTile1 = kT * kIpt1;  // msd1 / msd2 tiles: 8192 items
+constexpr int kIptP = 16;
+constexpr int kTileP = kT * kIptP;  // placement tiles: 4096 pairs (divides every group size 2^s >= 2^12)
+constexpr int kBucketCap2 = 2048;   // items per top-16 bucket a wave can finish
+constexpr int kRunCap = 16;         // longest run of equal codes the finish orders
+constexpr int kCurPad = 16;         // code-pass cursors one 64-byte line apart (atomic traffic)
+
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh /* >= 260 */) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[256 + w] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (int i = 0; i < w; ++i) pre += sh[256 + i];
+  __syncthreads();
+  return pre + x - v;
+}
+
+// ---------------------------------------------------------------- hist16
+// One 1024-thread block per (chunk, column): 65536 16-bit counters packed two per LDS word
+// (128 KiB), flushed with one global add per non-empty counter.  A counter reaching 65535 in
+// one block (a spike: a discrete-dominated correlated score) sets the column's state bit 0,
+// which routes it to the general path; so does a bucket above kBucketCap2 (k_hist16_scan).
+__global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ codes, int64_t ld, int64_t n,
+                                                 uint32_t* __restrict__ hist, int32_t* __restrict__ state) {
+  __shared__ uint32_t w[32768];
+  __shared__ int ovf;
+  const int c = blockIdx.y;
+  const uint32_t* cc = codes + (int64_t)c * ld;
+  for (int i = threadIdx.x; i < 32768; i += 1024) w[i] = 0;
+  if (threadIdx.x == 0) ovf = 0;
+  __syncthreads();
+  const int64_t chunk = ((n + gridDim.x - 1) / gridDim.x + 3) & ~(int64_t)3;
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  bool bad = false;
+  auto add = [&](uint32_t code) {
+    const uint32_t b = code >> 16, sh = (b & 1u) * 16u;
+    const uint32_t old = atomicAdd(&w[b >> 1], 1u << sh);
+    bad |= ((old >> sh) & 0xFFFFu) == 0xFFFFu;
+  };
+  if ((((uintptr_t)(cc + lo)) & 15) == 0) {
+    const int64_t n4 = (hi - lo) / 4;
+    const uint4* v4 = reinterpret_cast<const uint4*>(cc + lo);
+    for (int64_t i = threadIdx.x; i < n4; i += 1024) {
+      const uint4 v = v4[i];
+      add(v.x);
+      add(v.y);
+      add(v.z);
+      add(v.w);
+    }
+    for (int64_t i = lo + 4 * n4 + threadIdx.x; i < hi; i += 1024) add(cc[i]);
+  } else {
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 1024) add(cc[i]);
+  }
+  if (bad) ovf = 1;
+  __syncthreads();
+  uint32_t* hc = hist + (int64_t)c * 65536;
+  for (int j = threadIdx.x; j < 32768; j += 1024) {
+    const uint32_t v = w[j];
+    if (v & 0xFFFFu) atomicAdd(&hc[2 * j], v & 0xFFFFu);
+    if (v >> 16) atomicAdd(&hc[2 * j + 1], v >> 16);
+  }
+  if (threadIdx.x == 0 && ovf) atomicOr(&state[c], 1);
+}
+
+// One 1024-thread block per column: start[b] = exclusive prefix of the 65536 bucket counts
+// (start[65536] = n), the msd2 tile map (tiles of kTile1 inside every top-byte group: tpre[g]
+// = tiles before group g), and state bit 1 when a bucket exceeds kBucketCap2.
+__global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict__ hist, int64_t n,
+                                                      uint32_t* __restrict__ start, uint32_t* __restrict__ tpre,
+                                                      int32_t* __restrict__ state) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t gsize[256];
+  __shared__ int big;
+  const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t* hc = hist + (int64_t)c * 65536;
+  uint32_t* sc = start + (int64_t)c * 65537;
+  if (t == 0) big = 0;
+  uint32_t v[64], s = 0, mx = 0;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    v[j] = hc[t * 64 + j];
+    s += v[j];
+    mx = v[j] > mx ? v[j] : mx;
+  }
+  uint32_t x = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (int i = 0; i < wv; ++i) pre += wsum[i];
+  uint32_t run = pre + x - s;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    sc[t * 64 + j] = run;
+    run += v[j];
+  }
+  if (t == 1023) sc[65536] = run;
+  if (mx > (uint32_t)kBucketCap2) big = 1;
+  if ((t & 3) == 0) gsize[t >> 2] = 0;
+  __syncthreads();
+  atomicAdd(&gsize[t >> 2], s);  // top-byte group g = threads 4 g .. 4 g + 3 (256 buckets)
+  __syncthreads();
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (int g = 0; g < 256; ++g) {
+      tpre[(int64_t)c * 257 + g] = acc;
+      acc += (gsize[g] + kTile1 - 1) / kTile1;
+    }
+    tpre[(int64_t)c * 257 + 256] = acc;
+    if (big) atomicOr(&state[c], 2);
+  }
+}
+
+// ---------------------------------------------------------------- code passes
+// msd1: tile = kTile1 consecutive rows; digit = top code byte.
+__global__ __launch_bounds__(kT) void k_msd1(const uint32_t* __restrict__ codes, int64_t n,
+                                             const uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
+                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ rout,
+                                             const int32_t* __restrict__ state) {
+  if (*state) return;  // uniform: this column takes the general path
+  __shared__ uint32_t cnt[256], lst[264], gb[256];
+  __shared__ uint32_t sk[kTile1], sr[kTile1];
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTile1;
+  const int m = (int)((n - base) < kTile1 ? (n - base) : kTile1);
+  cnt[t] = 0;
+  __syncthreads();
+  uint32_t key[kIpt1], rk[kIpt1];
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    key[j] = p < m ? codes[base + p] : 0u;
+    rk[j] = p < m ? atomicAdd(&cnt[key[j] >> 24], 1u) : 0u;
+  }
+  __syncthreads();
+  const uint32_t my = cnt[t];
+  const uint32_t ex = block_excl_scan256(my, lst);
+  lst[t] = ex;
+  gb[t] = my ? start[t << 8] + atomicAdd(&cur[t * kCurPad], my) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    if (p < m) {
+      const uint32_t q = lst[key[j] >> 24] + rk[j];
+      sk[q] = key[j];
+      sr[q] = (uint32_t)(base + p);
+    }
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    if (p < m) {
+      const uint32_t k = sk[p], d = k >> 24;
+      const uint32_t o = gb[d] + ((uint32_t)p - lst[d]);
+      kout[o] = k;
+      rout[o] = sr[p];
+    }
+  }
+}
+
+// msd2: tiles of kTile1 inside each top-byte group (tile map tpre); digit = code byte 2; the
+// destination is the group's top-16 bucket (g << 8 | digit).  Writes the low 16 code bits.
+__global__ __launch_bounds__(kT) void k_msd2(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin,
+                                             const uint32_t* __restrict__ start, const uint32_t* __restrict__ tpre,
+                                             uint32_t* __restrict__ cur, uint16_t* __restrict__ kout,
+                                             uint32_t* __restrict__ rout, const int32_t* __restrict__ state) {
+  if (*state) return;
+  const uint32_t tile = blockIdx.x;
+  if (tile >= tpre[256]) return;
+  __shared__ uint32_t cnt[256], lst[264], gb[256];
+  __shared__ uint32_t sk[kTile1], sr[kTile1];
+  __shared__ int gsh;
+  const int t = threadIdx.x;
+  if (t == 0) {  // the group holding this tile: last g with tpre[g] <= tile
+    int lo = 0, hi = 256;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tpre[mid] <= tile)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    while (lo < 255 && tpre[lo + 1] <= tile) ++lo;  // skip empty groups
+    gsh = lo;
+  }
+  cnt[t] = 0;
+  __syncthreads();
+  const int g = gsh;
+  const int64_t gs = start[g << 8], ge = start[(g + 1) << 8];
+  const int64_t base = gs + (int64_t)(tile - tpre[g]) * kTile1;
+  const int m = (int)((ge - base) < kTile1 ? (ge - base) : kTile1);
+  uint32_t key[kIpt1], row[kIpt1], rk[kIpt1];
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    key[j] = p < m ? kin[base + p] : 0u;
+    row[j] = p < m ? rin[base + p] : 0u;
+    rk[j] = p < m ? atomicAdd(&cnt[(key[j] >> 16) & 255u], 1u) : 0u;
+  }
+  __syncthreads();
+  const uint32_t my = cnt[t];
+  const uint32_t ex = block_excl_scan256(my, lst);
+  lst[t] = ex;
+  const uint32_t b = ((uint32_t)g << 8) | (uint32_t)t;
+  gb[t] = my ? start[b] + atomicAdd(&cur[b], my) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    if (p < m) {
+      const uint32_t q = lst[(key[j] >> 16) & 255u] + rk[j];
+      sk[q] = key[j];
+      sr[q] = row[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    if (p < m) {
+      const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
+      const uint32_t o = gb[d] + ((uint32_t)p - lst[d]);
+      kout[o] = (uint16_t)kk;
+      rout[o] = sr[p];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- bucket finish
+// One wave per top-16 bucket: the low 16 bits and rows in registers (32 items per lane), a
+// non-stable LDS-atomic pass on the low byte and a stable ballot-ranked pass on the high byte
+// give the code order; runs of equal codes are put in CS order (exact ties flagged); every
+// position p then leaves as (row << 32 | p') with p' = the start of the bucket + p, or, inside a
+// group of exact ties [s, e], s + (e - s) / 2 (the int of the 'average' rank, minus one).
+constexpr int kWB = kBucketCap2 / 64;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct WaveBucket2 {
+  uint16_t key[kBucketCap2];
+  uint32_t row[kBucketCap2];
+  uint8_t eq[kBucketCap2];
+  uint32_t cnt[256];
+  uint16_t runs[256];
+};
+
+__device__ __forceinline__ void wb_scan_counts(WaveBucket2& B) {
+  const int lane = threadIdx.x & 63;
+  uint32_t v[4], sum = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = B.cnt[lane * 4 + q];
+    sum += v[q];
+  }
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  uint32_t run = incl - sum;
+  wave_sync();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    B.cnt[lane * 4 + q] = run;
+    run += v[q];
+  }
+  wave_sync();
+}
+
+template <int R>
+__device__ __forceinline__ bool resolve_run2(WaveBucket2& B, int p, int L, const double* __restrict__ x) {
+  uint32_t rr[R];
+  double v[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    rr[j] = j < L ? B.row[p + j] : 0u;
+    v[j] = j < L ? x[rr[j]] : 0.0;
+  }
+  bool any_tie = false;
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    int pos = 0;
+    bool tie = false;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const bool other = j < L && j != q;
+      pos += (other && (v[j] < v[q] || (v[j] == v[q] && j < q))) ? 1 : 0;
+      tie |= other && v[j] == v[q] && j < q;
+    }
+    if (q < L) {
+      B.row[p + pos] = rr[q];
+      B.eq[p + pos] = tie ? 1 : 0;
+      any_tie |= tie;
+    }
+  }
+  return any_tie;
+}
+
+constexpr int kBFWaves = 2;
+
+__global__ __launch_bounds__(64 * kBFWaves) void k_finish(const uint16_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ rows,
+                                                          const double* __restrict__ x,
+                                                          const uint32_t* __restrict__ start,
+                                                          uint64_t* __restrict__ out, int32_t* __restrict__ flags,
+                                                          const int32_t* __restrict__ state) {
+  if (*state) return;
+  __shared__ WaveBucket2 wb[kBFWaves];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  WaveBucket2& B = wb[w];
+  const int bkt = blockIdx.x * kBFWaves + w;
+  if (bkt >= 65536) return;
+  const int64_t s = start[bkt];
+  const int len = (int)((int64_t)start[bkt + 1] - s);  // <= kBucketCap2 (k_hist16_scan)
+  if (len == 0) return;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  uint32_t k[kWB], r[kWB];
+#pragma unroll
+  for (int j = 0; j < kWB; ++j) {
+    const int p = j * 64 + lane;
+    k[j] = p < len ? (uint32_t)keys[s + p] : 0u;
+    r[j] = p < len ? rows[s + p] : 0u;
+  }
+  // pass 1, low byte: LDS atomics (not stable: equal low and high bytes = equal codes, a run)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) B.cnt[lane * 4 + q] = 0;
+  wave_sync();
+  uint32_t rank[kWB];
+#pragma unroll
+  for (int j = 0; j < kWB; ++j) rank[j] = (j * 64 + lane < len) ? atomicAdd(&B.cnt[k[j] & 255u], 1u) : 0u;
+  wave_sync();
+  wb_scan_counts(B);
+#pragma unroll
+  for (int j = 0; j < kWB; ++j) {
+    if (j * 64 + lane < len) {
+      const uint32_t lp = B.cnt[k[j] & 255u] + rank[j];
+      B.key[lp] = (uint16_t)k[j];
+      B.row[lp] = r[j];
+    }
+  }
+  wave_sync();
+#pragma unroll
+  for (int j = 0; j < kWB; ++j) {
+    const int p = j * 64 + lane;
+    k[j] = p < len ? B.key[p] : 0u;
+    r[j] = p < len ? B.row[p] : 0u;
+  }
+  wave_sync();
+  // pass 2, high byte: stable (ballot peer matching against LDS digit counters)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) B.cnt[lane * 4 + q] = 0;
+  wave_sync();
+#pragma unroll
+  for (int j = 0; j < kWB; ++j) {
+    const bool valid = j * 64 + lane < len;
+    const uint32_t d = (k[j] >> 8) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) {
+      const uint64_t m = __ballot(valid && ((d >> bb) & 1u));
+      peers &= ((d >> bb) & 1u) ? m : ~m;
+    }
+    const uint32_t below = (uint32_t)__popcll(peers & lt);
+    const uint32_t c = valid ? B.cnt[d] : 0u;
+    rank[j] = c + below;
+    if (valid && below == 0) B.cnt[d] = c + (uint32_t)__popcll(peers);
+  }
+  wave_sync();
+  wb_scan_counts(B);
+#pragma unroll
+  for (int j = 0; j < kWB; ++j) {
+    if (j * 64 + lane < len) {
+      const uint32_t lp = B.cnt[(k[j] >> 8) & 255u] + rank[j];
+      B.key[lp] = (uint16_t)k[j];
+      B.row[lp] = r[j];
+    }
+  }
+  wave_sync();
+  // runs of equal codes, compacted into B.runs
+  int nrun = 0;
+#pragma unroll 4
+  for (int j = 0; j < kWB; ++j) {
+    const int p = j * 64 + lane;
+    bool st = false;
+    if (p < len) {
+      const uint16_t c = B.key[p];
+      st = p + 1 < len && B.key[p + 1] == c && (p == 0 || B.key[p - 1] != c);
+      B.eq[p] = 0;
+    }
+    const uint64_t m = __ballot(st);
+    const int slot = nrun + (int)__popcll(m & lt);
+    if (st && slot < 256) B.runs[slot] = (uint16_t)p;
+    nrun += (int)__popcll(m);
+  }
+  wave_sync();
+  if (nrun > 256) {
+    if (lane == 0) atomicOr(flags, 1);
+    return;
+  }
+  bool any_tie = false;
+  for (int i = lane; i < nrun; i += 64) {
+    const int p = B.runs[i];
+    const uint16_t c = B.key[p];
+    int L = 2;
+    while (p + L < len && B.key[p + L] == c && L <= kRunCap) ++L;
+    if (L > kRunCap) {
+      atomicOr(flags, 1);
+      continue;
+    }
+    if (L <= 4)
+      any_tie |= resolve_run2<4>(B, p, L, x);
+    else
+      any_tie |= resolve_run2<kRunCap>(B, p, L, x);
+  }
+  const bool ties = __ballot(any_tie) != 0ull;
+  wave_sync();
+#pragma unroll 4
+  for (int j = 0; j < kWB; ++j) {
+    const int p = j * 64 + lane;
+    if (p < len) {
+      int pp = p;
+      if (ties && (B.eq[p] || (p + 1 < len && B.eq[p + 1]))) {  // inside a group of exact ties
+        int a = p, e = p;
+        while (a > 0 && B.eq[a]) --a;
+        while (e + 1 < len && B.eq[e + 1]) ++e;
+        pp = a + (e - a) / 2;
+      }
+      out[s + p] = ((uint64_t)B.row[p] << 32) | (uint64_t)(uint32_t)(s + pp);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- row placement passes
+// Input grouped by row >> s_in (closed-form groups: rows are a permutation of [0, n), so group
+// g occupies positions [g << s_in, ...)); tiles of kTileP never straddle a group.  Digit =
+// (row >> s_out) within the group; destination = positions (row >> s_out) << s_out.
+__global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ in, int64_t n, int s_out,
+                                                  uint32_t* __restrict__ cur, uint64_t* __restrict__ out,
+                                                  const int32_t* __restrict__ state) {
+  if (state && *state) return;
+  __shared__ uint32_t cnt[256], lst[264], gb[256];
+  __shared__ uint64_t sv[kTileP];
+  __shared__ uint32_t gfirst;
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTileP;
+  const int m = (int)((n - base) < kTileP ? (n - base) : kTileP);
+  cnt[t] = 0;
+  if (t == 0) gfirst = 0xFFFFFFFFu;
+  __syncthreads();
+  uint64_t v[kIptP];
+  uint32_t rk[kIptP], dg[kIptP];
+#pragma unroll
+  for (int j = 0; j < kIptP; ++j) {
+    const int p = j * kT + t;
+    v[j] = p < m ? in[base + p] : 0ull;
+    dg[j] = (uint32_t)(v[j] >> (32 + s_out));  // global destination id (row >> s_out)
+  }
+  // the tile's destinations span < 256 consecutive ids starting at its smallest
+  uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+  for (int j = 0; j < kIptP; ++j)
+    if (j * kT + t < m) mn = dg[j] < mn ? dg[j] : mn;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t y = __shfl_xor(mn, o, 64);
+    mn = y < mn ? y : mn;
+  }
+  if ((t & 63) == 0) atomicMin(&gfirst, mn);
+  __syncthreads();
+  const uint32_t g0 = gfirst;
+#pragma unroll
+  for (int j = 0; j < kIptP; ++j) rk[j] = (j * kT + t < m) ? atomicAdd(&cnt[dg[j] - g0], 1u) : 0u;
+  __syncthreads();
+  const uint32_t my = cnt[t];
+  const uint32_t ex = block_excl_scan256(my, lst);
+  lst[t] = ex;
+  gb[t] = my ? (uint32_t)(((uint64_t)(g0 + t) << s_out) + atomicAdd(&cur[g0 + t], my)) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIptP; ++j)
+    if (j * kT + t < m) sv[lst[dg[j] - g0] + rk[j]] = v[j];
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < kIptP; ++j) {
+    const int p = j * kT + t;
+    if (p < m) {
+      const uint64_t x = sv[p];
+      const uint32_t d = (uint32_t)(x >> (32 + s_out)) - g0;
+      out[gb[d] + ((uint32_t)p - lst[d])] = x;
+    }
+  }
+}
+
+}  // namespace
+
+size_t step4_gen_shared_bytes(int k) {
+  // per column: hist 65536 + start 65537 + cur1 256 * pad + cur2 65536 + tpre 257 (u32), state
+  return (size_t)k * ((65536 + 65537 + 256 * kCurPad + 65536 + 257) * 4 + 64) + 256;
+}
+
+size_t step4_gen_column_bytes(int64_t n) {
+  // keys32 + rows (msd1 out) | keys16 + rows (msd2 out) | pairs x 2 | placement cursors
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const int64_t ncur = (n >> kGenPlaceShift) + 2;
+  return al((size_t)n * 4) * 2 + al((size_t)n * 2) + al((size_t)n * 4) + al((size_t)n * 8) * 2 + al((size_t)ncur * 4) * 2;
+}
+
+void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh) {
+  char* p = (char*)ws;
+  sh.k = k;
+  sh.hist = (uint32_t*)p;
+  p += (size_t)k * 65536 * 4;
+  sh.start = (uint32_t*)p;
+  p += (size_t)k * 65537 * 4;
+  sh.cur1 = (uint32_t*)p;
+  p += (size_t)k * 256 * kCurPad * 4;
+  sh.cur2 = (uint32_t*)p;
+  p += (size_t)k * 65536 * 4;
+  sh.tpre = (uint32_t*)p;
+  p += (size_t)k * 257 * 4;
+  p = (char*)(((uintptr_t)p + 63) & ~(uintptr_t)63);
+  sh.state = (int32_t*)p;   // k words: bit 0 counter overflow, bit 1 bucket over cap
+  sh.flags = sh.state + k;  // k words: bit 0 long run / too many runs in a bucket
+}
+
+void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb) {
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  char* p = (char*)ws;
+  cb.keys32 = (uint32_t*)p;
+  p += al((size_t)n * 4);
+  cb.rows1 = (uint32_t*)p;
+  p += al((size_t)n * 4);
+  cb.keys16 = (uint16_t*)p;
+  p += al((size_t)n * 2);
+  cb.rows2 = (uint32_t*)p;
+  p += al((size_t)n * 4);
+  cb.pairs[0] = (uint64_t*)p;
+  p += al((size_t)n * 8);
+  cb.pairs[1] = (uint64_t*)p;
+  p += al((size_t)n * 8);
+  const int64_t ncur = (n >> kGenPlaceShift) + 2;
+  cb.pcur[0] = (uint32_t*)p;
+  p += al((size_t)ncur * 4);
+  cb.pcur[1] = (uint32_t*)p;
+}
+
+int step4_streams() {
+  static const int v = [] {
+    const char* e = getenv("PBH_STEP4_STREAMS");
+    int x = e ? atoi(e) : 2;
+    return x < 1 ? 1 : (x > kStep4MaxStreams ? kStep4MaxStreams : x);
+  }();
+  return v;
+}
+
+hipStream_t step4_side_stream(int i) {
+  // created once per device and kept for the life of the process (non-blocking: no implicit
+  // ordering with the legacy default stream; the caller orders them with events)
+  static hipStream_t streams[64][kStep4MaxStreams] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (!streams[dev][i]) (void)hipStreamCreateWithFlags(&streams[dev][i], hipStreamNonBlocking);
+  return streams[dev][i];
+}
+
+void step4_sync_side_streams() {
+  for (int i = 0; i < step4_streams(); ++i) {
+    hipStream_t x = step4_side_stream(i);
+    if (x) (void)hipStreamSynchronize(x);
+  }
+}
+
+bool step4_gen_enabled(int64_t n) {
+  const char* e = getenv("PBH_STEP4");  // "lsd" / "legacy": the general path for every column
+  if (e && (strcmp(e, "lsd") == 0 || strcmp(e, "legacy") == 0)) return false;
+  return n >= 2 && n < ((int64_t)1 << 32);
+}
+
+int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Shared& sh, hipStream_t s) {
+  const int k = sh.k;
+  PBH_CHECK_HIP(hipMemsetAsync(sh.hist, 0, (size_t)k * 65536 * 4, s));
+  PBH_CHECK_HIP(hipMemsetAsync(sh.cur1, 0, (size_t)k * (256 * kCurPad + 65536) * 4, s));  // cur1 and cur2
+  PBH_CHECK_HIP(hipMemsetAsync(sh.state, 0, (size_t)2 * k * 4, s));
+  int64_t blocks = (n + 65535) / 65536;  // >= 64 K codes per block: a handful of flushes
+  if (blocks > 256) blocks = 256;
+  if (blocks < 1) blocks = 1;
+  PBH_TIMED(kKHist16, s,
+            hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)k), dim3(1024), 0, s, codes, ldc, n, sh.hist,
+                               sh.state));
+  PBH_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)k), dim3(1024), 0, s, sh.hist, n, sh.start, sh.tpre, sh.state);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, const Step4Shared& sh,
+                     const Step4Column& cb, hipStream_t s) {
+  const uint32_t* start = sh.start + (int64_t)c * 65537;
+  const int32_t* state = sh.state + c;
+  const int64_t t1 = (n + kTile1 - 1) / kTile1;
+  PBH_TIMED(kKMsd1, s,
+            hipLaunchKernelGGL(k_msd1, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
+                               sh.cur1 + (int64_t)c * 256 * kCurPad, cb.keys32, cb.rows1, state));
+  PBH_CHECK_LAUNCH();
+  PBH_TIMED(kKMsd2, s,
+            hipLaunchKernelGGL(k_msd2, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
+                               sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
+  PBH_CHECK_LAUNCH();
+  PBH_TIMED(kKFinish, s,
+            hipLaunchKernelGGL(k_finish, dim3(65536 / kBFWaves), dim3(64 * kBFWaves), 0, s, cb.keys16, cb.rows2, cs,
+                               start, cb.pairs[0], sh.flags + c, state));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int step4_gen_place_passes(int64_t n, const Step4Column& cb, const int32_t* state, hipStream_t s, int* out_buf) {
+  int bits = 0;
+  while (((int64_t)1 << bits) < n) ++bits;
+  // MSD levels on the row: shifts from high to kGenPlaceShift, at most 8 bits per level
+  int shifts[4], nl = 0;
+  for (int sh = kGenPlaceShift; sh < bits; sh += 8) shifts[nl++] = sh;
+  int cur = 0;
+  const int64_t tiles = (n + kTileP - 1) / kTileP;
+  for (int l = nl - 1; l >= 0; --l) {
+    const int64_t ncur = (n >> shifts[l]) + 1;
+    uint32_t* cr = cb.pcur[l & 1];
+    PBH_CHECK_HIP(hipMemsetAsync(cr, 0, (size_t)ncur * 4, s));
+    PBH_TIMED(kKPlaceMsd, s,
+              hipLaunchKernelGGL(k_place_msd, dim3((unsigned)tiles), dim3(kT), 0, s, cb.pairs[cur], n, shifts[l], cr,
+                                 cb.pairs[cur ^ 1], state));
+    PBH_CHECK_LAUNCH();
+    cur ^= 1;
+  }
+  *out_buf = cur;
+  return PBH_OK;
+}
+
+}  // namespace pbh

@@ -35,6 +35,12 @@ enum KernelId {
   kKTable,
   kKPermCorr,
   kKHbmCopy,
+  kKHist16,
+  kKMsd1,
+  kKMsd2,
+  kKFinish,
+  kKPlaceMsd,
+  kKPlaceGen,
   kKCount
 };
 

@@ -1,0 +1,98 @@
+"""Step 4 of Iman-Conover for generated LHS columns (pbh_step4.hip: MSD code passes, per-bucket
+LDS finish emitting (row, sorted position) pairs, row-placement passes, and gen_place
+regenerating sort(X)[p] from p) against the oracle's step 4 (correlation.py:418-423) on the
+same native quantiles, and against the general path (PBH_STEP4=legacy) bit for bit."""
+
+import numpy as np
+import pytest
+
+from conftest import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(n, dists, seed, C, debug_idx=True):
+    import ctypes
+
+    from probabilit_amd import _lib, device, qmc
+    from probabilit_amd.correlation import ImanConover
+    from probabilit_amd.modeling import Distribution
+
+    d = len(dists)
+    inst = ImanConover().set_target(C)
+    flags = device.zeros(d, "int32")
+    cols = []
+    for j, (nm, kw) in enumerate(dists):
+        v = Distribution(nm, **kw)
+        params = [float(p) for p in v._params(n)]
+        cols.append(_lib.ICColumn(qmc.seed_from(seed), j, _lib.DIST_IDS[nm], (ctypes.c_double * 3)(*params),
+                                  len(params), flags.data_ptr() + 4 * j))
+    dbg = {"idx": device.empty((d, n), "int32")} if debug_idx else None
+    Y = inst._transform_generated(cols, n, debug=dbg)
+    return device.to_host(Y).T, (device.to_host(dbg["idx"]).T if debug_idx else None)
+
+
+def _oracle(n, dists, seed, C):
+    from oracle import ic as oic
+    from oracle.pipeline import ppf_columns
+    from probabilit_amd import native
+
+    X = ppf_columns(native.fill_lhs(seed, n, len(dists)), dists, threads=8)
+    return oic.iman_conover(X, C, threads=8)
+
+
+@pytest.mark.parametrize("n,d,seed", [(10, 3, 1), (4097, 2, 6), (5000, 8, 2), (300_001, 8, 3), (2**20 + 17, 4, 4),
+                                      (4_500_000, 4, 5)])
+def test_generated_step4_vs_oracle(gpu, n, d, seed):
+    from oracle.pipeline import cfg3_corr, cfg_dists
+
+    dists, C = cfg_dists(d), cfg3_corr(d)
+    Y, idx = _run(n, dists, seed, C)
+    ref = _oracle(n, dists, seed, C)
+    np.testing.assert_array_equal(idx, ref["idx"])
+    assert_close(Y, ref["Y"], rtol=1e-10, what=f"generated step 4, n={n}")
+
+
+@pytest.mark.parametrize("n,d,seed", [(70_001, 8, 7), (5_000_000, 3, 8)])
+def test_generated_step4_equals_general_path(gpu, monkeypatch, n, d, seed):
+    """The regenerating path and the general path (sort(X) read from the workspace, one-sweep
+    code sort, value-carrying placement) give the same Y and indices bit for bit."""
+    from oracle.pipeline import cfg3_corr, cfg_dists
+
+    dists, C = cfg_dists(d), cfg3_corr(d)
+    Y, idx = _run(n, dists, seed, C)
+    Y2, _ = _run(n, dists, seed, C, debug_idx=False)
+    monkeypatch.setenv("PBH_STEP4", "legacy")
+    Yl, idxl = _run(n, dists, seed, C)
+    np.testing.assert_array_equal(idx, idxl)
+    np.testing.assert_array_equal(Y, Yl)
+    np.testing.assert_array_equal(Y2, Y)
+
+
+@pytest.mark.parametrize("n", [3000, 30_000])
+def test_generated_step4_exact_ties(gpu, n):
+    """poisson(mu=1e5) in the leading column: its van der Waerden scores tie in small groups
+    (each k holds ~2-3 of 3000 draws), so column 0's correlated scores tie exactly and step 4
+    takes the 'average' rank of every tie group (idx = int(avg) - 1 shared by the group).  At
+    n = 30000 the groups (~25-40 equal codes) exceed the finish's run capacity: the column is
+    flagged and redone by the general path."""
+    dists = [("poisson", {"mu": 1e5}), ("norm", {}), ("gamma", {"a": 2.0})]
+    C = np.array([[1.0, 0.5, 0.2], [0.5, 1.0, 0.3], [0.2, 0.3, 1.0]])
+    Y, idx = _run(n, dists, 9, C)
+    ref = _oracle(n, dists, 9, C)
+    assert len(np.unique(ref["idx"][:, 0])) < n  # the tie groups exist
+    np.testing.assert_array_equal(idx, ref["idx"])
+    assert_close(Y, ref["Y"], rtol=1e-10, what="tie groups")
+
+
+def test_generated_step4_long_runs_fall_back(gpu):
+    """poisson(mu=4) leading: its scores tie in runs of thousands, so the bucket finish flags
+    the column (runs longer than 16 equal codes) and it is redone by the general path; the
+    result still equals the oracle's."""
+    dists = [("poisson", {"mu": 4.0}), ("norm", {}), ("triang", {"c": 0.3})]
+    C = np.array([[1.0, 0.4, 0.1], [0.4, 1.0, 0.2], [0.1, 0.2, 1.0]])
+    n = 200_000
+    Y, idx = _run(n, dists, 3, C)
+    ref = _oracle(n, dists, 3, C)
+    np.testing.assert_array_equal(idx, ref["idx"])
+    assert_close(Y, ref["Y"], rtol=1e-10, what="long runs")
