@@ -51,16 +51,21 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    os.makedirs(BUILD, exist_ok=True)
+def build(force=False, verbose=False, variant=None, defines=()):
+    """variant: build libprobabilit_hip_<variant>.so with extra -D `defines` (A/B measurements,
+    selected at run time by PBH_LIB_VARIANT); the default library is untouched."""
+    bdir = BUILD if not variant else BUILD + "_" + variant
+    lib_path = LIB if not variant else os.path.join(HERE, f"libprobabilit_hip_{variant}.so")
+    os.makedirs(bdir, exist_ok=True)
     cc = hipcc()
     headers = _headers()
     objs, jobs = [], []
+    extra = [f"-D{d}" for d in defines]
     for src in _sources():
-        obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
+        obj = os.path.join(bdir, os.path.basename(src).replace(".hip", ".o"))
         objs.append(obj)
         if force or _stale(obj, [src] + headers):
-            jobs.append([cc, *CXXFLAGS, "-c", src, "-o", obj])
+            jobs.append([cc, *CXXFLAGS, *extra, "-c", src, "-o", obj])
 
     def run(cmd):
         if verbose:
@@ -75,14 +80,16 @@ def build(force=False, verbose=False):
         for warn in ex.map(run, jobs):
             if warn and verbose:
                 print(warn, file=sys.stderr)
-    if force or jobs or _stale(LIB, objs):
-        run([cc, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", LIB, *objs])
-    return LIB
+    if force or jobs or _stale(lib_path, objs):
+        run([cc, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", lib_path, *objs])
+    return lib_path
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--variant", default=None, help="build libprobabilit_hip_<variant>.so")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra preprocessor define")
     a = ap.parse_args()
-    print(build(force=a.force, verbose=a.verbose))
+    print(build(force=a.force, verbose=a.verbose, variant=a.variant, defines=a.defines))

@@ -22,7 +22,14 @@ constexpr int kBlock = 256;
 // full iteration, the per-element poisson search) inline, which would otherwise size the
 // register allocation of every wave (~256 VGPRs, one wave per SIMD) for code the hot path never
 // runs.  Capping at 4 waves per SIMD (128 VGPRs) spills inside those fallbacks instead.
-#define PBH_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#ifndef PBH_PPF_WAVES
+#define PBH_PPF_WAVES 4
+#endif
+#if PBH_PPF_WAVES > 0
+#define PBH_OCC __attribute__((amdgpu_waves_per_eu(PBH_PPF_WAVES)))
+#else
+#define PBH_OCC
+#endif
 constexpr double kInf = sf::kInf;
 constexpr double kNaN = sf::kNaN;
 

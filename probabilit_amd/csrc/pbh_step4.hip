@@ -31,7 +31,10 @@ namespace pbh {
 namespace {
 
 constexpr int kT = 256;
-constexpr int kIpt1 = 32;
+#ifndef PBH_MSD_IPT
+#define PBH_MSD_IPT 16
+#endif
+constexpr int kIpt1 = PBH_MSD_IPT;
 constexpr int kTile1 = kT * kIpt1;  // msd1 / msd2 tiles: 8192 items
 constexpr int kIptP = 16;
 constexpr int kTileP = kT * kIptP;  // placement tiles: 4096 pairs (divides every group size 2^s >= 2^12)
