@@ -290,6 +290,65 @@ int pbh_elementwise(int op, int compute_dtype, int out_dtype, const pbh_operand*
 int pbh_average(const double* const* parents_host, int m, int64_t n, double* out, int32_t* nonfinite_flag,
                 void* stream);
 
+/* ---------------------------------------------------------------- fused DAG program
+ * One pass over the rows for a whole graph of scalar-parameter leaf Distributions
+ * (norm / uniform / expon / lognorm / triang), Constants and float64 Transform nodes: the
+ * per-node loop of Node.sample (modeling.py:586-612, Distribution._sample :795-807, the
+ * Transform._sample methods :943-1075) as one kernel that keeps every intermediate row value
+ * in registers and writes only the nodes the garbage collector keeps
+ * (garbage_collector.py:40-71).  A straight-line program over row-vector registers r[0..7]
+ * (an operand index of -1 reads the op's immediate `value` instead):
+ *   PBH_DAG_GEN     r[dst] = ppf_{op = pbh_dist}(q(row); params)   q from sources[src]
+ *   PBH_DAG_LOAD    r[dst] = vectors[src][row]
+ *   PBH_DAG_CONST   r[dst] = value
+ *   PBH_DAG_BINARY  r[dst] = op(r[a], r[b])        (float64 pbh_op, numpy semantics)
+ *   PBH_DAG_UNARY   r[dst] = op(r[a])
+ *   PBH_DAG_STORE   (nothing but the store below) of r[a]
+ * Every op with store >= 0 also writes its value to vectors[store][row]; dst = -1 keeps it
+ * out of the registers.  Values are bit-identical to the per-node kernels (pbh_sobol_ppf /
+ * pbh_lhs_ppf / pbh_ppf, pbh_elementwise): same inline functions, -ffp-contract=off.  GEN /
+ * LOAD / BINARY / UNARY with flag >= 0 OR bit 0 into flags[flag] when a value is non-finite. */
+typedef enum pbh_dag_kind {
+  PBH_DAG_GEN = 0, PBH_DAG_LOAD = 1, PBH_DAG_CONST = 2, PBH_DAG_BINARY = 3, PBH_DAG_UNARY = 4, PBH_DAG_STORE = 5
+} pbh_dag_kind;
+#define PBH_DAG_MAX_REGS 8
+#define PBH_DAG_MAX_OPS 65536
+
+typedef struct pbh_dag_op {
+  int32_t kind;      /* pbh_dag_kind                                                   */
+  int32_t op;        /* BINARY / UNARY: pbh_op; GEN: pbh_dist (norm..triang)            */
+  int32_t dst, a, b; /* registers (-1: none / the immediate `value`)                    */
+  int32_t src;       /* GEN: source index; LOAD: vector index                           */
+  int32_t flag;      /* flag word index, -1 for none                                    */
+  int32_t store;     /* vector index the value is also written to, -1 for none          */
+  double value;      /* CONST, and the immediate operand of BINARY / UNARY / STORE      */
+  double params[3];  /* GEN: scalar parameters in scipy order (shape..., loc, scale)    */
+} pbh_dag_op;
+
+/* Quantile source of a GEN op: the same streams as the per-node kernels.
+ *   PBH_QSRC_SOBOL   q = (shift ^ xor of sv[b] over set bits of gray(row0 + i)) 2^-bits
+ *                    (pbh_sobol_ppf; sv = the column's `bits` direction numbers)
+ *   PBH_QSRC_LHS     the native LHS column `col` of an n_total-row design, row row0 + i
+ *                    (pbh_lhs_ppf)
+ *   PBH_QSRC_VECTOR  q[i * stride] (pbh_ppf) */
+typedef enum pbh_qsource_kind { PBH_QSRC_SOBOL = 0, PBH_QSRC_LHS = 1, PBH_QSRC_VECTOR = 2 } pbh_qsource_kind;
+typedef struct pbh_dag_qsource {
+  int32_t kind;
+  int32_t col;          /* LHS column                         */
+  int32_t bits;         /* Sobol' bits (1..32)                */
+  uint32_t shift;       /* Sobol' digital shift               */
+  uint32_t sv[32];      /* Sobol' direction numbers           */
+  uint64_t seed;        /* LHS seed                           */
+  int64_t n_total;      /* LHS design rows                    */
+  const double* q;      /* VECTOR quantiles (device)          */
+  int64_t stride;       /* VECTOR stride (elements)           */
+} pbh_dag_qsource;
+
+/* Evaluate rows [0, n) (global rows row0 + i of the Sobol' / LHS streams).  vectors_host:
+ * nvectors float64 device vectors of n rows (LOAD inputs and STORE outputs). */
+int pbh_dag_eval(const pbh_dag_op* ops_host, int nops, const pbh_dag_qsource* sources_host, int nsources,
+                 double* const* vectors_host, int nvectors, int64_t row0, int64_t n, int32_t* flags, void* stream);
+
 /* Column-major <-> row-major transpose of an (rows x cols) float64 matrix (LDS-tiled). */
 int pbh_transpose(const double* in, int64_t rows, int64_t cols, int64_t ld_in, double* out, int64_t ld_out,
                   void* stream);

@@ -48,7 +48,7 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_pcg64_random", "pbh_halton_workspace_size", "pbh_fill_halton",
            "pbh_affine_workspace_size", "pbh_affine_rows", "pbh_table_ppf", "pbh_permcorr_workspace_size",
            "pbh_permcorr_climb", "pbh_sobol_ppf", "pbh_lhs_reference_workspace_size",
-           "pbh_lhs_reference", "pbh_lhs_reference_perms", "pbh_hbm_copy"]
+           "pbh_lhs_reference", "pbh_lhs_reference_perms", "pbh_hbm_copy", "pbh_dag_eval"]
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
@@ -57,7 +57,7 @@ KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_ra
            "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>",
            "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine", "k_table_ppf",
            "k_permcorr", "k_hbm_copy", "k_hist16", "k_msd1", "k_msd2", "k_finish", "k_place_msd",
-           "k_place_gen"]
+           "k_place_gen", "k_dag"]
 
 
 class Param(ctypes.Structure):
@@ -79,6 +79,23 @@ class ICArgs(ctypes.Structure):
                 ("y_rs", ctypes.c_int64), ("y_cs", ctypes.c_int64), ("ws", ctypes.c_void_p),
                 ("ws_bytes", ctypes.c_size_t), ("scores_out", ctypes.c_void_p), ("cscores_out", ctypes.c_void_p),
                 ("idx_out", ctypes.c_void_p), ("corr_host_out", ctypes.c_void_p)]
+
+
+class DagOp(ctypes.Structure):  # pbh_dag_op
+    _fields_ = [("kind", ctypes.c_int32), ("op", ctypes.c_int32), ("dst", ctypes.c_int32), ("a", ctypes.c_int32),
+                ("b", ctypes.c_int32), ("src", ctypes.c_int32), ("flag", ctypes.c_int32), ("store", ctypes.c_int32),
+                ("value", ctypes.c_double), ("params", ctypes.c_double * 3)]
+
+
+class DagSource(ctypes.Structure):  # pbh_dag_qsource
+    _fields_ = [("kind", ctypes.c_int32), ("col", ctypes.c_int32), ("bits", ctypes.c_int32), ("shift", ctypes.c_uint32),
+                ("sv", ctypes.c_uint32 * 32), ("seed", ctypes.c_uint64), ("n_total", ctypes.c_int64),
+                ("q", ctypes.c_void_p), ("stride", ctypes.c_int64)]
+
+
+DAG_GEN, DAG_LOAD, DAG_CONST, DAG_BINARY, DAG_UNARY, DAG_STORE = range(6)
+QSRC_SOBOL, QSRC_LHS, QSRC_VECTOR = range(3)
+DAG_MAX_REGS = 8
 
 
 class NativeError(RuntimeError):
@@ -151,6 +168,8 @@ def load():
         "pbh_lhs_reference_workspace_size": ([i64, ctypes.c_int32, ctypes.POINTER(sz)], i32),
         "pbh_lhs_reference": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, i64, vp, sz, vp], i32),
         "pbh_hbm_copy": ([vp, vp, sz, vp], i32),
+        "pbh_dag_eval": ([ctypes.POINTER(DagOp), i32, ctypes.POINTER(DagSource), i32, ctypes.POINTER(vp), i32, i64, i64,
+                          vp, vp], i32),
         "pbh_lhs_reference_perms": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, vp], i32),
         "pbh_permcorr_climb": ([vp, vp, i64, ctypes.c_int32, i64, vp, vp, vp, vp, vp, vp, i64, dbl, vp, vp, vp, sz, vp],
                                i32),

@@ -1,0 +1,177 @@
+// Device pieces of the inverse-CDF kernels shared by pbh_ppf.hip and pbh_dag.hip: the
+// per-element ppf of the base distributions, the ndtri tail queue, and the Sobol' point tables.
+#pragma once
+#include <math.h>
+
+#include "pbh_error.h"
+#include "pbh_special.h"
+
+namespace pbh {
+namespace {
+
+constexpr int kPpfBlock = 256;
+constexpr double kInf = sf::kInf;
+constexpr double kNaN = sf::kNaN;
+
+struct Params {
+  const double* ptr[3];
+  double val[3];
+  PBH_DI double at(int j, int64_t i) const { return ptr[j] ? ptr[j][i] : val[j]; }
+};
+
+// Per-launch constants of the distribution (scalar parameters only).
+constexpr int kPoissonGuideBits = 11;  // 2048 guide buckets
+
+struct PoissonTable {
+  const double* cdf;  // poisson: cdf[j] = pdtr(k_lo + j, mu) for scalar mu, else NULL
+  const int32_t* cdf_guide;  // cdf_guide[b] = first j with cdf[j] >= b / 2^kPoissonGuideBits
+  int64_t k_lo;
+  int64_t len;
+  int has_gamma;      // gamma with scalar a: hoisted GammaAux + z-grid guide
+  sf::GammaAux aux;
+  sf::GammaGuide guide;
+};
+
+// smallest k >= 0 with pdtr(k, mu) >= q, by stepping from a Cornish-Fisher guess.
+PBH_DI double poisson_search(double q, double mu) {
+  if (mu == 0.0) return 0.0;
+  double z = sf::ndtri(q);  // a starting guess only (the search decides k)
+  double g = floor(mu + sqrt(mu) * z + (z * z - 1.0) / 6.0);
+  if (!(g >= 0.0)) g = 0.0;
+  if (g > 9.0e15) g = 9.0e15;
+  double k = g;
+  if (sf::pdtr(k, mu) >= q) {
+    while (k > 0.0 && sf::pdtr(k - 1.0, mu) >= q) k -= 1.0;
+  } else {
+    do {
+      k += 1.0;
+    } while (sf::pdtr(k, mu) < q && k < 1.0e18);
+  }
+  return k;
+}
+
+// First j with cdf[j] >= q, by the guide table (Chen & Asau 1974): q lies in bucket
+// b = floor(q 2^bits) (exact: a power-of-two scale), whose guide entry is the answer for
+// q = b / 2^bits <= q, so a short forward scan from it ends at the answer -- the same j as a
+// binary search over the table, in ~1 probe instead of log2(len) dependent ones.
+PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
+  int64_t lo = t.cdf_guide[(int)(q * (double)(1 << kPoissonGuideBits))];
+  while (lo < t.len && t.cdf[lo] < q) ++lo;
+  if (lo == t.len || (lo == 0 && t.k_lo > 0)) return poisson_search(q, mu);  // outside coverage
+  return (double)(t.k_lo + lo);
+}
+
+// ppf of one element for distribution D; p = (shape..., loc, scale) already resolved.
+// PART selects ndtri's branch for norm / lognorm (0: ndtri, 1: ndtri_centre, 2: ndtri_tail),
+// for the compacted kernels that know which one an element takes.
+template <int D, int PART = 0>
+PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTable& pt) {
+  if constexpr (D == PBH_DIST_POISSON) {
+    double mu = p0, loc = p1;
+    bool cond0 = (mu >= 0.0) && (loc == loc);
+    if (q == 0.0) return -1.0 + loc;
+    if (cond0 && q == 1.0) return kInf + loc;
+    if (cond0 && q > 0.0 && q < 1.0) {
+      double k = pt.cdf ? poisson_from_table(q, mu, pt) : poisson_search(q, mu);
+      return k + loc;
+    }
+    return kNaN;
+  } else {
+    double shape = 0.0, loc, scale;
+    bool arg_ok = true;
+    double lower = 0.0, upper = kInf;
+    if constexpr (D == PBH_DIST_NORM || D == PBH_DIST_UNIFORM || D == PBH_DIST_EXPON) {
+      loc = p0;
+      scale = p1;
+    } else {
+      shape = p0;
+      loc = p1;
+      scale = p2;
+    }
+    if constexpr (D == PBH_DIST_NORM) lower = -kInf;
+    if constexpr (D == PBH_DIST_UNIFORM || D == PBH_DIST_TRIANG) upper = 1.0;
+    if constexpr (D == PBH_DIST_TRIANG) arg_ok = (shape >= 0.0) && (shape <= 1.0);
+    if constexpr (D == PBH_DIST_GAMMA || D == PBH_DIST_LOGNORM) arg_ok = shape > 0.0;
+    bool cond0 = arg_ok && (scale > 0.0) && (loc == loc);
+    if (!cond0) return kNaN;
+    if (q == 0.0) return lower * scale + loc;
+    if (q == 1.0) return upper * scale + loc;
+    if (!(q > 0.0 && q < 1.0)) return kNaN;
+    double x;
+    if constexpr (D == PBH_DIST_NORM) {
+      x = PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q);
+    } else if constexpr (D == PBH_DIST_UNIFORM) {
+      x = q;
+    } else if constexpr (D == PBH_DIST_EXPON) {
+      x = -sf::log1p_(-q);  // scipy expon._ppf: -sc.log1p(-q), the Cephes log1p
+    } else if constexpr (D == PBH_DIST_LOGNORM) {
+      x = exp(shape * (PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q)));
+    } else if constexpr (D == PBH_DIST_TRIANG) {
+      // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
+      x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
+    } else {  // gamma
+      x = pt.has_gamma ? sf::igami_guided(shape, q, &pt.aux, pt.guide) : sf::igami(shape, q);
+    }
+    return x * scale + loc;
+  }
+}
+
+// ---------------------------------------------------------------- tail compaction
+// ndtri (norm / lognorm ppf, the van der Waerden scores) is one rational function for
+// min(q, 1 - q) > e^-2 (73% of uniform q) and an expensive tail (two logs, a sqrt, three
+// divisions) otherwise.  With q in random order nearly every wave holds both kinds, and a wave
+// executes every branch one of its lanes takes, so a plain grid-stride kernel pays centre + tail
+// for every element.  The compacted kernels give each thread kCIpt items of a block tile: centre
+// items are evaluated at once, tail items are queued in LDS (one LDS atomic per wave) and then
+// drained by all lanes of the block together, so the tail costs its 27% share.  Every value is
+// computed by the same inline function either way (bit-identical to the plain kernels); the
+// results pass through LDS so that the global stores stay coalesced.
+constexpr int kCIpt = 8;
+constexpr int kCTile = kPpfBlock * kCIpt;
+
+struct TailQueue {
+  double arg[kCTile];
+  uint16_t pos[kCTile];
+  int count;
+};
+
+template <class Queue>  // TailQueue, or a smaller queue with the same members
+PBH_DI void tail_push(Queue& tq, bool take, double a, int p) {
+  const uint64_t m = __ballot(take);
+  if (m == 0ull) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const int leader = __builtin_ctzll(m);
+  int base = 0;
+  if (lane == leader) base = atomicAdd(&tq.count, (int)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (take) {
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int slot = base + (int)__popcll(m & lt);
+    tq.arg[slot] = a;
+    tq.pos[slot] = (uint16_t)p;
+  }
+}
+
+// x(r) = shift XOR (the direction numbers of the set bits of gray(r) = r ^ (r >> 1)), by four
+// 256-entry tables of the XORs over each byte of gray(r) (built in LDS per block): 4 lookups per
+// point instead of a loop over ~15 set bits.  Identical values (XOR is associative).
+PBH_DI void build_sobol_tables(const uint32_t* sv, uint32_t* T) {
+  for (int t = threadIdx.x; t < 256; t += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+        if ((t >> b) & 1) v ^= sv[8 * k + b];
+      T[k * 256 + t] = v;
+    }
+  }
+}
+
+PBH_DI uint32_t sobol_point(const uint32_t* T, uint32_t shift, uint64_t r) {
+  const uint32_t g = (uint32_t)(r ^ (r >> 1));  // r < 2^bits <= 2^32
+  return shift ^ T[g & 255u] ^ T[256 + ((g >> 8) & 255u)] ^ T[512 + ((g >> 16) & 255u)] ^ T[768 + (g >> 24)];
+}
+
+}  // namespace
+}  // namespace pbh

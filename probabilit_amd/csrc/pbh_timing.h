@@ -41,6 +41,7 @@ enum KernelId {
   kKFinish,
   kKPlaceMsd,
   kKPlaceGen,
+  kKDag,
   kKCount
 };
 

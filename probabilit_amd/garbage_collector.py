@@ -45,3 +45,20 @@ class GarbageCollector:
                 freed.append(parent)
             assert count >= 0
         return freed
+
+    def freed_by(self, order):
+        """The parents decrement_and_delete would free over the nodes of `order`, with the
+        same bookkeeping but nothing deleted and this collector's counts untouched -- for the
+        fused evaluation (probabilit_amd.dag), which never materialises the freed nodes."""
+        if not hasattr(self, "sink"):
+            raise ValueError("You must call 'set_sink' first.")
+        if self.strategy is None:
+            return set()
+        counts = collections.defaultdict(int, self._unsampled_children)
+        freed = set()
+        for node in order:
+            for parent in node.get_parents():
+                counts[parent] -= 1
+                if counts[parent] == 0 and parent not in self.strategy:
+                    freed.add(parent)
+        return freed

@@ -31,7 +31,7 @@ import networkx as nx
 import numpy as np
 import scipy.stats
 
-from . import _lib, device, qmc
+from . import _lib, dag, device, qmc
 from .correlation import Cholesky, ImanConover, PermutationCorrelator, nearest_correlation_matrix
 from .garbage_collector import GarbageCollector
 from .utils import build_corrmat
@@ -427,75 +427,82 @@ class Node(abc.ABC):
             block = device.empty((len(all_variables), size))
             block_row = {v: j for j, v in enumerate(all_variables)}
 
-        for node in isns:  # (:529-538)
-            for anc in nx.topological_sort(G.subgraph(nx.ancestors(G, node))):
-                assert isinstance(anc, (Constant, Transform))
-                anc._set_device(anc._sample_device(ev))
-            assert isinstance(node, AbstractDistribution)
-            if generated and node in all_variables:
-                deferred[node] = source.next_column()
-                continue
-            out = block[block_row[node]] if node in block_row else None
-            node._set_device(node._sample_device(ev, source.next_column(), out=out))
+        # a graph of leaf draws, constants and float64 transforms runs as one kernel
+        fused = not correlations and dag.try_evaluate(list(nx.topological_sort(G)), isns, source, ev, gc)
+        if not fused:
+            for node in isns:  # (:529-538)
+                for anc in nx.topological_sort(G.subgraph(nx.ancestors(G, node))):
+                    assert isinstance(anc, (Constant, Transform))
+                    anc._set_device(anc._sample_device(ev))
+                assert isinstance(node, AbstractDistribution)
+                if generated and node in all_variables:
+                    deferred[node] = source.next_column()
+                    continue
+                out = block[block_row[node]] if node in block_row else None
+                node._set_device(node._sample_device(ev, source.next_column(), out=out))
 
-        for variables, _ in correlations:  # (:548-551)
-            for variable in variables:
-                if variable not in isns:
-                    raise ValueError(f"Cannot correlate variable: {variable}")
-        for vars1, vars2 in itertools.combinations(variable_sets, 2):  # (:554-558)
-            common = vars1.intersection(vars2)
-            if len(common) > 1:
-                raise ValueError(f"Correlations specified more than once: {common}")
+            for variables, _ in correlations:  # (:548-551)
+                for variable in variables:
+                    if variable not in isns:
+                        raise ValueError(f"Cannot correlate variable: {variable}")
+            for vars1, vars2 in itertools.combinations(variable_sets, 2):  # (:554-558)
+                common = vars1.intersection(vars2)
+                if len(common) > 1:
+                    raise ValueError(f"Correlations specified more than once: {common}")
 
-        if correlations:  # (:571-583)
-            var_to_int = {v: i for (i, v) in enumerate(all_variables)}
-            indexed = [(tuple(var_to_int[v] for v in vs), cm) for (vs, cm) in correlations]
-            C = nearest_correlation_matrix(build_corrmat(indexed))
-            inst = correlator().set_target(C)
-            if generated and world > 1:
-                from .distributed import LHSColumn, iman_conover_lhs
+            if correlations:  # (:571-583)
+                var_to_int = {v: i for (i, v) in enumerate(all_variables)}
+                indexed = [(tuple(var_to_int[v] for v in vs), cm) for (vs, cm) in correlations]
+                C = nearest_correlation_matrix(build_corrmat(indexed))
+                inst = correlator().set_target(C)
+                if generated and world > 1:
+                    from .distributed import LHSColumn, iman_conover_lhs
 
-                cols = []
-                for var in all_variables:
-                    _, seed, n_total, col, _ = deferred[var]
-                    cols.append(LHSColumn(seed, col, _lib.DIST_IDS[var.distr], [float(p) for p in var._params(size)]))
-                vflags = device.zeros(len(cols), "int32")
-                Y = iman_conover_lhs(cols, inst.P, source.n, group=group, flags=vflags)
-                for j, var in enumerate(all_variables):
-                    ev.flags[ev.slot[var]] |= vflags[j]  # bitmask words: OR, never add
-                    var._set_device(Y[j])
-            elif generated:
-                cols = []
-                for var in all_variables:
-                    _, seed, n_total, col, _ = deferred[var]
-                    params = [float(p) for p in var._params(size)]
-                    cols.append(_lib.ICColumn(seed, col, _lib.DIST_IDS[var.distr], (ctypes.c_double * 3)(*params),
-                                              len(params), ev.flag_ptr(var)))
-                Y = inst._transform_generated(cols, size)
-                for j, var in enumerate(all_variables):
-                    var._set_device(Y[j])
-            elif isinstance(inst, (ImanConover, Cholesky, PermutationCorrelator)):
-                Y = inst._transform_device(block, ev)
-                for j, var in enumerate(all_variables):
-                    var._set_device(Y[j])
-            else:  # a user correlator class: the reference's (N, K) ndarray protocol
-                X = np.vstack([v.samples_ for v in all_variables]).T
-                Yh = inst(X)
-                for var, col in zip(all_variables, Yh.T):
-                    var.samples_ = np.copy(col)
+                    cols = []
+                    for var in all_variables:
+                        _, seed, n_total, col, _ = deferred[var]
+                        cols.append(LHSColumn(seed, col, _lib.DIST_IDS[var.distr], [float(p) for p in var._params(size)]))
+                    vflags = device.zeros(len(cols), "int32")
+                    Y = iman_conover_lhs(cols, inst.P, source.n, group=group, flags=vflags)
+                    for j, var in enumerate(all_variables):
+                        ev.flags[ev.slot[var]] |= vflags[j]  # bitmask words: OR, never add
+                        var._set_device(Y[j])
+                elif generated:
+                    cols = []
+                    for var in all_variables:
+                        _, seed, n_total, col, _ = deferred[var]
+                        params = [float(p) for p in var._params(size)]
+                        cols.append(_lib.ICColumn(seed, col, _lib.DIST_IDS[var.distr], (ctypes.c_double * 3)(*params),
+                                                  len(params), ev.flag_ptr(var)))
+                    Y = inst._transform_generated(cols, size)
+                    for j, var in enumerate(all_variables):
+                        var._set_device(Y[j])
+                elif isinstance(inst, (ImanConover, Cholesky, PermutationCorrelator)):
+                    Y = inst._transform_device(block, ev)
+                    for j, var in enumerate(all_variables):
+                        var._set_device(Y[j])
+                else:  # a user correlator class: the reference's (N, K) ndarray protocol
+                    X = np.vstack([v.samples_ for v in all_variables]).T
+                    Yh = inst(X)
+                    for var, col in zip(all_variables, Yh.T):
+                        var.samples_ = np.copy(col)
 
-        for node in nx.topological_sort(G):  # (:586-612)
-            if "_smp" in node.__dict__:
-                pass
-            elif isinstance(node, Constant):
-                node._set_device(node._sample_device(ev))
-            elif isinstance(node, AbstractDistribution):
-                node._set_device(node._sample_device(ev, source.next_column()))
-            elif isinstance(node, Transform):
-                node._set_device(node._sample_device(ev))
-            else:
-                raise TypeError("Node must be Constant, AbstractDistribution or Transform.")
-            gc.decrement_and_delete(node)
+            # the per-node loop, or all of it as one fused kernel (probabilit_amd.dag)
+            order = list(nx.topological_sort(G))
+            if correlations and dag.try_evaluate(order, isns, source, ev, gc):
+                order = []
+            for node in order:  # (:586-612)
+                if "_smp" in node.__dict__:
+                    pass
+                elif isinstance(node, Constant):
+                    node._set_device(node._sample_device(ev))
+                elif isinstance(node, AbstractDistribution):
+                    node._set_device(node._sample_device(ev, source.next_column()))
+                elif isinstance(node, Transform):
+                    node._set_device(node._sample_device(ev))
+                else:
+                    raise TypeError("Node must be Constant, AbstractDistribution or Transform.")
+                gc.decrement_and_delete(node)
 
         # fused non-finite check (:600-606): first flagged node in topological order raises
         if world > 1:  # every rank raises the same error (flag words OR-combined, bits unchanged)

@@ -139,6 +139,23 @@ def column_gate(k, cs_ref, y_dev, sx, cs_dev=None, tol=1e-13):
                     break
                 if kind:
                     break
+            g = int(counts[r[row]])
+            if not kind and g > 1:
+                # a reference tie group (equal CS): rankdata's 'average' gives all g rows the index
+                # p = int(avg) - 1 of sorted positions [a, a + g); where the device's CS differ by an
+                # ulp it hands the group those g distinct values instead
+                p = int(r[row])
+                a = p + 1 - (g + 1) // 2
+                if sx[a] <= v <= sx[a + g - 1]:
+                    partners = [int(i) for i in np.flatnonzero(r == p) if i != row]
+                    dcs = max(abs(float(cs_ref[row]) - float(cs_ref[q])) for q in partners)
+                    if dcs < tol:
+                        kind = "ref_tie"
+                        ties.add(tuple(sorted([int(row)] + partners)))
+                        worst = max(worst, dcs)
+                        if len(detail) < 8:
+                            detail.append({"row": int(row), "partners": partners, "kind": kind, "abs_dcs_ref": dcs,
+                                           "group": g})
             viol += 0 if kind else 1
         out.update(swaps=len(swaps), ties=len(ties), max_abs_dcs_ref=worst, violations=viol, pairs=detail)
         if cs_dev is not None:
