@@ -61,7 +61,14 @@ PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k
                                   "k_scatter<unsigned int, double>"],
              "k_code_runs": ["k_code_buckets", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
              "k_apply": ["k_apply_mfma", "k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"],
-             "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"]}
+             "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"],
+             # one timing id over every variant that ran (the cfg3 set: norm, lognorm, triang,
+             # uniform, expon, gamma, poisson): traffic = their dispatch-weighted mean
+             "k_place_gen": ["k_place_gen<0>", "k_place_gen<1>", "k_place_gen<2>", "k_place_gen<3>", "k_place_gen<4>",
+                             "k_place_gen_gamma", "k_place_gen_poisson"],
+             "k_lhs_sorted_ppf": ["k_lhs_sorted_ppf<0>", "k_lhs_sorted_ppf<1>", "k_lhs_sorted_ppf<2>",
+                                  "k_lhs_sorted_ppf<3>", "k_lhs_sorted_ppf<4>", "k_lhs_sorted_ppf<5>",
+                                  "k_lhs_sorted_ppf<6>"]}
 
 
 def pmc_traffic(kernel):
@@ -78,12 +85,12 @@ def pmc_traffic(kernel):
     if not files:
         return None, None
     ks = json.load(open(files[-1]))["kernels"]
-    names = PMC_NAMES.get(kernel, [kernel])
-    for name in names:  # alternatives (the kernel variant that ran), first match wins
-        if name in ks:
-            k = ks[name]
-            return int(k["hbm_bytes"]), os.path.relpath(files[-1], ROOT)  # per dispatch (pmc_summary.py)
-    return None, None
+    names = [nm for nm in PMC_NAMES.get(kernel, [kernel]) if nm in ks]  # the variants that ran
+    disp = sum(ks[nm]["dispatches"] for nm in names)
+    if not disp:
+        return None, None
+    per = sum(ks[nm]["hbm_bytes"] * ks[nm]["dispatches"] for nm in names) / disp  # per dispatch (pmc_summary.py)
+    return int(per), os.path.relpath(files[-1], ROOT)
 
 
 def main():

@@ -311,7 +311,7 @@ int pbh_average(const double* const* parents_host, int m, int64_t n, double* out
 typedef enum pbh_dag_kind {
   PBH_DAG_GEN = 0, PBH_DAG_LOAD = 1, PBH_DAG_CONST = 2, PBH_DAG_BINARY = 3, PBH_DAG_UNARY = 4, PBH_DAG_STORE = 5
 } pbh_dag_kind;
-#define PBH_DAG_MAX_REGS 8
+#define PBH_DAG_MAX_REGS 16
 #define PBH_DAG_MAX_OPS 65536
 
 typedef struct pbh_dag_op {

@@ -95,7 +95,7 @@ class DagSource(ctypes.Structure):  # pbh_dag_qsource
 
 DAG_GEN, DAG_LOAD, DAG_CONST, DAG_BINARY, DAG_UNARY, DAG_STORE = range(6)
 QSRC_SOBOL, QSRC_LHS, QSRC_VECTOR = range(3)
-DAG_MAX_REGS = 8
+DAG_MAX_REGS = 16
 
 
 class NativeError(RuntimeError):

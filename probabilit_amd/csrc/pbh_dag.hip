@@ -19,6 +19,12 @@
 // LDS and drain them with the whole block (the tail compaction of pbh_ppf.hip), writing straight
 // into the destination row.  Same inline functions as the per-node kernels and
 // -ffp-contract=off, so every value is bit-identical to the unfused evaluation.
+//
+// Measured (cfg5, N=1e8, profiles/r02/dag_ab.jsonl): the kernel is bound by ndtri's FP64 work
+// (~1.1 ms per draw column); uncapped it takes 229 VGPRs (2 waves per SIMD: the rational
+// functions' float64 constants are hoisted out of the program loop), capped at 4 waves per
+// SIMD it spills a little in the tail and the generic-operator calls and runs 15% faster; 8
+// items per thread did not pay.
 #include <math.h>
 #include <string.h>
 
@@ -35,7 +41,18 @@ namespace pbh {
 namespace {
 
 constexpr int kDBlock = 256;
-constexpr int kDIpt = 4;
+#ifndef PBH_DAG_IPT
+#define PBH_DAG_IPT 4
+#endif
+#ifndef PBH_DAG_WAVES
+#define PBH_DAG_WAVES 4
+#endif
+#if PBH_DAG_WAVES > 0
+#define PBH_DAG_OCC __attribute__((amdgpu_waves_per_eu(PBH_DAG_WAVES)))
+#else
+#define PBH_DAG_OCC
+#endif
+constexpr int kDIpt = PBH_DAG_IPT;
 constexpr int kDTile = kDBlock * kDIpt;
 
 struct DagQueue {  // TailQueue sized to one DAG tile
@@ -86,11 +103,10 @@ PBH_DI void gen_quantiles(const DagSrc& s, const uint32_t* T, int64_t row0, int6
 }
 
 // out[item] = ppf_D(q) for the tile, ndtri's tail drained by the whole block (norm / lognorm).
+// The caller has reset tq.count and synchronised.
 template <int D>
 PBH_DI void gen_compacted(const double (&q)[kDIpt], const double* p, double* out, DagQueue& tq) {
   const PoissonTable pt{};
-  if (threadIdx.x == 0) tq.count = 0;
-  __syncthreads();
 #pragma unroll
   for (int j = 0; j < kDIpt; ++j) {
     const bool tail = sf::ndtri_takes_tail(q[j]);
@@ -145,7 +161,7 @@ PBH_DI void operand(const double* regs, int r, double imm, double (&x)[kDIpt]) {
   for (int j = 0; j < kDIpt; ++j) x[j] = r >= 0 ? regs[r * kDTile + item(j)] : imm;
 }
 
-__global__ __launch_bounds__(kDBlock) void k_dag(const pbh_dag_op* __restrict__ prog, int nops,
+__global__ __launch_bounds__(kDBlock) PBH_DAG_OCC void k_dag(const pbh_dag_op* __restrict__ prog, int nops,
                                                  const DagSrc* __restrict__ src, double* const* __restrict__ vec,
                                                  int64_t row0, int64_t n, int32_t* __restrict__ flags) {
   __shared__ DagQueue tq;
@@ -161,12 +177,13 @@ __global__ __launch_bounds__(kDBlock) void k_dag(const pbh_dag_op* __restrict__ 
       double x[kDIpt];
       bool have = true;  // x holds this op's result (GEN reads it back from its row)
       if (kind == PBH_DAG_GEN) {
+        // Every GEN ends with a barrier (below), so here the previous GEN's readers of T and of
+        // the tail queue are done: refill T, reset the queue, one barrier.
         const DagSrc& s = src[op.src];
-        if (s.kind == PBH_QSRC_SOBOL) {
-          __syncthreads();  // the previous GEN's readers of T are done
+        if (s.kind == PBH_QSRC_SOBOL)
           for (int t = threadIdx.x; t < 1024; t += kDBlock) T[t] = s.T[t];
-          __syncthreads();
-        }
+        if (threadIdx.x == 0) tq.count = 0;
+        __syncthreads();
         double q[kDIpt];
         gen_quantiles(s, T, row0, base, n, q);
         const double p[3] = {op.params[0], op.params[1], op.params[2]};

@@ -52,6 +52,7 @@ class _Plan:
         self.emitted = set()
         self.gens = []  # GEN nodes in emission order
         self.loads = []  # (node, tensor) LOAD inputs
+        self.need = {}  # node -> Sethi-Ullman register need
 
     def add(self, kind, dst=None, a=None, b=None, op=0, flag=None, value=0.0, params=(0.0, 0.0, 0.0), node=None):
         self.ops.append(dict(kind=kind, op=op, dst=dst, a=a, b=b, flag=flag, store=None, value=value,
@@ -86,6 +87,7 @@ def _classify(plan, node, isns):
             if _dtype_of(dev) != np.float64:
                 raise _Unfusable
             plan.val[node] = ("leaf", "load", dev)
+            plan.need[node] = 1
         return
     if isinstance(node, Constant):
         try:
@@ -100,61 +102,92 @@ def _classify(plan, node, isns):
         if not all(isinstance(p, float) for p in params):
             raise _Unfusable
         plan.val[node] = ("leaf", "gen", params)
+        plan.need[node] = 1
         return
     if isinstance(node, NoOp):
         plan.val[node] = ("none",)
         return
+    if isinstance(node, (Avg, VariadicTransform, BinaryTransform, UnaryTransform)):
+        if isinstance(node, VariadicTransform) and not isinstance(node, Avg):
+            if node.op_name not in ("add", "mul", "max", "min") or len(node.parents) < 2:
+                raise _Unfusable  # (reduce of one parent: that parent's own samples)
+        if isinstance(node, BinaryTransform) and node.op_name not in _BINARY:
+            raise _Unfusable
+        vals = [plan.val[p][0] for p in node.get_parents()]
+        if "none" in vals:
+            raise _Unfusable  # NoOp's samples are None: arithmetic on it raises in the reference
+        if all(v == "imm" for v in vals):
+            raise _Unfusable  # a numpy scalar result: the per-node path keeps it on the host
+        if not isinstance(node, Avg):
+            ops = list(node.get_parents())
+            if len(ops) >= 2 and all(plan.val[p][0] == "imm" for p in ops[:2]):
+                raise _Unfusable  # the first partial of the reduce is a scalar
+        plan.val[node] = ("xform",)
+        plan.need[node] = _need(plan, node)
+        return
+    raise _Unfusable
+
+
+def _need(plan, node):
+    """Registers to evaluate node's expression tree (Sethi-Ullman, sharing ignored)."""
+    needs = [plan.need.get(p, 0) for p in node.get_parents()]
+    if len(needs) == 1:
+        return max(needs[0], 1)
+    from .modeling import VariadicTransform
+
+    if isinstance(node, VariadicTransform):  # reduced in order: the accumulator plus the next parent
+        return max([needs[0]] + [1 + x for x in needs[1:]] + [1])
+    hi, lo = max(needs), min(needs)
+    return max(hi, lo + 1, 1)
+
+
+def _emit(plan, node):
+    """Emit node's ops after its operands' (depth first, the costlier operand of a binary op
+    first), so that few values are live at once."""
+    from .modeling import Avg, BinaryTransform, NoOp, UnaryTransform, VariadicTransform
+
+    if node in plan.emitted:
+        return
+    v = plan.val[node]
+    if v[0] == "leaf":
+        _emit_leaf(plan, node)
+        return
+    if v[0] != "xform":
+        if isinstance(node, NoOp):
+            plan.emitted.add(node)
+            for p in node.parents:
+                _emit(plan, p)
+        return
+    plan.emitted.add(node)
     flag = plan.ev.slot[node]
     if isinstance(node, Avg):  # k_average: s = p0 + p1 + ..., x = s / m, only x checked
         parts = list(node.parents)
-        if not any(plan.val[p][0] in ("leaf", "key") for p in parts):
-            raise _Unfusable
         acc = _operand(plan, parts[0])
         for j, p in enumerate(parts[1:]):
             b = _operand(plan, p)
-            if acc[0] == "imm" and b[0] == "imm":
-                raise _Unfusable
             key = ("tmp", node, j)
             plan.add(_lib.DAG_BINARY, dst=key, a=acc, b=b, op=_lib.OPS["add"], node=node)
             acc = ("key", key)
         plan.add(_lib.DAG_BINARY, dst=node, a=acc, b=("imm", float(len(parts))), op=_lib.OPS["truediv"], flag=flag,
                  node=node)
-        plan.val[node] = ("key", node)
-        return
-    if isinstance(node, VariadicTransform):
-        if node.op_name not in ("add", "mul", "max", "min"):
-            raise _Unfusable
+    elif isinstance(node, VariadicTransform):  # functools.reduce, each partial flagged (:943-959)
         parts = list(node.parents)
         acc = _operand(plan, parts[0])
-        if len(parts) == 1:  # functools.reduce of one element: the parent's own samples
-            raise _Unfusable
         for j, p in enumerate(parts[1:]):
             b = _operand(plan, p)
-            if acc[0] == "imm" and b[0] == "imm":
-                raise _Unfusable
-            last = j == len(parts) - 2
-            key = node if last else ("tmp", node, j)
+            key = node if j == len(parts) - 2 else ("tmp", node, j)
             plan.add(_lib.DAG_BINARY, dst=key, a=acc, b=b, op=_lib.OPS[node.op_name], flag=flag, node=node)
             acc = ("key", key)
-        plan.val[node] = ("key", node)
-        return
-    if isinstance(node, BinaryTransform):
-        if node.op_name not in _BINARY:
-            raise _Unfusable
-        a, b = (_operand(plan, p) for p in node.parents)
-        if a[0] == "imm" and b[0] == "imm":
-            raise _Unfusable
-        plan.add(_lib.DAG_BINARY, dst=node, a=a, b=b, op=_lib.OPS[node.op_name], flag=flag, node=node)
-        plan.val[node] = ("key", node)
-        return
-    if isinstance(node, UnaryTransform):
-        a = _operand(plan, node.parent)
-        if a[0] == "imm":
-            raise _Unfusable
-        plan.add(_lib.DAG_UNARY, dst=node, a=a, op=_lib.OPS[node.op_name], flag=flag, node=node)
-        plan.val[node] = ("key", node)
-        return
-    raise _Unfusable
+    elif isinstance(node, BinaryTransform):
+        pa, pb = node.parents
+        for p in sorted((pa, pb), key=lambda q: -plan.need.get(q, 0)):
+            _operand(plan, p)
+        plan.add(_lib.DAG_BINARY, dst=node, a=_operand(plan, pa), b=_operand(plan, pb), op=_lib.OPS[node.op_name],
+                 flag=flag, node=node)
+    else:
+        assert isinstance(node, UnaryTransform)
+        plan.add(_lib.DAG_UNARY, dst=node, a=_operand(plan, node.parent), op=_lib.OPS[node.op_name], flag=flag,
+                 node=node)
 
 
 def _emit_leaf(plan, node):
@@ -177,8 +210,7 @@ def _operand(plan, node):
         return v
     if v[0] == "none":
         raise _Unfusable  # NoOp's samples are None: arithmetic on it raises in the reference
-    if v[0] == "leaf":
-        _emit_leaf(plan, node)
+    _emit(plan, node)
     return ("key", node)
 
 
@@ -223,6 +255,33 @@ def _allocate(plan):
     return used
 
 
+def plan_graph(order, isns, ev, gc):
+    """The fused program for the graph whose nodes are `order` (topological), or None when
+    the graph is outside the fused subset.  Host-only (no device work): the plan's ops carry
+    registers (rd / ra / rb), and plan.kept / plan.freed / plan.stored / plan.gen_nodes say
+    which nodes keep samples, which the collector frees, which the kernel writes, and which
+    draws it makes (one quantile column each, in ISN order)."""
+    plan = _Plan(ev.size, ev)
+    try:
+        for node in order:
+            _classify(plan, node, isns)
+        _emit(plan, order[-1])  # the sink: the only node without children
+        for nd in isns:  # every draw is made (and flagged) even when nothing reads or keeps it
+            if plan.val[nd][:2] == ("leaf", "gen"):
+                _emit_leaf(plan, nd)
+        if not plan.ops or _allocate(plan) is None:
+            return None
+    except (_Unfusable, RecursionError):
+        return None
+    plan.gen_nodes = [nd for nd in isns if plan.val[nd][:2] == ("leaf", "gen")]
+    if len(plan.gen_nodes) != sum(1 for nd in isns if "_smp" not in nd.__dict__):
+        return None
+    plan.freed = gc.freed_by(order)
+    plan.kept = [nd for nd in order if nd not in plan.freed]
+    plan.stored = [nd for nd in plan.kept if plan.val[nd][0] == "xform" or plan.val[nd][:2] == ("leaf", "gen")]
+    return plan
+
+
 def try_evaluate(order, isns, source, ev, gc):
     """Evaluate the graph whose nodes are `order` (topological) with one fused kernel.
 
@@ -234,27 +293,11 @@ def try_evaluate(order, isns, source, ev, gc):
     from .modeling import Constant, NoOp, _Broadcast
 
     n = ev.size
-    plan = _Plan(n, ev)
-    try:
-        for node in order:
-            _classify(plan, node, isns)
-        freed = gc.freed_by(order)
-        kept = [nd for nd in order if nd not in freed]
-        for nd in isns:  # every draw is made (and flagged) even when nothing reads or keeps it
-            if plan.val[nd][:2] == ("leaf", "gen"):
-                _emit_leaf(plan, nd)
-        if not plan.ops:
-            return False
-        nregs = _allocate(plan)
-        if nregs is None:
-            counts["declined"] += 1
-            return False
-    except _Unfusable:
+    plan = plan_graph(order, isns, ev, gc)
+    if plan is None:
         counts["declined"] += 1
         return False
-    gen_nodes = [nd for nd in isns if plan.val[nd][:2] == ("leaf", "gen")]
-    if len(gen_nodes) != sum(1 for nd in isns if "_smp" not in nd.__dict__):
-        return False
+    gen_nodes, freed = plan.gen_nodes, plan.freed
 
     # ---- commit: quantile columns in ISN order (modeling.py:529-538), outputs, launch
     cols = {nd: source.next_column() for nd in gen_nodes}
@@ -285,12 +328,10 @@ def try_evaluate(order, isns, source, ev, gc):
         vindex[("in", nd)] = len(vectors)
         vectors.append(t)
     outputs = {}
-    for nd in kept:
-        v = plan.val[nd]
-        if v[0] == "key" or (v[0] == "leaf" and v[1] == "gen"):
-            outputs[nd] = device.empty(n)
-            vindex[("out", nd)] = len(vectors)
-            vectors.append(outputs[nd])
+    for nd in plan.stored:
+        outputs[nd] = device.empty(n)
+        vindex[("out", nd)] = len(vectors)
+        vectors.append(outputs[nd])
     ops = (_lib.DagOp * len(plan.ops))()
     for i, o in enumerate(plan.ops):
         d = ops[i]

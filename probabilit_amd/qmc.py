@@ -23,6 +23,7 @@ with stream="reference".
 """
 
 import ctypes
+import functools
 import numbers
 import os
 import warnings
@@ -118,6 +119,11 @@ MAXDIM = 21201
 
 def sobol_direction_matrix(d, bits=30):
     """Unscrambled direction matrix v (d x bits), Bratley & Fox recurrence."""
+    return _direction_matrix(d, bits).copy()
+
+
+@functools.lru_cache(maxsize=64)
+def _direction_matrix(d, bits):
     poly, vinit = _direction_numbers()
     v = np.zeros((d, bits), dtype=np.uint64)
     if d == 0:
@@ -142,24 +148,16 @@ def sobol_direction_matrix(d, bits=30):
 
 def _lms_scramble(sv, ltm, bits):
     """Linear matrix scramble: each direction number times a random lower-triangular binary
-    matrix (unit diagonal) over GF(2), MSB first."""
-    d = sv.shape[0]
-    ltm = ltm.copy()
+    matrix (unit diagonal) over GF(2), MSB first: bit (bits-1-p) of the result is the parity
+    of row p of the matrix AND-ed with the number (scipy's _cscramble loop, as one GF(2)
+    matrix product per dimension)."""
+    ltm = ltm.astype(np.int64, copy=True)
     idx = np.arange(bits)
     ltm[:, idx, idx] = 1
-    weights = np.array([1 << (bits - 1 - i) for i in range(bits)], dtype=object)
-    out = np.zeros_like(sv)
-    for k in range(d):
-        rows = [int(sum(int(x) * w for x, w in zip(ltm[k, p, :], weights))) for p in range(bits)]
-        for j in range(bits):
-            vkj = int(sv[k, j])
-            t2, l = 0, 1
-            for p in range(bits - 1, -1, -1):
-                t1 = bin(rows[p] & vkj).count("1") & 1
-                t2 += t1 * l
-                l <<= 1
-            out[k, j] = t2
-    return out
+    shifts = (bits - 1 - idx).astype(np.uint64)
+    vb = ((sv.astype(np.uint64)[:, :, None] >> shifts[None, None, :]) & 1).astype(np.int64)  # (d, j, i) MSB first
+    ob = np.einsum("kji,kpi->kjp", vb, ltm) & 1  # (d, j, p)
+    return (ob.astype(np.uint64) << shifts[None, None, :]).sum(axis=2).astype(sv.dtype)
 
 
 def sobol_setup(d, rng=None, bits=30, scramble=True):

@@ -33,6 +33,21 @@ def timed(fn, steps, sync):
     return (time.perf_counter() - t0) / steps
 
 
+def kernel_ms(lib, calls):
+    """Device time per call of each timed kernel (HIP events, pbh_timing_*) since the reset."""
+    import ctypes
+
+    from probabilit_amd import _lib
+
+    out = {}
+    for kid, name in enumerate(_lib.KERNELS):
+        t, c = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(lib.pbh_timing_read(kid, ctypes.byref(t), ctypes.byref(c)))
+        if c.value:
+            out[name] = {"ms_per_call": round(t.value / calls, 3), "launches_per_call": c.value / calls}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3)
@@ -93,14 +108,24 @@ def main():
             break
     sync()
     out["cfg5_seeds"] = good
+    from probabilit_amd import _lib, dag
+
+    lib = _lib.load()
     for gc, label, per_row in [(None, "gc_none", 8 * (3 * years)), ([], "gc_sink", 8)]:
         sink = fund()
+        fused0 = dag.counts["fused"]
+        lib.pbh_timing_reset()
+        lib.pbh_timing_enable(1)
         t = timed(lambda i: sink.sample_device(n5, random_state=good[i], method="sobol", gc_strategy=gc),
                   args.steps, sync)
+        lib.pbh_timing_enable(0)
+        calls = args.steps + 1
         out[f"cfg5_{label}"] = {"workload": f"20-step mutual fund, Sobol, N=1e8, gc_strategy={gc}",
                                 "ms": round(t * 1e3, 3), "Msamples_per_s": round(n5 * years / t / 1e6, 1),
                                 "hbm_GBps_retained_writes": round(per_row * n5 / t / 1e9, 1),
-                                "retained_bytes_per_row": per_row}
+                                "retained_bytes_per_row": per_row,
+                                "fused_calls": dag.counts["fused"] - fused0,
+                                "kernels": kernel_ms(lib, calls)}
     Q = scipy.stats.qmc.Sobol(d=years, rng=0).random(args.cpu_n)
     t0 = time.perf_counter()
     mutual_fund(Q, years)
