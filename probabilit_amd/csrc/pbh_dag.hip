@@ -72,7 +72,18 @@ struct DagSrc {
   int64_t n_total;
   const double* q;
   int64_t stride;
+  double p[3];  // the GEN's scalar parameters (one source per GEN)
 };
+
+// The program as the kernel reads it: 32 bytes per op, one scalar load (and the next op's
+// load in flight while this one runs).
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+struct DOp {
+  uint32_t head;  // kind | op << 8 | (dst + 1) << 16 | (a + 1) << 24
+  int32_t b, src, flag, store, pad;
+  double value;
+};
+static_assert(sizeof(DOp) == 32, "DOp is one 32-byte scalar load");
 
 PBH_DI int item(int j) { return j * kDBlock + threadIdx.x; }
 
@@ -103,27 +114,45 @@ PBH_DI void gen_quantiles(const DagSrc& s, const uint32_t* T, int64_t row0, int6
 }
 
 // out[item] = ppf_D(q) for the tile, ndtri's tail drained by the whole block (norm / lognorm).
-// The caller has reset tq.count and synchronised.
+// The caller has reset tq.count and synchronised.  Returns whether a valid row's value is
+// non-finite (each thread for the values it computed).
 template <int D>
-PBH_DI void gen_compacted(const double (&q)[kDIpt], const double* p, double* out, DagQueue& tq) {
+PBH_DI bool gen_compacted(const double (&q)[kDIpt], const bool (&valid)[kDIpt], const double* p, double* out,
+                          DagQueue& tq) {
   const PoissonTable pt{};
+  bool bad = false;
 #pragma unroll
   for (int j = 0; j < kDIpt; ++j) {
-    const bool tail = sf::ndtri_takes_tail(q[j]);
-    if (!tail) out[item(j)] = ppf_one<D, 1>(q[j], p[0], p[1], p[2], pt);
+    const bool tail = sf::ndtri_takes_tail(q[j]);  // never for rows past n (q = 0.5)
+    if (!tail) {
+      const double x = ppf_one<D, 1>(q[j], p[0], p[1], p[2], pt);
+      out[item(j)] = x;
+      bad |= valid[j] && !isfinite(x);
+    }
     tail_push(tq, tail, q[j], item(j));
   }
   __syncthreads();
   const int T = tq.count;
 #pragma unroll 1
-  for (int t = threadIdx.x; t < T; t += kDBlock) out[tq.pos[t]] = ppf_one<D, 2>(tq.arg[t], p[0], p[1], p[2], pt);
+  for (int t = threadIdx.x; t < T; t += kDBlock) {
+    const double x = ppf_one<D, 2>(tq.arg[t], p[0], p[1], p[2], pt);
+    out[tq.pos[t]] = x;
+    bad |= !isfinite(x);
+  }
+  return bad;
 }
 
 template <int D>
-PBH_DI void gen_plain(const double (&q)[kDIpt], const double* p, double* out) {
+PBH_DI bool gen_plain(const double (&q)[kDIpt], const bool (&valid)[kDIpt], const double* p, double* out) {
   const PoissonTable pt{};
+  bool bad = false;
 #pragma unroll
-  for (int j = 0; j < kDIpt; ++j) out[item(j)] = ppf_one<D>(q[j], p[0], p[1], p[2], pt);
+  for (int j = 0; j < kDIpt; ++j) {
+    const double x = ppf_one<D>(q[j], p[0], p[1], p[2], pt);
+    out[item(j)] = x;
+    bad |= valid[j] && !isfinite(x);
+  }
+  return bad;
 }
 
 // The operators beyond + - * / (pow, atan2, the transcendental unary ops), one element per
@@ -161,82 +190,88 @@ PBH_DI void operand(const double* regs, int r, double imm, double (&x)[kDIpt]) {
   for (int j = 0; j < kDIpt; ++j) x[j] = r >= 0 ? regs[r * kDTile + item(j)] : imm;
 }
 
-__global__ __launch_bounds__(kDBlock) PBH_DAG_OCC void k_dag(const pbh_dag_op* __restrict__ prog, int nops,
-                                                 const DagSrc* __restrict__ src, double* const* __restrict__ vec,
-                                                 int64_t row0, int64_t n, int32_t* __restrict__ flags) {
+__global__ __launch_bounds__(kDBlock) PBH_DAG_OCC void k_dag(const DOp* __restrict__ prog, int nops,
+                                                             const DagSrc* __restrict__ src,
+                                                             double* const* __restrict__ vec, int64_t row0, int64_t n,
+                                                             int32_t* __restrict__ flags) {
   __shared__ DagQueue tq;
   __shared__ uint32_t T[1024];
   extern __shared__ double regs[];  // [nregs][kDTile]
+  const u32x8* code = reinterpret_cast<const u32x8*>(prog);
   for (int64_t base = (int64_t)blockIdx.x * kDTile; base < n; base += (int64_t)gridDim.x * kDTile) {
     bool valid[kDIpt];
 #pragma unroll
     for (int j = 0; j < kDIpt; ++j) valid[j] = base + item(j) < n;
+    u32x8 next = code[0];
     for (int k = 0; k < nops; ++k) {
-      const pbh_dag_op& op = prog[k];
-      const int kind = op.kind;
+      const u32x8 w = next;
+      if (k + 1 < nops) next = code[k + 1];  // in flight while this op runs
+      const int kind = (int)(w[0] & 0xffu), opc = (int)((w[0] >> 8) & 0xffu);
+      const int dst = (int)((w[0] >> 16) & 0xffu) - 1, ra = (int)(w[0] >> 24) - 1;
+      const int rb = (int)w[1], si = (int)w[2], flag = (int)w[3], store = (int)w[4];
+      const double value = __builtin_bit_cast(double, ((uint64_t)w[7] << 32) | w[6]);
       double x[kDIpt];
-      bool have = true;  // x holds this op's result (GEN reads it back from its row)
+      bool have = true;  // x holds this op's result
+      bool bad = false;
       if (kind == PBH_DAG_GEN) {
         // Every GEN ends with a barrier (below), so here the previous GEN's readers of T and of
         // the tail queue are done: refill T, reset the queue, one barrier.
-        const DagSrc& s = src[op.src];
+        const DagSrc& s = src[si];
         if (s.kind == PBH_QSRC_SOBOL)
           for (int t = threadIdx.x; t < 1024; t += kDBlock) T[t] = s.T[t];
         if (threadIdx.x == 0) tq.count = 0;
         __syncthreads();
         double q[kDIpt];
         gen_quantiles(s, T, row0, base, n, q);
-        const double p[3] = {op.params[0], op.params[1], op.params[2]};
-        double* out = regs + op.dst * kDTile;
-        switch (op.op) {
-          case PBH_DIST_NORM: gen_compacted<PBH_DIST_NORM>(q, p, out, tq); break;
-          case PBH_DIST_LOGNORM: gen_compacted<PBH_DIST_LOGNORM>(q, p, out, tq); break;
-          case PBH_DIST_UNIFORM: gen_plain<PBH_DIST_UNIFORM>(q, p, out); break;
-          case PBH_DIST_EXPON: gen_plain<PBH_DIST_EXPON>(q, p, out); break;
-          default: gen_plain<PBH_DIST_TRIANG>(q, p, out); break;
+        const double p[3] = {s.p[0], s.p[1], s.p[2]};
+        double* out = regs + dst * kDTile;
+        switch (opc) {
+          case PBH_DIST_NORM: bad = gen_compacted<PBH_DIST_NORM>(q, valid, p, out, tq); break;
+          case PBH_DIST_LOGNORM: bad = gen_compacted<PBH_DIST_LOGNORM>(q, valid, p, out, tq); break;
+          case PBH_DIST_UNIFORM: bad = gen_plain<PBH_DIST_UNIFORM>(q, valid, p, out); break;
+          case PBH_DIST_EXPON: bad = gen_plain<PBH_DIST_EXPON>(q, valid, p, out); break;
+          default: bad = gen_plain<PBH_DIST_TRIANG>(q, valid, p, out); break;
         }
         __syncthreads();  // drained tail values are in the row
-        have = false;
-        if (op.store >= 0 || op.flag >= 0) {
-          operand(regs, op.dst, 0.0, x);
-          have = true;
+        have = store >= 0;
+        if (have) operand(regs, dst, 0.0, x);
+      } else {
+        if (kind == PBH_DAG_LOAD) {
+          const double* v = vec[si];
+#pragma unroll
+          for (int j = 0; j < kDIpt; ++j) x[j] = valid[j] ? v[base + item(j)] : 0.0;
+        } else if (kind == PBH_DAG_CONST) {
+#pragma unroll
+          for (int j = 0; j < kDIpt; ++j) x[j] = value;
+        } else if (kind == PBH_DAG_BINARY) {
+          double a[kDIpt], b[kDIpt];
+          operand(regs, ra, value, a);
+          operand(regs, rb, value, b);
+          binary(opc, a, b, x);
+        } else if (kind == PBH_DAG_UNARY) {
+          double a[kDIpt];
+          operand(regs, ra, value, a);
+#pragma unroll
+          for (int j = 0; j < kDIpt; ++j) x[j] = unary_call(opc, a[j]);
+        } else {  // STORE
+          operand(regs, ra, value, x);
         }
-      } else if (kind == PBH_DAG_LOAD) {
-        const double* v = vec[op.src];
+        if (kind != PBH_DAG_STORE && dst >= 0) {
 #pragma unroll
-        for (int j = 0; j < kDIpt; ++j) x[j] = valid[j] ? v[base + item(j)] : 0.0;
-      } else if (kind == PBH_DAG_CONST) {
+          for (int j = 0; j < kDIpt; ++j) regs[dst * kDTile + item(j)] = x[j];
+        }
+        if (flag >= 0) {
 #pragma unroll
-        for (int j = 0; j < kDIpt; ++j) x[j] = op.value;
-      } else if (kind == PBH_DAG_BINARY) {
-        double a[kDIpt], b[kDIpt];
-        operand(regs, op.a, op.value, a);
-        operand(regs, op.b, op.value, b);
-        binary(op.op, a, b, x);
-      } else if (kind == PBH_DAG_UNARY) {
-        double a[kDIpt];
-        operand(regs, op.a, op.value, a);
-#pragma unroll
-        for (int j = 0; j < kDIpt; ++j) x[j] = unary_call(op.op, a[j]);
-      } else {  // STORE
-        operand(regs, op.a, op.value, x);
+          for (int j = 0; j < kDIpt; ++j) bad |= valid[j] && !isfinite(x[j]);
+        }
       }
-      if (kind != PBH_DAG_GEN && kind != PBH_DAG_STORE && op.dst >= 0) {
-#pragma unroll
-        for (int j = 0; j < kDIpt; ++j) regs[op.dst * kDTile + item(j)] = x[j];
-      }
-      if (have && op.store >= 0) {
-        double* v = vec[op.store];
+      if (have && store >= 0) {
+        double* v = vec[store];
 #pragma unroll
         for (int j = 0; j < kDIpt; ++j)
           if (valid[j]) __builtin_nontemporal_store(x[j], v + base + item(j));
       }
-      if (have && op.flag >= 0) {
-        bool bad = false;
-#pragma unroll
-        for (int j = 0; j < kDIpt; ++j) bad |= valid[j] && !isfinite(x[j]);
-        flag_nonfinite(flags + op.flag, bad);
-      }
+      if (flag >= 0) flag_nonfinite(flags + flag, bad);
     }
   }
 }
@@ -321,44 +356,67 @@ extern "C" int pbh_dag_eval(const pbh_dag_op* ops_host, int nops, const pbh_dag_
   }
   if (n == 0 || nops == 0) return PBH_OK;
 
-  // one upload: program | sources | vector table | Sobol' XOR tables
-  const size_t b_ops = align256((size_t)nops * sizeof(pbh_dag_op));
-  const size_t b_src = align256((size_t)std::max(nsources, 1) * sizeof(DagSrc));
+  // one upload: program | sources | vector table | Sobol' XOR tables.  Every GEN gets a source
+  // entry of its own (the quantile stream plus the GEN's parameters).
+  int ngen = 0;
+  for (int k = 0; k < nops; ++k) ngen += ops_host[k].kind == PBH_DAG_GEN;
+  const int nsrc = ngen;
+  const size_t b_ops = align256((size_t)nops * sizeof(DOp));
+  const size_t b_src = align256((size_t)std::max(nsrc, 1) * sizeof(DagSrc));
   const size_t b_vec = align256((size_t)std::max(nvectors, 1) * sizeof(double*));
   const size_t b_tab = (size_t)nsobol * 1024 * 4;
   std::vector<uint8_t> host(b_ops + b_src + b_vec + b_tab, 0);
   hipStream_t st = as_stream(stream);
   uint8_t* dev = nullptr;
   PBH_CHECK_HIP(hipMallocAsync((void**)&dev, host.size(), st));
-  memcpy(host.data(), ops_host, (size_t)nops * sizeof(pbh_dag_op));
   DagSrc* hs = (DagSrc*)(host.data() + b_ops);
   uint32_t* ht = (uint32_t*)(host.data() + b_ops + b_src + b_vec);
   const uint32_t* dt = (const uint32_t*)(dev + b_ops + b_src + b_vec);
+  std::vector<int> table_of(nsources, -1);  // Sobol' XOR tables, one per source
   int t = 0;
   for (int s = 0; s < nsources; ++s) {
     const pbh_dag_qsource& q = sources_host[s];
-    DagSrc d = {};
-    d.kind = q.kind;
-    d.col = q.col;
-    d.shift = q.shift;
-    d.seed = q.seed;
-    d.n_total = q.n_total;
-    d.q = q.q;
-    d.stride = q.stride;
-    if (q.kind == PBH_QSRC_SOBOL) {
-      d.scale = 1.0 / (double)((uint64_t)1 << q.bits);
-      uint32_t* tb = ht + (size_t)t * 1024;
-      for (int e = 0; e < 256; ++e)
-        for (int g = 0; g < 4; ++g) {
-          uint32_t v = 0;
-          for (int b = 0; b < 8; ++b)
-            if (((e >> b) & 1) && 8 * g + b < q.bits) v ^= q.sv[8 * g + b];
-          tb[g * 256 + e] = v;
-        }
-      d.T = dt + (size_t)t * 1024;
-      ++t;
+    if (q.kind != PBH_QSRC_SOBOL) continue;
+    uint32_t* tb = ht + (size_t)t * 1024;
+    for (int e = 0; e < 256; ++e)
+      for (int g = 0; g < 4; ++g) {
+        uint32_t v = 0;
+        for (int b = 0; b < 8; ++b)
+          if (((e >> b) & 1) && 8 * g + b < q.bits) v ^= q.sv[8 * g + b];
+        tb[g * 256 + e] = v;
+      }
+    table_of[s] = t++;
+  }
+  DOp* hp = (DOp*)host.data();
+  int gi = 0;
+  for (int k = 0; k < nops; ++k) {
+    const pbh_dag_op& o = ops_host[k];
+    DOp d = {};
+    d.head = (uint32_t)o.kind | ((uint32_t)o.op << 8) | ((uint32_t)(o.dst + 1) << 16) | ((uint32_t)(o.a + 1) << 24);
+    d.b = o.b;
+    d.src = o.src;
+    d.flag = o.flag;
+    d.store = o.store;
+    d.value = o.value;
+    if (o.kind == PBH_DAG_GEN) {
+      const pbh_dag_qsource& q = sources_host[o.src];
+      DagSrc g = {};
+      g.kind = q.kind;
+      g.col = q.col;
+      g.shift = q.shift;
+      g.seed = q.seed;
+      g.n_total = q.n_total;
+      g.q = q.q;
+      g.stride = q.stride;
+      if (q.kind == PBH_QSRC_SOBOL) {
+        g.scale = 1.0 / (double)((uint64_t)1 << q.bits);
+        g.T = dt + (size_t)table_of[o.src] * 1024;
+      }
+      for (int j = 0; j < 3; ++j) g.p[j] = o.params[j];
+      hs[gi] = g;
+      d.src = gi++;
     }
-    hs[s] = d;
+    hp[k] = d;
   }
   if (nvectors) memcpy(host.data() + b_ops + b_src, vectors_host, (size_t)nvectors * sizeof(double*));
   int rc = PBH_OK;
@@ -366,7 +424,7 @@ extern "C" int pbh_dag_eval(const pbh_dag_op* ops_host, int nops, const pbh_dag_
     set_error("pbh_dag_eval: upload failed");
     rc = PBH_ERR_HIP;
   } else {
-    const pbh_dag_op* prog = (const pbh_dag_op*)dev;
+    const DOp* prog = (const DOp*)dev;
     const DagSrc* srcs = (const DagSrc*)(dev + b_ops);
     double* const* vecs = (double* const*)(dev + b_ops + b_src);
     dim3 g(grid_for(n, kDTile, 256 * 16)), b(kDBlock);

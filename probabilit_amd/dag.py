@@ -153,10 +153,11 @@ def _emit(plan, node):
         _emit_leaf(plan, node)
         return
     if v[0] != "xform":
-        if isinstance(node, NoOp):
+        if isinstance(node, NoOp):  # no value: its parents are evaluated, loaded vectors left alone
             plan.emitted.add(node)
             for p in node.parents:
-                _emit(plan, p)
+                if plan.val[p][:2] != ("leaf", "load"):
+                    _emit(plan, p)
         return
     plan.emitted.add(node)
     flag = plan.ev.slot[node]

@@ -140,3 +140,18 @@ def test_mixed_fits():
     plan, _ = _plan(_mixed()[0])
     assert plan is not None
     assert sum(k == _lib.DAG_GEN for k in _kinds(plan)) == 6
+
+
+def test_loaded_vectors_alone_give_no_program(monkeypatch):
+    """A NoOp over already sampled (correlated) vectors has nothing to compute: no kernel."""
+    import torch
+
+    ds = [m.Distribution("norm") for _ in range(3)]
+    sink = m.NoOp(*ds)
+    for d in ds:
+        d.__dict__["_smp"] = torch.zeros(4, dtype=torch.float64)
+    plan, _ = _plan(sink)
+    assert plan is None
+    s2 = m.NoOp(ds[0] * 2.0, ds[1])
+    plan, _ = _plan(s2)
+    assert [o["kind"] for o in plan.ops] == [_lib.DAG_LOAD, _lib.DAG_BINARY]
