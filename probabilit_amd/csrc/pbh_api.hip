@@ -61,6 +61,8 @@ struct IcLayout {
   double* colpart;              // K x perm_scores_blocks(n) per-block score sums (step-2 means)
   void* s4shared;               // step 4 of generated columns: per-column histograms, cursors
   void* s4column;               //   and one column's staging (pbh_step4.hip)
+  uint32_t* heads_all;          // K x kHeadsCap run heads of the generated columns (unordered, then sorted)
+  uint32_t* hcur;               // K head counts
 };
 
 size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
@@ -82,7 +84,11 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* colpart = c.take((size_t)k * perm_scores_blocks(n) * 8);
   void* s4s = c.take(step4_gen_shared_bytes(k));
   void* s4c = c.take(step4_gen_column_bytes(n) * step4_streams());
+  void* hall = c.take((size_t)k * kHeadsCap * 4);
+  void* hcur = c.take((size_t)k * 4);
   if (carve) {
+    L->heads_all = (uint32_t*)hall;
+    L->hcur = (uint32_t*)hcur;
     L->s4shared = s4s;
     L->s4column = s4c;
     L->colpart = (double*)colpart;
@@ -209,8 +215,10 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   PBH_CHECK_HIP(hipMemsetAsync(L.flag, 0, sizeof(int32_t), s));
   bool all_generated = true;  // every column's scores came from perm_scores (with partial sums)
   std::vector<char> regenerable(k, 0);  // step 4 may regenerate sort(X[:, c])[p] from p (gen_place)
-  // Generated columns: every sorted column first, with its tie / inversion counts, then one
-  // readback for all of them (instead of a stream sync per column).
+  // Generated columns: every sorted column first, with its tie / inversion counts and run heads
+  // but without storing it (step 4 regenerates sort(X)[p]; the fallbacks materialise it on
+  // demand), then one readback for all of them (instead of a stream sync per column).
+  std::vector<char> have_sx(k, 0);  // sorted_x column c holds sort(X[:, c])
   // the generated columns' inverse-CDF setups (tables built once, for step 1 and step 4)
   struct Gens {
     std::vector<GenColumn*> g;
@@ -219,6 +227,12 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       for (GenColumn* x : g) gen_destroy(x, s);
     }
   } gens{std::vector<GenColumn*>(a->columns ? k : 0, nullptr), s};
+  auto materialise = [&](int c) -> int {  // sort(X[:, c]) into the workspace, once
+    if (have_sx[c] || !a->columns || !gens.g[c]) return PBH_OK;
+    int r = gen_sorted(gens.g[c], 0, n, L.sorted_x + (int64_t)c * n, nullptr, nullptr, s);
+    if (r == PBH_OK) have_sx[c] = 1;
+    return r;
+  };
   if (a->columns) {
     for (int c = 0; c < k; ++c) {
       const pbh_ic_column& g = a->columns[c];
@@ -226,7 +240,8 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
       st = gen_create(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, &gens.g[c], s);
       if (st) return st;
-      st = gen_sorted(gens.g[c], 0, n, L.sorted_x + (int64_t)c * n, g.nonfinite_flag, L.counts + 2 * c, s);
+      st = gen_sorted(gens.g[c], 0, n, nullptr, g.nonfinite_flag, L.counts + 2 * c, s,
+                      L.heads_all + (int64_t)c * kHeadsCap, L.hcur + c, kHeadsCap);
       if (st) return st;
     }
     PBH_CHECK_HIP(hipMemcpyAsync(cnt_host.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
@@ -247,8 +262,15 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
         uint32_t* heads = nullptr;
         int64_t nheads = 0;
         if (cnt[0] != 0) {  // ties (discrete ppf): 'average' ranks from the runs of the sorted column
-          heads = (uint32_t*)L.tmp;
-          st = run_heads(sx_c, n, 0, false, heads, &nheads, L.heads_ws, s);
+          nheads = n - (int64_t)cnt[0];  // no inversion: one head per distinct value
+          if (nheads <= kHeadsCap) {  // the heads the counting pass appended, put in order
+            heads = L.heads_all + (int64_t)c * kHeadsCap;
+            st = sort_heads(heads, nheads, s);
+          } else {  // too many distinct values for the list: from the materialised column
+            heads = (uint32_t*)L.tmp;
+            st = materialise(c);
+            if (!st) st = run_heads(sx_c, n, 0, false, heads, &nheads, L.heads_ws, s);
+          }
           if (st) return st;
         }
         st = perm_scores(g.seed, n, g.lhs_col, 0, n, heads, nheads, S_c, s,
@@ -274,6 +296,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     out.sorted_x = sx_c;
     st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
     if (st) return st;
+    have_sx[c] = 1;
   }
   PBH_CHECK_HIP(hipMemcpyAsync(&flag_host, L.flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   if (a->scores_out)
@@ -310,6 +333,8 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
 
   // ---- step 4: Y[:, c] = sort(X[:, c])[rankdata(CS[:, c]).astype(int) - 1]
   auto general = [&](int c) {  // the general path (sorted X read from the workspace)
+    int r = materialise(c);
+    if (r) return r;
     return reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
                           a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n);
   };
@@ -376,6 +401,8 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       PBH_CHECK_HIP(hipStreamSynchronize(s));
     }
     for (int c = 0; c < k && st == PBH_OK; ++c) {
+      st = materialise(c);
+      if (st) break;
       const uint32_t* hc = hists ? hists + (size_t)c * 1024 : nullptr;
       const int flat = hists ? (code_hist_flat(hists_host.data() + (size_t)c * 1024, n) ? 1 : 0) : 1;
       st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs, a->y_rs,

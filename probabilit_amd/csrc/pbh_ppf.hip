@@ -308,11 +308,17 @@ size_t poisson_lds_bytes(int dist, const Params& prm, const PoissonTable& pt) {
 // inside the segment, counts[0] += #ties and counts[1] += #inversions (what k_check_sorted
 // would find, without re-reading the column): lane l compares with lane l + 1 through a wave
 // shuffle, the last lane of a wave evaluates stratum t + 1 itself; one atomic pair per block.
+//
+// out may be NULL (counts only: the step-4 finish regenerates the values, nothing reads the
+// stored column).  With heads != NULL the counting pass also appends, unordered, every run
+// head t + 1 with x[t] != x[t + 1] at heads[*hcur] (the caller seeds heads[0] = 0, *hcur = 1
+// for t0 = 0); at most hcap are written, *hcur counts them all (k_sort_heads orders them).
 template <int D>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt,
                                                            uint32_t col, Params prm, PoissonTable pt,
                                                            double* __restrict__ out, int32_t* flag,
-                                                           unsigned long long* counts) {
+                                                           unsigned long long* counts, uint32_t* __restrict__ heads,
+                                                           uint32_t* __restrict__ hcur, uint32_t hcap) {
   __shared__ unsigned long long sh[2][kBlock / 64];
   Philox ph(seed);
   auto value = [&](int64_t t) {  // stratum t's point: no permutation needed (lhs_sorted_quantile)
@@ -340,13 +346,27 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_sorted_ppf(uint64_t seed
       double x = 0.0;
       if (valid) {
         x = value(t0 + i);
-        if (lane < 63) out[i] = x;
+        if (out && lane < 63) out[i] = x;
       }
       flag_nonfinite(flag, valid && lane < 63 && !isfinite(x));
       const double nx = __shfl_down(x, 1, 64);
       const bool has_next = valid && lane < 63 && i + 1 < nt;
       ties += has_next && x == nx;
       inv += has_next && !(x <= nx);
+      if (heads) {
+        const bool hd = has_next && x != nx;
+        const uint32_t ht = (uint32_t)(t0 + i + 1);
+        const uint64_t m = __ballot(hd);
+        if (m) {  // wave-uniform
+          const int leader = __builtin_ctzll(m);
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(hcur, (uint32_t)__popcll(m));
+          base = __shfl(base, leader, 64);
+          const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+          const uint32_t slot = base + (uint32_t)__popcll(m & lt);
+          if (hd && slot < hcap) heads[slot] = ht;
+        }
+      }
     }
   }
   if (counts) {
@@ -521,6 +541,31 @@ __global__ __launch_bounds__(kBlock) void k_check_sorted(const double* __restric
     atomicAdd(&counts[0], ties);
     atomicAdd(&counts[1], inv);
   }
+}
+
+// Run heads appended out of order by k_lhs_sorted_ppf, sorted in place: one 1024-thread block,
+// bitonic network over the next power of two (<= kHeadsCap entries, padded with 0xFFFFFFFF) in LDS.
+__global__ __launch_bounds__(1024) void k_sort_heads(uint32_t* __restrict__ heads, int nh, int np2) {
+  __shared__ uint32_t v[kHeadsCap];
+  for (int i = threadIdx.x; i < np2; i += 1024) v[i] = i < nh ? heads[i] : 0xFFFFFFFFu;
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np2; i += 1024) {
+        const int p = i ^ j;
+        if (p > i) {
+          const bool up = (i & k) == 0;
+          const uint32_t a = v[i], b = v[p];
+          if ((a > b) == up) {
+            v[i] = b;
+            v[p] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < nh; i += 1024) heads[i] = v[i];
 }
 
 // 'average' rank of stratum t given the run heads (sorted, heads[0] = 0) of the sorted
@@ -976,11 +1021,17 @@ void gen_destroy(GenColumn* g, hipStream_t s) {
 }
 
 int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t* flag, unsigned long long* counts,
-               hipStream_t s) {
+               hipStream_t s, uint32_t* heads, uint32_t* hcur, uint32_t hcap) {
   const int64_t n = g->n;
   PBH_REQUIRE(t0 >= 0 && nt >= 0 && t0 + nt <= n, "lhs_sorted_ppf: strata [%lld, %lld) outside [0, %lld)",
               (long long)t0, (long long)(t0 + nt), (long long)n);
+  PBH_REQUIRE(out || counts, "gen_sorted: neither an output column nor counts");
+  PBH_REQUIRE(!heads || (counts && hcur && hcap >= 1 && t0 == 0), "gen_sorted: run heads need counts, t0 = 0");
   if (counts) PBH_CHECK_HIP(hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), s));
+  if (heads) {  // stratum 0 heads the first run
+    PBH_CHECK_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t), s));
+    PBH_CHECK_HIP(hipMemsetD32Async((hipDeviceptr_t)hcur, 1, 1, s));
+  }
   if (nt == 0) return PBH_OK;
   dim3 gr(ppf_grid(nt)), b(kBlock);
   switch (g->dist) {
@@ -988,7 +1039,7 @@ int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t*
   case D:                                                                                                      \
     PBH_TIMED(kKLhsSorted, s,                                                                                  \
               hipLaunchKernelGGL(k_lhs_sorted_ppf<D>, gr, b, 0, s, g->seed, n, t0, nt, g->col, g->prm, g->pt, out, \
-                                 flag, counts));                                                               \
+                                 flag, counts, heads, hcur, hcap));                                            \
     break;
     PBH_CASE(PBH_DIST_NORM)
     PBH_CASE(PBH_DIST_UNIFORM)
@@ -1059,6 +1110,15 @@ int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, in
   st = gen_sorted(g, t0, nt, out, flag, counts, s);
   gen_destroy(g, s);
   return st;
+}
+
+int sort_heads(uint32_t* heads, int64_t nh, hipStream_t s) {
+  PBH_REQUIRE(nh >= 1 && nh <= kHeadsCap, "sort_heads: %lld heads outside [1, %d]", (long long)nh, kHeadsCap);
+  int np2 = 1;
+  while (np2 < nh) np2 <<= 1;
+  hipLaunchKernelGGL(k_sort_heads, dim3(1), dim3(1024), 0, s, heads, (int)nh, np2);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
 }
 
 int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStream_t s) {

@@ -33,7 +33,7 @@ struct PoissonTable {
 };
 
 // smallest k >= 0 with pdtr(k, mu) >= q, by stepping from a Cornish-Fisher guess.
-PBH_DI double poisson_search(double q, double mu) {
+__attribute__((noinline)) __device__ double poisson_search(double q, double mu) {  // rare: a real call
   if (mu == 0.0) return 0.0;
   double z = sf::ndtri(q);  // a starting guess only (the search decides k)
   double g = floor(mu + sqrt(mu) * z + (z * z - 1.0) / 6.0);
@@ -110,7 +110,7 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
     } else {  // gamma
-      x = pt.has_gamma ? sf::igami_guided(shape, q, &pt.aux, pt.guide) : sf::igami(shape, q);
+      x = pt.has_gamma ? sf::igami_guided(shape, q, &pt.aux, pt.guide) : sf::igami_cold(shape, q);
     }
     return x * scale + loc;
   }

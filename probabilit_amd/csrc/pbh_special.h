@@ -789,16 +789,25 @@ PBH_HD inline double guide_interp(const GammaGuide& T, int j, double t) {
   return __builtin_fma(t, p, y0);
 }
 
+// The rarely taken branches of igami_guided as real calls: inlined, their register needs sized
+// the whole kernel and the common interpolation path spilled (scratch traffic on every element).
+inline __attribute__((noinline)) PBH_HD double igami_cold(double a, double p) { return igami(a, p); }
+inline __attribute__((noinline)) PBH_HD double gamma_halley_cold(double a, double p, double x, double lga, double lg1pa,
+                                                        double lanczos) {
+  const GammaAux g = {lga, lg1pa, lanczos};  // by value: no address of the caller's copy is taken
+  return gamma_halley(a, p, x, &g);
+}
+
 PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const GammaGuide& T) {
-  if (!(p > 0.0 && p < 1.0)) return igami(a, p);
+  if (!(p > 0.0 && p < 1.0)) return igami_cold(a, p);
   const double w = log(p / (1.0 - p));
   double u = (w - T.z0) * T.inv_h;
-  if (!(u >= 0.0 && u < (double)(T.m - 1))) return igami(a, p);
+  if (!(u >= 0.0 && u < (double)(T.m - 1))) return igami_cold(a, p);
   int j = (int)u;
   double y = guide_interp(T, j, u - (double)j);
-  if (!(y >= -680.0 && y <= 700.0)) return igami(a, p);  // NaN entries, subnormal / huge x
+  if (!(y >= -680.0 && y <= 700.0)) return igami_cold(a, p);  // NaN entries, subnormal / huge x
   double x = exp(y);
-  return T.ok[j] != 0.0 ? x : gamma_halley(a, p, x, g);
+  return T.ok[j] != 0.0 ? x : gamma_halley_cold(a, p, x, g->lga, g->lg1pa, g->lanczos);
 }
 
 // igami(a, p(w)), p(w) = 1 / (1 + e^-w); the upper half goes through the complement

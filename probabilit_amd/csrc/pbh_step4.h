@@ -19,6 +19,7 @@ struct Step4Shared {
   uint32_t* start;
   uint32_t* cur1;
   uint32_t* cur2;
+  uint32_t* curF;  // fused finish: cursors of the top row-placement level
   uint32_t* tpre;
   int32_t* state;
   int32_t* flags;
@@ -38,6 +39,8 @@ size_t step4_gen_column_bytes(int64_t n);
 void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh);
 void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb);
 bool step4_gen_enabled(int64_t n);
+// the bucket finish scatters straight into the top row-placement level (PBH_STEP4_FUSED, default on)
+bool step4_fused();
 // columns of step 4 run concurrently on this many streams (PBH_STEP4_STREAMS, default 2, at
 // most kStep4MaxStreams), each with its own Step4Column staging, so that one column's VALU- or
 // latency-bound kernels (bucket finish, gen_place) overlap another's bandwidth-bound passes
@@ -47,7 +50,8 @@ hipStream_t step4_side_stream(int i);
 void step4_sync_side_streams();
 // top-16 histograms, bucket starts and flatness of all k code columns (codes + c * ldc)
 int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Shared& sh, hipStream_t s);
-// code passes and bucket finish of column c: (row << 32 | p') pairs in position order in cb.pairs[0]
+// code passes and bucket finish of column c: (row << 32 | p') pairs in cb.pairs[0], in position
+// order, or (step4_fused) grouped by the top row-placement level
 int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, const Step4Shared& sh,
                      const Step4Column& cb, hipStream_t s);
 // row-placement MSD passes on cb.pairs[0]; *out_buf = the pairs buffer grouped by 4096-row block
@@ -59,9 +63,14 @@ struct GenColumn;
 int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* params, int nparams, GenColumn** out,
                hipStream_t s);
 void gen_destroy(GenColumn* g, hipStream_t s);
-// out[t - t0] = the column's value in stratum t (see lhs_sorted_ppf)
+// out[t - t0] = the column's value in stratum t (see lhs_sorted_ppf); out may be NULL when
+// counts (ties, inversions) is given.  heads (t0 = 0 only): the run heads, unordered, at most
+// hcap of them; *hcur = their number (= nt - ties when there is no inversion).
+constexpr int kHeadsCap = 16384;
 int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t* flag, unsigned long long* counts,
-               hipStream_t s);
+               hipStream_t s, uint32_t* heads = nullptr, uint32_t* hcur = nullptr, uint32_t hcap = 0);
+// heads[0 .. nh) in increasing order (nh <= kHeadsCap)
+int sort_heads(uint32_t* heads, int64_t nh, hipStream_t s);
 // y[row * y_rs] = value of stratum p for every pair (row << 32 | p) of `pairs`, grouped by
 // 4096-row block (block b = positions [b << 12, ...)); idx[row] = p when idx != NULL.
 // state (optional device word): skip when non-zero.

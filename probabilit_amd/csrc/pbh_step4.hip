@@ -485,6 +485,145 @@ __global__ __launch_bounds__(64 * kBFWaves) void k_finish(const uint16_t* __rest
   }
 }
 
+// ---------------------------------------------------------------- counting finish, fused row pass
+// One 256-thread block finishes kFBuckets consecutive top-16 buckets, one after the other, and
+// then scatters their (row << 32 | p') pairs straight into the groups of the first row-placement
+// level (row >> s_top; group g at positions [g << s_top, ...), closed form since the rows are a
+// permutation), so the pairs never exist in position order.  Per bucket:
+//   * a non-stable LDS-atomic counting pass on the top 12 of the 16 low code bits (4096 bins,
+//     ~0.4 items per bin at 1500 items per bucket) puts every bin together;
+//   * every item counts, inside its bin, the items below it: lt = #{smaller low bits} +
+//     #{equal code (a run), smaller CS value}, eq = #{equal code, equal CS} (exact ties);
+//   * p' = bucket start + bin start + lt + eq / 2: the sorted position, or for a group of exact
+//     ties [a, a + eq] its 'average' rank minus one, truncated (rankdata(...).astype(int) - 1).
+// No order inside a bin is ever materialised, so neither pass needs to be stable.  A bin above
+// kBinCap items (far from the ~0.4 expected: a discrete spike) flags the column for the
+// general path.
+constexpr int kFBuckets = 2;   // buckets per block (staging kFBuckets * kBucketCap2 pairs)
+constexpr int kFIpt = kBucketCap2 / kT;  // items per thread per bucket (8)
+constexpr int kFBins = 4096;
+constexpr int kBinCap = 32;
+
+union FinishLds {
+  struct {
+    uint32_t cnt[kFBins + 1];
+    uint16_t key[kBucketCap2];
+    uint32_t row[kBucketCap2];
+  } a;
+  uint64_t sv[kFBuckets * kBucketCap2];
+};
+
+__global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ rows,
+                                                     const double* __restrict__ x,
+                                                     const uint32_t* __restrict__ start, int s_top,
+                                                     uint32_t* __restrict__ gcur, uint64_t* __restrict__ out,
+                                                     int32_t* __restrict__ flags,
+                                                     const int32_t* __restrict__ state) {
+  if (*state) return;
+  __shared__ FinishLds L;
+  __shared__ uint32_t gcnt[256], goff[264], gbase[256];
+  __shared__ int bad;
+  const int t = threadIdx.x;
+  if (t == 0) bad = 0;
+  gcnt[t] = 0;
+  uint64_t pr[kFBuckets * kFIpt];
+  uint32_t grk[kFBuckets * kFIpt];
+  int total = 0;
+#pragma unroll
+  for (int bb = 0; bb < kFBuckets; ++bb) {
+    const int bkt = blockIdx.x * kFBuckets + bb;
+    const int64_t s = start[bkt];
+    const int len = (int)((int64_t)start[bkt + 1] - s);  // <= kBucketCap2 (k_hist16_scan)
+    for (int i = t; i <= kFBins; i += kT) L.a.cnt[i] = 0;
+    uint32_t k[kFIpt], r[kFIpt], rk[kFIpt];
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j) {
+      const int p = j * kT + t;
+      k[j] = p < len ? (uint32_t)keys[s + p] : 0u;
+      r[j] = p < len ? rows[s + p] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j) rk[j] = (j * kT + t < len) ? atomicAdd(&L.a.cnt[k[j] >> 4], 1u) : 0u;
+    __syncthreads();
+    // exclusive prefix over the 4096 bins: thread t owns bins 16 t .. 16 t + 15
+    uint32_t c16[16], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      c16[q] = L.a.cnt[16 * t + q];
+      sum += c16[q];
+    }
+    uint32_t run = block_excl_scan256(sum, goff);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      L.a.cnt[16 * t + q] = run;
+      run += c16[q];
+    }
+    if (t == kT - 1) L.a.cnt[kFBins] = run;  // == len
+    __syncthreads();
+    uint32_t pos[kFIpt];
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j) {
+      if (j * kT + t < len) {
+        pos[j] = L.a.cnt[k[j] >> 4] + rk[j];
+        L.a.key[pos[j]] = (uint16_t)k[j];
+        L.a.row[pos[j]] = r[j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j) {
+      const int slot = bb * kFIpt + j;
+      if (j * kT + t >= len) {
+        pr[slot] = ~0ull;
+        continue;
+      }
+      const uint32_t bs = L.a.cnt[k[j] >> 4], be = L.a.cnt[(k[j] >> 4) + 1];
+      uint32_t lt = 0, eq = 0;
+      if (be - bs > 1) {
+        if (be - bs > (uint32_t)kBinCap) bad = 1;
+        bool have = false;
+        double xv = 0.0;
+        for (uint32_t m = bs; m < be; ++m) {
+          const uint32_t km = L.a.key[m];
+          lt += km < k[j];
+          if (km == k[j] && m != pos[j]) {  // a run of equal codes: order by the CS value
+            if (!have) {
+              xv = x[r[j]];
+              have = true;
+            }
+            const double xm = x[L.a.row[m]];
+            lt += xm < xv;
+            eq += xm == xv;
+          }
+        }
+      }
+      const uint32_t p = (uint32_t)s + bs + lt + eq / 2;
+      pr[slot] = ((uint64_t)r[j] << 32) | (uint64_t)p;
+      grk[slot] = atomicAdd(&gcnt[r[j] >> s_top], 1u);
+    }
+    total += len;
+    __syncthreads();  // the bucket's LDS is reused by the next one
+  }
+  // scatter into the row groups: one cursor add per (block, group)
+  const uint32_t my = gcnt[t];
+  const uint32_t ex = block_excl_scan256(my, goff);
+  goff[t] = ex;
+  gbase[t] = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * kCurPad], my)) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int slot = 0; slot < kFBuckets * kFIpt; ++slot)
+    if (pr[slot] != ~0ull) L.sv[goff[(uint32_t)(pr[slot] >> (32 + s_top))] + grk[slot]] = pr[slot];
+  __syncthreads();
+  for (int p = t; p < total; p += kT) {
+    const uint64_t v = L.sv[p];
+    const uint32_t g = (uint32_t)(v >> (32 + s_top));
+    out[gbase[g] + ((uint32_t)p - goff[g])] = v;
+  }
+  if (t == 0 && bad) atomicOr(flags, 1);
+}
+
 // ---------------------------------------------------------------- row placement passes
 // Input grouped by row >> s_in (closed-form groups: rows are a permutation of [0, n), so group
 // g occupies positions [g << s_in, ...)); tiles of kTileP never straddle a group.  Digit =
@@ -549,8 +688,9 @@ __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ i
 }  // namespace
 
 size_t step4_gen_shared_bytes(int k) {
-  // per column: hist 65536 + start 65537 + cur1 256 * pad + cur2 65536 + tpre 257 (u32), state
-  return (size_t)k * ((65536 + 65537 + 256 * kCurPad + 65536 + 257) * 4 + 64) + 256;
+  // per column: hist 65536 + start 65537 + cur1 256 * pad + cur2 65536 + curF 256 * pad + tpre 257
+  // (u32), state
+  return (size_t)k * ((65536 + 65537 + 256 * kCurPad + 65536 + 256 * kCurPad + 257) * 4 + 64) + 256;
 }
 
 size_t step4_gen_column_bytes(int64_t n) {
@@ -571,6 +711,8 @@ void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh) {
   p += (size_t)k * 256 * kCurPad * 4;
   sh.cur2 = (uint32_t*)p;
   p += (size_t)k * 65536 * 4;
+  sh.curF = (uint32_t*)p;
+  p += (size_t)k * 256 * kCurPad * 4;
   sh.tpre = (uint32_t*)p;
   p += (size_t)k * 257 * 4;
   p = (char*)(((uintptr_t)p + 63) & ~(uintptr_t)63);
@@ -626,6 +768,23 @@ void step4_sync_side_streams() {
   }
 }
 
+bool step4_fused() {
+  static const bool v = [] {
+    const char* e = getenv("PBH_STEP4_FUSED");  // "0": position-order finish + every placement level
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// MSD levels of the row placement: shifts from kGenPlaceShift up, at most 8 bits per level
+static int place_levels(int64_t n, int* shifts) {
+  int bits = 0;
+  while (((int64_t)1 << bits) < n) ++bits;
+  int nl = 0;
+  for (int sh = kGenPlaceShift; sh < bits; sh += 8) shifts[nl++] = sh;
+  return nl;
+}
+
 bool step4_gen_enabled(int64_t n) {
   const char* e = getenv("PBH_STEP4");  // "lsd" / "legacy": the general path for every column
   if (e && (strcmp(e, "lsd") == 0 || strcmp(e, "legacy") == 0)) return false;
@@ -635,7 +794,7 @@ bool step4_gen_enabled(int64_t n) {
 int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Shared& sh, hipStream_t s) {
   const int k = sh.k;
   PBH_CHECK_HIP(hipMemsetAsync(sh.hist, 0, (size_t)k * 65536 * 4, s));
-  PBH_CHECK_HIP(hipMemsetAsync(sh.cur1, 0, (size_t)k * (256 * kCurPad + 65536) * 4, s));  // cur1 and cur2
+  PBH_CHECK_HIP(hipMemsetAsync(sh.cur1, 0, (size_t)k * (2 * 256 * kCurPad + 65536) * 4, s));  // cur1, cur2, curF
   PBH_CHECK_HIP(hipMemsetAsync(sh.state, 0, (size_t)2 * k * 4, s));
   int64_t blocks = (n + 65535) / 65536;  // >= 64 K codes per block: a handful of flushes
   if (blocks > 256) blocks = 256;
@@ -662,19 +821,27 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
             hipLaunchKernelGGL(k_msd2, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
                                sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
   PBH_CHECK_LAUNCH();
-  PBH_TIMED(kKFinish, s,
-            hipLaunchKernelGGL(k_finish, dim3(65536 / kBFWaves), dim3(64 * kBFWaves), 0, s, cb.keys16, cb.rows2, cs,
-                               start, cb.pairs[0], sh.flags + c, state));
+  if (step4_fused()) {
+    int shifts[4];
+    const int nl = place_levels(n, shifts);
+    const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
+    PBH_TIMED(kKFinish, s,
+              hipLaunchKernelGGL(k_finish_fused, dim3(65536 / kFBuckets), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
+                                 start, s_top, sh.curF + (int64_t)c * 256 * kCurPad, cb.pairs[0], sh.flags + c,
+                                 state));
+  } else {
+    PBH_TIMED(kKFinish, s,
+              hipLaunchKernelGGL(k_finish, dim3(65536 / kBFWaves), dim3(64 * kBFWaves), 0, s, cb.keys16, cb.rows2, cs,
+                                 start, cb.pairs[0], sh.flags + c, state));
+  }
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
 
 int step4_gen_place_passes(int64_t n, const Step4Column& cb, const int32_t* state, hipStream_t s, int* out_buf) {
-  int bits = 0;
-  while (((int64_t)1 << bits) < n) ++bits;
-  // MSD levels on the row: shifts from high to kGenPlaceShift, at most 8 bits per level
-  int shifts[4], nl = 0;
-  for (int sh = kGenPlaceShift; sh < bits; sh += 8) shifts[nl++] = sh;
+  int shifts[4];
+  int nl = place_levels(n, shifts);
+  if (step4_fused() && nl > 0) --nl;  // the finish scattered the top level
   int cur = 0;
   const int64_t tiles = (n + kTileP - 1) / kTileP;
   for (int l = nl - 1; l >= 0; --l) {
