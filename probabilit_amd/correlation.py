@@ -105,6 +105,17 @@ def _is_positive_definite(X):
         return False
 
 
+# The device correlators hold K x K matrices and per-variable state in fixed workspaces
+# (pbh_iman_conover, the Gram / affine kernels, the permutation climb): K <= 128 variables.
+# The reference has no such limit; a larger K raises this ValueError instead of a native error.
+MAX_VARIABLES = 128
+
+
+def _check_k(K):
+    if K > MAX_VARIABLES:
+        raise ValueError(f"probabilit_amd correlates at most {MAX_VARIABLES} variables on the device; got {K}")
+
+
 class Correlator:
     """Correlator protocol (correlation.py:161-202): set_target validates and factors C."""
 
@@ -140,6 +151,7 @@ class Correlator:
                              f"({self.P.shape})")
         if check_rows_cols and N <= K:
             raise ValueError(f"The matrix X must have rows > columns. Got shape: {tuple(X.shape)}")
+        _check_k(K)
         return N, K
 
 
@@ -225,6 +237,7 @@ def decorrelate(X, remove_variance=True):
     or L / sqrt(var) when remove_variance is False."""
     import scipy.linalg
 
+    _check_k(np.shape(X)[1])
     block, on_device = _as_block(X)
     K, N = block.shape
     mean, G = _block_stats(block)
@@ -317,6 +330,7 @@ class ImanConover(Correlator):
             raise ValueError(f"Shape of `X` ({(n, K)}) does not match shape of correlation matrix ({self.P.shape})")
         if n <= K:
             raise ValueError(f"The matrix X must have rows > columns. Got shape: {(n, K)}")
+        _check_k(K)
         Y = device.empty((K, n))
         self._run(None, n, K, 1, n, Y, 1, n, columns=columns, debug=debug)
         return Y

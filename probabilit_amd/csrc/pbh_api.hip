@@ -4,6 +4,7 @@
 // the positive-definiteness check and the Cholesky factor of correlation.py:398-405 are
 // O(K^3) with K <= 128 and run on the host between two device phases (one 8 KB D2H).
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -240,8 +241,12 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
       st = gen_create(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, &gens.g[c], s);
       if (st) return st;
+      // run heads only for a discrete column (few runs); a continuous one ties rarely, if ever,
+      // and would append every stratum
+      const bool discrete = g.dist == PBH_DIST_POISSON;
       st = gen_sorted(gens.g[c], 0, n, nullptr, g.nonfinite_flag, L.counts + 2 * c, s,
-                      L.heads_all + (int64_t)c * kHeadsCap, L.hcur + c, kHeadsCap);
+                      discrete ? L.heads_all + (int64_t)c * kHeadsCap : nullptr, discrete ? L.hcur + c : nullptr,
+                      discrete ? kHeadsCap : 0);
       if (st) return st;
     }
     PBH_CHECK_HIP(hipMemcpyAsync(cnt_host.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
@@ -263,7 +268,12 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
         int64_t nheads = 0;
         if (cnt[0] != 0) {  // ties (discrete ppf): 'average' ranks from the runs of the sorted column
           nheads = n - (int64_t)cnt[0];  // no inversion: one head per distinct value
-          if (nheads <= kHeadsCap) {  // the heads the counting pass appended, put in order
+          const int64_t cap = [] {  // PBH_HEADS_CAP (tests): a smaller list, to reach the fallback
+            const char* e = getenv("PBH_HEADS_CAP");
+            const int64_t v = e ? atoll(e) : kHeadsCap;
+            return v < 1 ? 1 : (v > kHeadsCap ? (int64_t)kHeadsCap : v);
+          }();
+          if (a->columns[c].dist == PBH_DIST_POISSON && nheads <= cap) {  // appended heads, put in order
             heads = L.heads_all + (int64_t)c * kHeadsCap;
             st = sort_heads(heads, nheads, s);
           } else {  // too many distinct values for the list: from the materialised column

@@ -173,8 +173,31 @@ struct FeistelPerm {
 // perm (not the row): the point of row r is stratum pi(r) with that stratum's jitter, which
 // is as random as a per-row jitter (pi is a random bijection) and lets the stratum-ordered
 // (sorted) column be generated without evaluating pi^-1 at all (lhs_sorted_quantile).
+//
+// The jitter is output t of a SplitMix64 generator (Steele, Lea & Flood, OOPSLA 2014; Java's
+// SplittableRandom) whose start is keyed by (seed, column): z = key + (t + 1) * golden gamma,
+// then the Stafford "mix13" finalizer.  It is evaluated once per element by the stratum-ordered
+// generator and again, in random stratum order, by the step-4 placement, so its cost matters:
+// 11 32-bit multiplies (quarter-rate on CDNA) against 40 for a Philox4x32-10 block, whose other
+// 75 bits a single jitter would throw away.  The permutation keeps its Feistel network.
+PBH_HD inline uint64_t splitmix_finalize(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+PBH_HD inline uint64_t lhs_jitter_key(const Philox& ph, uint32_t col) {
+  const uint64_t seed = ((uint64_t)ph.k1 << 32) | ph.k0;
+  return splitmix_finalize(seed ^ splitmix_finalize(((uint64_t)col << 32) | kPurposeLhsU));
+}
+
 PBH_HD inline double lhs_sorted_quantile(const Philox& ph, uint64_t t, uint32_t col, uint64_t n) {
+#ifdef PBH_JITTER_PHILOX  // the round-1 jitter (A/B builds only)
   const double u = ph.uniform(t, col, kPurposeLhsU);
+#else
+  const uint64_t z = splitmix_finalize(lhs_jitter_key(ph, col) + (t + 1) * 0x9E3779B97F4A7C15ull);
+  const double u = (double)(z >> 11) * 0x1.0p-53;
+#endif
   return ((double)(t + 1) - u) / (double)n;
 }
 

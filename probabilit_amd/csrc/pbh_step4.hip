@@ -161,13 +161,16 @@ __global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict
 
 // ---------------------------------------------------------------- code passes
 // msd1: tile = kTile1 consecutive rows; digit = top code byte.
+// SPLIT: one 32-bit staging array, used twice (keys, then rows): 32 KiB of LDS per block instead
+// of 64, so 4 blocks per CU instead of 2, for two more barriers.
+template <bool SPLIT>
 __global__ __launch_bounds__(kT) void k_msd1(const uint32_t* __restrict__ codes, int64_t n,
                                              const uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
                                              uint32_t* __restrict__ kout, uint32_t* __restrict__ rout,
                                              const int32_t* __restrict__ state) {
   if (*state) return;  // uniform: this column takes the general path
   __shared__ uint32_t cnt[256], lst[264], gb[256];
-  __shared__ uint32_t sk[kTile1], sr[kTile1];
+  __shared__ uint32_t sk[kTile1], sr[SPLIT ? 1 : kTile1];
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kTile1;
   const int m = (int)((n - base) < kTile1 ? (n - base) : kTile1);
@@ -186,30 +189,62 @@ __global__ __launch_bounds__(kT) void k_msd1(const uint32_t* __restrict__ codes,
   lst[t] = ex;
   gb[t] = my ? start[t << 8] + atomicAdd(&cur[t * kCurPad], my) : 0u;
   __syncthreads();
+  if constexpr (SPLIT) {
+    uint32_t dst[kIpt1];  // where slot p = j * kT + t's key goes, kept for the rows round
 #pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    if (p < m) {
-      const uint32_t q = lst[key[j] >> 24] + rk[j];
-      sk[q] = key[j];
-      sr[q] = (uint32_t)(base + p);
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) sk[lst[key[j] >> 24] + rk[j]] = key[j];
     }
-  }
-  __syncthreads();
+    __syncthreads();
 #pragma unroll 4
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    if (p < m) {
-      const uint32_t k = sk[p], d = k >> 24;
-      const uint32_t o = gb[d] + ((uint32_t)p - lst[d]);
-      kout[o] = k;
-      rout[o] = sr[p];
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) {
+        const uint32_t k = sk[p], d = k >> 24;
+        dst[j] = gb[d] + ((uint32_t)p - lst[d]);
+        kout[dst[j]] = k;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) sk[lst[key[j] >> 24] + rk[j]] = (uint32_t)(base + p);
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) rout[dst[j]] = sk[p];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) {
+        const uint32_t q = lst[key[j] >> 24] + rk[j];
+        sk[q] = key[j];
+        sr[q] = (uint32_t)(base + p);
+      }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) {
+        const uint32_t k = sk[p], d = k >> 24;
+        const uint32_t o = gb[d] + ((uint32_t)p - lst[d]);
+        kout[o] = k;
+        rout[o] = sr[p];
+      }
     }
   }
 }
 
 // msd2: tiles of kTile1 inside each top-byte group (tile map tpre); digit = code byte 2; the
 // destination is the group's top-16 bucket (g << 8 | digit).  Writes the low 16 code bits.
+template <bool SPLIT>
 __global__ __launch_bounds__(kT) void k_msd2(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin,
                                              const uint32_t* __restrict__ start, const uint32_t* __restrict__ tpre,
                                              uint32_t* __restrict__ cur, uint16_t* __restrict__ kout,
@@ -218,7 +253,7 @@ __global__ __launch_bounds__(kT) void k_msd2(const uint32_t* __restrict__ kin, c
   const uint32_t tile = blockIdx.x;
   if (tile >= tpre[256]) return;
   __shared__ uint32_t cnt[256], lst[264], gb[256];
-  __shared__ uint32_t sk[kTile1], sr[kTile1];
+  __shared__ uint32_t sk[kTile1], sr[SPLIT ? 1 : kTile1];
   __shared__ int gsh;
   const int t = threadIdx.x;
   if (t == 0) {  // the group holding this tile: last g with tpre[g] <= tile
@@ -254,24 +289,55 @@ __global__ __launch_bounds__(kT) void k_msd2(const uint32_t* __restrict__ kin, c
   const uint32_t b = ((uint32_t)g << 8) | (uint32_t)t;
   gb[t] = my ? start[b] + atomicAdd(&cur[b], my) : 0u;
   __syncthreads();
+  if constexpr (SPLIT) {
+    uint32_t dst[kIpt1];
 #pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    if (p < m) {
-      const uint32_t q = lst[(key[j] >> 16) & 255u] + rk[j];
-      sk[q] = key[j];
-      sr[q] = row[j];
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) sk[lst[(key[j] >> 16) & 255u] + rk[j]] = key[j];
     }
-  }
-  __syncthreads();
+    __syncthreads();
 #pragma unroll 4
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    if (p < m) {
-      const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
-      const uint32_t o = gb[d] + ((uint32_t)p - lst[d]);
-      kout[o] = (uint16_t)kk;
-      rout[o] = sr[p];
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) {
+        const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
+        dst[j] = gb[d] + ((uint32_t)p - lst[d]);
+        kout[dst[j]] = (uint16_t)kk;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) sk[lst[(key[j] >> 16) & 255u] + rk[j]] = row[j];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) rout[dst[j]] = sk[p];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) {
+        const uint32_t q = lst[(key[j] >> 16) & 255u] + rk[j];
+        sk[q] = key[j];
+        sr[q] = row[j];
+      }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < kIpt1; ++j) {
+      const int p = j * kT + t;
+      if (p < m) {
+        const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
+        const uint32_t o = gb[d] + ((uint32_t)p - lst[d]);
+        kout[o] = (uint16_t)kk;
+        rout[o] = sr[p];
+      }
     }
   }
 }
@@ -499,20 +565,22 @@ __global__ __launch_bounds__(64 * kBFWaves) void k_finish(const uint16_t* __rest
 // No order inside a bin is ever materialised, so neither pass needs to be stable.  A bin above
 // kBinCap items (far from the ~0.4 expected: a discrete spike) flags the column for the
 // general path.
-constexpr int kFBuckets = 2;   // buckets per block (staging kFBuckets * kBucketCap2 pairs)
 constexpr int kFIpt = kBucketCap2 / kT;  // items per thread per bucket (8)
-constexpr int kFBins = 4096;
 constexpr int kBinCap = 32;
 
+template <int FB, int BINS>
 union FinishLds {
   struct {
-    uint32_t cnt[kFBins + 1];
+    uint32_t cnt[BINS + 1];
     uint16_t key[kBucketCap2];
     uint32_t row[kBucketCap2];
   } a;
-  uint64_t sv[kFBuckets * kBucketCap2];
+  uint64_t sv[FB * kBucketCap2];
 };
 
+// FB buckets per block (staging FB * kBucketCap2 pairs); BINS counting bins on the top
+// log2(BINS) of the 16 low code bits
+template <int FB, int BINS>
 __global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ rows,
                                                      const double* __restrict__ x,
@@ -521,21 +589,23 @@ __global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict_
                                                      int32_t* __restrict__ flags,
                                                      const int32_t* __restrict__ state) {
   if (*state) return;
-  __shared__ FinishLds L;
+  constexpr int kShift = 16 - __builtin_ctz(BINS);  // bin = key >> kShift
+  constexpr int kPer = BINS / kT;                   // bins per thread in the scan
+  __shared__ FinishLds<FB, BINS> L;
   __shared__ uint32_t gcnt[256], goff[264], gbase[256];
   __shared__ int bad;
   const int t = threadIdx.x;
   if (t == 0) bad = 0;
   gcnt[t] = 0;
-  uint64_t pr[kFBuckets * kFIpt];
-  uint32_t grk[kFBuckets * kFIpt];
+  uint64_t pr[FB * kFIpt];
+  uint32_t grk[FB * kFIpt];
   int total = 0;
 #pragma unroll
-  for (int bb = 0; bb < kFBuckets; ++bb) {
-    const int bkt = blockIdx.x * kFBuckets + bb;
+  for (int bb = 0; bb < FB; ++bb) {
+    const int bkt = blockIdx.x * FB + bb;
     const int64_t s = start[bkt];
     const int len = (int)((int64_t)start[bkt + 1] - s);  // <= kBucketCap2 (k_hist16_scan)
-    for (int i = t; i <= kFBins; i += kT) L.a.cnt[i] = 0;
+    for (int i = t; i <= BINS; i += kT) L.a.cnt[i] = 0;
     uint32_t k[kFIpt], r[kFIpt], rk[kFIpt];
 #pragma unroll
     for (int j = 0; j < kFIpt; ++j) {
@@ -545,28 +615,28 @@ __global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict_
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kFIpt; ++j) rk[j] = (j * kT + t < len) ? atomicAdd(&L.a.cnt[k[j] >> 4], 1u) : 0u;
+    for (int j = 0; j < kFIpt; ++j) rk[j] = (j * kT + t < len) ? atomicAdd(&L.a.cnt[k[j] >> kShift], 1u) : 0u;
     __syncthreads();
-    // exclusive prefix over the 4096 bins: thread t owns bins 16 t .. 16 t + 15
-    uint32_t c16[16], sum = 0;
+    // exclusive prefix over the bins: thread t owns bins kPer t .. kPer t + kPer - 1
+    uint32_t cb[kPer], sum = 0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      c16[q] = L.a.cnt[16 * t + q];
-      sum += c16[q];
+    for (int q = 0; q < kPer; ++q) {
+      cb[q] = L.a.cnt[kPer * t + q];
+      sum += cb[q];
     }
     uint32_t run = block_excl_scan256(sum, goff);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      L.a.cnt[16 * t + q] = run;
-      run += c16[q];
+    for (int q = 0; q < kPer; ++q) {
+      L.a.cnt[kPer * t + q] = run;
+      run += cb[q];
     }
-    if (t == kT - 1) L.a.cnt[kFBins] = run;  // == len
+    if (t == kT - 1) L.a.cnt[BINS] = run;  // == len
     __syncthreads();
     uint32_t pos[kFIpt];
 #pragma unroll
     for (int j = 0; j < kFIpt; ++j) {
       if (j * kT + t < len) {
-        pos[j] = L.a.cnt[k[j] >> 4] + rk[j];
+        pos[j] = L.a.cnt[k[j] >> kShift] + rk[j];
         L.a.key[pos[j]] = (uint16_t)k[j];
         L.a.row[pos[j]] = r[j];
       }
@@ -579,7 +649,7 @@ __global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict_
         pr[slot] = ~0ull;
         continue;
       }
-      const uint32_t bs = L.a.cnt[k[j] >> 4], be = L.a.cnt[(k[j] >> 4) + 1];
+      const uint32_t bs = L.a.cnt[k[j] >> kShift], be = L.a.cnt[(k[j] >> kShift) + 1];
       uint32_t lt = 0, eq = 0;
       if (be - bs > 1) {
         if (be - bs > (uint32_t)kBinCap) bad = 1;
@@ -613,7 +683,7 @@ __global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict_
   gbase[t] = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * kCurPad], my)) : 0u;
   __syncthreads();
 #pragma unroll
-  for (int slot = 0; slot < kFBuckets * kFIpt; ++slot)
+  for (int slot = 0; slot < FB * kFIpt; ++slot)
     if (pr[slot] != ~0ull) L.sv[goff[(uint32_t)(pr[slot] >> (32 + s_top))] + grk[slot]] = pr[slot];
   __syncthreads();
   for (int p = t; p < total; p += kT) {
@@ -628,12 +698,14 @@ __global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict_
 // Input grouped by row >> s_in (closed-form groups: rows are a permutation of [0, n), so group
 // g occupies positions [g << s_in, ...)); tiles of kTileP never straddle a group.  Digit =
 // (row >> s_out) within the group; destination = positions (row >> s_out) << s_out.
+template <bool SPLIT>  // SPLIT: the pairs staged as two 32-bit halves through one 16 KiB array
 __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ in, int64_t n, int s_out,
                                                   uint32_t* __restrict__ cur, uint64_t* __restrict__ out,
                                                   const int32_t* __restrict__ state) {
   if (state && *state) return;
   __shared__ uint32_t cnt[256], lst[264], gb[256];
-  __shared__ uint64_t sv[kTileP];
+  __shared__ uint64_t sv[SPLIT ? 1 : kTileP];
+  __shared__ uint32_t sh32[SPLIT ? kTileP : 1];
   __shared__ uint32_t gfirst;
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kTileP;
@@ -670,17 +742,48 @@ __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ i
   lst[t] = ex;
   gb[t] = my ? (uint32_t)(((uint64_t)(g0 + t) << s_out) + atomicAdd(&cur[g0 + t], my)) : 0u;
   __syncthreads();
+  if constexpr (SPLIT) {
+    // round 1: the high halves (rows) give each slot's destination; round 2: the low halves
+    uint32_t dst[kIptP], hi[kIptP], slot[kIptP], lo[kIptP];
 #pragma unroll
-  for (int j = 0; j < kIptP; ++j)
-    if (j * kT + t < m) sv[lst[dg[j] - g0] + rk[j]] = v[j];
-  __syncthreads();
+    for (int j = 0; j < kIptP; ++j) {
+      slot[j] = lst[dg[j] - g0] + rk[j];
+      lo[j] = (uint32_t)v[j];
+      if (j * kT + t < m) sh32[slot[j]] = (uint32_t)(v[j] >> 32);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kIptP; ++j) {
+      const int p = j * kT + t;
+      if (p < m) {
+        hi[j] = sh32[p];
+        const uint32_t d = (hi[j] >> s_out) - g0;
+        dst[j] = gb[d] + ((uint32_t)p - lst[d]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kIptP; ++j)
+      if (j * kT + t < m) sh32[slot[j]] = lo[j];
+    __syncthreads();
 #pragma unroll 4
-  for (int j = 0; j < kIptP; ++j) {
-    const int p = j * kT + t;
-    if (p < m) {
-      const uint64_t x = sv[p];
-      const uint32_t d = (uint32_t)(x >> (32 + s_out)) - g0;
-      out[gb[d] + ((uint32_t)p - lst[d])] = x;
+    for (int j = 0; j < kIptP; ++j) {
+      const int p = j * kT + t;
+      if (p < m) out[dst[j]] = ((uint64_t)hi[j] << 32) | sh32[p];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kIptP; ++j)
+      if (j * kT + t < m) sv[lst[dg[j] - g0] + rk[j]] = v[j];
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < kIptP; ++j) {
+      const int p = j * kT + t;
+      if (p < m) {
+        const uint64_t x = sv[p];
+        const uint32_t d = (uint32_t)(x >> (32 + s_out)) - g0;
+        out[gb[d] + ((uint32_t)p - lst[d])] = x;
+      }
     }
   }
 }
@@ -813,22 +916,51 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
   const uint32_t* start = sh.start + (int64_t)c * 65537;
   const int32_t* state = sh.state + c;
   const int64_t t1 = (n + kTile1 - 1) / kTile1;
-  PBH_TIMED(kKMsd1, s,
-            hipLaunchKernelGGL(k_msd1, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
-                               sh.cur1 + (int64_t)c * 256 * kCurPad, cb.keys32, cb.rows1, state));
-  PBH_CHECK_LAUNCH();
-  PBH_TIMED(kKMsd2, s,
-            hipLaunchKernelGGL(k_msd2, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
-                               sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
+  static const bool split = [] {  // PBH_MSD_SPLIT=0: keys and rows staged together (64 KiB)
+    const char* e = getenv("PBH_MSD_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  if (split) {
+    PBH_TIMED(kKMsd1, s,
+              hipLaunchKernelGGL(k_msd1<true>, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
+                                 sh.cur1 + (int64_t)c * 256 * kCurPad, cb.keys32, cb.rows1, state));
+    PBH_CHECK_LAUNCH();
+    PBH_TIMED(kKMsd2, s,
+              hipLaunchKernelGGL(k_msd2<true>, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
+                                 sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
+  } else {
+    PBH_TIMED(kKMsd1, s,
+              hipLaunchKernelGGL(k_msd1<false>, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
+                                 sh.cur1 + (int64_t)c * 256 * kCurPad, cb.keys32, cb.rows1, state));
+    PBH_CHECK_LAUNCH();
+    PBH_TIMED(kKMsd2, s,
+              hipLaunchKernelGGL(k_msd2<false>, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
+                                 sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
+  }
   PBH_CHECK_LAUNCH();
   if (step4_fused()) {
     int shifts[4];
     const int nl = place_levels(n, shifts);
     const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
-    PBH_TIMED(kKFinish, s,
-              hipLaunchKernelGGL(k_finish_fused, dim3(65536 / kFBuckets), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
-                                 start, s_top, sh.curF + (int64_t)c * 256 * kCurPad, cb.pairs[0], sh.flags + c,
-                                 state));
+    // PBH_FINISH_CFG: <buckets per block><log2 bins - 10> (A/B measurements), default "22"
+    static const int cfg = [] {
+      const char* e = getenv("PBH_FINISH_CFG");
+      return e ? atoi(e) : 22;
+    }();
+    uint32_t* gc = sh.curF + (int64_t)c * 256 * kCurPad;
+#define PBH_FIN(FB, BINS)                                                                                         \
+  PBH_TIMED(kKFinish, s,                                                                                          \
+            hipLaunchKernelGGL((k_finish_fused<FB, BINS>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16, cb.rows2, cs, \
+                               start, s_top, gc, cb.pairs[0], sh.flags + c, state))
+    switch (cfg) {
+      case 11: PBH_FIN(1, 2048); break;
+      case 12: PBH_FIN(1, 4096); break;
+      case 21: PBH_FIN(2, 2048); break;
+      case 41: PBH_FIN(4, 2048); break;
+      case 42: PBH_FIN(4, 4096); break;
+      default: PBH_FIN(2, 4096); break;
+    }
+#undef PBH_FIN
   } else {
     PBH_TIMED(kKFinish, s,
               hipLaunchKernelGGL(k_finish, dim3(65536 / kBFWaves), dim3(64 * kBFWaves), 0, s, cb.keys16, cb.rows2, cs,
@@ -848,9 +980,18 @@ int step4_gen_place_passes(int64_t n, const Step4Column& cb, const int32_t* stat
     const int64_t ncur = (n >> shifts[l]) + 1;
     uint32_t* cr = cb.pcur[l & 1];
     PBH_CHECK_HIP(hipMemsetAsync(cr, 0, (size_t)ncur * 4, s));
-    PBH_TIMED(kKPlaceMsd, s,
-              hipLaunchKernelGGL(k_place_msd, dim3((unsigned)tiles), dim3(kT), 0, s, cb.pairs[cur], n, shifts[l], cr,
-                                 cb.pairs[cur ^ 1], state));
+    static const bool split = [] {  // PBH_PLACE_SPLIT=0: the pairs staged whole (32 KiB)
+      const char* e = getenv("PBH_PLACE_SPLIT");
+      return !(e && e[0] == '0');
+    }();
+    if (split)
+      PBH_TIMED(kKPlaceMsd, s,
+                hipLaunchKernelGGL(k_place_msd<true>, dim3((unsigned)tiles), dim3(kT), 0, s, cb.pairs[cur], n, shifts[l],
+                                   cr, cb.pairs[cur ^ 1], state));
+    else
+      PBH_TIMED(kKPlaceMsd, s,
+                hipLaunchKernelGGL(k_place_msd<false>, dim3((unsigned)tiles), dim3(kT), 0, s, cb.pairs[cur], n,
+                                   shifts[l], cr, cb.pairs[cur ^ 1], state));
     PBH_CHECK_LAUNCH();
     cur ^= 1;
   }

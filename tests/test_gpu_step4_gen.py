@@ -96,3 +96,23 @@ def test_generated_step4_long_runs_fall_back(gpu):
     ref = _oracle(n, dists, 3, C)
     np.testing.assert_array_equal(idx, ref["idx"])
     assert_close(Y, ref["Y"], rtol=1e-10, what="long runs")
+
+
+@pytest.mark.parametrize("cap", [None, "16"])
+def test_generated_step4_run_heads_paths(gpu, monkeypatch, cap):
+    """Run heads of a discrete (poisson) column come from the counting pass itself (appended,
+    then sorted) when the column has at most PBH_HEADS_CAP distinct values (16384 by default),
+    or from the materialised sorted column beyond that (poisson(30) has ~50 distinct values
+    in 300 001 draws: the list with the default cap, the fallback with cap 16).  Both give the
+    oracle's 'average' ranks and step-4 indices.  (A large mu would reach the fallback with the
+    default cap, but scipy's cdflib ppf misses the definition there for ~1 draw in 1e5,
+    DESIGN.md section 4, so the oracle's tie groups would differ.)"""
+    if cap:
+        monkeypatch.setenv("PBH_HEADS_CAP", cap)
+    dists = [("poisson", {"mu": 30.0}), ("norm", {}), ("gamma", {"a": 2.0})]
+    C = np.array([[1.0, 0.3, 0.2], [0.3, 1.0, 0.4], [0.2, 0.4, 1.0]])
+    n = 300_001
+    Y, idx = _run(n, dists, 11, C)
+    ref = _oracle(n, dists, 11, C)
+    np.testing.assert_array_equal(idx, ref["idx"])
+    assert_close(Y, ref["Y"], rtol=1e-10, what=f"poisson heads, cap={cap}")

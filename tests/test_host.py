@@ -274,3 +274,15 @@ def test_top_level_names_match_reference():
     assert probabilit_amd.__all__ == ref_all
     for name in ref_all:
         assert callable(getattr(probabilit_amd, name))
+
+
+@pytest.mark.parametrize("cls", ["ImanConover", "Cholesky", "PermutationCorrelator"])
+def test_more_than_128_variables_raise_value_error(cls):
+    """The device correlators hold K <= 128 variables (README / INTEGRATION.md); a larger K is a
+    clear ValueError before any device work, not a native error."""
+    from probabilit_amd import correlation
+
+    K = correlation.MAX_VARIABLES + 1
+    c = getattr(correlation, cls)().set_target(np.eye(K))
+    with pytest.raises(ValueError, match="at most 128 variables"):
+        c(np.zeros((K + 5, K)))
