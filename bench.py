@@ -32,7 +32,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 
 # figures, restated for the kernels this build runs; step 4 = the generated-column path of
 # pbh_step4.hip).  A launch covers one column, except the kernels in ALL_COLUMNS (k columns).
 LAUNCH_BYTES = {
-    "k_lhs_sorted_ppf": 8,       # write sort(X) 8 (stratum-ordered generation, fused tie/inversion counts)
+    "k_lhs_sorted_ppf": 0,       # stratum-ordered generation for the tie / inversion counts only: nothing stored
     "k_perm_scores": 8,          # write S 8 (ranks from the LHS permutation: no sort of X)
     "k_gram": 8,                 # read S 8                                   (all columns)
     "k_apply": 20,               # read S 8, write CS 8 + code 4              (all columns)
@@ -62,10 +62,16 @@ PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k
              "k_code_runs": ["k_code_buckets", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
              "k_apply": ["k_apply_mfma", "k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"],
              "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"],
+             "k_finish": ["k_finish_fused<2, 4096>", "k_finish_fused<1, 4096>", "k_finish_fused<2, 2048>",
+                          "k_finish_fused<1, 2048>", "k_finish_fused<4, 2048>", "k_finish_fused<4, 4096>", "k_finish"],
+             "k_msd1": ["k_msd1<true>", "k_msd1<false>", "k_msd1"], "k_msd2": ["k_msd2<true>", "k_msd2<false>", "k_msd2"],
+             "k_place_msd": ["k_place_msd<true>", "k_place_msd<false>", "k_place_msd"],
+             "k_hist16": ["k_hist16"],
              # one timing id over every variant that ran (the cfg3 set: norm, lognorm, triang,
              # uniform, expon, gamma, poisson): traffic = their dispatch-weighted mean
              "k_place_gen": ["k_place_gen<0>", "k_place_gen<1>", "k_place_gen<2>", "k_place_gen<3>", "k_place_gen<4>",
-                             "k_place_gen_gamma", "k_place_gen_poisson"],
+                             "k_place_gen_direct<0>", "k_place_gen_direct<3>", "k_place_gen_gamma",
+                             "k_place_gen_poisson"],
              "k_lhs_sorted_ppf": ["k_lhs_sorted_ppf<0>", "k_lhs_sorted_ppf<1>", "k_lhs_sorted_ppf<2>",
                                   "k_lhs_sorted_ppf<3>", "k_lhs_sorted_ppf<4>", "k_lhs_sorted_ppf<5>",
                                   "k_lhs_sorted_ppf<6>"]}

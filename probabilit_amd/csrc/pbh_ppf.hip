@@ -459,65 +459,6 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
   }
 }
 
-// norm / lognorm: every value goes straight to its row instead of through the LDS block.  A
-// workgroup takes whole 4096-row blocks, so the block's 32 KiB of Y is written by one CU.
-// Measured (profiles/r02, j2): 0.92 ms against 1.00 ms per 1e8 with the LDS assembly; the
-// same direct writes cost gamma 1.77 -> 2.91, poisson 0.70 -> 1.13 and triang 0.49 -> 1.00 ms,
-// which keep the assembly.  ndtri's tail is still queued (positions = row offsets in the
-// block) and drained with full waves.
-template <int D>
-__global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_direct(const uint64_t* __restrict__ pairs, int64_t n,
-                                                      uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
-                                                      double* __restrict__ y, int64_t y_rs, int32_t* __restrict__ idx,
-                                                      const int32_t* __restrict__ state) {
-  if (state && *state) return;
-  constexpr bool kCompact = true;  // norm / lognorm only
-  __shared__ TailQueue tq;
-  Philox ph(seed);
-  const double p0 = prm.val[0], p1 = prm.val[1], p2 = prm.val[2];
-  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
-    const int64_t r0 = b << kGenPlaceShift;
-    const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
-    for (int h = 0; h < kGenRows; h += kCTile) {
-      if (kCompact) {
-        if (threadIdx.x == 0) tq.count = 0;
-        __syncthreads();
-      }
-      uint64_t pr[kCIpt];
-#pragma unroll
-      for (int j = 0; j < kCIpt; ++j) {
-        const int p = h + j * kBlock + threadIdx.x;
-        pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
-      }
-#pragma unroll
-      for (int j = 0; j < kCIpt; ++j) {
-        const bool valid = pr[j] != ~0ull;
-        const uint32_t t = (uint32_t)pr[j];
-        const int64_t row = (int64_t)(pr[j] >> 32);
-        double q = 0.5;
-        if (valid) {
-          if (idx) idx[row] = (int32_t)t;
-          q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
-        }
-        if constexpr (kCompact) {
-          const bool tail = valid && sf::ndtri_takes_tail(q);
-          if (valid && !tail) y[row * y_rs] = ppf_one<D, 1>(q, p0, p1, p2, pt);
-          tail_push(tq, tail, q, valid ? (int)(row - r0) : 0);
-        } else {
-          if (valid) y[row * y_rs] = ppf_one<D>(q, p0, p1, p2, pt);
-        }
-      }
-      if (kCompact) {
-        __syncthreads();
-        const int T = tq.count;
-        for (int i = threadIdx.x; i < T; i += kBlock)
-          y[(r0 + tq.pos[i]) * y_rs] = ppf_one<D, 2>(tq.arg[i], p0, p1, p2, pt);
-        __syncthreads();  // the queue is reset by the next tile
-      }
-    }
-  }
-}
-
 // gamma with the guide table in LDS (120 KiB) next to the block (32 KiB): one 1024-thread
 // workgroup per CU
 __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __restrict__ pairs, int64_t n,
@@ -533,12 +474,26 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
   for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
     const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
-    for (int p = threadIdx.x; p < cnt; p += kGBlock) {
-      const uint64_t pr = pairs[r0 + p];
-      const uint32_t t = (uint32_t)pr;
-      const int64_t row = (int64_t)(pr >> 32);
-      if (idx) idx[row] = (int32_t)t;
-      buf[row - r0] = gamma_ppf_lds(lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n), prm, pt, T);
+    // the block's 4 pairs per thread as independent chains (the guide's log / LDS gathers / exp
+    // are long dependent sequences; one at a time left 76% of wave cycles waiting)
+    constexpr int kPer = kGenRows / kGBlock;
+    uint64_t pr[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int p = j * kGBlock + threadIdx.x;
+      pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
+    }
+    double v[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      v[j] = gamma_ppf_lds(lhs_sorted_quantile(ph, (uint64_t)(uint32_t)pr[j], col, (uint64_t)n), prm, pt, T);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (pr[j] != ~0ull) {
+        const int64_t row = (int64_t)(pr[j] >> 32);
+        if (idx) idx[row] = (int32_t)(uint32_t)pr[j];
+        buf[row - r0] = v[j];
+      }
     }
     __syncthreads();
     if (y_rs == 1) {
@@ -564,13 +519,26 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_poisson(const uint
   for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
     const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
-    for (int p = threadIdx.x; p < cnt; p += kBlock) {
-      const uint64_t pr = pairs[r0 + p];
-      const uint32_t t = (uint32_t)pr;
-      const int64_t row = (int64_t)(pr >> 32);
-      if (idx) idx[row] = (int32_t)t;
-      const double q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
-      buf[row - r0] = ppf_one<PBH_DIST_POISSON>(q, prm.val[0], prm.val[1], prm.val[2], T);
+    for (int h = 0; h < kGenRows; h += 4 * kBlock) {  // 4 independent chains per thread
+      uint64_t pr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = h + j * kBlock + threadIdx.x;
+        pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
+      }
+      double v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v[j] = ppf_one<PBH_DIST_POISSON>(lhs_sorted_quantile(ph, (uint64_t)(uint32_t)pr[j], col, (uint64_t)n),
+                                         prm.val[0], prm.val[1], prm.val[2], T);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (pr[j] != ~0ull) {
+          const int64_t row = (int64_t)(pr[j] >> 32);
+          if (idx) idx[row] = (int32_t)(uint32_t)pr[j];
+          buf[row - r0] = v[j];
+        }
+      }
     }
     __syncthreads();
     if (y_rs == 1) {
@@ -1132,18 +1100,6 @@ int gen_place(const GenColumn* g, const uint64_t* pairs, int64_t n, double* y, i
     PBH_TIMED(kKPlaceGen, s,
               hipLaunchKernelGGL(k_place_gen_poisson, dim3(gr), dim3(kBlock), pl, s, pairs, n, g->seed, g->col, g->prm,
                                  g->pt, y, y_rs, idx, state));
-    PBH_CHECK_LAUNCH();
-    return PBH_OK;
-  }
-  if (g->dist == PBH_DIST_NORM || g->dist == PBH_DIST_LOGNORM) {
-    if (g->dist == PBH_DIST_NORM)
-      PBH_TIMED(kKPlaceGen, s,
-                hipLaunchKernelGGL(k_place_gen_direct<PBH_DIST_NORM>, dim3(gr), dim3(kBlock), 0, s, pairs, n, g->seed,
-                                   g->col, g->prm, g->pt, y, y_rs, idx, state));
-    else
-      PBH_TIMED(kKPlaceGen, s,
-                hipLaunchKernelGGL(k_place_gen_direct<PBH_DIST_LOGNORM>, dim3(gr), dim3(kBlock), 0, s, pairs, n, g->seed,
-                                   g->col, g->prm, g->pt, y, y_rs, idx, state));
     PBH_CHECK_LAUNCH();
     return PBH_OK;
   }

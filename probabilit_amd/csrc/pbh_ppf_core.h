@@ -110,7 +110,11 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
     } else {  // gamma
+#ifdef PBH_GAMMA_COLD  // A/B: the unguided igami as a real call (smaller kernels, but a call site)
       x = pt.has_gamma ? sf::igami_guided(shape, q, &pt.aux, pt.guide) : sf::igami_cold(shape, q);
+#else
+      x = pt.has_gamma ? sf::igami_guided(shape, q, &pt.aux, pt.guide) : sf::igami(shape, q);
+#endif
     }
     return x * scale + loc;
   }

@@ -899,8 +899,11 @@ int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Sha
   PBH_CHECK_HIP(hipMemsetAsync(sh.hist, 0, (size_t)k * 65536 * 4, s));
   PBH_CHECK_HIP(hipMemsetAsync(sh.cur1, 0, (size_t)k * (2 * 256 * kCurPad + 65536) * 4, s));  // cur1, cur2, curF
   PBH_CHECK_HIP(hipMemsetAsync(sh.state, 0, (size_t)2 * k * 4, s));
-  int64_t blocks = (n + 65535) / 65536;  // >= 64 K codes per block: a handful of flushes
-  if (blocks > 256) blocks = 256;
+  // >= 64 K codes per block and at most 64 blocks per column: every block flushes its non-empty
+  // counters with global atomics (~64 K each), which the PMC pass counted as ~2 GB of writes at
+  // 256 blocks per column (pmc_traffic_r72_ck1.json)
+  int64_t blocks = (n + 65535) / 65536;
+  if (blocks > 64) blocks = 64;
   if (blocks < 1) blocks = 1;
   PBH_TIMED(kKHist16, s,
             hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)k), dim3(1024), 0, s, codes, ldc, n, sh.hist,

@@ -21,3 +21,11 @@ done
 cd /tmp && export TMPDIR=/tmp
 PBH_STEP4_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_${TAG} -o bench --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-e2e --ppf-rows 0 > $R/gpurun_out/${TAG}_prof_bench.json 2> $R/gpurun_out/${TAG}_prof.err
 echo "prof exit $?"
+if [ -n "$PROF2_ENV" ]; then
+  env PBH_STEP4_STREAMS=1 $PROF2_ENV timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_${TAG}_2 -o bench --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-e2e --ppf-rows 0 > $R/gpurun_out/${TAG}_prof2_bench.json 2> $R/gpurun_out/${TAG}_prof2.err
+  echo "prof2 exit $?"
+fi
+timeout -k 10 300 python -u $R/tools/ppf_sweep.py > $R/gpurun_out/${TAG}_sweep.json 2> $R/gpurun_out/${TAG}_sweep.err
+echo "sweep exit $?"
+PBH_LIB_VARIANT=${SWEEP_VARIANT:-} timeout -k 10 300 python -u $R/tools/ppf_sweep.py > $R/gpurun_out/${TAG}_sweep_v.json 2> $R/gpurun_out/${TAG}_sweep_v.err
+echo "sweep variant exit $?"
