@@ -67,8 +67,9 @@ int pbh_init(int device);
  * Rows are counter-addressed, so any row range (a shard) is generated independently. */
 
 /* Native Latin hypercube (replaces scipy.stats.qmc.LatinHypercube._random_lhs reached via
- * modeling.py:480,488): q = (pi_c(r) + 1 - u_c(r)) / n where pi_c is a keyed bijection of
- * [0, n) (Feistel network + cycle walking) and u_c(r) a Philox4x32-10 uniform. */
+ * modeling.py:480,488): q = (pi_c(r) + 1 - u_c(pi_c(r))) / n where pi_c is a keyed bijection of
+ * [0, n) (4-round Feistel network + cycle walking) and u_c(t) the jitter of stratum t (output t
+ * of a SplitMix64 generator keyed by (seed, c)). */
 int pbh_fill_lhs(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col0, int ncols, double* q,
                  int64_t ldq, void* stream);
 

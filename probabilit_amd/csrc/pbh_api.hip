@@ -396,15 +396,19 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     }
   } else {
     // The code histograms of all columns up front, one readback for the bucket-path decisions.
-    uint32_t* hists = nullptr;
+    struct AsyncBuf {  // freed on every return (stream-ordered, before the guard's final sync)
+      uint32_t* p = nullptr;
+      hipStream_t s;
+      ~AsyncBuf() {
+        if (p) (void)hipFreeAsync(p, s);
+      }
+    } hb{nullptr, s};
+    uint32_t*& hists = hb.p;
     if (code_buckets_enabled(n)) {
       PBH_CHECK_HIP(hipMallocAsync((void**)&hists, (size_t)k * 1024 * 4, s));
       for (int c = 0; c < k; ++c) {
         st = code_hist(L.codes + (int64_t)c * n, n, hists + (size_t)c * 1024, s);
-        if (st) {
-          (void)hipFreeAsync(hists, s);
-          return st;
-        }
+        if (st) return st;
       }
       hists_host.resize((size_t)k * 1024);
       PBH_CHECK_HIP(hipMemcpyAsync(hists_host.data(), hists, (size_t)k * 1024 * 4, hipMemcpyDeviceToHost, s));
@@ -419,7 +423,6 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
                           a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n, hc,
                           flat);
     }
-    if (hists) PBH_CHECK_HIP(hipFreeAsync(hists, s));
     if (st) return st;
   }
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // host vectors above were sources of async copies

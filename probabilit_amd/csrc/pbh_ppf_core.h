@@ -64,7 +64,8 @@ PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
 // ppf of one element for distribution D; p = (shape..., loc, scale) already resolved.
 // PART selects ndtri's branch for norm / lognorm (0: ndtri, 1: ndtri_centre, 2: ndtri_tail),
 // for the compacted kernels that know which one an element takes.
-template <int D, int PART = 0>
+// COLD_GAMMA: igami_guided's fallbacks as a call (see igami_guided)
+template <int D, int PART = 0, bool COLD_GAMMA = false>
 PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTable& pt) {
   if constexpr (D == PBH_DIST_POISSON) {
     double mu = p0, loc = p1;
@@ -110,11 +111,7 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
     } else {  // gamma
-#ifdef PBH_GAMMA_COLD  // A/B: the unguided igami as a real call (smaller kernels, but a call site)
-      x = pt.has_gamma ? sf::igami_guided(shape, q, &pt.aux, pt.guide) : sf::igami_cold(shape, q);
-#else
-      x = pt.has_gamma ? sf::igami_guided(shape, q, &pt.aux, pt.guide) : sf::igami(shape, q);
-#endif
+      x = pt.has_gamma ? sf::igami_guided<COLD_GAMMA>(shape, q, &pt.aux, pt.guide) : sf::igami(shape, q);
     }
     return x * scale + loc;
   }

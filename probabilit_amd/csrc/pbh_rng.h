@@ -76,10 +76,16 @@ PBH_HD inline uint32_t mix32(uint32_t x) {  // lowbias32 finalizer
 // bijection of its half, so the network is a bijection of [0, A B); values >= n are cycle-
 // walked, which happens with probability < 1 / B (~1e-4 at n = 1e8), so a SIMD lane almost
 // never waits on a neighbour's walk -- unlike a power-of-two domain, where 2^b can be ~2n and
-// the wave-wide maximum walk count is ~4.  F = lowbias32 of the half, reduced to the radix by
-// a multiply-high (Lemire), 4 32-bit multiplies per round.
+// the wave-wide maximum walk count is ~4.  F = lowbias32 of (half XOR round key), reduced to
+// the radix by a multiply-high (Lemire): 3 32-bit multiplies (quarter-rate on CDNA) per round,
+// 4 rounds (Luby-Rackoff: a pseudo-random permutation from 4 rounds of pseudo-random round
+// functions).  The van der Waerden scores kernel evaluates this network once per element and is
+// VALU-issue bound (87% VALU-busy with the round-1 network of 6 rounds and a premultiply, 24
+// multiplies): the network is most of its instructions.  tests/test_streams_host.py checks the
+// permutation statistically on the host (rank correlations across columns, with the row index
+// and along rows; the jitter's uniformity).
 struct FeistelPerm {
-  static constexpr int kRounds = 6;
+  static constexpr int kRounds = 4;
   uint64_t n;
   uint32_t A, B;
   double inv_b;
@@ -96,18 +102,11 @@ struct FeistelPerm {
     inv_b = 1.0 / (double)B;
     uint32_t c[4] = {col, 0u, 0u, kPurposeFeistel};
     ph(c);
-    uint32_t d[4] = {col, 1u, 0u, kPurposeFeistel};
-    ph(d);
-    rk[0] = c[0];
-    rk[1] = c[1];
-    rk[2] = c[2];
-    rk[3] = c[3];
-    rk[4] = d[0];
-    rk[5] = d[1];
+    for (int i = 0; i < kRounds; ++i) rk[i] = c[i];
   }
 
   PBH_HD static inline uint32_t reduce(uint32_t h, uint32_t m) { return (uint32_t)(((uint64_t)h * m) >> 32); }
-  PBH_HD inline uint32_t F(uint32_t v, uint32_t k) const { return mix32(v * 0x9E3779B1u ^ k); }
+  PBH_HD inline uint32_t F(uint32_t v, uint32_t k) const { return mix32(v ^ k); }
 
   PBH_HD inline void split(uint64_t x, uint32_t& L, uint32_t& R) const {
     // x < 2^32 and the product's relative error is ~1e-16, so q is off by at most one:

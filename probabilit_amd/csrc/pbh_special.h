@@ -793,53 +793,50 @@ PBH_HD inline double guide_interp(const GammaGuide& T, int j, double t) {
   return guide_interp_arr(T.y, T.d1, T.d2, T.h, j, t);
 }
 
-// igami as a real call, for the per-element-parameter gamma path (no guide table).  The guided
-// path keeps its fallbacks inline: as calls they slowed the stratum-ordered gamma generator
-// 1.44 -> 2.13 ms per 1e8 (profiles/r02, j2).
-inline __attribute__((noinline)) PBH_HD double igami_cold(double a, double p) { return igami(a, p); }
-
-#ifdef PBH_GAMMA_FALLBACK_CALL
-// A/B: igami_guided's rarely taken branches behind one real call with scalar arguments only (no
-// address of the caller's GammaAux is taken, which would move it to scratch): the inlined
-// fallbacks size the register allocation of the whole kernel.
+// igami_guided's rarely taken branches behind one real call with scalar arguments only (no
+// address of the caller's GammaAux is taken, which would move it to scratch).  COLD = true
+// routes them there: the stratum-ordered generator (k_lhs_sorted_ppf, global table read at
+// consecutive nodes) then stops spilling on its hot path (1.45 -> 0.90 ms per 1e8, and 1.09 GB
+// of scratch writes per launch gone); the LDS-table kernels keep them inline (as calls they
+// measured 1.38 -> 2.15 ms for the step-4 placement, 0.92 -> 1.51 ms for the ppf sweep).
 inline __attribute__((noinline)) PBH_HD double igami_guided_fallback(double a, double p, double x, bool halley,
                                                                      double lga, double lg1pa, double lanczos) {
   if (!halley) return igami(a, p);
   const GammaAux g = {lga, lg1pa, lanczos};
   return gamma_halley(a, p, x, &g);
 }
-#endif
 
+template <bool COLD = false>
 PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const GammaGuide& T) {
-#ifdef PBH_GAMMA_FALLBACK_CALL
-  double x = 0.0;
-  bool halley = false, slow = !(p > 0.0 && p < 1.0);
-  if (!slow) {
-    const double w = log(p / (1.0 - p));
-    double u = (w - T.z0) * T.inv_h;
-    slow = !(u >= 0.0 && u < (double)(T.m - 1));
+  if constexpr (COLD) {
+    double x = 0.0;
+    bool halley = false, slow = !(p > 0.0 && p < 1.0);
     if (!slow) {
-      int j = (int)u;
-      double y = guide_interp(T, j, u - (double)j);
-      slow = !(y >= -680.0 && y <= 700.0);  // NaN entries, subnormal / huge x
+      const double w = log(p / (1.0 - p));
+      double u = (w - T.z0) * T.inv_h;
+      slow = !(u >= 0.0 && u < (double)(T.m - 1));
       if (!slow) {
-        x = exp(y);
-        halley = T.ok[j] == 0.0;
+        int j = (int)u;
+        double y = guide_interp(T, j, u - (double)j);
+        slow = !(y >= -680.0 && y <= 700.0);  // NaN entries, subnormal / huge x
+        if (!slow) {
+          x = exp(y);
+          halley = T.ok[j] == 0.0;
+        }
       }
     }
+    return (slow || halley) ? igami_guided_fallback(a, p, x, halley, g->lga, g->lg1pa, g->lanczos) : x;
+  } else {
+    if (!(p > 0.0 && p < 1.0)) return igami(a, p);
+    const double w = log(p / (1.0 - p));
+    double u = (w - T.z0) * T.inv_h;
+    if (!(u >= 0.0 && u < (double)(T.m - 1))) return igami(a, p);
+    int j = (int)u;
+    double y = guide_interp(T, j, u - (double)j);
+    if (!(y >= -680.0 && y <= 700.0)) return igami(a, p);  // NaN entries, subnormal / huge x
+    double x = exp(y);
+    return T.ok[j] != 0.0 ? x : gamma_halley(a, p, x, g);
   }
-  return (slow || halley) ? igami_guided_fallback(a, p, x, halley, g->lga, g->lg1pa, g->lanczos) : x;
-#else
-  if (!(p > 0.0 && p < 1.0)) return igami(a, p);
-  const double w = log(p / (1.0 - p));
-  double u = (w - T.z0) * T.inv_h;
-  if (!(u >= 0.0 && u < (double)(T.m - 1))) return igami(a, p);
-  int j = (int)u;
-  double y = guide_interp(T, j, u - (double)j);
-  if (!(y >= -680.0 && y <= 700.0)) return igami(a, p);  // NaN entries, subnormal / huge x
-  double x = exp(y);
-  return T.ok[j] != 0.0 ? x : gamma_halley(a, p, x, g);
-#endif
 }
 
 // igami(a, p(w)), p(w) = 1 / (1 + e^-w); the upper half goes through the complement

@@ -41,7 +41,7 @@ void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb);
 bool step4_gen_enabled(int64_t n);
 // the bucket finish scatters straight into the top row-placement level (PBH_STEP4_FUSED, default on)
 bool step4_fused();
-// columns of step 4 run concurrently on this many streams (PBH_STEP4_STREAMS, default 2, at
+// columns of step 4 run concurrently on this many streams (PBH_STEP4_STREAMS, default 3, at
 // most kStep4MaxStreams), each with its own Step4Column staging, so that one column's VALU- or
 // latency-bound kernels (bucket finish, gen_place) overlap another's bandwidth-bound passes
 constexpr int kStep4MaxStreams = 4;

@@ -580,8 +580,8 @@ union FinishLds {
 
 // FB buckets per block (staging FB * kBucketCap2 pairs); BINS counting bins on the top
 // log2(BINS) of the 16 low code bits
-template <int FB, int BINS>
-__global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict__ keys,
+template <int FB, int BINS, bool PF = false>  // PF: the next bucket's keys / rows loaded ahead
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_finish_fused(const uint16_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ rows,
                                                      const double* __restrict__ x,
                                                      const uint32_t* __restrict__ start, int s_top,
@@ -600,6 +600,18 @@ __global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict_
   uint64_t pr[FB * kFIpt];
   uint32_t grk[FB * kFIpt];
   int total = 0;
+  uint32_t kn[kFIpt], rn[kFIpt];
+  auto load = [&](int bkt, uint32_t* kk, uint32_t* rr) {
+    const int64_t s0 = start[bkt];
+    const int l0 = (int)((int64_t)start[bkt + 1] - s0);
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j) {
+      const int p = j * kT + t;
+      kk[j] = p < l0 ? (uint32_t)keys[s0 + p] : 0u;
+      rr[j] = p < l0 ? rows[s0 + p] : 0u;
+    }
+  };
+  if (PF) load(blockIdx.x * FB, kn, rn);
 #pragma unroll
   for (int bb = 0; bb < FB; ++bb) {
     const int bkt = blockIdx.x * FB + bb;
@@ -607,11 +619,15 @@ __global__ __launch_bounds__(kT) void k_finish_fused(const uint16_t* __restrict_
     const int len = (int)((int64_t)start[bkt + 1] - s);  // <= kBucketCap2 (k_hist16_scan)
     for (int i = t; i <= BINS; i += kT) L.a.cnt[i] = 0;
     uint32_t k[kFIpt], r[kFIpt], rk[kFIpt];
+    if (PF) {
 #pragma unroll
-    for (int j = 0; j < kFIpt; ++j) {
-      const int p = j * kT + t;
-      k[j] = p < len ? (uint32_t)keys[s + p] : 0u;
-      r[j] = p < len ? rows[s + p] : 0u;
+      for (int j = 0; j < kFIpt; ++j) {
+        k[j] = kn[j];
+        r[j] = rn[j];
+      }
+      if (bb + 1 < FB) load(bkt + 1, kn, rn);
+    } else {
+      load(bkt, k, r);
     }
     __syncthreads();
 #pragma unroll
@@ -847,7 +863,7 @@ void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb) {
 int step4_streams() {
   static const int v = [] {
     const char* e = getenv("PBH_STEP4_STREAMS");
-    int x = e ? atoi(e) : 2;
+    int x = e ? atoi(e) : 3;
     return x < 1 ? 1 : (x > kStep4MaxStreams ? kStep4MaxStreams : x);
   }();
   return v;
@@ -951,6 +967,10 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
       return e ? atoi(e) : 22;
     }();
     uint32_t* gc = sh.curF + (int64_t)c * 256 * kCurPad;
+#define PBH_FIN2(FB, BINS)                                                                                        \
+  PBH_TIMED(kKFinish, s,                                                                                          \
+            hipLaunchKernelGGL((k_finish_fused<FB, BINS, true>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16,     \
+                               cb.rows2, cs, start, s_top, gc, cb.pairs[0], sh.flags + c, state))
 #define PBH_FIN(FB, BINS)                                                                                         \
   PBH_TIMED(kKFinish, s,                                                                                          \
             hipLaunchKernelGGL((k_finish_fused<FB, BINS>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16, cb.rows2, cs, \
@@ -961,9 +981,11 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
       case 21: PBH_FIN(2, 2048); break;
       case 41: PBH_FIN(4, 2048); break;
       case 42: PBH_FIN(4, 4096); break;
+      case 23: PBH_FIN2(2, 4096); break;
       default: PBH_FIN(2, 4096); break;
     }
 #undef PBH_FIN
+#undef PBH_FIN2
   } else {
     PBH_TIMED(kKFinish, s,
               hipLaunchKernelGGL(k_finish, dim3(65536 / kBFWaves), dim3(64 * kBFWaves), 0, s, cb.keys16, cb.rows2, cs,

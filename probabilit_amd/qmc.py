@@ -5,7 +5,8 @@
                     gives at modeling.py:484-486 (pbh_mt19937_random, pbh_pcg64_random:
                     device jump-ahead, the caller's generator advanced exactly as numpy does)
     method="lhs"    native Latin hypercube (default): per column a keyed Feistel bijection of
-                    the strata plus a Philox jitter, fused into the ppf kernel (pbh_lhs_ppf);
+                    the strata plus a SplitMix64 jitter keyed by (seed, column, stratum), fused
+                    into the ppf kernel (pbh_lhs_ppf);
                     with stream="reference": scipy's LatinHypercube stream bit for bit
                     (pbh_lhs_reference: device PCG64 uniforms + host Fisher-Yates shuffles)
     method="sobol"  scrambled Sobol', bit-exact with scipy.stats.qmc.Sobol (pbh_fill_sobol);

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "pbh_mt.h"
+#include "pbh_rng.h"
 
 using namespace pbh;
 
@@ -59,6 +60,17 @@ void sh_pcg_doubles(uint64_t s_lo, uint64_t s_hi, uint64_t inc_lo, uint64_t inc_
   for (int64_t i = 0; i < n; ++i) {
     s = s * pcg::kMult + inc;
     out[i] = pcg::to_double(pcg::output(s));
+  }
+}
+
+// The native LHS quantiles (pbh_rng.h lhs_quantile: keyed Feistel stratum + SplitMix64 jitter)
+// of columns col0 .. col0 + ncols - 1 for rows 0 .. n - 1, q[c * n + r] -- the same inline
+// functions the device kernels evaluate, compiled for the host.
+void sh_native_lhs(uint64_t seed, int64_t n, int col0, int ncols, double* q) {
+  Philox ph(seed);
+  for (int c = 0; c < ncols; ++c) {
+    FeistelPerm fp(ph, (uint64_t)n, (uint32_t)(col0 + c));
+    for (int64_t r = 0; r < n; ++r) q[(int64_t)c * n + r] = lhs_quantile(ph, fp, (uint64_t)r, (uint32_t)(col0 + c));
   }
 }
 }

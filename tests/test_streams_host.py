@@ -22,7 +22,7 @@ def sh():
     hipcc = "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else shutil.which("hipcc")
     if hipcc is None:
         pytest.skip("hipcc not available")
-    deps = [SRC] + [os.path.join(ROOT, "probabilit_amd", "csrc", f) for f in ("pbh_mt.h", "pbh_common.h")]
+    deps = [SRC] + [os.path.join(ROOT, "probabilit_amd", "csrc", f) for f in ("pbh_mt.h", "pbh_common.h", "pbh_rng.h")]
     if not os.path.exists(OUT) or any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
         subprocess.run([hipcc, "-O2", "-std=c++17", "-fPIC", "-shared", "-I", os.path.join(ROOT, "probabilit_amd", "csrc"),
@@ -154,3 +154,28 @@ def test_lhs_reference_perms_vs_oracle_restatement():
     sw, iw = qmc._u128_words(qmc.pcg64_advance(s, inc, n * d)), qmc._u128_words(inc)
     _lib.check(lib.pbh_lhs_reference_perms(_lib.np_ptr(sw), _lib.np_ptr(iw), 0, 0, n, d, _lib.np_ptr(out), None))
     np.testing.assert_array_equal(out.T, np.ceil(q * n).astype(np.int64))
+
+
+def test_native_lhs_statistics(sh):
+    """The native LHS design (pbh_rng.h: 4-round keyed FE2 Feistel stratum + SplitMix64 jitter),
+    host-compiled: every column is a Latin hypercube column, and at n = 1e6 the Spearman
+    correlations between columns, with the row index, and between consecutive rows are those of
+    independent random permutations (|rho| < 5 / sqrt(n)); the in-stratum jitter is uniform
+    (Kolmogorov-Smirnov)."""
+    import scipy.stats
+
+    n, d = 1_000_000, 8
+    q = np.empty(n * d)
+    sh.sh_native_lhs(ctypes.c_uint64(1234), ctypes.c_int64(n), 0, d, _p(q))
+    q = q.reshape(d, n)
+    strata = np.floor(q * n).astype(np.int64)
+    bound = 5.0 / np.sqrt(n)
+    rows = np.arange(n)
+    for c in range(d):
+        assert np.array_equal(np.sort(strata[c]), rows), f"column {c} is not a Latin hypercube column"
+        assert abs(np.corrcoef(strata[c], rows)[0, 1]) < bound
+        assert abs(np.corrcoef(strata[c][:-1], strata[c][1:])[0, 1]) < bound
+        for c2 in range(c):
+            assert abs(np.corrcoef(strata[c], strata[c2])[0, 1]) < bound, (c, c2)
+    jitter = (q * n - strata).ravel()
+    assert scipy.stats.kstest(jitter, "uniform").pvalue > 1e-4
