@@ -471,31 +471,22 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
   __shared__ double buf[kGenRows];
   const sf::GammaGuide T = stage_guide(pt.guide, lds);
   Philox ph(seed);
-  // the block's 4 pairs per thread as independent chains (the guide's log / LDS gathers / exp
-  // are long dependent sequences; one at a time left 76% of wave cycles waiting), and the next
-  // block's pairs loaded before this block's values are computed (one workgroup per CU: nothing
-  // else would hide that latency)
-  constexpr int kPer = kGenRows / kGBlock;
-  auto load = [&](int64_t b, uint64_t* pr) {
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
-    const int cnt = (r0 < n) ? (int)((n - r0) < kGenRows ? (n - r0) : kGenRows) : 0;
+    const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
+    // the block's 4 pairs per thread as independent chains (the guide's log / LDS gathers / exp
+    // are long dependent sequences; one at a time left 76% of wave cycles waiting)
+    constexpr int kPer = kGenRows / kGBlock;
+    uint64_t pr[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int p = j * kGBlock + threadIdx.x;
       pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
     }
-  };
-  uint64_t pr[kPer];
-  load(blockIdx.x, pr);
-  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
-    const int64_t r0 = b << kGenPlaceShift;
-    const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
     double v[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
       v[j] = gamma_ppf_lds(lhs_sorted_quantile(ph, (uint64_t)(uint32_t)pr[j], col, (uint64_t)n), prm, pt, T);
-    uint64_t nx[kPer];
-    load(b + gridDim.x, nx);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       if (pr[j] != ~0ull) {
@@ -511,8 +502,6 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
       for (int p = threadIdx.x; p < cnt; p += kGBlock) y[(r0 + p) * y_rs] = buf[p];
     }
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) pr[j] = nx[j];
   }
 }
 

@@ -20,6 +20,8 @@ struct Step4Shared {
   uint32_t* cur1;
   uint32_t* cur2;
   uint32_t* curF;  // fused finish: cursors of the top row-placement level
+  uint32_t* cls;     // per column: top-byte counts of each msd1 tile class (8 x 256)
+  uint32_t* cstart;  // per column: each class's start in every top-byte group (8 x 256)
   uint32_t* tpre;
   int32_t* state;
   int32_t* flags;

@@ -40,7 +40,19 @@ constexpr int kIptP = 16;
 constexpr int kTileP = kT * kIptP;  // placement tiles: 4096 pairs (divides every group size 2^s >= 2^12)
 constexpr int kBucketCap2 = 2048;   // items per top-16 bucket a wave can finish
 constexpr int kRunCap = 16;         // longest run of equal codes the finish orders
-constexpr int kCurPad = 16;         // code-pass cursors one 64-byte line apart (atomic traffic)
+// Cursor spacing (u32 words) of the code-pass and finish cursors: atomics on neighbouring lines
+// also share a memory channel; PBH_CUR_PAD (power of two, default 16 = one 64-byte line) spreads
+// them further.
+static int cur_pad() {
+  static const int v = [] {
+    const char* e = getenv("PBH_CUR_PAD");
+    int x = e ? atoi(e) : 16;
+    int p = 1;
+    while (p < x && p < 4096) p <<= 1;
+    return p;
+  }();
+  return v;
+}
 
 __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh /* >= 260 */) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -63,37 +75,46 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh 
 // (128 KiB), flushed with one global add per non-empty counter.  A counter reaching 65535 in
 // one block (a spike: a discrete-dominated correlated score) sets the column's state bit 0,
 // which routes it to the general path; so does a bucket above kBucketCap2 (k_hist16_scan).
+//
+// It also counts, per column, the top code byte of every tile class x = (row / kTile1) mod 8
+// (cls[x][byte]): k_msd1 tile i runs as block i, and blocks b and b + 8 share an XCD, so the
+// code pass gives each class its own cursors and sub-ranges (see k_msd1).
 __global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ codes, int64_t ld, int64_t n,
-                                                 uint32_t* __restrict__ hist, int32_t* __restrict__ state) {
+                                                 uint32_t* __restrict__ hist, uint32_t* __restrict__ cls,
+                                                 int32_t* __restrict__ state) {
   __shared__ uint32_t w[32768];
+  __shared__ uint32_t cw[8 * 256];
   __shared__ int ovf;
   const int c = blockIdx.y;
   const uint32_t* cc = codes + (int64_t)c * ld;
   for (int i = threadIdx.x; i < 32768; i += 1024) w[i] = 0;
+  for (int i = threadIdx.x; i < 8 * 256; i += 1024) cw[i] = 0;
   if (threadIdx.x == 0) ovf = 0;
   __syncthreads();
   const int64_t chunk = ((n + gridDim.x - 1) / gridDim.x + 3) & ~(int64_t)3;
   const int64_t lo = (int64_t)blockIdx.x * chunk;
   const int64_t hi = lo + chunk < n ? lo + chunk : n;
   bool bad = false;
-  auto add = [&](uint32_t code) {
+  auto add = [&](uint32_t code, int64_t row) {
     const uint32_t b = code >> 16, sh = (b & 1u) * 16u;
     const uint32_t old = atomicAdd(&w[b >> 1], 1u << sh);
     bad |= ((old >> sh) & 0xFFFFu) == 0xFFFFu;
+    atomicAdd(&cw[(((uint32_t)(row / kTile1) & 7u) << 8) | (code >> 24)], 1u);
   };
   if ((((uintptr_t)(cc + lo)) & 15) == 0) {
     const int64_t n4 = (hi - lo) / 4;
     const uint4* v4 = reinterpret_cast<const uint4*>(cc + lo);
     for (int64_t i = threadIdx.x; i < n4; i += 1024) {
       const uint4 v = v4[i];
-      add(v.x);
-      add(v.y);
-      add(v.z);
-      add(v.w);
+      const int64_t r = lo + 4 * i;
+      add(v.x, r);
+      add(v.y, r + 1);
+      add(v.z, r + 2);
+      add(v.w, r + 3);
     }
-    for (int64_t i = lo + 4 * n4 + threadIdx.x; i < hi; i += 1024) add(cc[i]);
+    for (int64_t i = lo + 4 * n4 + threadIdx.x; i < hi; i += 1024) add(cc[i], i);
   } else {
-    for (int64_t i = lo + threadIdx.x; i < hi; i += 1024) add(cc[i]);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 1024) add(cc[i], i);
   }
   if (bad) ovf = 1;
   __syncthreads();
@@ -103,17 +124,22 @@ __global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ co
     if (v & 0xFFFFu) atomicAdd(&hc[2 * j], v & 0xFFFFu);
     if (v >> 16) atomicAdd(&hc[2 * j + 1], v >> 16);
   }
+  for (int j = threadIdx.x; j < 8 * 256; j += 1024)
+    if (cw[j]) atomicAdd(&cls[(int64_t)c * 2048 + j], cw[j]);
   if (threadIdx.x == 0 && ovf) atomicOr(&state[c], 1);
 }
 
 // One 1024-thread block per column: start[b] = exclusive prefix of the 65536 bucket counts
 // (start[65536] = n), the msd2 tile map (tiles of kTile1 inside every top-byte group: tpre[g]
 // = tiles before group g), and state bit 1 when a bucket exceeds kBucketCap2.
+// cstart[x][g] = start of top byte g + the counts of classes < x in it (k_msd1's sub-ranges).
 __global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict__ hist, int64_t n,
                                                       uint32_t* __restrict__ start, uint32_t* __restrict__ tpre,
+                                                      const uint32_t* __restrict__ cls, uint32_t* __restrict__ cstart,
                                                       int32_t* __restrict__ state) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t gsize[256];
+  __shared__ uint32_t gstart[256];
   __shared__ int big;
   const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t* hc = hist + (int64_t)c * 65536;
@@ -137,6 +163,7 @@ __global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict
   uint32_t pre = 0;
   for (int i = 0; i < wv; ++i) pre += wsum[i];
   uint32_t run = pre + x - s;
+  if ((t & 3) == 0) gstart[t >> 2] = run;  // start of top byte t / 4 (= bucket 64 t)
 #pragma unroll
   for (int j = 0; j < 64; ++j) {
     sc[t * 64 + j] = run;
@@ -148,6 +175,13 @@ __global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict
   __syncthreads();
   atomicAdd(&gsize[t >> 2], s);  // top-byte group g = threads 4 g .. 4 g + 3 (256 buckets)
   __syncthreads();
+  if (t < 256) {
+    uint32_t r = gstart[t];
+    for (int xc = 0; xc < 8; ++xc) {
+      cstart[(int64_t)c * 2048 + xc * 256 + t] = r;
+      r += cls[(int64_t)c * 2048 + xc * 256 + t];
+    }
+  }
   if (t == 0) {
     uint32_t acc = 0;
     for (int g = 0; g < 256; ++g) {
@@ -163,10 +197,14 @@ __global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict
 // msd1: tile = kTile1 consecutive rows; digit = top code byte.
 // SPLIT: one 32-bit staging array, used twice (keys, then rows): 32 KiB of LDS per block instead
 // of 64, so 4 blocks per CU instead of 2, for two more barriers.
+// XCD: the block's tile class x = blockIdx.x mod 8 appends to its own sub-range of every top-byte
+// group through its own cursor (cstart, cur + x * 256): 1/8 of the tiles contend on a cursor,
+// and the runs of one sub-range are all written from one XCD (its L2 merges the lines).
 template <bool SPLIT>
 __global__ __launch_bounds__(kT) void k_msd1(const uint32_t* __restrict__ codes, int64_t n,
                                              const uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
                                              uint32_t* __restrict__ kout, uint32_t* __restrict__ rout,
+                                             const uint32_t* __restrict__ cstart, int cpad,
                                              const int32_t* __restrict__ state) {
   if (*state) return;  // uniform: this column takes the general path
   __shared__ uint32_t cnt[256], lst[264], gb[256];
@@ -187,7 +225,12 @@ __global__ __launch_bounds__(kT) void k_msd1(const uint32_t* __restrict__ codes,
   const uint32_t my = cnt[t];
   const uint32_t ex = block_excl_scan256(my, lst);
   lst[t] = ex;
-  gb[t] = my ? start[t << 8] + atomicAdd(&cur[t * kCurPad], my) : 0u;
+  if (cstart) {
+    const uint32_t xc = blockIdx.x & 7u;
+    gb[t] = my ? cstart[(xc << 8) + t] + atomicAdd(&cur[((xc << 8) + t) * cpad], my) : 0u;
+  } else {
+    gb[t] = my ? start[t << 8] + atomicAdd(&cur[t * cpad], my) : 0u;
+  }
   __syncthreads();
   if constexpr (SPLIT) {
     uint32_t dst[kIpt1];  // where slot p = j * kT + t's key goes, kept for the rows round
@@ -585,7 +628,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                                      const uint32_t* __restrict__ rows,
                                                      const double* __restrict__ x,
                                                      const uint32_t* __restrict__ start, int s_top,
-                                                     uint32_t* __restrict__ gcur, uint64_t* __restrict__ out,
+                                                     uint32_t* __restrict__ gcur, int cpad, uint64_t* __restrict__ out,
                                                      int32_t* __restrict__ flags,
                                                      const int32_t* __restrict__ state) {
   if (*state) return;
@@ -696,7 +739,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const uint32_t my = gcnt[t];
   const uint32_t ex = block_excl_scan256(my, goff);
   goff[t] = ex;
-  gbase[t] = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * kCurPad], my)) : 0u;
+  gbase[t] = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * cpad], my)) : 0u;
   __syncthreads();
 #pragma unroll
   for (int slot = 0; slot < FB * kFIpt; ++slot)
@@ -807,9 +850,10 @@ __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ i
 }  // namespace
 
 size_t step4_gen_shared_bytes(int k) {
-  // per column: hist 65536 + start 65537 + cur1 256 * pad + cur2 65536 + curF 256 * pad + tpre 257
-  // (u32), state
-  return (size_t)k * ((65536 + 65537 + 256 * kCurPad + 65536 + 256 * kCurPad + 257) * 4 + 64) + 256;
+  // per column: hist 65536 + start 65537 + cur1 8 x 256 * pad + cur2 65536 + curF 256 * pad +
+  // cls 2048 + cstart 2048 + tpre 257 (u32), state
+  const size_t pad = (size_t)cur_pad();
+  return (size_t)k * ((65536 + 65537 + 8 * 256 * pad + 65536 + 256 * pad + 2048 + 2048 + 257) * 4 + 64) + 256;
 }
 
 size_t step4_gen_column_bytes(int64_t n) {
@@ -827,11 +871,15 @@ void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh) {
   sh.start = (uint32_t*)p;
   p += (size_t)k * 65537 * 4;
   sh.cur1 = (uint32_t*)p;
-  p += (size_t)k * 256 * kCurPad * 4;
+  p += (size_t)k * 8 * 256 * cur_pad() * 4;
   sh.cur2 = (uint32_t*)p;
   p += (size_t)k * 65536 * 4;
   sh.curF = (uint32_t*)p;
-  p += (size_t)k * 256 * kCurPad * 4;
+  p += (size_t)k * 256 * cur_pad() * 4;
+  sh.cls = (uint32_t*)p;
+  p += (size_t)k * 2048 * 4;
+  sh.cstart = (uint32_t*)p;
+  p += (size_t)k * 2048 * 4;
   sh.tpre = (uint32_t*)p;
   p += (size_t)k * 257 * 4;
   p = (char*)(((uintptr_t)p + 63) & ~(uintptr_t)63);
@@ -913,7 +961,7 @@ bool step4_gen_enabled(int64_t n) {
 int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Shared& sh, hipStream_t s) {
   const int k = sh.k;
   PBH_CHECK_HIP(hipMemsetAsync(sh.hist, 0, (size_t)k * 65536 * 4, s));
-  PBH_CHECK_HIP(hipMemsetAsync(sh.cur1, 0, (size_t)k * (2 * 256 * kCurPad + 65536) * 4, s));  // cur1, cur2, curF
+  PBH_CHECK_HIP(hipMemsetAsync(sh.cur1, 0, (size_t)k * (9 * 256 * (size_t)cur_pad() + 65536 + 2048) * 4, s));  // cur1, cur2, curF, cls
   PBH_CHECK_HIP(hipMemsetAsync(sh.state, 0, (size_t)2 * k * 4, s));
   // >= 64 K codes per block and at most 64 blocks per column: every block flushes its non-empty
   // counters with global atomics (~64 K each), which the PMC pass counted as ~2 GB of writes at
@@ -923,9 +971,10 @@ int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Sha
   if (blocks < 1) blocks = 1;
   PBH_TIMED(kKHist16, s,
             hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)k), dim3(1024), 0, s, codes, ldc, n, sh.hist,
-                               sh.state));
+                               sh.cls, sh.state));
   PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)k), dim3(1024), 0, s, sh.hist, n, sh.start, sh.tpre, sh.state);
+  hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)k), dim3(1024), 0, s, sh.hist, n, sh.start, sh.tpre, sh.cls,
+                     sh.cstart, sh.state);
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
@@ -935,6 +984,11 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
   const uint32_t* start = sh.start + (int64_t)c * 65537;
   const int32_t* state = sh.state + c;
   const int64_t t1 = (n + kTile1 - 1) / kTile1;
+  static const bool xcd = [] {  // PBH_MSD1_XCD=0: one cursor per top byte for every tile
+    const char* e = getenv("PBH_MSD1_XCD");
+    return !(e && e[0] == '0');
+  }();
+  const uint32_t* cst = xcd ? sh.cstart + (int64_t)c * 2048 : nullptr;
   static const bool split = [] {  // PBH_MSD_SPLIT=0: keys and rows staged together (64 KiB)
     const char* e = getenv("PBH_MSD_SPLIT");
     return !(e && e[0] == '0');
@@ -942,7 +996,7 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
   if (split) {
     PBH_TIMED(kKMsd1, s,
               hipLaunchKernelGGL(k_msd1<true>, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
-                                 sh.cur1 + (int64_t)c * 256 * kCurPad, cb.keys32, cb.rows1, state));
+                                 sh.cur1 + (int64_t)c * 8 * 256 * cur_pad(), cb.keys32, cb.rows1, cst, cur_pad(), state));
     PBH_CHECK_LAUNCH();
     PBH_TIMED(kKMsd2, s,
               hipLaunchKernelGGL(k_msd2<true>, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
@@ -950,7 +1004,7 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
   } else {
     PBH_TIMED(kKMsd1, s,
               hipLaunchKernelGGL(k_msd1<false>, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
-                                 sh.cur1 + (int64_t)c * 256 * kCurPad, cb.keys32, cb.rows1, state));
+                                 sh.cur1 + (int64_t)c * 8 * 256 * cur_pad(), cb.keys32, cb.rows1, cst, cur_pad(), state));
     PBH_CHECK_LAUNCH();
     PBH_TIMED(kKMsd2, s,
               hipLaunchKernelGGL(k_msd2<false>, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
@@ -966,15 +1020,16 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
       const char* e = getenv("PBH_FINISH_CFG");
       return e ? atoi(e) : 22;
     }();
-    uint32_t* gc = sh.curF + (int64_t)c * 256 * kCurPad;
+    uint32_t* gc = sh.curF + (int64_t)c * 256 * cur_pad();
+    const int cpad = cur_pad();
 #define PBH_FIN2(FB, BINS)                                                                                        \
   PBH_TIMED(kKFinish, s,                                                                                          \
             hipLaunchKernelGGL((k_finish_fused<FB, BINS, true>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16,     \
-                               cb.rows2, cs, start, s_top, gc, cb.pairs[0], sh.flags + c, state))
+                               cb.rows2, cs, start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state))
 #define PBH_FIN(FB, BINS)                                                                                         \
   PBH_TIMED(kKFinish, s,                                                                                          \
             hipLaunchKernelGGL((k_finish_fused<FB, BINS>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16, cb.rows2, cs, \
-                               start, s_top, gc, cb.pairs[0], sh.flags + c, state))
+                               start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state))
     switch (cfg) {
       case 11: PBH_FIN(1, 2048); break;
       case 12: PBH_FIN(1, 4096); break;
