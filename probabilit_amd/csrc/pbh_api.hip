@@ -377,7 +377,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       st = step4_gen_column(c, L.codes + (int64_t)c * n, L.S + (int64_t)c * n, n, sh, cbs[i], cs_);
       if (st) return st;
       int buf = 0;
-      st = step4_gen_place_passes(n, cbs[i], sh.flags + c, cs_, &buf);
+      st = step4_gen_place_passes(c, n, sh, cbs[i], cs_, &buf);
       if (st) return st;
       st = gen_place(gens.g[c], cbs[i].pairs[buf], n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
                      a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, sh.flags + c, cs_);

@@ -34,6 +34,7 @@ struct Step4Column {
   uint32_t* rows2;
   uint64_t* pairs[2];
   uint32_t* pcur[2];
+  uint32_t* segtp;  // tile map of the segmented finish output (k_seg_tiles)
 };
 
 size_t step4_gen_shared_bytes(int k);
@@ -57,7 +58,7 @@ int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Sha
 int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, const Step4Shared& sh,
                      const Step4Column& cb, hipStream_t s);
 // row-placement MSD passes on cb.pairs[0]; *out_buf = the pairs buffer grouped by 4096-row block
-int step4_gen_place_passes(int64_t n, const Step4Column& cb, const int32_t* state, hipStream_t s, int* out_buf);
+int step4_gen_place_passes(int c, int64_t n, const Step4Shared& sh, const Step4Column& cb, hipStream_t s, int* out_buf);
 
 // A generated LHS column's inverse-CDF setup (scalar parameters; gamma guide / poisson CDF
 // tables built once), shared by the stratum-ordered generator and the final placement.

@@ -20,6 +20,7 @@
 // writes each value at its own row.  Host decisions are batched: one readback after hist16 for
 // all columns (flatness), one at the end (buckets that met a run longer than kRunCap), whose
 // columns are redone by the general path (pbh_phases.hip reorder_column).
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -628,7 +629,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                                      const uint32_t* __restrict__ rows,
                                                      const double* __restrict__ x,
                                                      const uint32_t* __restrict__ start, int s_top,
-                                                     uint32_t* __restrict__ gcur, int cpad, uint64_t* __restrict__ out,
+                                                     uint32_t* __restrict__ gcur, int cpad, uint32_t segcap,
+                                                     uint64_t* __restrict__ out,
                                                      int32_t* __restrict__ flags,
                                                      const int32_t* __restrict__ state) {
   if (*state) return;
@@ -739,7 +741,18 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const uint32_t my = gcnt[t];
   const uint32_t ex = block_excl_scan256(my, goff);
   goff[t] = ex;
-  gbase[t] = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * cpad], my)) : 0u;
+  if (segcap) {  // XCD-class segments: group t, class blockIdx.x mod 8 (see k_seg_tiles)
+    const uint32_t sg = ((uint32_t)t << 3) | (blockIdx.x & 7u);
+    uint32_t pos = my ? atomicAdd(&gcur[(int64_t)sg * cpad], my) : 0u;
+    if (my && pos + my > segcap) {  // past the segment's capacity: the column takes the general path
+      bad = 1;
+      gbase[t] = 0xFFFFFFFFu;
+    } else {
+      gbase[t] = sg * segcap + pos;
+    }
+  } else {
+    gbase[t] = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * cpad], my)) : 0u;
+  }
   __syncthreads();
 #pragma unroll
   for (int slot = 0; slot < FB * kFIpt; ++slot)
@@ -748,8 +761,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (int p = t; p < total; p += kT) {
     const uint64_t v = L.sv[p];
     const uint32_t g = (uint32_t)(v >> (32 + s_top));
-    out[gbase[g] + ((uint32_t)p - goff[g])] = v;
+    if (gbase[g] != 0xFFFFFFFFu) out[gbase[g] + ((uint32_t)p - goff[g])] = v;
   }
+  __syncthreads();
   if (t == 0 && bad) atomicOr(flags, 1);
 }
 
@@ -757,18 +771,51 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // Input grouped by row >> s_in (closed-form groups: rows are a permutation of [0, n), so group
 // g occupies positions [g << s_in, ...)); tiles of kTileP never straddle a group.  Digit =
 // (row >> s_out) within the group; destination = positions (row >> s_out) << s_out.
-template <bool SPLIT>  // SPLIT: the pairs staged as two 32-bit halves through one 16 KiB array
+// SPLIT: the pairs staged as two 32-bit halves through one 16 KiB array.
+// seg != NULL: the input is the segmented output of k_finish_fused (XCD classes): segment i at
+// [i cap, i cap + min(segcur[i cpad], cap)), tiles of kTileP inside every segment, seg[i] = tiles
+// before segment i (seg[nseg] = all tiles); blocks past them exit.
+template <bool SPLIT>
 __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ in, int64_t n, int s_out,
                                                   uint32_t* __restrict__ cur, uint64_t* __restrict__ out,
-                                                  const int32_t* __restrict__ state) {
+                                                  const int32_t* __restrict__ state, const uint32_t* __restrict__ seg,
+                                                  const uint32_t* __restrict__ segcur, int cpad, uint32_t cap,
+                                                  int nseg) {
   if (state && *state) return;
   __shared__ uint32_t cnt[256], lst[264], gb[256];
   __shared__ uint64_t sv[SPLIT ? 1 : kTileP];
   __shared__ uint32_t sh32[SPLIT ? kTileP : 1];
   __shared__ uint32_t gfirst;
+  __shared__ int64_t sbase;
+  __shared__ int sm;
   const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kTileP;
-  const int m = (int)((n - base) < kTileP ? (n - base) : kTileP);
+  int64_t base;
+  int m;
+  if (seg) {
+    const uint32_t tile = blockIdx.x;
+    if (tile >= seg[nseg]) return;
+    if (t == 0) {  // the segment holding this tile: last i with seg[i] <= tile
+      int lo = 0, hi = nseg;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (seg[mid] <= tile)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      while (lo + 1 < nseg && seg[lo + 1] <= tile) ++lo;  // skip empty segments
+      const uint32_t len = min(segcur[(int64_t)lo * cpad], cap);
+      const uint32_t off = (tile - seg[lo]) * (uint32_t)kTileP;
+      sbase = (int64_t)lo * cap + off;
+      sm = (int)min(len - off, (uint32_t)kTileP);
+    }
+    __syncthreads();
+    base = sbase;
+    m = sm;
+  } else {
+    base = (int64_t)blockIdx.x * kTileP;
+    m = (int)((n - base) < kTileP ? (n - base) : kTileP);
+  }
   cnt[t] = 0;
   if (t == 0) gfirst = 0xFFFFFFFFu;
   __syncthreads();
@@ -847,20 +894,51 @@ __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ i
   }
 }
 
+// Tile map of the segmented finish output: tiles of kTileP in every segment (count = its cursor,
+// capped at cap; a segment past its capacity flags the column), exclusive prefix in seg[0..nseg].
+__global__ __launch_bounds__(256) void k_seg_tiles(const uint32_t* __restrict__ segcur, int cpad, uint32_t cap,
+                                                   int nseg, uint32_t* __restrict__ seg, int32_t* __restrict__ flags) {
+  __shared__ uint32_t sh[264];
+  const int t = threadIdx.x;
+  constexpr int kPer = 2048 / 256;  // nseg <= 8 x 256
+  uint32_t v[kPer], sum = 0;
+  bool over = false;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int i = t * kPer + q;
+    const uint32_t c = i < nseg ? segcur[(int64_t)i * cpad] : 0u;
+    over |= c > cap;
+    v[q] = ((c < cap ? c : cap) + kTileP - 1) / kTileP;
+    sum += v[q];
+  }
+  uint32_t run = block_excl_scan256(sum, sh);
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int i = t * kPer + q;
+    if (i < nseg) seg[i] = run;
+    run += v[q];
+  }
+  if (t == 255) seg[nseg] = run;
+  if (over) atomicOr(flags, 1);
+}
+
 }  // namespace
+
+static int64_t fin_slots(int64_t n);
 
 size_t step4_gen_shared_bytes(int k) {
   // per column: hist 65536 + start 65537 + cur1 8 x 256 * pad + cur2 65536 + curF 256 * pad +
   // cls 2048 + cstart 2048 + tpre 257 (u32), state
   const size_t pad = (size_t)cur_pad();
-  return (size_t)k * ((65536 + 65537 + 8 * 256 * pad + 65536 + 256 * pad + 2048 + 2048 + 257) * 4 + 64) + 256;
+  return (size_t)k * ((65536 + 65537 + 8 * 256 * pad + 65536 + 8 * 256 * pad + 2048 + 2048 + 257) * 4 + 64) + 256;
 }
 
 size_t step4_gen_column_bytes(int64_t n) {
   // keys32 + rows (msd1 out) | keys16 + rows (msd2 out) | pairs x 2 | placement cursors
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const int64_t ncur = (n >> kGenPlaceShift) + 2;
-  return al((size_t)n * 4) * 2 + al((size_t)n * 2) + al((size_t)n * 4) + al((size_t)n * 8) * 2 + al((size_t)ncur * 4) * 2;
+  return al((size_t)n * 4) * 2 + al((size_t)n * 2) + al((size_t)n * 4) + al((size_t)fin_slots(n) * 8) +
+         al((size_t)n * 8) + al((size_t)ncur * 4) * 2 + al(2049 * 4);
 }
 
 void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh) {
@@ -875,7 +953,7 @@ void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh) {
   sh.cur2 = (uint32_t*)p;
   p += (size_t)k * 65536 * 4;
   sh.curF = (uint32_t*)p;
-  p += (size_t)k * 256 * cur_pad() * 4;
+  p += (size_t)k * 8 * 256 * cur_pad() * 4;
   sh.cls = (uint32_t*)p;
   p += (size_t)k * 2048 * 4;
   sh.cstart = (uint32_t*)p;
@@ -899,13 +977,15 @@ void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb) {
   cb.rows2 = (uint32_t*)p;
   p += al((size_t)n * 4);
   cb.pairs[0] = (uint64_t*)p;
-  p += al((size_t)n * 8);
+  p += al((size_t)fin_slots(n) * 8);
   cb.pairs[1] = (uint64_t*)p;
   p += al((size_t)n * 8);
   const int64_t ncur = (n >> kGenPlaceShift) + 2;
   cb.pcur[0] = (uint32_t*)p;
   p += al((size_t)ncur * 4);
   cb.pcur[1] = (uint32_t*)p;
+  p += al((size_t)ncur * 4);
+  cb.segtp = (uint32_t*)p;
 }
 
 int step4_streams() {
@@ -952,6 +1032,30 @@ static int place_levels(int64_t n, int* shifts) {
   return nl;
 }
 
+// Segment capacity of the XCD-class finish output (PBH_FINISH_XCD, default on): two row-placement
+// levels (n <= 2^28), each group of 2^s rows split into 8 class segments of cap = 2^s / 8 +
+// 8 sqrt(2^s) + 256 slots (a class holds ~1/8 of its group, sd ~ sqrt(2^s) / 3: overflow is a
+// > 20-sigma event, and it is caught); 0 = the closed-form group layout.
+static uint32_t fin_segcap(int64_t n) {
+  const char* e = getenv("PBH_FINISH_XCD");  // read per call (the tests switch it)
+  const bool on = !(e && e[0] == '0');
+  int shifts[4];
+  if (!on || !step4_fused() || place_levels(n, shifts) != 2) return 0;
+  const double size = (double)((int64_t)1 << shifts[1]);
+  if (const char* e = getenv("PBH_FINISH_SEGCAP")) return (uint32_t)atoll(e);  // tests: force an overflow
+  return (uint32_t)(size / 8 + 8 * sqrt(size) + 256);
+}
+
+static int64_t fin_slots(int64_t n) {  // pair slots of the finish output buffer
+  const uint32_t cap = fin_segcap(n);
+  if (!cap) return n;
+  int shifts[4];
+  place_levels(n, shifts);
+  const int64_t groups = ((n - 1) >> shifts[1]) + 1;
+  const int64_t slots = groups * 8 * (int64_t)cap;
+  return slots > n ? slots : n;
+}
+
 bool step4_gen_enabled(int64_t n) {
   const char* e = getenv("PBH_STEP4");  // "lsd" / "legacy": the general path for every column
   if (e && (strcmp(e, "lsd") == 0 || strcmp(e, "legacy") == 0)) return false;
@@ -961,7 +1065,7 @@ bool step4_gen_enabled(int64_t n) {
 int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Shared& sh, hipStream_t s) {
   const int k = sh.k;
   PBH_CHECK_HIP(hipMemsetAsync(sh.hist, 0, (size_t)k * 65536 * 4, s));
-  PBH_CHECK_HIP(hipMemsetAsync(sh.cur1, 0, (size_t)k * (9 * 256 * (size_t)cur_pad() + 65536 + 2048) * 4, s));  // cur1, cur2, curF, cls
+  PBH_CHECK_HIP(hipMemsetAsync(sh.cur1, 0, (size_t)k * (16 * 256 * (size_t)cur_pad() + 65536 + 2048) * 4, s));  // cur1, cur2, curF, cls
   PBH_CHECK_HIP(hipMemsetAsync(sh.state, 0, (size_t)2 * k * 4, s));
   // >= 64 K codes per block and at most 64 blocks per column: every block flushes its non-empty
   // counters with global atomics (~64 K each), which the PMC pass counted as ~2 GB of writes at
@@ -1020,22 +1124,21 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
       const char* e = getenv("PBH_FINISH_CFG");
       return e ? atoi(e) : 22;
     }();
-    uint32_t* gc = sh.curF + (int64_t)c * 256 * cur_pad();
+    uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
     const int cpad = cur_pad();
+    const uint32_t segcap = fin_segcap(n);
 #define PBH_FIN2(FB, BINS)                                                                                        \
   PBH_TIMED(kKFinish, s,                                                                                          \
             hipLaunchKernelGGL((k_finish_fused<FB, BINS, true>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16,     \
-                               cb.rows2, cs, start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state))
+                               cb.rows2, cs, start, s_top, gc, cpad, segcap, cb.pairs[0], sh.flags + c, state))
 #define PBH_FIN(FB, BINS)                                                                                         \
   PBH_TIMED(kKFinish, s,                                                                                          \
             hipLaunchKernelGGL((k_finish_fused<FB, BINS>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16, cb.rows2, cs, \
-                               start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state))
+                               start, s_top, gc, cpad, segcap, cb.pairs[0], sh.flags + c, state))
     switch (cfg) {
       case 11: PBH_FIN(1, 2048); break;
       case 12: PBH_FIN(1, 4096); break;
       case 21: PBH_FIN(2, 2048); break;
-      case 41: PBH_FIN(4, 2048); break;
-      case 42: PBH_FIN(4, 4096); break;
       case 23: PBH_FIN2(2, 4096); break;
       default: PBH_FIN(2, 4096); break;
     }
@@ -1050,13 +1153,25 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
   return PBH_OK;
 }
 
-int step4_gen_place_passes(int64_t n, const Step4Column& cb, const int32_t* state, hipStream_t s, int* out_buf) {
+int step4_gen_place_passes(int c, int64_t n, const Step4Shared& sh, const Step4Column& cb, hipStream_t s,
+                           int* out_buf) {
+  int32_t* state = sh.flags + c;
   int shifts[4];
   int nl = place_levels(n, shifts);
   if (step4_fused() && nl > 0) --nl;  // the finish scattered the top level
   int cur = 0;
   const int64_t tiles = (n + kTileP - 1) / kTileP;
+  const uint32_t segcap = fin_segcap(n);
+  const int cpad = cur_pad();
+  const uint32_t* segcur = sh.curF + (int64_t)c * 8 * 256 * cpad;
+  const int nseg = segcap ? (int)((((n - 1) >> shifts[1]) + 1) * 8) : 0;
+  if (segcap) {
+    hipLaunchKernelGGL(k_seg_tiles, dim3(1), dim3(256), 0, s, segcur, cpad, segcap, nseg, cb.segtp, state);
+    PBH_CHECK_LAUNCH();
+  }
   for (int l = nl - 1; l >= 0; --l) {
+    const bool sg = segcap && l == nl - 1;  // the first pass reads the finish's segments
+    const int64_t grid = sg ? tiles + nseg : tiles;
     const int64_t ncur = (n >> shifts[l]) + 1;
     uint32_t* cr = cb.pcur[l & 1];
     PBH_CHECK_HIP(hipMemsetAsync(cr, 0, (size_t)ncur * 4, s));
@@ -1064,14 +1179,15 @@ int step4_gen_place_passes(int64_t n, const Step4Column& cb, const int32_t* stat
       const char* e = getenv("PBH_PLACE_SPLIT");
       return !(e && e[0] == '0');
     }();
+    const uint32_t* segp = sg ? cb.segtp : nullptr;
     if (split)
       PBH_TIMED(kKPlaceMsd, s,
-                hipLaunchKernelGGL(k_place_msd<true>, dim3((unsigned)tiles), dim3(kT), 0, s, cb.pairs[cur], n, shifts[l],
-                                   cr, cb.pairs[cur ^ 1], state));
+                hipLaunchKernelGGL(k_place_msd<true>, dim3((unsigned)grid), dim3(kT), 0, s, cb.pairs[cur], n, shifts[l],
+                                   cr, cb.pairs[cur ^ 1], state, segp, segcur, cpad, segcap, nseg));
     else
       PBH_TIMED(kKPlaceMsd, s,
-                hipLaunchKernelGGL(k_place_msd<false>, dim3((unsigned)tiles), dim3(kT), 0, s, cb.pairs[cur], n,
-                                   shifts[l], cr, cb.pairs[cur ^ 1], state));
+                hipLaunchKernelGGL(k_place_msd<false>, dim3((unsigned)grid), dim3(kT), 0, s, cb.pairs[cur], n,
+                                   shifts[l], cr, cb.pairs[cur ^ 1], state, segp, segcur, cpad, segcap, nseg));
     PBH_CHECK_LAUNCH();
     cur ^= 1;
   }

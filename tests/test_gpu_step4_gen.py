@@ -116,3 +116,22 @@ def test_generated_step4_run_heads_paths(gpu, monkeypatch, cap):
     ref = _oracle(n, dists, 11, C)
     np.testing.assert_array_equal(idx, ref["idx"])
     assert_close(Y, ref["Y"], rtol=1e-10, what=f"poisson heads, cap={cap}")
+
+
+@pytest.mark.parametrize("env", [{}, {"PBH_FINISH_XCD": "0"}, {"PBH_FINISH_SEGCAP": "100000"}])
+def test_generated_step4_finish_segments(gpu, monkeypatch, env):
+    """The bucket finish writes its (row, position) pairs into per-XCD-class segments of every
+    row group (2 placement levels: 2^20 < n <= 2^28), read back through a tile map; with the
+    closed-form layout (PBH_FINISH_XCD=0) and with segments too small for their class
+    (PBH_FINISH_SEGCAP: the overflow flags every column, which the general path redoes) the
+    result is the same and equals the oracle's."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    from oracle.pipeline import cfg3_corr, cfg_dists
+
+    n, d = 2**21 + 5, 3
+    dists, C = cfg_dists(d), cfg3_corr(d)
+    Y, idx = _run(n, dists, 12, C)
+    ref = _oracle(n, dists, 12, C)
+    np.testing.assert_array_equal(idx, ref["idx"])
+    assert_close(Y, ref["Y"], rtol=1e-10, what=f"finish segments {env}")
