@@ -175,8 +175,30 @@ extern "C" int pbh_rankdata_average(const double* x, int64_t stride, int64_t n, 
   return rank_finish(kModeRanks, sb.keys[buf], sb.vals[buf], n, tb, out, s);
 }
 
+namespace {
+constexpr int kRedo = 1000;  // internal: a deferred tie / inversion check failed, run again undeferred
+
+// defer: the tie / inversion counts of the generated continuous columns (which tie or invert with
+// probability ~1e-8 per column at N = 1e8) run on a side stream next to steps 1-3 instead of
+// before them, their scores computed as untied; the counts are checked before step 4 and, if any
+// is non-zero, the whole call is redone with them first (kRedo).  The VALU-bound counting
+// overlaps the bandwidth-bound Gram and step 3.
+int ic_run(const pbh_ic_args* a, void* stream, bool defer);
+}  // namespace
+
 extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   PBH_REQUIRE(a != nullptr, "pbh_iman_conover: args must not be NULL");
+  static const bool defer = [] {
+    const char* e = getenv("PBH_DEFER_COUNTS");
+    return !(e && e[0] == '0');
+  }();
+  int st = ic_run(a, stream, defer);
+  if (st == kRedo) st = ic_run(a, stream, false);
+  return st;
+}
+
+namespace {
+int ic_run(const pbh_ic_args* a, void* stream, bool defer) {
   const int64_t n = a->n;
   const int k = a->k;
   PBH_REQUIRE((a->X || a->columns) && a->Y && a->ws && a->target_chol_host,
@@ -234,6 +256,10 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     if (r == PBH_OK) have_sx[c] = 1;
     return r;
   };
+  std::vector<char> deferred(k, 0);
+  bool any_deferred = false;
+  if (a->columns && defer)
+    for (int c = 0; c < k; ++c) any_deferred |= (deferred[c] = a->columns[c].dist != PBH_DIST_POISSON) != 0;
   if (a->columns) {
     for (int c = 0; c < k; ++c) {
       const pbh_ic_column& g = a->columns[c];
@@ -241,6 +267,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
       for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
       st = gen_create(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, &gens.g[c], s);
       if (st) return st;
+      if (deferred[c]) continue;  // counted next to steps 1-3 (below)
       // run heads only for a discrete column (few runs); a continuous one ties rarely, if ever,
       // and would append every stratum
       const bool discrete = g.dist == PBH_DIST_POISSON;
@@ -251,6 +278,8 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     }
     PBH_CHECK_HIP(hipMemcpyAsync(cnt_host.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
     PBH_CHECK_HIP(hipStreamSynchronize(s));
+    for (int c = 0; c < k; ++c)
+      if (deferred[c]) cnt_host[2 * c] = cnt_host[2 * c + 1] = 0;  // assumed; checked before step 4
   }
   for (int c = 0; c < k; ++c) {
     double* S_c = L.S + (int64_t)c * n;
@@ -308,6 +337,35 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     if (st) return st;
     have_sx[c] = 1;
   }
+  struct Ev {
+    hipEvent_t e = nullptr;
+    hipStream_t wait_on = nullptr;  // ev_counts: the caller's stream waits for the side stream
+    ~Ev() {                         // (destroyed before gens, whose tables are freed on s)
+      if (e && wait_on) (void)hipStreamWaitEvent(wait_on, e, 0);
+      if (e) (void)hipEventDestroy(e);
+    }
+  } ev_scores, ev_counts;
+  ev_counts.wait_on = s;
+  hipStream_t side = any_deferred ? step4_side_stream(0) : nullptr;
+  if (any_deferred && side) {
+    sync_on_exit.side = true;
+    PBH_CHECK_HIP(hipEventCreateWithFlags(&ev_scores.e, hipEventDisableTiming));
+    PBH_CHECK_HIP(hipEventCreateWithFlags(&ev_counts.e, hipEventDisableTiming));
+    PBH_CHECK_HIP(hipEventRecord(ev_scores.e, s));  // the gens' tables are built; the scores are queued
+    PBH_CHECK_HIP(hipStreamWaitEvent(side, ev_scores.e, 0));
+    for (int c = 0; c < k; ++c) {
+      if (!deferred[c]) continue;
+      st = gen_sorted(gens.g[c], 0, n, nullptr, a->columns[c].nonfinite_flag, L.counts + 2 * c, side);
+      if (st) return st;
+    }
+    PBH_CHECK_HIP(hipEventRecord(ev_counts.e, side));
+  } else if (any_deferred) {  // no side stream: count in order
+    for (int c = 0; c < k; ++c) {
+      if (!deferred[c]) continue;
+      st = gen_sorted(gens.g[c], 0, n, nullptr, a->columns[c].nonfinite_flag, L.counts + 2 * c, s);
+      if (st) return st;
+    }
+  }
   PBH_CHECK_HIP(hipMemcpyAsync(&flag_host, L.flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   if (a->scores_out)
     PBH_CHECK_HIP(hipMemcpyAsync(a->scores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
@@ -340,6 +398,16 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   if (st) return st;
   if (a->cscores_out)
     PBH_CHECK_HIP(hipMemcpyAsync(a->cscores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
+
+  // the deferred counts: any tie or inversion means the scores assumed untied were wrong
+  if (any_deferred) {
+    if (ev_counts.e) PBH_CHECK_HIP(hipStreamWaitEvent(s, ev_counts.e, 0));
+    std::vector<unsigned long long> dc(2 * (size_t)k, 0);
+    PBH_CHECK_HIP(hipMemcpyAsync(dc.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+    for (int c = 0; c < k; ++c)
+      if (deferred[c] && (dc[2 * c] | dc[2 * c + 1])) return kRedo;
+  }
 
   // ---- step 4: Y[:, c] = sort(X[:, c])[rankdata(CS[:, c]).astype(int) - 1]
   auto general = [&](int c) {  // the general path (sorted X read from the workspace)
@@ -428,3 +496,4 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // host vectors above were sources of async copies
   return PBH_OK;
 }
+}  // namespace

@@ -767,6 +767,136 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   if (t == 0 && bad) atomicOr(flags, 1);
 }
 
+// The same finish with the group-cursor atomics hoisted (PBH_FINISH_CFG=24): both buckets' rows
+// are loaded first, their row groups counted and the global cursor adds issued before the
+// buckets are worked on, so the adds' round trip overlaps the bucket work instead of ending the
+// block.  Closed-form group layout only.
+template <int BINS>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_finish_ah(
+    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ rows, const double* __restrict__ x,
+    const uint32_t* __restrict__ start, int s_top, uint32_t* __restrict__ gcur, int cpad, uint64_t* __restrict__ out,
+    int32_t* __restrict__ flags, const int32_t* __restrict__ state) {
+  if (*state) return;
+  constexpr int FB = 2;
+  constexpr int kShift = 16 - __builtin_ctz(BINS);
+  constexpr int kPer = BINS / kT;
+  __shared__ FinishLds<FB, BINS> L;
+  __shared__ uint32_t gcnt[256], goff[264], gbase[256];
+  __shared__ int bad;
+  const int t = threadIdx.x;
+  if (t == 0) bad = 0;
+  gcnt[t] = 0;
+  uint32_t kk[FB][kFIpt], rr[FB][kFIpt], grk[FB * kFIpt];
+  int64_t s0[FB];
+  int l0[FB];
+#pragma unroll
+  for (int bb = 0; bb < FB; ++bb) {
+    const int bkt = blockIdx.x * FB + bb;
+    s0[bb] = start[bkt];
+    l0[bb] = (int)((int64_t)start[bkt + 1] - s0[bb]);
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j) {
+      const int p = j * kT + t;
+      kk[bb][j] = p < l0[bb] ? (uint32_t)keys[s0[bb] + p] : 0u;
+      rr[bb][j] = p < l0[bb] ? rows[s0[bb] + p] : 0u;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int bb = 0; bb < FB; ++bb)
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j)
+      grk[bb * kFIpt + j] = (j * kT + t < l0[bb]) ? atomicAdd(&gcnt[rr[bb][j] >> s_top], 1u) : 0u;
+  __syncthreads();
+  const uint32_t my = gcnt[t];
+  goff[t] = block_excl_scan256(my, goff);
+  const uint32_t mybase = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * cpad], my)) : 0u;
+  uint64_t pr[FB * kFIpt];
+  int total = 0;
+#pragma unroll
+  for (int bb = 0; bb < FB; ++bb) {
+    const int64_t s = s0[bb];
+    const int len = l0[bb];
+    for (int i = t; i <= BINS; i += kT) L.a.cnt[i] = 0;
+    __syncthreads();
+    uint32_t rk[kFIpt];
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j)
+      rk[j] = (j * kT + t < len) ? atomicAdd(&L.a.cnt[kk[bb][j] >> kShift], 1u) : 0u;
+    __syncthreads();
+    uint32_t cb[kPer], sum = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      cb[q] = L.a.cnt[kPer * t + q];
+      sum += cb[q];
+    }
+    uint32_t run = block_excl_scan256(sum, goff);  // scratch goff[256..259]; goff[0..255] kept
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      L.a.cnt[kPer * t + q] = run;
+      run += cb[q];
+    }
+    if (t == kT - 1) L.a.cnt[BINS] = run;
+    __syncthreads();
+    uint32_t pos[kFIpt];
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j) {
+      if (j * kT + t < len) {
+        pos[j] = L.a.cnt[kk[bb][j] >> kShift] + rk[j];
+        L.a.key[pos[j]] = (uint16_t)kk[bb][j];
+        L.a.row[pos[j]] = rr[bb][j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kFIpt; ++j) {
+      const int slot = bb * kFIpt + j;
+      if (j * kT + t >= len) {
+        pr[slot] = ~0ull;
+        continue;
+      }
+      const uint32_t kj = kk[bb][j];
+      const uint32_t bs = L.a.cnt[kj >> kShift], be = L.a.cnt[(kj >> kShift) + 1];
+      uint32_t lt = 0, eq = 0;
+      if (be - bs > 1) {
+        if (be - bs > (uint32_t)kBinCap) bad = 1;
+        bool have = false;
+        double xv = 0.0;
+        for (uint32_t m = bs; m < be; ++m) {
+          const uint32_t km = L.a.key[m];
+          lt += km < kj;
+          if (km == kj && m != pos[j]) {
+            if (!have) {
+              xv = x[rr[bb][j]];
+              have = true;
+            }
+            const double xm = x[L.a.row[m]];
+            lt += xm < xv;
+            eq += xm == xv;
+          }
+        }
+      }
+      const uint32_t p = (uint32_t)s + bs + lt + eq / 2;
+      pr[slot] = ((uint64_t)rr[bb][j] << 32) | (uint64_t)p;
+    }
+    total += len;
+    __syncthreads();
+  }
+  gbase[t] = mybase;
+  __syncthreads();
+#pragma unroll
+  for (int slot = 0; slot < FB * kFIpt; ++slot)
+    if (pr[slot] != ~0ull) L.sv[goff[(uint32_t)(pr[slot] >> (32 + s_top))] + grk[slot]] = pr[slot];
+  __syncthreads();
+  for (int p = t; p < total; p += kT) {
+    const uint64_t v = L.sv[p];
+    const uint32_t g = (uint32_t)(v >> (32 + s_top));
+    out[gbase[g] + ((uint32_t)p - goff[g])] = v;
+  }
+  __syncthreads();
+  if (t == 0 && bad) atomicOr(flags, 1);
+}
+
 // ---------------------------------------------------------------- row placement passes
 // Input grouped by row >> s_in (closed-form groups: rows are a permutation of [0, n), so group
 // g occupies positions [g << s_in, ...)); tiles of kTileP never straddle a group.  Digit =
@@ -1032,13 +1162,14 @@ static int place_levels(int64_t n, int* shifts) {
   return nl;
 }
 
-// Segment capacity of the XCD-class finish output (PBH_FINISH_XCD, default on): two row-placement
+// Segment capacity of the XCD-class finish output (PBH_FINISH_XCD=1; off by default: measured
+// 171.8 against 169.5 ms per step with the closed-form layout, profiles/r02 j11): two row-placement
 // levels (n <= 2^28), each group of 2^s rows split into 8 class segments of cap = 2^s / 8 +
 // 8 sqrt(2^s) + 256 slots (a class holds ~1/8 of its group, sd ~ sqrt(2^s) / 3: overflow is a
 // > 20-sigma event, and it is caught); 0 = the closed-form group layout.
 static uint32_t fin_segcap(int64_t n) {
   const char* e = getenv("PBH_FINISH_XCD");  // read per call (the tests switch it)
-  const bool on = !(e && e[0] == '0');
+  const bool on = e && e[0] == '1';
   int shifts[4];
   if (!on || !step4_fused() || place_levels(n, shifts) != 2) return 0;
   const double size = (double)((int64_t)1 << shifts[1]);
@@ -1140,6 +1271,15 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
       case 12: PBH_FIN(1, 4096); break;
       case 21: PBH_FIN(2, 2048); break;
       case 23: PBH_FIN2(2, 4096); break;
+      case 24:
+        if (!segcap) {
+          PBH_TIMED(kKFinish, s,
+                    hipLaunchKernelGGL((k_finish_ah<4096>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
+                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
+          break;
+        }
+        PBH_FIN(2, 4096);
+        break;
       default: PBH_FIN(2, 4096); break;
     }
 #undef PBH_FIN

@@ -118,13 +118,13 @@ def test_generated_step4_run_heads_paths(gpu, monkeypatch, cap):
     assert_close(Y, ref["Y"], rtol=1e-10, what=f"poisson heads, cap={cap}")
 
 
-@pytest.mark.parametrize("env", [{}, {"PBH_FINISH_XCD": "0"}, {"PBH_FINISH_SEGCAP": "100000"}])
+@pytest.mark.parametrize("env", [{}, {"PBH_FINISH_XCD": "1"}, {"PBH_FINISH_XCD": "1", "PBH_FINISH_SEGCAP": "100000"}])
 def test_generated_step4_finish_segments(gpu, monkeypatch, env):
     """The bucket finish writes its (row, position) pairs into per-XCD-class segments of every
-    row group (2 placement levels: 2^20 < n <= 2^28), read back through a tile map; with the
-    closed-form layout (PBH_FINISH_XCD=0) and with segments too small for their class
-    (PBH_FINISH_SEGCAP: the overflow flags every column, which the general path redoes) the
-    result is the same and equals the oracle's."""
+    row group (PBH_FINISH_XCD=1, 2 placement levels: 2^20 < n <= 2^28), read back through a
+    tile map; the default is the closed-form group layout.  Either, and segments too small for
+    their class (PBH_FINISH_SEGCAP: the overflow flags every column, which the general path
+    redoes), give the same result, the oracle's."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     from oracle.pipeline import cfg3_corr, cfg_dists
@@ -135,3 +135,18 @@ def test_generated_step4_finish_segments(gpu, monkeypatch, env):
     ref = _oracle(n, dists, 12, C)
     np.testing.assert_array_equal(idx, ref["idx"])
     assert_close(Y, ref["Y"], rtol=1e-10, what=f"finish segments {env}")
+
+
+def test_deferred_tie_check_redoes_the_call(gpu):
+    """The tie / inversion counts of continuous generated columns run next to steps 1-3 with
+    their scores computed as untied; a column that does tie -- uniform(loc=2**40, scale=1): its
+    ulp (2^-12) spans ~24 strata at n = 1e5 -- fails the check before step 4 and the call is
+    redone with the counts first, so its 'average' ranks and step-4 indices are the oracle's."""
+    dists = [("uniform", {"loc": 2.0**40, "scale": 1.0}), ("norm", {}), ("gamma", {"a": 2.0})]
+    C = np.array([[1.0, 0.3, 0.2], [0.3, 1.0, 0.4], [0.2, 0.4, 1.0]])
+    n = 100_000
+    Y, idx = _run(n, dists, 13, C)
+    ref = _oracle(n, dists, 13, C)
+    assert len(np.unique(ref["Y"][:, 0])) < n // 10  # the column does tie
+    np.testing.assert_array_equal(idx, ref["idx"])
+    assert_close(Y, ref["Y"], rtol=1e-10, what="deferred tie check")
