@@ -469,31 +469,66 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
   if (state && *state) return;
   __shared__ double lds[kGTable];
   __shared__ double buf[kGenRows];
+  // items whose value needs igami's own iteration (outside the grid, an interval that failed its
+  // check, q at 0 or 1, invalid parameters): queued by position in the block and evaluated by
+  // gamma_ppf_lds after the interpolated ones -- so the hot loop carries no igami code (inlined,
+  // it sized the registers of the whole kernel and spilled, 1.6 GB of scratch reloads per launch)
+  constexpr int kQCap = 2048;
+  __shared__ uint16_t slowq[kQCap];
+  __shared__ int nslow;
   const sf::GammaGuide T = stage_guide(pt.guide, lds);
   Philox ph(seed);
+  const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
+  const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
+  constexpr int kPer = kGenRows / kGBlock;
   for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
     const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
-    // the block's 4 pairs per thread as independent chains (the guide's log / LDS gathers / exp
-    // are long dependent sequences; one at a time left 76% of wave cycles waiting)
-    constexpr int kPer = kGenRows / kGBlock;
+    if (threadIdx.x == 0) nslow = 0;
+    __syncthreads();
     uint64_t pr[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int p = j * kGBlock + threadIdx.x;
       pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
     }
-    double v[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; ++j)
-      v[j] = gamma_ppf_lds(lhs_sorted_quantile(ph, (uint64_t)(uint32_t)pr[j], col, (uint64_t)n), prm, pt, T);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      if (pr[j] != ~0ull) {
+      const bool valid = pr[j] != ~0ull;
+      const double q = lhs_sorted_quantile(ph, (uint64_t)(uint32_t)pr[j], col, (uint64_t)n);
+      // igami_guided's interpolation branch, operation for operation
+      bool fast = valid && cond0 && q > 0.0 && q < 1.0;
+      double v = 0.0;
+      if (fast) {
+        const double w = log(q / (1.0 - q));
+        const double u = (w - T.z0) * T.inv_h;
+        fast = u >= 0.0 && u < (double)(T.m - 1);
+        if (fast) {
+          const int jj = (int)u;
+          const double yy = sf::guide_interp(T, jj, u - (double)jj);
+          fast = yy >= -680.0 && yy <= 700.0 && T.ok[jj] != 0.0;
+          if (fast) v = exp(yy) * scale + loc;
+        }
+      }
+      if (valid) {
         const int64_t row = (int64_t)(pr[j] >> 32);
         if (idx) idx[row] = (int32_t)(uint32_t)pr[j];
-        buf[row - r0] = v[j];
+        if (fast) {
+          buf[row - r0] = v;
+        } else {
+          const int slot = atomicAdd(&nslow, 1);
+          if (slot < kQCap) slowq[slot] = (uint16_t)(j * kGBlock + threadIdx.x);
+        }
       }
+    }
+    __syncthreads();
+    const int ns = nslow;
+    const int nd = ns <= kQCap ? ns : cnt;  // queue overflow: recompute the whole block
+    for (int i = threadIdx.x; i < nd; i += kGBlock) {
+      const int p = ns <= kQCap ? slowq[i] : i;
+      const uint64_t prr = pairs[r0 + p];
+      buf[(int64_t)(prr >> 32) - r0] =
+          gamma_ppf_lds(lhs_sorted_quantile(ph, (uint64_t)(uint32_t)prr, col, (uint64_t)n), prm, pt, T);
     }
     __syncthreads();
     if (y_rs == 1) {

@@ -226,11 +226,14 @@ __global__ __launch_bounds__(kT) void k_msd1(const uint32_t* __restrict__ codes,
   const uint32_t my = cnt[t];
   const uint32_t ex = block_excl_scan256(my, lst);
   lst[t] = ex;
+  // the cursor add's round trip overlaps the first LDS scatter: its result is stored to gb only
+  // after that scatter (the barrier that follows publishes it)
+  uint32_t myb;
   if (cstart) {
     const uint32_t xc = blockIdx.x & 7u;
-    gb[t] = my ? cstart[(xc << 8) + t] + atomicAdd(&cur[((xc << 8) + t) * cpad], my) : 0u;
+    myb = my ? cstart[(xc << 8) + t] + atomicAdd(&cur[((xc << 8) + t) * cpad], my) : 0u;
   } else {
-    gb[t] = my ? start[t << 8] + atomicAdd(&cur[t * cpad], my) : 0u;
+    myb = my ? start[t << 8] + atomicAdd(&cur[t * cpad], my) : 0u;
   }
   __syncthreads();
   if constexpr (SPLIT) {
@@ -240,6 +243,7 @@ __global__ __launch_bounds__(kT) void k_msd1(const uint32_t* __restrict__ codes,
       const int p = j * kT + t;
       if (p < m) sk[lst[key[j] >> 24] + rk[j]] = key[j];
     }
+    gb[t] = myb;
     __syncthreads();
 #pragma unroll 4
     for (int j = 0; j < kIpt1; ++j) {
@@ -272,6 +276,7 @@ __global__ __launch_bounds__(kT) void k_msd1(const uint32_t* __restrict__ codes,
         sr[q] = (uint32_t)(base + p);
       }
     }
+    gb[t] = myb;
     __syncthreads();
 #pragma unroll 4
     for (int j = 0; j < kIpt1; ++j) {
@@ -331,7 +336,7 @@ __global__ __launch_bounds__(kT) void k_msd2(const uint32_t* __restrict__ kin, c
   const uint32_t ex = block_excl_scan256(my, lst);
   lst[t] = ex;
   const uint32_t b = ((uint32_t)g << 8) | (uint32_t)t;
-  gb[t] = my ? start[b] + atomicAdd(&cur[b], my) : 0u;
+  const uint32_t myb = my ? start[b] + atomicAdd(&cur[b], my) : 0u;  // stored after the first scatter
   __syncthreads();
   if constexpr (SPLIT) {
     uint32_t dst[kIpt1];
@@ -340,6 +345,7 @@ __global__ __launch_bounds__(kT) void k_msd2(const uint32_t* __restrict__ kin, c
       const int p = j * kT + t;
       if (p < m) sk[lst[(key[j] >> 16) & 255u] + rk[j]] = key[j];
     }
+    gb[t] = myb;
     __syncthreads();
 #pragma unroll 4
     for (int j = 0; j < kIpt1; ++j) {
@@ -372,6 +378,7 @@ __global__ __launch_bounds__(kT) void k_msd2(const uint32_t* __restrict__ kin, c
         sr[q] = row[j];
       }
     }
+    gb[t] = myb;
     __syncthreads();
 #pragma unroll 4
     for (int j = 0; j < kIpt1; ++j) {
@@ -976,8 +983,8 @@ __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ i
   const uint32_t my = cnt[t];
   const uint32_t ex = block_excl_scan256(my, lst);
   lst[t] = ex;
-  gb[t] = my ? (uint32_t)(((uint64_t)(g0 + t) << s_out) + atomicAdd(&cur[g0 + t], my)) : 0u;
-  __syncthreads();
+  const uint32_t myb = my ? (uint32_t)(((uint64_t)(g0 + t) << s_out) + atomicAdd(&cur[g0 + t], my)) : 0u;
+  __syncthreads();  // (myb is stored to gb after the first scatter)
   if constexpr (SPLIT) {
     // round 1: the high halves (rows) give each slot's destination; round 2: the low halves
     uint32_t dst[kIptP], hi[kIptP], slot[kIptP], lo[kIptP];
@@ -987,6 +994,7 @@ __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ i
       lo[j] = (uint32_t)v[j];
       if (j * kT + t < m) sh32[slot[j]] = (uint32_t)(v[j] >> 32);
     }
+    gb[t] = myb;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kIptP; ++j) {
@@ -1011,6 +1019,7 @@ __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ i
 #pragma unroll
     for (int j = 0; j < kIptP; ++j)
       if (j * kT + t < m) sv[lst[dg[j] - g0] + rk[j]] = v[j];
+    gb[t] = myb;
     __syncthreads();
 #pragma unroll 4
     for (int j = 0; j < kIptP; ++j) {
@@ -1250,10 +1259,11 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     int shifts[4];
     const int nl = place_levels(n, shifts);
     const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
-    // PBH_FINISH_CFG: <buckets per block><log2 bins - 10> (A/B measurements), default "22"
+    // PBH_FINISH_CFG (A/B measurements): 24 (default) = 2 buckets x 4096 bins with the cursor adds
+    // hoisted (k_finish_ah); otherwise <buckets per block><log2 bins - 10>, 23 = with prefetch
     static const int cfg = [] {
       const char* e = getenv("PBH_FINISH_CFG");
-      return e ? atoi(e) : 22;
+      return e ? atoi(e) : 24;
     }();
     uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
     const int cpad = cur_pad();
