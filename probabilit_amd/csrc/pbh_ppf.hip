@@ -205,15 +205,63 @@ PBH_DI double gamma_ppf_lds(double q, const Params& prm, const PoissonTable& pt,
   return ppf_one<PBH_DIST_GAMMA>(q, prm.val[0], prm.val[1], prm.val[2], local);
 }
 
+// igami_guided's interpolation branch and ppf_one's gamma wrapper, operation for operation:
+// true and *v = the value when the element needs no iteration; false sends it to the slow queue
+// (gamma_ppf_lds), so that the hot loops carry no igami code.
+PBH_DI bool gamma_fast(double q, const sf::GammaGuide& T, double scale, double loc, bool cond0, double* v) {
+  if (!(cond0 && q > 0.0 && q < 1.0)) return false;
+  const double w = log(q / (1.0 - q));
+  const double u = (w - T.z0) * T.inv_h;
+  if (!(u >= 0.0 && u < (double)(T.m - 1))) return false;
+  const int j = (int)u;
+  const double y = sf::guide_interp(T, j, u - (double)j);
+  if (!(y >= -680.0 && y <= 700.0 && T.ok[j] != 0.0)) return false;
+  *v = exp(y) * scale + loc;
+  return true;
+}
+
 __global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restrict__ q, int64_t q_stride, int64_t n,
                                                            Params prm, PoissonTable pt, double* __restrict__ out,
                                                            int32_t* flag) {
   __shared__ double lds[kGTable];
+  constexpr int kPer = 4, kTile = kPer * kGBlock, kQCap = 2048;
+  __shared__ uint16_t slowq[kQCap];
+  __shared__ int nslow;
   const sf::GammaGuide T = stage_guide(pt.guide, lds);
-  for (int64_t i = (int64_t)blockIdx.x * kGBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kGBlock) {
-    const double x = gamma_ppf_lds(q[i * q_stride], prm, pt, T);
-    out[i] = x;
-    flag_nonfinite(flag, !isfinite(x));
+  const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
+  const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
+  for (int64_t base = (int64_t)blockIdx.x * kTile; base < n; base += (int64_t)gridDim.x * kTile) {
+    if (threadIdx.x == 0) nslow = 0;
+    __syncthreads();
+    double qv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = base + j * kGBlock + threadIdx.x;
+      qv[j] = i < n ? q[i * q_stride] : 0.5;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = base + j * kGBlock + threadIdx.x;
+      if (i >= n) continue;
+      double v;
+      if (gamma_fast(qv[j], T, scale, loc, cond0, &v)) {
+        out[i] = v;
+        flag_nonfinite(flag, !isfinite(v));
+      } else {
+        const int slot = atomicAdd(&nslow, 1);
+        if (slot < kQCap) slowq[slot] = (uint16_t)(j * kGBlock + threadIdx.x);
+      }
+    }
+    __syncthreads();
+    const int ns = nslow;
+    const int nd = ns <= kQCap ? ns : kTile;  // queue overflow: the whole tile again
+    for (int t = threadIdx.x; t < nd; t += kGBlock) {
+      const int64_t i = base + (ns <= kQCap ? slowq[t] : t);
+      if (i >= n) continue;
+      const double x = gamma_ppf_lds(q[i * q_stride], prm, pt, T);
+      out[i] = x;
+      flag_nonfinite(flag, !isfinite(x));
+    }
   }
 }
 
