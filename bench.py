@@ -62,7 +62,8 @@ PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k
              "k_code_runs": ["k_code_buckets", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
              "k_apply": ["k_apply_mfma", "k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"],
              "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"],
-             "k_finish": ["k_finish_fused<2, 4096>", "k_finish_fused<1, 4096>", "k_finish_fused<2, 2048>",
+             "k_finish": ["k_finish_ah<4096>", "k_finish_fused<2, 4096>", "k_finish_fused<2, 4096, false>",
+                          "k_finish_fused<2, 4096, true>", "k_finish_fused<1, 4096>", "k_finish_fused<2, 2048>",
                           "k_finish_fused<1, 2048>", "k_finish_fused<4, 2048>", "k_finish_fused<4, 4096>", "k_finish"],
              "k_msd1": ["k_msd1<true>", "k_msd1<false>", "k_msd1"], "k_msd2": ["k_msd2<true>", "k_msd2<false>", "k_msd2"],
              "k_place_msd": ["k_place_msd<true>", "k_place_msd<false>", "k_place_msd"],
@@ -194,9 +195,10 @@ def main():
                 "avg_launch_ms": dk["avg_ms"], "bytes_per_launch": dk["bytes_per_launch"]}
 
     # whole-step roofline: SURVEY.md §8(d)'s 96 algorithmic bytes per draw over the step time
-    pipeline = {"bytes_per_draw": 96, "achieved": round(96 * n * d * world / (ms_per_step / 1e3) / 1e9, 1),
-                "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                "frac": round(96 * n * d * world / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+    # (the N-row job is row-sharded over `world` GPUs: n * d draws in all, against world x the peak)
+    pipeline = {"bytes_per_draw": 96, "achieved": round(96 * n * d / (ms_per_step / 1e3) / 1e9, 1),
+                "unit": "GB/s", "peak": HBM_PEAK_GBS * world,
+                "frac": round(96 * n * d / (ms_per_step / 1e3) / 1e9 / (HBM_PEAK_GBS * world), 4),
                 "kernel_time_ms_per_step": round(sum(k["total_ms_per_step"] for k in kernels.values()), 3)}
     copy_peak = hbm_copy_peak(lib) if rank == 0 else None
     if copy_peak:

@@ -26,6 +26,15 @@ def main():
 
     from oracle.pipeline import lhs_ic
 
+    import threading
+
+    def heartbeat():  # a long CPU run must keep writing (the GPU box's watchdog kills silent runs)
+        t0 = time.perf_counter()
+        while True:
+            time.sleep(30)
+            print(f"... {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     out = []
     for n in a.rows:
         t0 = time.perf_counter()
