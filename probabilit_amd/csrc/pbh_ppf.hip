@@ -6,6 +6,8 @@
 // are HBM-bound, gamma (igami) and per-element poisson searches are FP64-VALU-bound.
 #include <math.h>
 
+#include <type_traits>
+
 #include "pbh_error.h"
 #include "pbh_ppf_core.h"
 #include "pbh_ppf_ext.h"
@@ -458,7 +460,13 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
   if (state && *state) return;
   constexpr bool kCompact = D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM;
   __shared__ double buf[kGenRows];
-  __shared__ TailQueue tq;
+  // the tail queue only where ndtri is evaluated (20 KiB of LDS the others would hold for nothing)
+  struct NoQueue {
+    double arg[1];
+    uint16_t pos[1];
+    int count;
+  };
+  __shared__ std::conditional_t<kCompact, TailQueue, NoQueue> tq[1];
   Philox ph(seed);
   const double p0 = prm.val[0], p1 = prm.val[1], p2 = prm.val[2];
   for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
@@ -466,7 +474,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
     const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
     for (int h = 0; h < kGenRows; h += kCTile) {
       if (kCompact) {
-        if (threadIdx.x == 0) tq.count = 0;
+        if (threadIdx.x == 0) tq[0].count = 0;
         __syncthreads();
       }
 #pragma unroll
@@ -486,15 +494,15 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
         if constexpr (kCompact) {
           const bool tail = valid && sf::ndtri_takes_tail(q);
           if (valid && !tail) buf[off] = ppf_one<D, 1>(q, p0, p1, p2, pt);
-          tail_push(tq, tail, q, off);
+          tail_push(tq[0], tail, q, off);
         } else {
           if (valid) buf[off] = ppf_one<D>(q, p0, p1, p2, pt);
         }
       }
       if (kCompact) {
         __syncthreads();
-        const int T = tq.count;
-        for (int i = threadIdx.x; i < T; i += kBlock) buf[tq.pos[i]] = ppf_one<D, 2>(tq.arg[i], p0, p1, p2, pt);
+        const int T = tq[0].count;
+        for (int i = threadIdx.x; i < T; i += kBlock) buf[tq[0].pos[i]] = ppf_one<D, 2>(tq[0].arg[i], p0, p1, p2, pt);
       }
     }
     __syncthreads();

@@ -89,6 +89,7 @@ struct FeistelPerm {
   uint64_t n;
   uint32_t A, B;
   double inv_b;
+  bool small;  // A B < 2^32: split / join in 32 bits
   uint32_t rk[kRounds];
 
   PBH_HD FeistelPerm(const Philox& ph, uint64_t n_, uint32_t col) : n(n_) {
@@ -100,6 +101,7 @@ struct FeistelPerm {
     B = (uint32_t)((n_ + A - 1) / A);
     if (B == 0) B = 1;
     inv_b = 1.0 / (double)B;
+    small = (uint64_t)A * B + B <= 0xFFFFFFFFull && A < (1u << 24) && B < (1u << 24);  // q B (q off by one) fits too
     uint32_t c[4] = {col, 0u, 0u, kPurposeFeistel};
     ph(c);
     for (int i = 0; i < kRounds; ++i) rk[i] = c[i];
@@ -108,14 +110,40 @@ struct FeistelPerm {
   PBH_HD static inline uint32_t reduce(uint32_t h, uint32_t m) { return (uint32_t)(((uint64_t)h * m) >> 32); }
   PBH_HD inline uint32_t F(uint32_t v, uint32_t k) const { return mix32(v ^ k); }
 
+  PBH_HD static inline uint32_t mul24(uint32_t a, uint32_t b) {  // a, b < 2^24, a b < 2^32
+#ifdef __HIP_DEVICE_COMPILE__
+    return __umul24(a, b);  // v_mul_u32_u24: full rate (a 32-bit multiply is quarter rate)
+#else
+    return a * b;
+#endif
+  }
+
   PBH_HD inline void split(uint64_t x, uint32_t& L, uint32_t& R) const {
     // x < 2^32 and the product's relative error is ~1e-16, so q is off by at most one:
     // one branch-free correction each way (keeps independent evaluations interleavable)
+    if (small) {  // A B < 2^32 (every n < 2^32 but the last ~2^16): 32-bit, 24-bit multiplies
+      const uint32_t x32 = (uint32_t)x;
+      uint32_t q = (uint32_t)((double)x32 * inv_b);
+      uint32_t qb = mul24(q, B);
+      const bool lo = qb > x32;
+      q -= lo ? 1u : 0u;
+      qb -= lo ? B : 0u;
+      const bool hi = x32 - qb >= B;
+      q += hi ? 1u : 0u;
+      qb += hi ? B : 0u;
+      L = q;
+      R = x32 - qb;
+      return;
+    }
     uint64_t q = (uint64_t)((double)x * inv_b);
     q -= (q * B > x) ? 1 : 0;
     q += (x - q * B >= B) ? 1 : 0;
     L = (uint32_t)q;
     R = (uint32_t)(x - q * B);
+  }
+
+  PBH_HD inline uint64_t join(uint32_t L, uint32_t R) const {
+    return small ? (uint64_t)(mul24(L, B) + R) : (uint64_t)L * B + R;
   }
 
   PBH_HD inline uint64_t round_trip(uint64_t x) const {
@@ -131,7 +159,7 @@ struct FeistelPerm {
         L = L + h >= A ? L + h - A : L + h;
       }
     }
-    return (uint64_t)L * B + R;
+    return join(L, R);
   }
 
   PBH_HD inline uint64_t round_trip_inv(uint64_t y) const {
@@ -147,7 +175,7 @@ struct FeistelPerm {
         L = L >= h ? L - h : L + A - h;
       }
     }
-    return (uint64_t)L * B + R;
+    return join(L, R);
   }
 
   // Bijection of [0, n) by cycle walking.

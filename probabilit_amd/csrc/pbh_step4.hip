@@ -1259,11 +1259,12 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     int shifts[4];
     const int nl = place_levels(n, shifts);
     const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
-    // PBH_FINISH_CFG (A/B measurements): 24 (default) = 2 buckets x 4096 bins with the cursor adds
-    // hoisted (k_finish_ah); otherwise <buckets per block><log2 bins - 10>, 23 = with prefetch
+    // PBH_FINISH_CFG (A/B measurements): 25 (default) / 24 / 26 = k_finish_ah (2 buckets per block,
+    // cursor adds hoisted) with 2048 / 4096 / 1024 bins; otherwise k_finish_fused with
+    // <buckets per block><log2 bins - 10>, 23 = with prefetch
     static const int cfg = [] {
       const char* e = getenv("PBH_FINISH_CFG");
-      return e ? atoi(e) : 24;
+      return e ? atoi(e) : 25;
     }();
     uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
     const int cpad = cur_pad();
@@ -1281,6 +1282,24 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
       case 12: PBH_FIN(1, 4096); break;
       case 21: PBH_FIN(2, 2048); break;
       case 23: PBH_FIN2(2, 4096); break;
+      case 26:
+        if (!segcap) {
+          PBH_TIMED(kKFinish, s,
+                    hipLaunchKernelGGL((k_finish_ah<1024>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
+                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
+          break;
+        }
+        PBH_FIN(2, 4096);
+        break;
+      case 25:
+        if (!segcap) {
+          PBH_TIMED(kKFinish, s,
+                    hipLaunchKernelGGL((k_finish_ah<2048>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
+                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
+          break;
+        }
+        PBH_FIN(2, 4096);
+        break;
       case 24:
         if (!segcap) {
           PBH_TIMED(kKFinish, s,
