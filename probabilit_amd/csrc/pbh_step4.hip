@@ -1259,12 +1259,12 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     int shifts[4];
     const int nl = place_levels(n, shifts);
     const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
-    // PBH_FINISH_CFG (A/B measurements): 25 (default) / 24 / 26 = k_finish_ah (2 buckets per block,
-    // cursor adds hoisted) with 2048 / 4096 / 1024 bins; otherwise k_finish_fused with
+    // PBH_FINISH_CFG (A/B measurements): 26 (default) / 25 / 24 = k_finish_ah (2 buckets per block,
+    // cursor adds hoisted) with 1024 / 2048 / 4096 bins; otherwise k_finish_fused with
     // <buckets per block><log2 bins - 10>, 23 = with prefetch
     static const int cfg = [] {
       const char* e = getenv("PBH_FINISH_CFG");
-      return e ? atoi(e) : 25;
+      return e ? atoi(e) : 26;
     }();
     uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
     const int cpad = cur_pad();
