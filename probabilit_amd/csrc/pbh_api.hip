@@ -183,22 +183,24 @@ constexpr int kRedo = 1000;  // internal: a deferred tie / inversion check faile
 // before them, their scores computed as untied; the counts are checked before step 4 and, if any
 // is non-zero, the whole call is redone with them first (kRedo).  The VALU-bound counting
 // overlaps the bandwidth-bound Gram and step 3.
-int ic_run(const pbh_ic_args* a, void* stream, bool defer);
+int ic_run(const pbh_ic_args* a, void* stream, int defer);
 }  // namespace
 
 extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   PBH_REQUIRE(a != nullptr, "pbh_iman_conover: args must not be NULL");
-  static const bool defer = [] {
+  // PBH_DEFER_COUNTS: 0 = counts first; 1 = next to steps 1-3, checked before step 4;
+  // 2 = next to step 4 (latency-bound passes: room for VALU work), checked at the end
+  static const int defer = [] {
     const char* e = getenv("PBH_DEFER_COUNTS");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : 1;
   }();
   int st = ic_run(a, stream, defer);
-  if (st == kRedo) st = ic_run(a, stream, false);
+  if (st == kRedo) st = ic_run(a, stream, 0);
   return st;
 }
 
 namespace {
-int ic_run(const pbh_ic_args* a, void* stream, bool defer) {
+int ic_run(const pbh_ic_args* a, void* stream, int defer) {
   const int64_t n = a->n;
   const int k = a->k;
   PBH_REQUIRE((a->X || a->columns) && a->Y && a->ws && a->target_chol_host,
@@ -346,8 +348,33 @@ int ic_run(const pbh_ic_args* a, void* stream, bool defer) {
     }
   } ev_scores, ev_counts;
   ev_counts.wait_on = s;
-  hipStream_t side = any_deferred ? step4_side_stream(0) : nullptr;
-  if (any_deferred && side) {
+  hipStream_t side = any_deferred ? step4_side_stream(defer == 2 ? kStep4MaxStreams - 1 : 0) : nullptr;
+  auto launch_counts = [&]() -> int {  // the deferred columns' counts on `side`, after s's work so far
+    sync_on_exit.side = true;
+    PBH_CHECK_HIP(hipEventCreateWithFlags(&ev_scores.e, hipEventDisableTiming));
+    PBH_CHECK_HIP(hipEventCreateWithFlags(&ev_counts.e, hipEventDisableTiming));
+    PBH_CHECK_HIP(hipEventRecord(ev_scores.e, s));
+    PBH_CHECK_HIP(hipStreamWaitEvent(side, ev_scores.e, 0));
+    for (int c = 0; c < k; ++c) {
+      if (!deferred[c]) continue;
+      int r = gen_sorted(gens.g[c], 0, n, nullptr, a->columns[c].nonfinite_flag, L.counts + 2 * c, side);
+      if (r) return r;
+    }
+    PBH_CHECK_HIP(hipEventRecord(ev_counts.e, side));
+    return PBH_OK;
+  };
+  auto check_counts = [&]() -> int {  // PBH_OK, or kRedo when a deferred column ties / inverts
+    if (ev_counts.e) PBH_CHECK_HIP(hipStreamWaitEvent(s, ev_counts.e, 0));
+    std::vector<unsigned long long> dc(2 * (size_t)k, 0);
+    PBH_CHECK_HIP(hipMemcpyAsync(dc.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+    for (int c = 0; c < k; ++c)
+      if (deferred[c] && (dc[2 * c] | dc[2 * c + 1])) return kRedo;
+    return PBH_OK;
+  };
+  if (any_deferred && side && defer == 2) {
+    // launched after step 3 (below)
+  } else if (any_deferred && side) {
     sync_on_exit.side = true;
     PBH_CHECK_HIP(hipEventCreateWithFlags(&ev_scores.e, hipEventDisableTiming));
     PBH_CHECK_HIP(hipEventCreateWithFlags(&ev_counts.e, hipEventDisableTiming));
@@ -400,13 +427,12 @@ int ic_run(const pbh_ic_args* a, void* stream, bool defer) {
     PBH_CHECK_HIP(hipMemcpyAsync(a->cscores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
 
   // the deferred counts: any tie or inversion means the scores assumed untied were wrong
-  if (any_deferred) {
-    if (ev_counts.e) PBH_CHECK_HIP(hipStreamWaitEvent(s, ev_counts.e, 0));
-    std::vector<unsigned long long> dc(2 * (size_t)k, 0);
-    PBH_CHECK_HIP(hipMemcpyAsync(dc.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
-    PBH_CHECK_HIP(hipStreamSynchronize(s));
-    for (int c = 0; c < k; ++c)
-      if (deferred[c] && (dc[2 * c] | dc[2 * c + 1])) return kRedo;
+  if (any_deferred && side && defer == 2) {
+    st = launch_counts();  // next to step 4; checked at the end
+    if (st) return st;
+  } else if (any_deferred) {
+    st = check_counts();
+    if (st) return st;
   }
 
   // ---- step 4: Y[:, c] = sort(X[:, c])[rankdata(CS[:, c]).astype(int) - 1]
@@ -425,7 +451,7 @@ int ic_run(const pbh_ic_args* a, void* stream, bool defer) {
     Step4Shared sh;
     step4_gen_carve_shared(L.s4shared, k, sh);
     const int ns = step4_streams();
-    sync_on_exit.side = ns > 1;
+    sync_on_exit.side = sync_on_exit.side || ns > 1;
     Step4Column cbs[kStep4MaxStreams];
     hipStream_t ss[kStep4MaxStreams];
     for (int i = 0; i < ns; ++i) {
@@ -491,6 +517,10 @@ int ic_run(const pbh_ic_args* a, void* stream, bool defer) {
                           a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n, hc,
                           flat);
     }
+    if (st) return st;
+  }
+  if (any_deferred && side && defer == 2) {
+    st = check_counts();
     if (st) return st;
   }
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // host vectors above were sources of async copies

@@ -1148,7 +1148,7 @@ hipStream_t step4_side_stream(int i) {
 }
 
 void step4_sync_side_streams() {
-  for (int i = 0; i < step4_streams(); ++i) {
+  for (int i = 0; i < kStep4MaxStreams; ++i) {  // every one (the deferred counts may use the last)
     hipStream_t x = step4_side_stream(i);
     if (x) (void)hipStreamSynchronize(x);
   }
