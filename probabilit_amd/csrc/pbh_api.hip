@@ -189,7 +189,8 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer);
 extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   PBH_REQUIRE(a != nullptr, "pbh_iman_conover: args must not be NULL");
   // PBH_DEFER_COUNTS: 0 = counts first; 1 = next to steps 1-3, checked before step 4;
-  // 2 = next to step 4 (latency-bound passes: room for VALU work), checked at the end
+  // 2 = next to step 4 (latency-bound passes: room for VALU work), checked at the end;
+  // 3 = next to steps 1-3 (as 1), checked at the end: step 4 does not wait for them
   static const int defer = [] {
     const char* e = getenv("PBH_DEFER_COUNTS");
     return e ? atoi(e) : 1;
@@ -430,7 +431,7 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
   if (any_deferred && side && defer == 2) {
     st = launch_counts();  // next to step 4; checked at the end
     if (st) return st;
-  } else if (any_deferred) {
+  } else if (any_deferred && !(side && defer == 3)) {
     st = check_counts();
     if (st) return st;
   }
@@ -519,7 +520,7 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     }
     if (st) return st;
   }
-  if (any_deferred && side && defer == 2) {
+  if (any_deferred && side && defer >= 2) {
     st = check_counts();
     if (st) return st;
   }
