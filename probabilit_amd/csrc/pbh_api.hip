@@ -193,7 +193,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
   // 3 = next to steps 1-3 (as 1), checked at the end: step 4 does not wait for them
   static const int defer = [] {
     const char* e = getenv("PBH_DEFER_COUNTS");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 3;
   }();
   int st = ic_run(a, stream, defer);
   if (st == kRedo) st = ic_run(a, stream, 0);
