@@ -100,6 +100,24 @@ def pmc_traffic(kernel):
     return int(per), os.path.relpath(files[-1], ROOT)
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` started without torch.distributed.run: start N rank processes under it
+    as children (before this process touches the GPU: no exec) and exit with their status."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -112,20 +130,31 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (D2H included) side measurement")
     ap.add_argument("--ppf-rows", type=int, default=100_000_000, help="rows of the ppf-sweep side measurement (0: skip)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--check-out", default=None,
+                    help="write each rank's per-column SHA-1 of its rows of Y (JSON) into this directory")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     import numpy as np
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    backend = None
     if world > 1:
         import torch.distributed as dist
 
-        # modulo: PBH_DIST_BACKEND=gloo rehearses several ranks on a one-GPU box
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
-        # RCCL; PBH_DIST_BACKEND=gloo rehearses the sharded path with several ranks on one GPU
-        dist.init_process_group(os.environ.get("PBH_DIST_BACKEND", "nccl"))
+        ndev = torch.cuda.device_count()  # counts devices without initialising the GPU
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        # one GPU per rank over RCCL; fewer GPUs than ranks (a one-GPU box) rehearses the same
+        # sharded path over gloo with the ranks sharing the device (PBH_DIST_BACKEND overrides)
+        backend = os.environ.get("PBH_DIST_BACKEND", "nccl" if ndev >= local_world else "gloo")
+        torch.cuda.set_device(local % ndev)
+        dist.init_process_group(backend)
     else:
         dist = None
 
@@ -145,7 +174,7 @@ def main():
     group = dist.group.WORLD if dist is not None else None
 
     def step(i):
-        root.sample_device(n, random_state=args.seed + i, method="lhs", group=group)
+        return root.sample_device(n, random_state=args.seed + i, method="lhs", group=group)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -165,6 +194,14 @@ def main():
     t1 = time.perf_counter()
     lib.pbh_timing_enable(0)
     elapsed = t1 - t0
+    if args.check_out:  # the last timed step's rows of every column (tests compare with one GPU)
+        import hashlib
+
+        os.makedirs(args.check_out, exist_ok=True)
+        digests = [hashlib.sha1(x.samples_device.cpu().numpy().tobytes()).hexdigest() for x in ds]
+        with open(os.path.join(args.check_out, f"rank{rank}.json"), "w") as f:
+            json.dump({"rank": rank, "world": world, "rows": n, "seed": args.seed + args.warmup + args.steps - 1,
+                       "sha1": digests}, f)
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -206,7 +243,7 @@ def main():
         roofline["frac_of_measured_copy"] = round(achieved / copy_peak["GBps"], 4)
     e2e = end_to_end(step, ds, n, d, args.warmup + args.steps, barrier) if (world == 1 and not args.no_e2e) else None
 
-    sweep = ppf_sweep(lib, base, args.ppf_rows, args.seed) if args.ppf_rows > 0 else None
+    sweep = ppf_sweep(lib, base, args.ppf_rows, args.seed) if (args.ppf_rows > 0 and rank == 0) else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -222,8 +259,9 @@ def main():
                 "config": {"workload": ("cfg4: " if world > 1 else "cfg3: ") +
                                        "d=32 (cfg2 set x4), LHS + ppf + ImanConover, N rows",
                            "rows": n, "d": d,
-                           "parallelism": f"row-sharded x{world} (RCCL all-reduce + all-to-all)" if world > 1
-                           else "single"},
+                           "parallelism": (f"row-sharded x{world} ({backend}: all-reduce + all-to-all of scores "
+                                           "out, positions back)") if world > 1 else "single",
+                           "devices": torch.cuda.device_count() if world > 1 else 1},
                 "roofline": roofline, "pipeline_roofline": pipeline, "hbm_copy_peak": copy_peak,
                 "end_to_end": e2e, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels}
         print(json.dumps(line))

@@ -215,6 +215,18 @@ int pbh_iman_conover(const pbh_ic_args* args, void* stream);
 int pbh_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist,
                        const double* params_host, int nparams, double* out, int32_t* nonfinite_flag,
                        void* stream);
+/* The same segment [t0, t0 + nt) counted, not stored (asynchronous; the step-1 check of a
+ * shard before its scores, correlation.py:394): counts_dev (2 device u64, zeroed first) +=
+ * (#(x[t] == x[t+1]), #!(x[t] <= x[t+1])) over the pairs inside the segment.  heads (optional,
+ * device u32, hcap entries): the run heads -- every t in (t0, t0 + nt) whose value differs from
+ * stratum t - 1's, plus t0 itself when t0 == 0 -- unordered, at most hcap written; *hcur_dev
+ * (device u32) counts them all.  A shard starting at row0 > 0 passes t0 = row0 - 1, so that the
+ * pair across the shard boundary is counted exactly once. */
+int pbh_lhs_sorted_counts(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist,
+                          const double* params_host, int nparams, unsigned long long* counts_dev, uint32_t* heads,
+                          uint32_t* hcur_dev, uint32_t hcap, int32_t* nonfinite_flag, void* stream);
+/* heads[0 .. nh) in increasing order, nh <= 16384 (the run heads pbh_lhs_sorted_counts appends). */
+int pbh_sort_heads(uint32_t* heads, int64_t nh, void* stream);
 /* Adjacent-pair check of a column: *ties = #(x[t] == x[t+1]), *inversions = #!(x[t] <= x[t+1]).
  * ws: 256 bytes of device memory.  Synchronises the stream. */
 int pbh_sorted_check(const double* x, int64_t n, int64_t* ties, int64_t* inversions, void* ws, void* stream);
@@ -250,6 +262,46 @@ int pbh_ic_apply(double* S, int64_t n, int32_t k, int64_t ld, const double* L_ho
 int pbh_ic_reorder_workspace_size(int64_t n, size_t* bytes);
 int pbh_ic_reorder(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx_out,
                    void* ws, size_t ws_bytes, void* stream);
+
+/* Step 4 of the columns a rank owns in a row-sharded run (correlation.py:418-423 for the column
+ * owner): m generated columns (as pbh_iman_conover's `columns`) of an
+ * n-row design whose correlated scores arrive whole, one column at a time.
+ *   pbh_ic_owned_create   gen tables + workspace carve (stream-ordered on `stream`)
+ *   pbh_ic_owned_column   column i: y[r * y_rs] = sort(X[:, i])[rank(cs[r]) - 1] by the single-GPU
+ *                         step-4 passes (codes, top-16 histogram with the adaptive code map, MSD
+ *                         code passes, bucket finish, row placement, sort(X)[p] regenerated), on a
+ *                         step-4 side stream that first waits for ready_event (a pbh event; NULL:
+ *                         `stream`'s work so far); done_event (optional) is recorded when y is
+ *                         complete.  With p_out (device u32, n) the sorted positions p[r] =
+ *                         rank(cs[r]) - 1 are written instead of y (y may be NULL): 4 bytes a row
+ *                         to send back, the row owners regenerate Y with pbh_lhs_values_at.  No
+ *                         host synchronisation.  cs, y / p_out must stay valid until
+ *                         pbh_ic_owned_finish returns.
+ *   pbh_ic_owned_finish   the caller's stream joins the lanes; one readback of every column's
+ *                         verdict; a column the fast passes rejected (spiky codes, runs of equal
+ *                         codes beyond the finish) is redone by the general path, redone_host[i]
+ *                         = 1 for it (its y changed after done_event).  Synchronises `stream`.
+ *   pbh_ic_owned_destroy  frees the tables (after the lanes).
+ * Calls on one device are not concurrent (one host thread per device). */
+typedef struct pbh_ic_owned pbh_ic_owned;
+int pbh_ic_owned_workspace_size(int64_t n, int32_t m, size_t* bytes);
+int pbh_ic_owned_create(const pbh_ic_column* columns, int32_t m, int64_t n, void* ws, size_t ws_bytes,
+                        pbh_ic_owned** out, void* stream);
+int pbh_ic_owned_column(pbh_ic_owned* h, int32_t i, const double* cs, double* y, int64_t y_rs, uint32_t* p_out,
+                        void* ready_event, void* done_event, void* stream);
+int pbh_ic_owned_finish(pbh_ic_owned* h, int32_t* redone_host, void* stream);
+int pbh_ic_owned_destroy(pbh_ic_owned* h, void* stream);
+/* y[i * y_rs] = sort(X[:, column])[p[i]] for i < m: a generated column's value at sorted
+ * positions p (the row owner's half of a row-sharded step 4: Y[r] = sort(X)[rank - 1],
+ * correlation.py:423, p from the column's owner). */
+int pbh_lhs_values_at(const pbh_ic_column* column, int64_t n, const uint32_t* p, int64_t m, double* y, int64_t y_rs,
+                      void* stream);
+/* HIP events for ordering the caller's streams (torch / RCCL) with the library's lanes. */
+int pbh_event_create(void** event);
+int pbh_event_destroy(void* event);
+int pbh_event_record(void* event, void* stream);
+int pbh_stream_wait_event(void* stream, void* event);
+int pbh_event_synchronize(void* event);
 
 /* rankdata(x, method='average') of one device column (scipy:stats/_stats_py.py _rankdata,
  * called at correlation.py:394 and :422).  ws >= pbh_rank_workspace_size(n). */

@@ -176,6 +176,61 @@ extern "C" int pbh_rankdata_average(const double* x, int64_t stride, int64_t n, 
 }
 
 namespace {
+int launch_wait(hipEvent_t e, hipStream_t s) {
+  if (e) PBH_CHECK_HIP(hipStreamWaitEvent(s, e, 0));
+  return PBH_OK;
+}
+
+// Step 4's lanes: the side streams, each with one column's staging (and, for the owned columns
+// of a row-sharded run, one column of codes); columns are dealt round robin.  begin(): every
+// lane continues after the caller's stream so far; join(to): `to` continues after every lane.
+// Events only, no host synchronisation.
+struct Step4Lanes {
+  int ns = 1;
+  int rr = 0;
+  hipStream_t s;
+  hipStream_t ss[kStep4MaxStreams];
+  Step4Column cb[kStep4MaxStreams];
+  uint32_t* codes[kStep4MaxStreams];
+  std::vector<hipEvent_t> events;
+  Step4Lanes(int64_t n, void* column_ws, void* codes_ws, hipStream_t s_) : s(s_) {
+    ns = step4_streams();
+    for (int i = 0; i < ns; ++i) {
+      step4_gen_carve_column((char*)column_ws + (size_t)i * step4_gen_column_bytes(n), n, cb[i]);
+      codes[i] = codes_ws ? (uint32_t*)((char*)codes_ws + (size_t)i * align256((size_t)n * 4)) : nullptr;
+      ss[i] = ns > 1 ? step4_side_stream(i) : s;
+      if (!ss[i]) ss[i] = s;
+    }
+  }
+  ~Step4Lanes() {
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+  }
+  int order(hipStream_t from, hipStream_t to) {  // `to` continues after `from`'s work so far
+    if (from == to) return PBH_OK;
+    hipEvent_t e = nullptr;
+    PBH_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    events.push_back(e);
+    PBH_CHECK_HIP(hipEventRecord(e, from));
+    PBH_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
+    return PBH_OK;
+  }
+  int begin() {
+    for (int i = 0; i < ns; ++i) {
+      int st = order(s, ss[i]);
+      if (st) return st;
+    }
+    return PBH_OK;
+  }
+  int next() { return rr++ % ns; }
+  int join(hipStream_t to = nullptr) {
+    for (int i = 0; i < ns; ++i) {
+      int st = order(ss[i], to ? to : s);
+      if (st) return st;
+    }
+    return PBH_OK;
+  }
+};
+
 constexpr int kRedo = 1000;  // internal: a deferred tie / inversion check failed, run again undeferred
 
 // defer: the tie / inversion counts of the generated continuous columns (which tie or invert with
@@ -223,6 +278,16 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
   std::vector<int32_t> state(k), flags(k);
   std::vector<uint32_t> hists_host;
   int32_t flag_host = 0;
+  // the generated columns' inverse-CDF setups (tables built once, for step 1 and step 4);
+  // declared before the guard below, so that on every return the tables are freed (stream
+  // ordered, on s) only after the guard has synchronised the side streams that read them
+  struct Gens {
+    std::vector<GenColumn*> g;
+    hipStream_t s;
+    ~Gens() {
+      for (GenColumn* x : g) gen_destroy(x, s);
+    }
+  } gens{std::vector<GenColumn*>(a->columns ? k : 0, nullptr), s};
   struct SyncOnExit {
     hipStream_t s;
     bool side = false;
@@ -245,14 +310,6 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
   // but without storing it (step 4 regenerates sort(X)[p]; the fallbacks materialise it on
   // demand), then one readback for all of them (instead of a stream sync per column).
   std::vector<char> have_sx(k, 0);  // sorted_x column c holds sort(X[:, c])
-  // the generated columns' inverse-CDF setups (tables built once, for step 1 and step 4)
-  struct Gens {
-    std::vector<GenColumn*> g;
-    hipStream_t s;
-    ~Gens() {
-      for (GenColumn* x : g) gen_destroy(x, s);
-    }
-  } gens{std::vector<GenColumn*>(a->columns ? k : 0, nullptr), s};
   auto materialise = [&](int c) -> int {  // sort(X[:, c]) into the workspace, once
     if (have_sx[c] || !a->columns || !gens.g[c]) return PBH_OK;
     int r = gen_sorted(gens.g[c], 0, n, L.sorted_x + (int64_t)c * n, nullptr, nullptr, s);
@@ -349,7 +406,9 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     }
   } ev_scores, ev_counts;
   ev_counts.wait_on = s;
-  hipStream_t side = any_deferred ? step4_side_stream(defer == 2 ? kStep4MaxStreams - 1 : 0) : nullptr;
+  // the last side stream: step 4's lanes use streams 0 .. step4_streams() - 1 (3 by default), so
+  // the counts never queue ahead of a step-4 column
+  hipStream_t side = any_deferred ? step4_side_stream(kStep4MaxStreams - 1) : nullptr;
   auto launch_counts = [&]() -> int {  // the deferred columns' counts on `side`, after s's work so far
     sync_on_exit.side = true;
     PBH_CHECK_HIP(hipEventCreateWithFlags(&ev_scores.e, hipEventDisableTiming));
@@ -447,45 +506,49 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
   for (int c = 0; c < k; ++c) any_regen |= regenerable[c] != 0;
   if (a->columns && any_regen && step4_gen_enabled(n)) {
     // generated columns: MSD code passes + bucket finish + row placement, sort(X)[p]
-    // regenerated (pbh_step4.hip); one readback for all columns' flatness before, one for
-    // over-long runs after
+    // regenerated (pbh_step4.hip), on the side-stream lanes without a host round trip; a column
+    // whose codes stay spiky after the adaptive code map, or that meets a run of equal codes
+    // beyond the finish, is skipped on the device and redone by the general path after one
+    // readback of every column's verdict at the end
     Step4Shared sh;
     step4_gen_carve_shared(L.s4shared, k, sh);
-    const int ns = step4_streams();
-    sync_on_exit.side = sync_on_exit.side || ns > 1;
-    Step4Column cbs[kStep4MaxStreams];
-    hipStream_t ss[kStep4MaxStreams];
-    for (int i = 0; i < ns; ++i) {
-      step4_gen_carve_column((char*)L.s4column + (size_t)i * step4_gen_column_bytes(n), n, cbs[i]);
-      ss[i] = ns > 1 ? step4_side_stream(i) : s;
-      if (!ss[i]) ss[i] = s;
-    }
-    st = step4_gen_hist(L.codes, n, n, sh, s);
+    Step4Lanes lanes(n, L.s4column, nullptr, s);
+    sync_on_exit.side = sync_on_exit.side || lanes.ns > 1;
+    st = step4_gen_hist(L.codes, n, L.S, n, n, sh, 0, k, s);
     if (st) return st;
-    PBH_CHECK_HIP(hipMemcpyAsync(state.data(), sh.state, (size_t)k * 4, hipMemcpyDeviceToHost, s));
-    PBH_CHECK_HIP(hipStreamSynchronize(s));  // everything before is complete: the side streams may start
-    int next = 0;
+    st = lanes.begin();
+    if (st) return st;
     for (int c = 0; c < k; ++c) {
-      if (state[c] != 0 || !regenerable[c]) continue;
-      const int i = next++ % ns;
-      hipStream_t cs_ = ss[i];
-      st = step4_gen_column(c, L.codes + (int64_t)c * n, L.S + (int64_t)c * n, n, sh, cbs[i], cs_);
+      if (!regenerable[c]) continue;
+      const int i = lanes.next();
+      hipStream_t cs_ = lanes.ss[i];
+      st = step4_gen_column(c, L.codes + (int64_t)c * n, L.S + (int64_t)c * n, n, sh, lanes.cb[i], cs_);
       if (st) return st;
       int buf = 0;
-      st = step4_gen_place_passes(c, n, sh, cbs[i], cs_, &buf);
+      st = step4_gen_place_passes(c, n, sh, lanes.cb[i], cs_, &buf);
       if (st) return st;
-      st = gen_place(gens.g[c], cbs[i].pairs[buf], n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
+      st = gen_place(gens.g[c], lanes.cb[i].pairs[buf], n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
                      a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, sh.flags + c, cs_);
       if (st) return st;
     }
-    for (int i = 0; i < ns; ++i) {  // the caller's stream continues after every side stream
-      if (ss[i] == s) continue;
-      PBH_CHECK_HIP(hipStreamSynchronize(ss[i]));
+    st = lanes.join();  // the caller's stream continues after every lane
+    if (st) return st;
+    // one readback: every column's state and flags (contiguous), and the deferred counts
+    std::vector<int32_t> verdict(2 * (size_t)k);
+    std::vector<unsigned long long> dc(2 * (size_t)k, 0);
+    const bool late_counts = any_deferred && side && defer >= 2;
+    if (late_counts) {
+      st = launch_wait(ev_counts.e, s);
+      if (st) return st;
+      PBH_CHECK_HIP(hipMemcpyAsync(dc.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
     }
-    PBH_CHECK_HIP(hipMemcpyAsync(flags.data(), sh.flags, (size_t)k * 4, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipMemcpyAsync(verdict.data(), sh.state, 8 * (size_t)k, hipMemcpyDeviceToHost, s));
     PBH_CHECK_HIP(hipStreamSynchronize(s));
+    if (late_counts)
+      for (int c = 0; c < k; ++c)
+        if (deferred[c] && (dc[2 * c] | dc[2 * c + 1])) return kRedo;
     for (int c = 0; c < k; ++c) {
-      if (state[c] == 0 && regenerable[c] && flags[c] == 0) continue;
+      if (verdict[c] == 0 && regenerable[c] && verdict[k + c] == 0) continue;
       st = general(c);  // not flat, not regenerable, or a run of equal codes beyond the finish
       if (st) return st;
     }
@@ -520,11 +583,211 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     }
     if (st) return st;
   }
-  if (any_deferred && side && defer >= 2) {
-    st = check_counts();
+  if (any_deferred && side && defer >= 2 && !(a->columns && any_regen && step4_gen_enabled(n))) {
+    st = check_counts();  // (checked with the step-4 verdicts above on the generated path)
     if (st) return st;
   }
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // host vectors above were sources of async copies
   return PBH_OK;
 }
 }  // namespace
+
+// ---------------------------------------------------------------- owned columns (row-sharded runs)
+// Step 4 of the columns a rank owns in the row-sharded Iman-Conover (probabilit_amd/
+// distributed.py): each column's correlated scores arrive whole (an all-to-all from the row
+// shards) and are ranked by the same passes as the single-GPU call -- codes, top-16 histogram
+// (+ the adaptive code map), MSD code passes, bucket finish, row placement, gen_place -- on the
+// step-4 lanes, column i starting when its `ready` event fires and recording `done` when its Y
+// column is complete, so that exchanges and ranking overlap.  finish() reads every column's
+// verdict once and redoes the rare rejected column by the general path.
+struct pbh_ic_owned {
+  int m = 0;
+  int64_t n = 0;
+  std::vector<GenColumn*> gens;
+  Step4Shared sh;
+  Step4Lanes* lanes = nullptr;
+  ReorderWs rw;
+  double* tmp = nullptr;   // the general path's sort(X)
+  double* tmp2 = nullptr;  // and its Y when the caller asked for positions
+  std::vector<const double*> cs;
+  std::vector<uint32_t*> p_out;
+  std::vector<double*> y;
+  std::vector<int64_t> y_rs;
+  std::vector<char> launched;
+};
+
+namespace {
+struct OwnedLayout {
+  void* shared;
+  void* lanes;
+  void* codes;
+  void* reorder;
+  void* tmp;
+  void* tmp2;
+};
+size_t owned_bytes(int64_t n, int m, void* base, OwnedLayout* o) {
+  Carver c(base);
+  OwnedLayout l;
+  l.shared = c.take(step4_gen_shared_bytes(m));
+  l.lanes = c.take(step4_gen_column_bytes(n) * kStep4MaxStreams);
+  l.codes = c.take(align256((size_t)n * 4) * kStep4MaxStreams);
+  l.reorder = c.take(reorder_ws_bytes(n));
+  l.tmp = c.take((size_t)n * 8);
+  l.tmp2 = c.take((size_t)n * 8);
+  if (o) *o = l;
+  return c.used;
+}
+}  // namespace
+
+extern "C" int pbh_ic_owned_workspace_size(int64_t n, int32_t m, size_t* bytes) {
+  PBH_REQUIRE(bytes && n >= 2 && n < ((int64_t)1 << 32) && m >= 1 && m <= 128,
+              "pbh_ic_owned_workspace_size: bad arguments");
+  *bytes = owned_bytes(n, m, nullptr, nullptr);
+  return PBH_OK;
+}
+
+extern "C" int pbh_ic_owned_create(const pbh_ic_column* columns, int32_t m, int64_t n, void* ws, size_t ws_bytes,
+                                   pbh_ic_owned** out, void* stream) {
+  PBH_REQUIRE(columns && ws && out && m >= 1 && m <= 128, "pbh_ic_owned_create: bad arguments");
+  PBH_REQUIRE(n >= 2 && n < ((int64_t)1 << 32), "pbh_ic_owned_create: need 2 <= N < 2^32 (N=%lld)", (long long)n);
+  const size_t need = owned_bytes(n, m, nullptr, nullptr);
+  if (ws_bytes < need) {
+    set_error("pbh_ic_owned_create: workspace %zu < %zu bytes", ws_bytes, need);
+    return PBH_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  pbh_ic_owned* h = new pbh_ic_owned();
+  h->m = m;
+  h->n = n;
+  h->gens.assign(m, nullptr);
+  h->cs.assign(m, nullptr);
+  h->y.assign(m, nullptr);
+  h->y_rs.assign(m, 1);
+  h->p_out.assign(m, nullptr);
+  h->launched.assign(m, 0);
+  OwnedLayout lay;
+  owned_bytes(n, m, ws, &lay);
+  step4_gen_carve_shared(lay.shared, m, h->sh);
+  h->tmp = (double*)lay.tmp;
+  h->tmp2 = (double*)lay.tmp2;
+  int st = reorder_carve(lay.reorder, n, h->rw, s);
+  for (int i = 0; st == PBH_OK && i < m; ++i) {
+    const pbh_ic_column& g = columns[i];
+    pbh_param prm[3];
+    for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
+    st = gen_create(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, &h->gens[i], s);
+  }
+  if (st == PBH_OK) {
+    h->lanes = new Step4Lanes(n, lay.lanes, lay.codes, s);
+    st = h->lanes->begin();  // the lanes start after the tables and the code map
+  }
+  if (st != PBH_OK) {
+    (void)hipStreamSynchronize(s);
+    for (GenColumn* g : h->gens) gen_destroy(g, s);
+    delete h->lanes;
+    delete h;
+    return st;
+  }
+  *out = h;
+  return PBH_OK;
+}
+
+extern "C" int pbh_ic_owned_column(pbh_ic_owned* h, int32_t i, const double* cs, double* y, int64_t y_rs,
+                                   uint32_t* p_out, void* ready_event, void* done_event, void* stream) {
+  PBH_REQUIRE(h && cs && (y || p_out) && i >= 0 && i < h->m, "pbh_ic_owned_column: bad arguments");
+  PBH_REQUIRE(!h->launched[i], "pbh_ic_owned_column: column %d already launched", i);
+  Step4Lanes& L = *h->lanes;
+  const int j = L.next();
+  hipStream_t ls = L.ss[j];
+  if (ready_event)
+    PBH_CHECK_HIP(hipStreamWaitEvent(ls, (hipEvent_t)ready_event, 0));
+  else {
+    int st = L.order(as_stream(stream), ls);
+    if (st) return st;
+  }
+  const int64_t n = h->n;
+  int st = make_codes(cs, n, h->rw.cm, L.codes[j], ls);
+  if (!st) st = step4_gen_hist(L.codes[j], n, cs, n, n, h->sh, i, 1, ls);
+  if (!st) st = step4_gen_column(i, L.codes[j], cs, n, h->sh, L.cb[j], ls);
+  int buf = 0;
+  if (!st) st = step4_gen_place_passes(i, n, h->sh, L.cb[j], ls, &buf);
+  if (!st)
+    st = p_out ? place_positions(L.cb[j].pairs[buf], n, p_out, h->sh.flags + i, ls)
+               : gen_place(h->gens[i], L.cb[j].pairs[buf], n, y, y_rs, nullptr, h->sh.flags + i, ls);
+  if (st) return st;
+  if (done_event) PBH_CHECK_HIP(hipEventRecord((hipEvent_t)done_event, ls));
+  h->cs[i] = cs;
+  h->p_out[i] = p_out;
+  h->y[i] = y;
+  h->y_rs[i] = y_rs;
+  h->launched[i] = 1;
+  return PBH_OK;
+}
+
+extern "C" int pbh_ic_owned_finish(pbh_ic_owned* h, int32_t* redone_host, void* stream) {
+  PBH_REQUIRE(h, "pbh_ic_owned_finish: null handle");
+  hipStream_t s = as_stream(stream);
+  const int m = h->m;
+  int st = h->lanes->join(s);
+  if (st) return st;
+  std::vector<int32_t> verdict(2 * (size_t)m);
+  PBH_CHECK_HIP(hipMemcpyAsync(verdict.data(), h->sh.state, 8 * (size_t)m, hipMemcpyDeviceToHost, s));
+  PBH_CHECK_HIP(hipStreamSynchronize(s));
+  for (int i = 0; i < m; ++i) {
+    const bool redo = h->launched[i] && (verdict[i] != 0 || verdict[m + i] != 0);
+    if (redone_host) redone_host[i] = redo ? 1 : 0;
+    if (!redo) continue;
+    // the general path: sort(X) materialised, the column ranked by the code sort
+    st = gen_sorted(h->gens[i], 0, h->n, h->tmp, nullptr, nullptr, s);
+    if (!st && h->p_out[i])  // the positions: rank - 1 of every row (its Y is not needed)
+      st = reorder_column(h->cs[i], h->n, h->tmp, h->tmp2, 1, (int32_t*)h->p_out[i], h->rw, s);
+    else if (!st)
+      st = reorder_column(h->cs[i], h->n, h->tmp, h->y[i], h->y_rs[i], nullptr, h->rw, s);
+    if (st) return st;
+  }
+  PBH_CHECK_HIP(hipStreamSynchronize(s));
+  return PBH_OK;
+}
+
+extern "C" int pbh_ic_owned_destroy(pbh_ic_owned* h, void* stream) {
+  if (!h) return PBH_OK;
+  hipStream_t s = as_stream(stream);
+  if (h->lanes) (void)h->lanes->join(s);  // no lane may still read the tables being freed
+  for (GenColumn* g : h->gens) gen_destroy(g, s);
+  (void)hipStreamSynchronize(s);
+  delete h->lanes;
+  delete h;
+  return PBH_OK;
+}
+
+// ---------------------------------------------------------------- events (stream ordering for callers)
+extern "C" int pbh_event_create(void** event) {
+  PBH_REQUIRE(event, "pbh_event_create: null pointer");
+  hipEvent_t e = nullptr;
+  PBH_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  *event = (void*)e;
+  return PBH_OK;
+}
+
+extern "C" int pbh_event_destroy(void* event) {
+  if (event) PBH_CHECK_HIP(hipEventDestroy((hipEvent_t)event));
+  return PBH_OK;
+}
+
+extern "C" int pbh_event_record(void* event, void* stream) {
+  PBH_REQUIRE(event, "pbh_event_record: null event");
+  PBH_CHECK_HIP(hipEventRecord((hipEvent_t)event, as_stream(stream)));
+  return PBH_OK;
+}
+
+extern "C" int pbh_stream_wait_event(void* stream, void* event) {
+  PBH_REQUIRE(event, "pbh_stream_wait_event: null event");
+  PBH_CHECK_HIP(hipStreamWaitEvent(as_stream(stream), (hipEvent_t)event, 0));
+  return PBH_OK;
+}
+
+extern "C" int pbh_event_synchronize(void* event) {
+  PBH_REQUIRE(event, "pbh_event_synchronize: null event");
+  PBH_CHECK_HIP(hipEventSynchronize((hipEvent_t)event));
+  return PBH_OK;
+}

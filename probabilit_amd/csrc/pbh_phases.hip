@@ -14,6 +14,7 @@
 #include "pbh_ic.h"
 #include "pbh_lhs.h"
 #include "pbh_sort.h"
+#include "pbh_step4.h"
 
 namespace pbh {
 
@@ -177,6 +178,47 @@ extern "C" int pbh_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t 
   pbh_param prm[3];
   for (int j = 0; j < nparams; ++j) prm[j] = pbh_param{nullptr, params_host[j]};
   return lhs_sorted_ppf(seed, n, t0, nt, col, dist, prm, nparams, out, nonfinite_flag, as_stream(stream));
+}
+
+extern "C" int pbh_lhs_sorted_counts(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist,
+                                     const double* params_host, int nparams, unsigned long long* counts,
+                                     uint32_t* heads, uint32_t* hcur, uint32_t hcap, int32_t* nonfinite_flag,
+                                     void* stream) {
+  PBH_REQUIRE(counts && nparams >= 0 && nparams <= 3 && (nparams == 0 || params_host),
+              "pbh_lhs_sorted_counts: bad arguments");
+  PBH_REQUIRE(!heads || (hcur && hcap >= 1), "pbh_lhs_sorted_counts: heads need hcur and hcap >= 1");
+  PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "pbh_lhs_sorted_counts: n out of range");
+  hipStream_t s = as_stream(stream);
+  pbh_param prm[3];
+  for (int j = 0; j < nparams; ++j) prm[j] = pbh_param{nullptr, params_host[j]};
+  GenColumn* g = nullptr;
+  int st = gen_create(seed, n, col, dist, prm, nparams, &g, s);
+  if (st != PBH_OK) return st;
+  st = gen_sorted(g, t0, nt, nullptr, nonfinite_flag, counts, s, heads, hcur, heads ? hcap : 0);
+  gen_destroy(g, s);  // stream-ordered: the tables are freed after the kernel
+  return st;
+}
+
+extern "C" int pbh_lhs_values_at(const pbh_ic_column* column, int64_t n, const uint32_t* p, int64_t m, double* y,
+                                 int64_t y_rs, void* stream) {
+  PBH_REQUIRE(column && (m == 0 || (p && y)) && m >= 0, "pbh_lhs_values_at: bad arguments");
+  PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "pbh_lhs_values_at: n out of range");
+  if (m == 0) return PBH_OK;
+  hipStream_t s = as_stream(stream);
+  pbh_param prm[3];
+  for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, column->params[j]};
+  GenColumn* g = nullptr;
+  int st = gen_create(column->seed, n, column->lhs_col, column->dist, prm, column->nparams, &g, s);
+  if (st != PBH_OK) return st;
+  st = gen_values_at(g, p, m, y, y_rs, s);
+  gen_destroy(g, s);
+  return st;
+}
+
+extern "C" int pbh_sort_heads(uint32_t* heads, int64_t nh, void* stream) {
+  PBH_REQUIRE(heads, "pbh_sort_heads: null pointer");
+  if (nh <= 1) return PBH_OK;
+  return sort_heads(heads, nh, as_stream(stream));
 }
 
 extern "C" int pbh_sorted_check(const double* x, int64_t n, int64_t* ties, int64_t* inversions, void* ws,

@@ -452,8 +452,12 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_sorted_ppf(uint64_t seed
 // offsets in the block); gamma / poisson stage their tables in LDS (random p: table gathers).
 constexpr int kGenRows = 1 << kGenPlaceShift;
 
-template <int D>
-__global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __restrict__ pairs, int64_t n,
+// BYROW (the row owner of a row-sharded run, pbh_lhs_values_at): the item at position p of a block
+// is row r0 + p itself, its stratum pidx[r0 + p] -- the sorted positions the column's owner sent
+// back -- for `rows` rows of an n-row design; otherwise the (row << 32 | p) pairs, rows == n.
+template <int D, bool BYROW = false>
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __restrict__ pairs,
+                                                      const uint32_t* __restrict__ pidx, int64_t rows, int64_t n,
                                                       uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
                                                       double* __restrict__ y, int64_t y_rs, int32_t* __restrict__ idx,
                                                       const int32_t* __restrict__ state) {
@@ -469,9 +473,9 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
   __shared__ std::conditional_t<kCompact, TailQueue, NoQueue> tq[1];
   Philox ph(seed);
   const double p0 = prm.val[0], p1 = prm.val[1], p2 = prm.val[2];
-  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
-    const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
+    const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
     for (int h = 0; h < kGenRows; h += kCTile) {
       if (kCompact) {
         if (threadIdx.x == 0) tq[0].count = 0;
@@ -484,11 +488,17 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
         double q = 0.5;
         int off = 0;
         if (valid) {
-          const uint64_t pr = pairs[r0 + p];
-          const uint32_t t = (uint32_t)pr;
-          const int64_t row = (int64_t)(pr >> 32);
-          if (idx) idx[row] = (int32_t)t;
-          off = (int)(row - r0);
+          uint32_t t;
+          if constexpr (BYROW) {
+            t = pidx[r0 + p];
+            off = p;
+          } else {
+            const uint64_t pr = pairs[r0 + p];
+            t = (uint32_t)pr;
+            const int64_t row = (int64_t)(pr >> 32);
+            if (idx) idx[row] = (int32_t)t;
+            off = (int)(row - r0);
+          }
           q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
         }
         if constexpr (kCompact) {
@@ -517,7 +527,9 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
 
 // gamma with the guide table in LDS (120 KiB) next to the block (32 KiB): one 1024-thread
 // workgroup per CU
-__global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __restrict__ pairs, int64_t n,
+template <bool BYROW = false>
+__global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __restrict__ pairs,
+                                                             const uint32_t* __restrict__ pidx, int64_t rows, int64_t n,
                                                              uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
                                                              double* __restrict__ y, int64_t y_rs,
                                                              int32_t* __restrict__ idx,
@@ -537,16 +549,19 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
   const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
   const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
   constexpr int kPer = kGenRows / kGBlock;
-  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
-    const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
+    const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
     if (threadIdx.x == 0) nslow = 0;
     __syncthreads();
-    uint64_t pr[kPer];
+    uint64_t pr[kPer];  // BYROW: the same (row << 32 | p) form, built from the row and pidx
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int p = j * kGBlock + threadIdx.x;
-      pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
+      if constexpr (BYROW)
+        pr[j] = p < cnt ? ((uint64_t)(r0 + p) << 32) | pidx[r0 + p] : ~0ull;
+      else
+        pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
     }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -568,7 +583,7 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
       }
       if (valid) {
         const int64_t row = (int64_t)(pr[j] >> 32);
-        if (idx) idx[row] = (int32_t)(uint32_t)pr[j];
+        if (!BYROW && idx) idx[row] = (int32_t)(uint32_t)pr[j];
         if (fast) {
           buf[row - r0] = v;
         } else {
@@ -582,7 +597,7 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
     const int nd = ns <= kQCap ? ns : cnt;  // queue overflow: recompute the whole block
     for (int i = threadIdx.x; i < nd; i += kGBlock) {
       const int p = ns <= kQCap ? slowq[i] : i;
-      const uint64_t prr = pairs[r0 + p];
+      const uint64_t prr = BYROW ? ((uint64_t)(r0 + p) << 32) | pidx[r0 + p] : pairs[r0 + p];
       buf[(int64_t)(prr >> 32) - r0] =
           gamma_ppf_lds(lhs_sorted_quantile(ph, (uint64_t)(uint32_t)prr, col, (uint64_t)n), prm, pt, T);
     }
@@ -597,8 +612,10 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
 }
 
 // poisson with the CDF table + guide in (dynamic) LDS
-__global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_poisson(const uint64_t* __restrict__ pairs, int64_t n,
-                                                              uint64_t seed, uint32_t col, Params prm,
+template <bool BYROW = false>
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_poisson(const uint64_t* __restrict__ pairs,
+                                                              const uint32_t* __restrict__ pidx, int64_t rows,
+                                                              int64_t n, uint64_t seed, uint32_t col, Params prm,
                                                               PoissonTable pt, double* __restrict__ y, int64_t y_rs,
                                                               int32_t* __restrict__ idx,
                                                               const int32_t* __restrict__ state) {
@@ -607,15 +624,18 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_poisson(const uint
   __shared__ double buf[kGenRows];
   const PoissonTable T = stage_poisson(pt, plds);
   Philox ph(seed);
-  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
-    const int cnt = (int)((n - r0) < kGenRows ? (n - r0) : kGenRows);
+    const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
     for (int h = 0; h < kGenRows; h += 4 * kBlock) {  // 4 independent chains per thread
       uint64_t pr[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int p = h + j * kBlock + threadIdx.x;
-        pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
+        if constexpr (BYROW)
+          pr[j] = p < cnt ? ((uint64_t)(r0 + p) << 32) | pidx[r0 + p] : ~0ull;
+        else
+          pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
       }
       double v[4];
 #pragma unroll
@@ -626,7 +646,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_poisson(const uint
       for (int j = 0; j < 4; ++j) {
         if (pr[j] != ~0ull) {
           const int64_t row = (int64_t)(pr[j] >> 32);
-          if (idx) idx[row] = (int32_t)(uint32_t)pr[j];
+          if (!BYROW && idx) idx[row] = (int32_t)(uint32_t)pr[j];
           buf[row - r0] = v[j];
         }
       }
@@ -1144,11 +1164,13 @@ int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t*
   PBH_REQUIRE(t0 >= 0 && nt >= 0 && t0 + nt <= n, "lhs_sorted_ppf: strata [%lld, %lld) outside [0, %lld)",
               (long long)t0, (long long)(t0 + nt), (long long)n);
   PBH_REQUIRE(out || counts, "gen_sorted: neither an output column nor counts");
-  PBH_REQUIRE(!heads || (counts && hcur && hcap >= 1 && t0 == 0), "gen_sorted: run heads need counts, t0 = 0");
+  PBH_REQUIRE(!heads || (counts && hcur && hcap >= 1), "gen_sorted: run heads need counts");
   if (counts) PBH_CHECK_HIP(hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), s));
-  if (heads) {  // stratum 0 heads the first run
+  if (heads && t0 == 0) {  // stratum 0 heads the first run
     PBH_CHECK_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t), s));
     PBH_CHECK_HIP(hipMemsetD32Async((hipDeviceptr_t)hcur, 1, 1, s));
+  } else if (heads) {  // a later segment: its first stratum is the previous shard's last one
+    PBH_CHECK_HIP(hipMemsetAsync(hcur, 0, sizeof(uint32_t), s));
   }
   if (nt == 0) return PBH_OK;
   dim3 gr(ppf_grid(nt)), b(kBlock);
@@ -1175,31 +1197,33 @@ int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t*
   return PBH_OK;
 }
 
-int gen_place(const GenColumn* g, const uint64_t* pairs, int64_t n, double* y, int64_t y_rs, int32_t* idx,
-              const int32_t* state, hipStream_t s) {
-  PBH_REQUIRE(n == g->n, "gen_place: %lld rows for a column of %lld", (long long)n, (long long)g->n);
-  const int64_t blocks = (n + kGenRows - 1) / kGenRows;
+template <bool BYROW>
+static int place_launch(const GenColumn* g, const uint64_t* pairs, const uint32_t* pidx, int64_t rows, double* y,
+                        int64_t y_rs, int32_t* idx, const int32_t* state, hipStream_t s) {
+  const int64_t n = g->n;
+  const int64_t blocks = (rows + kGenRows - 1) / kGenRows;
+  if (blocks <= 0) return PBH_OK;
   if (gamma_lds_ok(g->dist, g->prm, g->pt)) {
     PBH_TIMED(kKPlaceGen, s,
-              hipLaunchKernelGGL(k_place_gen_gamma, dim3((unsigned)(blocks < 256 ? blocks : 256)), dim3(kGBlock), 0, s,
-                                 pairs, n, g->seed, g->col, g->prm, g->pt, y, y_rs, idx, state));
+              hipLaunchKernelGGL(k_place_gen_gamma<BYROW>, dim3((unsigned)(blocks < 256 ? blocks : 256)), dim3(kGBlock),
+                                 0, s, pairs, pidx, rows, n, g->seed, g->col, g->prm, g->pt, y, y_rs, idx, state));
     PBH_CHECK_LAUNCH();
     return PBH_OK;
   }
   const unsigned gr = (unsigned)(blocks < 256 * 8 ? blocks : 256 * 8);
   if (const size_t pl = poisson_lds_bytes(g->dist, g->prm, g->pt)) {
     PBH_TIMED(kKPlaceGen, s,
-              hipLaunchKernelGGL(k_place_gen_poisson, dim3(gr), dim3(kBlock), pl, s, pairs, n, g->seed, g->col, g->prm,
-                                 g->pt, y, y_rs, idx, state));
+              hipLaunchKernelGGL(k_place_gen_poisson<BYROW>, dim3(gr), dim3(kBlock), pl, s, pairs, pidx, rows, n,
+                                 g->seed, g->col, g->prm, g->pt, y, y_rs, idx, state));
     PBH_CHECK_LAUNCH();
     return PBH_OK;
   }
   switch (g->dist) {
-#define PBH_CASE(D)                                                                                           \
-  case D:                                                                                                     \
-    PBH_TIMED(kKPlaceGen, s,                                                                                     \
-              hipLaunchKernelGGL(k_place_gen<D>, dim3(gr), dim3(kBlock), 0, s, pairs, n, g->seed, g->col, g->prm, \
-                                 g->pt, y, y_rs, idx, state));                                                \
+#define PBH_CASE(D)                                                                                          \
+  case D:                                                                                                    \
+    PBH_TIMED(kKPlaceGen, s,                                                                                 \
+              hipLaunchKernelGGL((k_place_gen<D, BYROW>), dim3(gr), dim3(kBlock), 0, s, pairs, pidx, rows, n,  \
+                                 g->seed, g->col, g->prm, g->pt, y, y_rs, idx, state));                      \
     break;
     PBH_CASE(PBH_DIST_NORM)
     PBH_CASE(PBH_DIST_UNIFORM)
@@ -1215,6 +1239,16 @@ int gen_place(const GenColumn* g, const uint64_t* pairs, int64_t n, double* y, i
   }
   PBH_CHECK_LAUNCH();
   return PBH_OK;
+}
+
+int gen_place(const GenColumn* g, const uint64_t* pairs, int64_t n, double* y, int64_t y_rs, int32_t* idx,
+              const int32_t* state, hipStream_t s) {
+  PBH_REQUIRE(n == g->n, "gen_place: %lld rows for a column of %lld", (long long)n, (long long)g->n);
+  return place_launch<false>(g, pairs, nullptr, n, y, y_rs, idx, state, s);
+}
+
+int gen_values_at(const GenColumn* g, const uint32_t* p, int64_t m, double* y, int64_t y_rs, hipStream_t s) {
+  return place_launch<true>(g, nullptr, p, m, y, y_rs, nullptr, nullptr, s);
 }
 
 int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist, const pbh_param* params,

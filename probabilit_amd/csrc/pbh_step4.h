@@ -10,9 +10,13 @@ namespace pbh {
 constexpr int kGenPlaceShift = 12;  // final placement blocks of 4096 rows (32 KB of LDS)
 
 // per-call state of all k columns (device): histograms, bucket starts, cursors, tile maps,
-// state[c] (bit 0 counter overflow, bit 1 bucket above the finish capacity: the column takes
-// the general path) and flags[c] (bit 0: a run of equal codes too long for the finish: the
-// column is redone by the general path after the others)
+// state[c] (bit 0 counter overflow, bit 1 bucket above the finish capacity: the column is not
+// flat) and flags[c] (bit 0: a run of equal codes too long for the finish; bit 2: the column is
+// still not flat after the adaptive code map -- every later pass skips it, and it is redone by
+// the general path after the others).  A column that is not flat under the fixed N(0, 1) code
+// map (a score dominated by a discrete column: a mixture of narrow peaks) is re-coded once with
+// a code map built from its own histogram (retry[c] = 1; seghist, amap) and re-counted.
+constexpr int kAdaptSegments = 4096;  // adaptive code map: segments of [-8.5, 8.5]
 struct Step4Shared {
   int k;
   uint32_t* hist;
@@ -23,9 +27,16 @@ struct Step4Shared {
   uint32_t* cls;     // per column: top-byte counts of each msd1 tile class (8 x 256)
   uint32_t* cstart;  // per column: each class's start in every top-byte group (8 x 256)
   uint32_t* tpre;
+  uint32_t* seghist;  // per column: kAdaptSegments counts of CS (adaptive code map)
+  uint32_t* amap;     // per column: adaptive code map, kAdaptMapWords words (bases, then slopes)
   int32_t* state;
   int32_t* flags;
+  int32_t* retry;
 };
+// words of one column's adaptive code map: kAdaptSegments + 1 bases (padded to 8 bytes), then
+// kAdaptSegments double slopes
+constexpr int kAdaptBaseWords = (kAdaptSegments + 2) & ~1;
+constexpr int kAdaptMapWords = kAdaptBaseWords + 2 * kAdaptSegments;
 // one column's staging (reused column after column)
 struct Step4Column {
   uint32_t* keys32;
@@ -49,10 +60,15 @@ bool step4_fused();
 // latency-bound kernels (bucket finish, gen_place) overlap another's bandwidth-bound passes
 constexpr int kStep4MaxStreams = 4;
 int step4_streams();
+// the side streams of this device, created once (thread-safe) and kept for the process
 hipStream_t step4_side_stream(int i);
 void step4_sync_side_streams();
-// top-16 histograms, bucket starts and flatness of all k code columns (codes + c * ldc)
-int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Shared& sh, hipStream_t s);
+// top-16 histograms, bucket starts and flatness of the code columns c0 .. c0 + kk - 1 (column c
+// at codes + (c - c0) * ldc).  With cs (column c at cs + (c - c0) * ldcs; PBH_ADAPT=0 disables),
+// a column that is not flat is re-coded with its adaptive code map and counted again, all on
+// the device (the codes are rewritten in place); state / flags then hold the final verdict.
+int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,
+                   int c0, int kk, hipStream_t s);
 // code passes and bucket finish of column c: (row << 32 | p') pairs in cb.pairs[0], in position
 // order, or (step4_fused) grouped by the top row-placement level
 int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, const Step4Shared& sh,
@@ -67,8 +83,9 @@ int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* par
                hipStream_t s);
 void gen_destroy(GenColumn* g, hipStream_t s);
 // out[t - t0] = the column's value in stratum t (see lhs_sorted_ppf); out may be NULL when
-// counts (ties, inversions) is given.  heads (t0 = 0 only): the run heads, unordered, at most
-// hcap of them; *hcur = their number (= nt - ties when there is no inversion).
+// counts (ties, inversions) is given.  heads: the run heads, unordered, at most hcap of them --
+// every t in (t0, t0 + nt) whose value differs from stratum t - 1's, and t0 itself when t0 = 0;
+// *hcur = their number (= nt - ties when t0 = 0 and there is no inversion).
 constexpr int kHeadsCap = 16384;
 int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t* flag, unsigned long long* counts,
                hipStream_t s, uint32_t* heads = nullptr, uint32_t* hcur = nullptr, uint32_t hcap = 0);
@@ -79,5 +96,12 @@ int sort_heads(uint32_t* heads, int64_t nh, hipStream_t s);
 // state (optional device word): skip when non-zero.
 int gen_place(const GenColumn* g, const uint64_t* pairs, int64_t n, double* y, int64_t y_rs, int32_t* idx,
               const int32_t* state, hipStream_t s);
+// y[i * y_rs] = value of stratum p[i] for i < m (the row owner of a row-sharded run: the sorted
+// positions of its rows, sent back by the column's owner; the same kernels as gen_place)
+int gen_values_at(const GenColumn* g, const uint32_t* p, int64_t m, double* y, int64_t y_rs, hipStream_t s);
+// p_out[row] = p for every pair (row << 32 | p) of `pairs` grouped by 4096-row block, the block
+// assembled in LDS and written contiguously (the owner's step-4 output of a row-sharded run);
+// state (optional device word): skip when non-zero
+int place_positions(const uint64_t* pairs, int64_t n, uint32_t* p_out, const int32_t* state, hipStream_t s);
 
 }  // namespace pbh

@@ -24,7 +24,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "pbh_error.h"
+#include "pbh_ic.h"
 #include "pbh_step4.h"
 #include "pbh_timing.h"
 
@@ -82,11 +85,12 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh 
 // code pass gives each class its own cursors and sub-ranges (see k_msd1).
 __global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ codes, int64_t ld, int64_t n,
                                                  uint32_t* __restrict__ hist, uint32_t* __restrict__ cls,
-                                                 int32_t* __restrict__ state) {
+                                                 int32_t* __restrict__ state, const int32_t* __restrict__ gate) {
   __shared__ uint32_t w[32768];
   __shared__ uint32_t cw[8 * 256];
   __shared__ int ovf;
   const int c = blockIdx.y;
+  if (gate && !gate[c]) return;  // the adaptive re-count: only the re-coded columns
   const uint32_t* cc = codes + (int64_t)c * ld;
   for (int i = threadIdx.x; i < 32768; i += 1024) w[i] = 0;
   for (int i = threadIdx.x; i < 8 * 256; i += 1024) cw[i] = 0;
@@ -137,12 +141,14 @@ __global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ co
 __global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict__ hist, int64_t n,
                                                       uint32_t* __restrict__ start, uint32_t* __restrict__ tpre,
                                                       const uint32_t* __restrict__ cls, uint32_t* __restrict__ cstart,
-                                                      int32_t* __restrict__ state) {
+                                                      int32_t* __restrict__ state, int32_t* __restrict__ flags,
+                                                      const int32_t* __restrict__ gate) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t gsize[256];
   __shared__ uint32_t gstart[256];
   __shared__ int big;
   const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (gate && !gate[c]) return;
   const uint32_t* hc = hist + (int64_t)c * 65536;
   uint32_t* sc = start + (int64_t)c * 65537;
   if (t == 0) big = 0;
@@ -191,7 +197,141 @@ __global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict
     }
     tpre[(int64_t)c * 257 + 256] = acc;
     if (big) atomicOr(&state[c], 2);
+    // not flat (this kernel's verdict or k_hist16's counter overflow): the placement passes and
+    // gen_place, which test flags, skip the column as the code passes and the finish do on state
+    if (big || state[c]) atomicOr(&flags[c], 4);
   }
+}
+
+// ---------------------------------------------------------------- adaptive code map
+// A column that is not flat under the fixed map (code_of: Phi of an N(0, 1) score) gets a map
+// built from its own distribution: kAdaptSegments equal segments of [-8.5, 8.5], segment j's
+// codes [base_j, base_j+1) in proportion to its share of the column.  code(x) stays
+// non-decreasing in x (bases strictly increasing, offsets monotone and clamped), so sorting by
+// code and ordering equal-code runs by value is still the exact float64 order.
+constexpr double kAdaptX0 = -8.5;
+constexpr double kAdaptW = 17.0 / kAdaptSegments;
+
+// one block per column: retry[c] = (state[c] != 0); a retried column's histograms, cursors and
+// verdict words are cleared for the second count
+__global__ __launch_bounds__(1024) void k_adapt_reset(int32_t* __restrict__ state, int32_t* __restrict__ flags,
+                                                      int32_t* __restrict__ retry, uint32_t* __restrict__ hist,
+                                                      uint32_t* __restrict__ cur1, uint32_t* __restrict__ cur2,
+                                                      uint32_t* __restrict__ curF, uint32_t* __restrict__ cls,
+                                                      uint32_t* __restrict__ seghist, int cpad) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  const bool again = state[c] != 0;
+  __syncthreads();  // every thread has read state[c] before thread 0 clears it
+  if (!again) {
+    if (t == 0) retry[c] = 0;
+    return;
+  }
+  for (int i = t; i < 65536; i += 1024) {
+    hist[(int64_t)c * 65536 + i] = 0u;
+    cur2[(int64_t)c * 65536 + i] = 0u;
+  }
+  for (int i = t; i < 8 * 256 * cpad; i += 1024) {
+    cur1[(int64_t)c * 8 * 256 * cpad + i] = 0u;
+    curF[(int64_t)c * 8 * 256 * cpad + i] = 0u;
+  }
+  for (int i = t; i < 2048; i += 1024) cls[(int64_t)c * 2048 + i] = 0u;
+  for (int i = t; i < kAdaptSegments; i += 1024) seghist[(int64_t)c * kAdaptSegments + i] = 0u;
+  if (t == 0) {
+    state[c] = 0;
+    flags[c] = 0;
+    retry[c] = 1;
+  }
+}
+
+// segment counts of the retried columns' CS values (values outside [-8.5, 8.5] are not counted:
+// they take code 0 / 0xFFFFFFFF)
+__global__ __launch_bounds__(1024) void k_seg_hist(const double* __restrict__ cs, int64_t ld, int64_t n,
+                                                   const int32_t* __restrict__ retry, uint32_t* __restrict__ seghist) {
+  __shared__ uint32_t h[kAdaptSegments];
+  const int c = blockIdx.y;
+  if (!retry[c]) return;
+  for (int i = threadIdx.x; i < kAdaptSegments; i += 1024) h[i] = 0u;
+  __syncthreads();
+  const double* x = cs + (int64_t)c * ld;
+  for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 1024) {
+    const double u = (x[i] - kAdaptX0) * (1.0 / kAdaptW);
+    if (u >= 0.0 && u < (double)kAdaptSegments) atomicAdd(&h[(int)u], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kAdaptSegments; i += 1024)
+    if (h[i]) atomicAdd(&seghist[(int64_t)c * kAdaptSegments + i], h[i]);
+}
+
+// one block per retried column: bases from the exclusive prefix of the segment counts
+// (base_j = floor(cum_j span / total) + j: strictly increasing), slopes = codes per unit x
+__global__ __launch_bounds__(1024) void k_seg_map(const uint32_t* __restrict__ seghist, const int32_t* __restrict__ retry,
+                                                  uint32_t* __restrict__ amap) {
+  constexpr int kPer = kAdaptSegments / 1024;
+  __shared__ uint32_t sh[1024 + 16];
+  __shared__ uint32_t bs[kAdaptSegments + 1];
+  const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (!retry[c]) return;
+  const uint32_t* h = seghist + (int64_t)c * kAdaptSegments;
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    v[q] = h[t * kPer + q];
+    sum += v[q];
+  }
+  uint32_t x = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[1024 + wv] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (int i = 0; i < wv; ++i) pre += sh[1024 + i];
+  uint32_t run = pre + x - sum;
+  if (t == 1023) sh[0] = run + sum;  // the total (read after the barrier below)
+  __syncthreads();
+  const double total = sh[0] ? (double)sh[0] : 1.0;
+  const double span = 4294967295.0 - kAdaptSegments;
+  uint32_t* base = amap + (int64_t)c * kAdaptMapWords;
+  double* slope = (double*)(base + kAdaptBaseWords);
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int j = t * kPer + q;
+    bs[j] = (uint32_t)floor((double)run * span / total) + (uint32_t)j;
+    run += v[q];
+  }
+  if (t == 1023) bs[kAdaptSegments] = 4294967295u;  // floor(total span / total) + m
+  __syncthreads();
+  for (int j = t; j <= kAdaptSegments; j += 1024) base[j] = bs[j];
+  for (int j = t; j < kAdaptSegments; j += 1024) slope[j] = (double)(bs[j + 1] - bs[j]) * (1.0 / kAdaptW);
+}
+
+// codes of the retried columns under their adaptive maps (staged in LDS), rewritten in place
+__global__ __launch_bounds__(256) void k_make_codes_adapt(const double* __restrict__ cs, int64_t ld, int64_t n,
+                                                          const int32_t* __restrict__ retry,
+                                                          const uint32_t* __restrict__ amap,
+                                                          uint32_t* __restrict__ codes, int64_t ldc) {
+  __shared__ uint32_t lb[kAdaptSegments + 1];
+  __shared__ double ls[kAdaptSegments];
+  const int c = blockIdx.y;
+  if (!retry[c]) return;
+  const uint32_t* base = amap + (int64_t)c * kAdaptMapWords;
+  const double* slope = (const double*)(base + kAdaptBaseWords);
+  for (int j = threadIdx.x; j <= kAdaptSegments; j += 256) lb[j] = base[j];
+  for (int j = threadIdx.x; j < kAdaptSegments; j += 256) ls[j] = slope[j];
+  __syncthreads();
+  CodeMap cm;
+  cm.x0 = kAdaptX0;
+  cm.w = kAdaptW;
+  cm.inv_w = 1.0 / kAdaptW;
+  cm.m = kAdaptSegments;
+  cm.base = lb;
+  cm.scale = ls;
+  const double* x = cs + (int64_t)c * ld;
+  uint32_t* out = codes + (int64_t)c * ldc;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = code_of(x[i], cm);
 }
 
 // ---------------------------------------------------------------- code passes
@@ -1061,15 +1201,48 @@ __global__ __launch_bounds__(256) void k_seg_tiles(const uint32_t* __restrict__ 
   if (over) atomicOr(flags, 1);
 }
 
+// p_out[row] = p of the pairs (row << 32 | p) of every 4096-row block, assembled in LDS and
+// written contiguously: a row-sharded run's owner sends these sorted positions back (4 bytes a
+// row instead of the 8 of Y; the row owner regenerates sort(X)[p], gen_values_at)
+__global__ __launch_bounds__(256) void k_place_positions(const uint64_t* __restrict__ pairs, int64_t n,
+                                                         uint32_t* __restrict__ p_out,
+                                                         const int32_t* __restrict__ state) {
+  if (state && *state) return;
+  constexpr int kRows = 1 << kGenPlaceShift;
+  __shared__ uint32_t buf[kRows];
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((n - r0) < kRows ? (n - r0) : kRows);
+    for (int p = threadIdx.x; p < cnt; p += 256) {
+      const uint64_t pr = pairs[r0 + p];
+      buf[(int64_t)(pr >> 32) - r0] = (uint32_t)pr;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < cnt; p += 256) p_out[r0 + p] = buf[p];
+    __syncthreads();
+  }
+}
+
 }  // namespace
+
+int place_positions(const uint64_t* pairs, int64_t n, uint32_t* p_out, const int32_t* state, hipStream_t s) {
+  const int64_t blocks = (n + (1 << kGenPlaceShift) - 1) >> kGenPlaceShift;
+  if (blocks <= 0) return PBH_OK;
+  PBH_TIMED(kKPlaceGen, s,
+            hipLaunchKernelGGL(k_place_positions, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, s,
+                               pairs, n, p_out, state));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
 
 static int64_t fin_slots(int64_t n);
 
 size_t step4_gen_shared_bytes(int k) {
   // per column: hist 65536 + start 65537 + cur1 8 x 256 * pad + cur2 65536 + curF 256 * pad +
-  // cls 2048 + cstart 2048 + tpre 257 (u32), state
+  // cls 2048 + cstart 2048 + tpre 257 + seghist + amap (u32), state / flags / retry
   const size_t pad = (size_t)cur_pad();
-  return (size_t)k * ((65536 + 65537 + 8 * 256 * pad + 65536 + 8 * 256 * pad + 2048 + 2048 + 257) * 4 + 64) + 256;
+  return (size_t)k * ((65536 + 65537 + 8 * 256 * pad + 65536 + 8 * 256 * pad + 2048 + 2048 + 257 + kAdaptSegments +
+                       kAdaptMapWords) * 4 + 64) + 512;
 }
 
 size_t step4_gen_column_bytes(int64_t n) {
@@ -1099,9 +1272,15 @@ void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh) {
   p += (size_t)k * 2048 * 4;
   sh.tpre = (uint32_t*)p;
   p += (size_t)k * 257 * 4;
+  sh.seghist = (uint32_t*)p;
+  p += (size_t)k * kAdaptSegments * 4;
+  p = (char*)(((uintptr_t)p + 63) & ~(uintptr_t)63);
+  sh.amap = (uint32_t*)p;  // 8-byte aligned slopes: kAdaptBaseWords is even
+  p += (size_t)k * kAdaptMapWords * 4;
   p = (char*)(((uintptr_t)p + 63) & ~(uintptr_t)63);
   sh.state = (int32_t*)p;   // k words: bit 0 counter overflow, bit 1 bucket over cap
-  sh.flags = sh.state + k;  // k words: bit 0 long run / too many runs in a bucket
+  sh.flags = sh.state + k;  // k words: bit 0 long run / too many runs in a bucket, bit 2 not flat
+  sh.retry = sh.flags + k;  // k words: re-coded with the adaptive map
 }
 
 void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb) {
@@ -1138,17 +1317,21 @@ int step4_streams() {
 
 hipStream_t step4_side_stream(int i) {
   // created once per device and kept for the life of the process (non-blocking: no implicit
-  // ordering with the legacy default stream; the caller orders them with events)
+  // ordering with the legacy default stream; the caller orders them with events).  Creation is
+  // serialised: two host threads may reach it at once (calls on one device are not otherwise
+  // concurrent: probabilit_hip.h).
   static hipStream_t streams[64][kStep4MaxStreams] = {};
+  static std::mutex mu;
   int dev = 0;
   (void)hipGetDevice(&dev);
-  if (dev < 0 || dev >= 64) return nullptr;
+  if (dev < 0 || dev >= 64 || i < 0 || i >= kStep4MaxStreams) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
   if (!streams[dev][i]) (void)hipStreamCreateWithFlags(&streams[dev][i], hipStreamNonBlocking);
   return streams[dev][i];
 }
 
 void step4_sync_side_streams() {
-  for (int i = 0; i < kStep4MaxStreams; ++i) {  // every one (the deferred counts may use the last)
+  for (int i = 0; i < kStep4MaxStreams; ++i) {  // every one (the deferred counts use the last)
     hipStream_t x = step4_side_stream(i);
     if (x) (void)hipStreamSynchronize(x);
   }
@@ -1202,25 +1385,64 @@ bool step4_gen_enabled(int64_t n) {
   return n >= 2 && n < ((int64_t)1 << 32);
 }
 
-int step4_gen_hist(const uint32_t* codes, int64_t ldc, int64_t n, const Step4Shared& sh, hipStream_t s) {
-  const int k = sh.k;
-  PBH_CHECK_HIP(hipMemsetAsync(sh.hist, 0, (size_t)k * 65536 * 4, s));
-  PBH_CHECK_HIP(hipMemsetAsync(sh.cur1, 0, (size_t)k * (16 * 256 * (size_t)cur_pad() + 65536 + 2048) * 4, s));  // cur1, cur2, curF, cls
-  PBH_CHECK_HIP(hipMemsetAsync(sh.state, 0, (size_t)2 * k * 4, s));
+int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,
+                   int c0, int kk, hipStream_t s) {
+  PBH_REQUIRE(c0 >= 0 && kk >= 1 && c0 + kk <= sh.k, "step4_gen_hist: columns [%d, %d) outside [0, %d)", c0, c0 + kk,
+              sh.k);
+  const int cpad = cur_pad();
+  const size_t cw = (size_t)8 * 256 * cpad;
+  uint32_t* hist = sh.hist + (int64_t)c0 * 65536;
+  uint32_t* cls = sh.cls + (int64_t)c0 * 2048;
+  int32_t* state = sh.state + c0;
+  int32_t* flags = sh.flags + c0;
+  int32_t* retry = sh.retry + c0;
+  PBH_CHECK_HIP(hipMemsetAsync(hist, 0, (size_t)kk * 65536 * 4, s));
+  PBH_CHECK_HIP(hipMemsetAsync(sh.cur1 + c0 * cw, 0, kk * cw * 4, s));
+  PBH_CHECK_HIP(hipMemsetAsync(sh.cur2 + (int64_t)c0 * 65536, 0, (size_t)kk * 65536 * 4, s));
+  PBH_CHECK_HIP(hipMemsetAsync(sh.curF + c0 * cw, 0, kk * cw * 4, s));
+  PBH_CHECK_HIP(hipMemsetAsync(cls, 0, (size_t)kk * 2048 * 4, s));
+  PBH_CHECK_HIP(hipMemsetAsync(state, 0, (size_t)kk * 4, s));
+  PBH_CHECK_HIP(hipMemsetAsync(flags, 0, (size_t)kk * 4, s));
   // >= 64 K codes per block and at most 64 blocks per column: every block flushes its non-empty
   // counters with global atomics (~64 K each), which the PMC pass counted as ~2 GB of writes at
   // 256 blocks per column (pmc_traffic_r72_ck1.json)
   int64_t blocks = (n + 65535) / 65536;
   if (blocks > 64) blocks = 64;
   if (blocks < 1) blocks = 1;
-  PBH_TIMED(kKHist16, s,
-            hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)k), dim3(1024), 0, s, codes, ldc, n, sh.hist,
-                               sh.cls, sh.state));
+  auto count = [&](const int32_t* gate) -> int {
+    PBH_TIMED(kKHist16, s,
+              hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)kk), dim3(1024), 0, s, codes, ldc, n, hist,
+                                 cls, state, gate));
+    PBH_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)kk), dim3(1024), 0, s, hist, n, sh.start + (int64_t)c0 * 65537,
+                       sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, gate);
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  };
+  int st = count(nullptr);
+  if (st) return st;
+  static const bool adapt = [] {
+    const char* e = getenv("PBH_ADAPT");  // "0": a column that is not flat goes to the general path
+    return !(e && e[0] == '0');
+  }();
+  if (!cs || !adapt) return PBH_OK;
+  // the re-code of the columns that are not flat: every kernel exits at once for the others
+  hipLaunchKernelGGL(k_adapt_reset, dim3((unsigned)kk), dim3(1024), 0, s, state, flags, retry, hist,
+                     sh.cur1 + c0 * cw, sh.cur2 + (int64_t)c0 * 65536, sh.curF + c0 * cw, cls,
+                     sh.seghist + (int64_t)c0 * kAdaptSegments, cpad);
   PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)k), dim3(1024), 0, s, sh.hist, n, sh.start, sh.tpre, sh.cls,
-                     sh.cstart, sh.state);
+  hipLaunchKernelGGL(k_seg_hist, dim3(64, (unsigned)kk), dim3(1024), 0, s, cs, ldcs, n, retry,
+                     sh.seghist + (int64_t)c0 * kAdaptSegments);
   PBH_CHECK_LAUNCH();
-  return PBH_OK;
+  uint32_t* amap = sh.amap + (int64_t)c0 * kAdaptMapWords;
+  hipLaunchKernelGGL(k_seg_map, dim3((unsigned)kk), dim3(1024), 0, s, sh.seghist + (int64_t)c0 * kAdaptSegments, retry,
+                     amap);
+  PBH_CHECK_LAUNCH();
+  const int64_t cb = (n + 256 * 16 - 1) / (256 * 16);
+  hipLaunchKernelGGL(k_make_codes_adapt, dim3((unsigned)(cb < 1024 ? (cb < 1 ? 1 : cb) : 1024), (unsigned)kk),
+                     dim3(256), 0, s, cs, ldcs, n, retry, amap, codes, ldc);
+  PBH_CHECK_LAUNCH();
+  return count(retry);
 }
 
 int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, const Step4Shared& sh,

@@ -118,10 +118,11 @@ def _classify(plan, node, isns):
             raise _Unfusable  # NoOp's samples are None: arithmetic on it raises in the reference
         if all(v == "imm" for v in vals):
             raise _Unfusable  # a numpy scalar result: the per-node path keeps it on the host
-        if not isinstance(node, Avg):
-            ops = list(node.get_parents())
-            if len(ops) >= 2 and all(plan.val[p][0] == "imm" for p in ops[:2]):
-                raise _Unfusable  # the first partial of the reduce is a scalar
+        ops = list(node.get_parents())
+        if len(ops) >= 2 and all(plan.val[p][0] == "imm" for p in ops[:2]):
+            # the first partial of the reduce (Avg's running sum too) is a scalar: the op has one
+            # immediate slot, so this shape stays on the per-node path
+            raise _Unfusable
         plan.val[node] = ("xform",)
         plan.need[node] = _need(plan, node)
         return

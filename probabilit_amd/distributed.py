@@ -5,16 +5,26 @@ the rows [N r / R, N (r + 1) / R) of every column and the columns [K o / R, K (o
 for step 4.  The reference's single-process ImanConover.__call__ (correlation.py:368-425)
 is split where its data dependencies cross rows:
 
-    step 1  scores of the local rows, from the LHS permutation (no sort).  Discrete
-            columns need the run heads of the sorted column: every rank extracts the heads
-            of its own strata, one all-gather of the (short) head lists.
+    step 1  the tie / inversion counts of each column's strata in this shard (counted, not
+            stored; the pair across a shard boundary counted once), summed over ranks by one
+            all-reduce; a discrete column's run heads from every shard, one all-gather of the
+            (short) sorted lists; then the scores of the local rows from the LHS permutation
+            (no sort).
     step 2  column sums, then the centered Gram matrix of the local rows; each summed over
             ranks by an all-reduce (K and K x K doubles), then E = corrcoef and
             L = cholesky(E) on every rank's host (identical inputs -> identical L).
     step 3  CS = S L^-T P^T on the local rows.
-    step 4  all-to-all of CS (row shards -> column owners), each owner ranks its full
-            columns against their sorted values (generated locally), all-to-all of Y back
-            to row shards.
+    step 4  per owned-column index i, one all-to-all brings the i-th owned column of every
+            owner from the row shards (8 bytes a row); the owner ranks it with the single-GPU
+            step-4 passes (pbh_ic_owned_*: codes, top-16 histogram with the adaptive code map,
+            MSD code passes, bucket finish, row placement) into the sorted position p of every
+            row; a second all-to-all sends the positions back (4 bytes a row); every rank then
+            regenerates its rows of Y = sort(X)[p] (pbh_lhs_values_at) -- sort(X) of a generated
+            column is a function of p, so no value crosses a link.
+
+On RCCL every all-to-all is asynchronous on the communicator's stream and ordered with the
+library's step-4 lanes by events: column i + 1's scores arrive while column i is ranked, and
+column i's positions leave as soon as its lane finishes.
 
 The returned block is this rank's rows of every correlated column, (K, rows) on its GPU.
 The compute of every phase goes through a `phases` object: `HipPhases` (the C-ABI of
@@ -27,6 +37,9 @@ import ctypes
 import numpy as np
 
 from . import _lib, device
+
+HEADS_CAP = 16384  # run heads a discrete column's shard may append (kHeadsCap, pbh_step4.h)
+DISCRETE = {_lib.DIST_IDS["poisson"]}  # the generated distributions whose sorted column has runs
 
 
 def shard_bounds(n, world):
@@ -43,6 +56,20 @@ class LHSColumn:
         self.dist = int(dist)
         self.params = [float(p) for p in params]
 
+    def ic_column(self):
+        return _lib.ICColumn(self.seed, self.lhs_col, self.dist, (ctypes.c_double * 3)(*self.params),
+                             len(self.params), None)
+
+
+class _Owned:
+    """A pbh_ic_owned handle with its workspace and the events it handed out."""
+
+    def __init__(self, handle, ws, cols):
+        self.handle = handle
+        self.ws = ws
+        self.cols = cols
+        self.events = []
+
 
 class HipPhases:
     """The Iman-Conover phases of include/probabilit_hip.h on this process's GPU."""
@@ -55,35 +82,59 @@ class HipPhases:
     def empty(self, shape, dtype="float64"):
         return device.empty(shape, dtype)
 
+    def zeros(self, shape, dtype="float64"):
+        return device.zeros(shape, dtype)
+
     def _ws(self, nbytes):
         return device.empty(max(int(nbytes), 256), "uint8")
 
+    # -- stream ordering ------------------------------------------------------------------
+    def _event(self):
+        ev = ctypes.c_void_p()
+        _lib.check(self.lib.pbh_event_create(ctypes.byref(ev)), "pbh_event_create")
+        return ev
+
+    def ready(self, owned):
+        """An event recorded on the current stream (its work so far), owned by `owned`."""
+        ev = self._event()
+        owned.events.append(ev)
+        _lib.check(self.lib.pbh_event_record(ev, device.stream()), "pbh_event_record")
+        return ev
+
+    def wait(self, ev, stream=None):
+        """`stream` (default: the current one) continues after event `ev`."""
+        if ev is not None:
+            _lib.check(self.lib.pbh_stream_wait_event(stream if stream is not None else device.stream(), ev),
+                       "pbh_stream_wait_event")
+
     # -- step 1 ---------------------------------------------------------------------------
-    def sorted_segment(self, col, n, t0, nt, flag):
+    def sorted_counts(self, col, n, t0, nt, flag, counts, heads=None, hcur=None):
+        prm = (ctypes.c_double * 3)(*col.params)
+        _lib.check(self.lib.pbh_lhs_sorted_counts(col.seed, n, t0, nt, col.lhs_col, col.dist, prm, len(col.params),
+                                                  counts.data_ptr(), heads.data_ptr() if heads is not None else None,
+                                                  hcur.data_ptr() if hcur is not None else None,
+                                                  heads.shape[0] if heads is not None else 0, flag.data_ptr(),
+                                                  device.stream()), "pbh_lhs_sorted_counts")
+
+    def sort_heads(self, heads):
+        _lib.check(self.lib.pbh_sort_heads(heads.data_ptr(), heads.shape[0], device.stream()), "pbh_sort_heads")
+
+    def segment_heads(self, col, n, t0, nt, first_is_prev, flag):
+        """Run heads of strata [t0, t0 + nt) from the materialised segment (the rare fallback:
+        a continuous column that ties, or a discrete one with more heads than HEADS_CAP)."""
         out = device.empty(max(nt, 1))
         prm = (ctypes.c_double * 3)(*col.params)
         _lib.check(self.lib.pbh_lhs_sorted_ppf(col.seed, n, t0, nt, col.lhs_col, col.dist, prm, len(col.params),
                                                out.data_ptr(), flag.data_ptr(), device.stream()),
                    "pbh_lhs_sorted_ppf")
-        return out[:nt]
-
-    def sorted_check(self, x):
-        ws = self._ws(256)
-        ties, inv = ctypes.c_int64(), ctypes.c_int64()
-        _lib.check(self.lib.pbh_sorted_check(x.data_ptr(), x.shape[0], ctypes.byref(ties), ctypes.byref(inv),
-                                             ws.data_ptr(), device.stream()), "pbh_sorted_check")
-        return ties.value, inv.value
-
-    def run_heads(self, x, t0, first_is_prev):
-        m = x.shape[0]
         nbytes = ctypes.c_size_t()
-        _lib.check(self.lib.pbh_run_heads_workspace_size(m, ctypes.byref(nbytes)))
+        _lib.check(self.lib.pbh_run_heads_workspace_size(nt, ctypes.byref(nbytes)))
         ws = self._ws(nbytes.value)
-        heads = device.empty(max(m, 1), "int32")
+        heads = device.empty(max(nt, 1), "int32")
         count = ctypes.c_int64()
-        _lib.check(self.lib.pbh_run_heads(x.data_ptr(), m, t0, int(first_is_prev), heads.data_ptr(),
-                                          ctypes.byref(count), ws.data_ptr(), nbytes.value, device.stream()),
-                   "pbh_run_heads")
+        _lib.check(self.lib.pbh_run_heads(out.data_ptr(), nt, t0 + 1 if first_is_prev else t0, int(first_is_prev),
+                                          heads.data_ptr(), ctypes.byref(count), ws.data_ptr(), nbytes.value,
+                                          device.stream()), "pbh_run_heads")
         return heads[:count.value]
 
     def scores(self, col, n, row0, nrows, heads, out):
@@ -134,13 +185,53 @@ class HipPhases:
                                          ws.data_ptr(), (2 * k * k + k) * 8, device.stream()), "pbh_ic_apply")
 
     # -- step 4 ---------------------------------------------------------------------------
-    def reorder(self, cs, sorted_src, out):
-        n = cs.shape[0]
+    def owned_begin(self, cols, n):
+        arr = (_lib.ICColumn * len(cols))(*[c.ic_column() for c in cols])
         nbytes = ctypes.c_size_t()
-        _lib.check(self.lib.pbh_ic_reorder_workspace_size(n, ctypes.byref(nbytes)))
+        _lib.check(self.lib.pbh_ic_owned_workspace_size(n, len(cols), ctypes.byref(nbytes)))
         ws = self._ws(nbytes.value)
-        _lib.check(self.lib.pbh_ic_reorder(cs.data_ptr(), n, sorted_src.data_ptr(), out.data_ptr(), 1, None,
-                                           ws.data_ptr(), nbytes.value, device.stream()), "pbh_ic_reorder")
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.pbh_ic_owned_create(arr, len(cols), n, ws.data_ptr(), nbytes.value, ctypes.byref(h),
+                                                device.stream()), "pbh_ic_owned_create")
+        return _Owned(h, ws, arr)
+
+    def owned_column(self, owned, i, cs, p_out, ready):
+        """Rank column i of `owned` from its full correlated scores cs into the positions
+        p_out (after event `ready`); returns the event recorded when p_out is complete."""
+        done = self._event()
+        owned.events.append(done)
+        _lib.check(self.lib.pbh_ic_owned_column(owned.handle, i, cs.data_ptr(), None, 1, p_out.data_ptr(), ready, done,
+                                                device.stream()), "pbh_ic_owned_column")
+        return done
+
+    def owned_finish(self, owned):
+        """Join the lanes; the indices of the columns the general path redid (their positions
+        changed after their done events)."""
+        m = len(owned.cols)
+        redone = np.zeros(m, dtype=np.int32)
+        _lib.check(self.lib.pbh_ic_owned_finish(owned.handle, redone.ctypes.data, device.stream()),
+                   "pbh_ic_owned_finish")
+        return [i for i in range(m) if redone[i]]
+
+    def owned_end(self, owned):
+        _lib.check(self.lib.pbh_ic_owned_destroy(owned.handle, device.stream()), "pbh_ic_owned_destroy")
+        for ev in owned.events:
+            self.lib.pbh_event_destroy(ev)
+        owned.events = []
+
+    def values_at(self, col, n, p, y):
+        """y[r] = sort(X[:, col])[p[r]] for the rows of this shard."""
+        c = col.ic_column()
+        _lib.check(self.lib.pbh_lhs_values_at(ctypes.byref(c), n, p.data_ptr(), p.shape[0], y.data_ptr(), 1,
+                                              device.stream()), "pbh_lhs_values_at")
+
+
+def _solo(world):
+    """world == 1 skips the collectives -- unless PBH_FORCE_COLLECTIVES=1, which runs them on a
+    one-rank communicator (tests: the RCCL calls, streams and events on a one-GPU box)."""
+    import os
+
+    return world == 1 and os.environ.get("PBH_FORCE_COLLECTIVES") != "1"
 
 
 def _staged(group):
@@ -151,20 +242,22 @@ def _staged(group):
     return dist.get_backend(group) == "gloo"
 
 
-def _all_gather_varlen(t, group, world):
-    """Concatenation over ranks (in rank order) of 1-D tensors of different lengths."""
+def _all_gather_varlen(t, group, world, sizes=None):
+    """Concatenation over ranks (in rank order) of 1-D tensors of different lengths (`sizes`,
+    when every rank already knows them, saves one exchange)."""
     import torch
     import torch.distributed as dist
 
-    if world == 1:
+    if _solo(world):
         return t
     dev = t.device
     if _staged(group):
         t = t.cpu()
-    size = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
-    sizes = [torch.zeros_like(size) for _ in range(world)]
-    dist.all_gather(sizes, size, group=group)
-    sizes = [int(s.item()) for s in sizes]
+    if sizes is None:
+        size = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+        got = [torch.zeros_like(size) for _ in range(world)]
+        dist.all_gather(got, size, group=group)
+        sizes = [int(s.item()) for s in got]
     m = max(max(sizes), 1)
     padded = torch.zeros(m, dtype=t.dtype, device=t.device)
     padded[:t.shape[0]] = t
@@ -173,10 +266,24 @@ def _all_gather_varlen(t, group, world):
     return torch.cat([p[:s] for p, s in zip(parts, sizes)]).to(dev)
 
 
+def _all_gather_rows(t, group, world):
+    """(world, *t.shape) stack of every rank's `t` (same shape everywhere)."""
+    import torch
+    import torch.distributed as dist
+
+    if _solo(world):
+        return t[None]
+    dev = t.device
+    src = t.cpu() if _staged(group) else t
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src, group=group)
+    return torch.stack(parts).to(dev)
+
+
 def _all_reduce(t, group, world, op="sum"):
     import torch.distributed as dist
 
-    if world > 1:
+    if not _solo(world):
         red = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
         if _staged(group) and t.device.type != "cpu":
             h = t.cpu()
@@ -207,24 +314,34 @@ class _Done:
         return None
 
 
-def _all_to_all(out, inp, out_splits, in_splits, group, world, async_op=False):
-    """all_to_all_single; with async_op the returned handle's wait() orders the caller's stream
-    after the exchange (RCCL runs it on its own stream meanwhile).  gloo (host staging) and
-    world == 1 complete before returning."""
+def _exchange(out_list, in_list, group, world, phases, after=None, side_stream=None):
+    """All-to-all of tensor lists (in_list[d] goes to rank d, out_list[s] comes from rank s).
+    `after`: an event the exchange must wait for (a lane's done event).  On RCCL the exchange is
+    asynchronous on the communicator's stream -- issued from `side_stream` when `after` is given,
+    so that the caller's stream is not held back -- and the returned handle's wait() orders the
+    caller's stream after it.  gloo (host staging) and world == 1 complete before returning."""
+    import torch
     import torch.distributed as dist
 
-    if world == 1:
-        out.copy_(inp)
-        return _Done() if async_op else out
-    if _staged(group) and out.device.type != "cpu":
-        h = out.cpu()
-        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
-        out.copy_(h)
-        return _Done() if async_op else out
-    if async_op:
-        return dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=True)
-    dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
-    return out
+    if _solo(world):
+        phases.wait(after)
+        out_list[0].copy_(in_list[0])
+        return _Done()
+    if _staged(group):
+        phases.wait(after)  # the host copy below synchronises the current stream, now after `after`
+        hin = torch.cat([t.reshape(-1) for t in in_list]).cpu()
+        hout = torch.empty(sum(t.numel() for t in out_list), dtype=hin.dtype)
+        dist.all_to_all_single(hout, hin, [t.numel() for t in out_list], [t.numel() for t in in_list], group=group)
+        off = 0
+        for t in out_list:
+            t.copy_(hout[off:off + t.numel()].view(t.shape))
+            off += t.numel()
+        return _Done()
+    if after is None:
+        return dist.all_to_all(out_list, in_list, group=group, async_op=True)
+    with torch.cuda.stream(side_stream):
+        phases.wait(after, side_stream.cuda_stream)
+        return dist.all_to_all(out_list, in_list, group=group, async_op=True)
 
 
 def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
@@ -244,38 +361,50 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
         world, rank = 1, 0
     phases = phases or HipPhases()
     K = len(columns)
-    if not (1 <= K <= 128) or n <= K:
+    if n <= K:
         raise ValueError(f"The matrix X must have rows > columns. Got shape: {(n, K)}")
+    if not 1 <= K <= 128:
+        raise ValueError(f"Iman-Conover on the device takes 1 to 128 variables, got {K}")
     rb = shard_bounds(n, world)
-    row0, nrows = rb[rank], rb[rank + 1] - rb[rank]
+    row0, row1 = rb[rank], rb[rank + 1]
+    nrows = row1 - row0
     cb = shard_bounds(K, world)
     if flags is None:
-        flags = phases.empty(K, "int32").zero_()
+        flags = phases.zeros(K, "int32")
 
-    # ---- step 1: scores of the local rows -----------------------------------------------
-    # Each rank generates its own strata [row0, row1) of the sorted column, plus stratum
-    # row0 - 1 so that adjacent pairs (ties, order) are checked across shard boundaries.
-    S = phases.empty((K, nrows))
+    # ---- step 1: tie / inversion counts of every column's strata in this shard ----------
+    # The segment starts one stratum early (row0 - 1) so that the pair across the shard
+    # boundary is counted here, and only here; a discrete column also appends its run heads.
     first_is_prev = row0 > 0
     seg_t0 = row0 - 1 if first_is_prev else row0
-    stats = np.zeros(2 * K, dtype=np.int64)
-    segments = []
+    seg_len = row1 - seg_t0
+    disc = [c for c, col in enumerate(columns) if col.dist in DISCRETE]
+    counts = phases.zeros((K, 2), "int64")
+    hcur = phases.zeros(K, "int32")
+    heads_buf = phases.empty((max(len(disc), 1), HEADS_CAP), "int32")
     for c, col in enumerate(columns):
-        seg = phases.sorted_segment(col, n, seg_t0, rb[rank + 1] - seg_t0, flags[c:c + 1])
-        stats[2 * c:2 * c + 2] = phases.sorted_check(seg)
-        segments.append(seg)
-    stats_d = torch.from_numpy(stats).to(S.device)
-    stats = _all_reduce(stats_d, group, world).cpu().numpy()
+        hb = heads_buf[disc.index(c)] if c in disc else None
+        phases.sorted_counts(col, n, seg_t0, seg_len, flags[c:c + 1], counts[c], heads=hb,
+                             hcur=hcur[c:c + 1] if hb is not None else None)
+    stats = _all_reduce(counts, group, world).cpu().numpy()
+    hc_all = _all_gather_rows(hcur, group, world).cpu().numpy()  # (world, K) appended heads per shard
+
+    S = phases.empty((K, nrows))
     for c, col in enumerate(columns):
-        if stats[2 * c + 1]:
+        if stats[c, 1]:
             raise NotImplementedError(f"column {c}: the inverse CDF is not monotone on the LHS grid; the sharded "
                                       "path needs a monotone ppf")
         heads = None
-        if stats[2 * c]:  # ties: 'average' ranks from the global run heads
-            local = phases.run_heads(segments[c], row0, first_is_prev)
-            heads = _all_gather_varlen(local, group, world)
+        if stats[c, 0]:  # ties: 'average' ranks from the global run heads
+            if c in disc and hc_all[:, c].max() <= HEADS_CAP:
+                local = heads_buf[disc.index(c)][:int(hc_all[rank, c])]
+                phases.sort_heads(local)
+                heads = _all_gather_varlen(local, group, world, sizes=[int(v) for v in hc_all[:, c]])
+            else:
+                local = phases.segment_heads(col, n, seg_t0, seg_len, first_is_prev, flags[c:c + 1])
+                heads = _all_gather_varlen(local, group, world)
         phases.scores(col, n, row0, nrows, heads, S[c])
-    del segments
+    del heads_buf
 
     # ---- step 2: E from the all-reduced Gram matrix ------------------------------------
     sums = _all_reduce(phases.column_sums(S), group, world)
@@ -287,64 +416,61 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
     phases.apply(S, L, np.asarray(P, dtype=np.float64))
 
     # ---- step 4: column owners rank their full columns, pipelined -----------------------------
-    # Exchange i (i < max k_own) moves the i-th owned column of every owner: its rows from all
-    # ranks to the owner (all-to-all), the owner ranks it, and its result rows go back (a second
-    # all-to-all).  On RCCL the exchanges run asynchronously on the communicator's stream, so
-    # column i + 1's CS arrives and column i - 1's Y leaves while column i is being ranked.
     own = [cb[o + 1] - cb[o] for o in range(world)]
     k_own, m = own[rank], max(own)
-    Y = phases.empty((K, nrows))
     rows_of = [rb[s + 1] - rb[s] for s in range(world)]
+    cs_cols = [phases.empty(n) for _ in range(k_own)]  # owned columns' scores, all rows
+    p_cols = [phases.empty(n, "int32") for _ in range(k_own)]  # their sorted positions, all rows
+    p_back = phases.empty((K, nrows), "int32")  # this shard's positions in every column
+    owned = phases.owned_begin(columns[cb[rank]:cb[rank + 1]], n) if k_own else None
+    nothing = phases.empty(0)
+    nothing32 = phases.empty(0, "int32")
 
-    def cs_exchange(i):
-        owners = [o for o in range(world) if i < own[o]]
-        send = torch.cat([S[cb[o] + i] for o in owners]) if owners else phases.empty(0)
-        in_splits = [nrows if i < own[o] else 0 for o in range(world)]
-        out_splits = [rows_of[s] if i < k_own else 0 for s in range(world)]
-        recv = phases.empty(sum(out_splits))
-        work = _all_to_all(recv, send, out_splits, in_splits, group, world, async_op=True)
-        return recv, work, send
+    def cs_lists(i):
+        send = [S[cb[o] + i] if i < own[o] else nothing for o in range(world)]
+        recv = [cs_cols[i][rb[s]:rb[s + 1]] if i < k_own else nothing for s in range(world)]
+        return recv, send
 
-    def y_exchange(i, y_col):
-        in_splits = [rows_of[s] if i < k_own else 0 for s in range(world)]
-        out_splits = [nrows if i < own[o] else 0 for o in range(world)]
-        send = y_col if i < k_own else phases.empty(0)
-        recv = phases.empty(sum(out_splits))
-        work = _all_to_all(recv, send, out_splits, in_splits, group, world, async_op=True)
-        return recv, work, send
+    def p_lists(i):
+        send = [p_cols[i][rb[s]:rb[s + 1]] if i < k_own else nothing32 for s in range(world)]
+        recv = [p_back[cb[o] + i] if i < own[o] else nothing32 for o in range(world)]
+        return recv, send
 
-    def y_scatter(i, recv):
-        off = 0
-        for o in range(world):
-            if i < own[o]:
-                Y[cb[o] + i].copy_(recv[off:off + nrows])
-                off += nrows
+    side = None
+    if not _solo(world) and not _staged(group):
+        side = torch.cuda.Stream(device=S.device)
+        side.wait_stream(torch.cuda.current_stream(S.device))
+    try:
+        # every scores exchange up front (the communicator runs them in order); then per column:
+        # rank it when its scores are in, send its positions back when its lane is done
+        cs_work = [_exchange(*cs_lists(i), group, world, phases) for i in range(m)]
+        p_work = []
+        for i in range(m):
+            cs_work[i].wait()
+            done = None
+            if i < k_own:
+                done = phases.owned_column(owned, i, cs_cols[i], p_cols[i], phases.ready(owned))
+            p_work.append(_exchange(*p_lists(i), group, world, phases, after=done, side_stream=side))
+        redone = phases.owned_finish(owned) if owned is not None else []
+        for w in p_work:
+            w.wait()
+        # a column the fast passes rejected was redone after its positions left: send it again
+        again = phases.zeros(max(m, 1), "int32")
+        for i in redone:
+            again[i] = 1
+        again = _all_reduce(again, group, world, op="max").cpu().numpy()
+        for i in range(m):
+            if again[i]:
+                _exchange(*p_lists(i), group, world, phases).wait()
+    finally:
+        if owned is not None:
+            phases.owned_end(owned)
+    del cs_cols, p_cols, S
 
-    pending_cs = cs_exchange(0) if m else None
-    pending_y = []
-    for i in range(m):
-        cur = pending_cs  # (recv, work, send): the send buffer stays referenced until the wait
-        pending_cs = cs_exchange(i + 1) if i + 1 < m else None
-        recv_cs, work_cs, _ = cur
-        work_cs.wait()
-        del cur
-        y_col = None
-        if i < k_own:
-            col = columns[cb[rank] + i]
-            sorted_full = phases.sorted_segment(col, n, 0, n, flags[cb[rank] + i:cb[rank] + i + 1])
-            y_col = phases.empty(n)
-            phases.reorder(recv_cs, sorted_full, y_col)
-            del sorted_full
-        del recv_cs
-        pending_y.append((i,) + y_exchange(i, y_col))
-        while len(pending_y) > 2:  # bound the buffers in flight
-            j, recv_y, work_y, _ = pending_y.pop(0)
-            work_y.wait()
-            y_scatter(j, recv_y)
-    for j, recv_y, work_y, _ in pending_y:
-        work_y.wait()
-        y_scatter(j, recv_y)
-    del S
+    # ---- Y of this shard: sort(X)[p] regenerated from the positions ----------------------
+    Y = phases.empty((K, nrows))
+    for c, col in enumerate(columns):
+        phases.values_at(col, n, p_back[c], Y[c])
     _all_reduce_flags(flags, group, world)
     return Y
 

@@ -45,31 +45,49 @@ def _ppf(col, q):
 
 
 class CpuPhases:
-    def __init__(self, perms, us):
+    """redo: owned column indices whose first ranking is "rejected" (garbage positions leave
+    first, the correct ones after owned_finish), to exercise the re-send of a redone column."""
+
+    def __init__(self, perms, us, redo=()):
         self.perms = perms
         self.us = us
         self.inv = [np.argsort(p) for p in perms]
+        self.redo = set(redo)
 
     def empty(self, shape, dtype="float64"):
         return torch.empty(shape, dtype=getattr(torch, dtype))
 
-    def sorted_segment(self, col, n, t0, nt, flag):
-        t = np.arange(t0, t0 + nt)
+    def zeros(self, shape, dtype="float64"):
+        return torch.zeros(shape, dtype=getattr(torch, dtype))
+
+    def _sorted(self, col, n, t):
         rows = self.inv[col.lhs_col][t]
         q = (t + 1 - self.us[col.lhs_col][rows]) / n
-        x = _ppf(col, q)
+        return _ppf(col, q)
+
+    # -- step 1
+    def sorted_counts(self, col, n, t0, nt, flag, counts, heads=None, hcur=None):
+        x = self._sorted(col, n, np.arange(t0, t0 + nt))
         if not np.isfinite(x).all():
             flag |= 1  # the kernels' atomicOr of bit 0
-        return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64))
+        counts[0] = int((x[:-1] == x[1:]).sum())
+        counts[1] = int((~(x[:-1] <= x[1:])).sum())
+        if heads is not None:
+            h = np.flatnonzero(x[1:] != x[:-1]) + t0 + 1
+            if t0 == 0:
+                h = np.concatenate([[0], h])
+            h = h[::-1]  # appended out of order, as the kernel's atomics do
+            cap = heads.shape[0]
+            heads[:min(len(h), cap)] = torch.from_numpy(h[:cap].astype(np.int32))
+            hcur[0] = len(h)
 
-    def sorted_check(self, x):
-        a = x.numpy()
-        return int((a[:-1] == a[1:]).sum()), int((~(a[:-1] <= a[1:])).sum())
+    def sort_heads(self, heads):
+        heads.copy_(torch.sort(heads).values)
 
-    def run_heads(self, x, t0, first_is_prev):
-        a = x.numpy()
+    def segment_heads(self, col, n, t0, nt, first_is_prev, flag):
+        a = self._sorted(col, n, np.arange(t0, t0 + nt))
         if first_is_prev:
-            h = np.flatnonzero(a[1:] != a[:-1]) + t0
+            h = np.flatnonzero(a[1:] != a[:-1]) + t0 + 1
         else:
             h = np.concatenate([[0], np.flatnonzero(a[1:] != a[:-1]) + 1]) + t0
         return torch.from_numpy(h.astype(np.int32))
@@ -86,6 +104,7 @@ class CpuPhases:
             rank = (s + 1).astype(float) + (e - s) / 2.0
         out.copy_(torch.from_numpy(scipy.special.ndtri(rank / (n + 1))))
 
+    # -- steps 2 and 3
     def column_sums(self, S):
         return torch.from_numpy(S.numpy().sum(axis=1))
 
@@ -107,6 +126,32 @@ class CpuPhases:
         D = scipy.linalg.solve_triangular(L, S.numpy(), lower=True)
         S.copy_(torch.from_numpy(np.tril(P) @ D))
 
-    def reorder(self, cs, sorted_src, out):
+    # -- step 4 (synchronous: no events)
+    def ready(self, owned):
+        return None
+
+    def wait(self, ev, stream=None):
+        pass
+
+    def owned_begin(self, cols, n):
+        return {"cols": cols, "n": n, "pending": {}}
+
+    def owned_column(self, owned, i, cs, p_out, ready):
         idx = rankdata_average(cs.numpy()).astype(int) - 1
-        out.copy_(torch.from_numpy(sorted_src.numpy()[idx]))
+        if i in self.redo:
+            owned["pending"][i] = (p_out, idx)
+            p_out.fill_(0)  # what leaves first: wrong
+        else:
+            p_out.copy_(torch.from_numpy(idx.astype(np.int32)))
+        return None
+
+    def owned_finish(self, owned):
+        for p_out, idx in owned["pending"].values():
+            p_out.copy_(torch.from_numpy(idx.astype(np.int32)))
+        return sorted(owned["pending"])
+
+    def owned_end(self, owned):
+        pass
+
+    def values_at(self, col, n, p, y):
+        y.copy_(torch.from_numpy(self._sorted(col, n, p.numpy().astype(np.int64))))

@@ -89,6 +89,7 @@ def test_dead_draw_still_generated():
     lambda: m.Distribution("norm") < 0.5,  # bool result
     lambda: m.Distribution("norm", loc=m.Distribution("uniform")) * 2.0,  # composite parameter
     lambda: m.Add(1.0, 2.0, m.Distribution("norm")),  # first partial is a numpy scalar
+    lambda: m.Avg(1.0, 2.0, m.Distribution("norm")),  # Avg's first partial sum is a scalar too
     lambda: m.Abs(m.Constant(-1.0)) + m.Distribution("norm"),  # transform of a constant
     lambda: m.Add(*[d * 2.0 for d in [m.Distribution("norm", i) for i in range(20)]])
     + m.Multiply(*[m.Distribution("norm", i) for i in range(20)]),  # fits (each draw read once)

@@ -16,42 +16,94 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SPEC = [(0, [0.0, 1.0]), (5, [2.0, 0.0, 1.0]), (4, [0.3, 0.0, 1.0]), (6, [4.0, 0.0]), (0, [5.0, 2.0]),
-        (5, [0.7, 0.0, 3.0]), (4, [0.8, 1.0, 2.0]), (6, [30.0, 0.0])]
+SPECS = {
+    # the cfg2 set: continuous columns and poisson columns with runs (run heads from every shard)
+    "cfg2": [(0, [0.0, 1.0]), (5, [2.0, 0.0, 1.0]), (4, [0.3, 0.0, 1.0]), (6, [4.0, 0.0]), (0, [5.0, 2.0]),
+             (5, [0.7, 0.0, 3.0]), (4, [0.8, 1.0, 2.0]), (6, [30.0, 0.0])],
+    # a leading poisson column: its correlated score IS its tied scores (runs of equal codes beyond
+    # the finish), so the owner's fast passes reject it and the general path redoes it
+    "tied_first": [(6, [4.0, 0.0]), (0, [0.0, 1.0]), (5, [2.0, 0.0, 1.0]), (4, [0.3, 0.0, 1.0])],
+}
+SPEC = SPECS["cfg2"]
 N = 300_007
 SEED = 12345
 
 
-def _target():
+def _target(k=len(SPEC)):
     from oracle.pipeline import cfg3_corr
 
-    return cfg3_corr(len(SPEC))
+    return cfg3_corr(k)
 
 
-def _single_call():
+def _single_call(spec=SPEC):
     from probabilit_amd import _lib, device
     from probabilit_amd.correlation import ImanConover
 
-    flags = device.zeros(len(SPEC), "int32")
+    flags = device.zeros(len(spec), "int32")
     cols = [_lib.ICColumn(SEED, c, d, (ctypes.c_double * 3)(*p), len(p), flags.data_ptr() + 4 * c)
-            for c, (d, p) in enumerate(SPEC)]
-    Y = ImanConover().set_target(_target())._transform_generated(cols, N)
+            for c, (d, p) in enumerate(spec)]
+    Y = ImanConover().set_target(_target(len(spec)))._transform_generated(cols, N)
     return device.to_host(Y)
 
 
-def _columns():
+def _columns(spec=SPEC):
     from probabilit_amd.distributed import LHSColumn
 
-    return [LHSColumn(SEED, c, d, p) for c, (d, p) in enumerate(SPEC)]
+    return [LHSColumn(SEED, c, d, p) for c, (d, p) in enumerate(spec)]
 
 
-def test_world1_matches_single_call(gpu):
+@pytest.mark.parametrize("spec", sorted(SPECS))
+def test_world1_matches_single_call(gpu, spec):
+    """The sharded orchestration on one rank (owned-column step 4 with positions sent back and
+    Y regenerated from them) equals the single-call fast path bit for bit."""
     from probabilit_amd import device
     from probabilit_amd.distributed import iman_conover_lhs
 
-    ref = _single_call()
-    Y = iman_conover_lhs(_columns(), np.linalg.cholesky(_target()), N)
+    sp = SPECS[spec]
+    ref = _single_call(sp)
+    Y = iman_conover_lhs(_columns(sp), np.linalg.cholesky(_target(len(sp))), N)
     np.testing.assert_array_equal(device.to_host(Y), ref)
+
+
+def test_owned_columns_values_and_positions(gpu):
+    """pbh_ic_owned_* directly: a column ranked into Y (gen_place) and the same column ranked
+    into positions p then regenerated (pbh_lhs_values_at) agree, and equal the single call;
+    the tied leading column is reported redone by the general path."""
+    import torch
+
+    from probabilit_amd import _lib, device
+    from probabilit_amd.correlation import ImanConover
+    from probabilit_amd.distributed import HipPhases
+
+    sp = SPECS["tied_first"]
+    cols = _columns(sp)
+    lib = _lib.load()
+    flags = device.zeros(len(sp), "int32")
+    icc = [_lib.ICColumn(SEED, c, d, (ctypes.c_double * 3)(*p), len(p), flags.data_ptr() + 4 * c)
+           for c, (d, p) in enumerate(sp)]
+    inst = ImanConover().set_target(_target(len(sp)))
+    CS = device.empty((len(sp), N))
+    Yref = device.to_host(inst._transform_generated(icc, N, debug={"CS": CS}))
+    ph = HipPhases()
+    for mode in ("y", "p"):
+        owned = ph.owned_begin(cols, N)
+        Y = device.empty((len(sp), N))
+        P = device.empty((len(sp), N), "int32")
+        for i in range(len(sp)):
+            done = ph._event()
+            owned.events.append(done)
+            yp = Y[i].data_ptr() if mode == "y" else None
+            pp = P[i].data_ptr() if mode == "p" else None
+            _lib.check(lib.pbh_ic_owned_column(owned.handle, i, CS[i].data_ptr(), yp, 1, pp, None, done,
+                                               device.stream()))
+        redone = ph.owned_finish(owned)
+        ph.owned_end(owned)
+        assert redone == [0]
+        if mode == "p":
+            for c, col in enumerate(cols):
+                ph.values_at(col, N, P[c], Y[c])
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(device.to_host(Y), Yref)
 
 
 def _free_port():
@@ -60,16 +112,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, spec="cfg2", backend="gloo"):
+    import torch
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         from probabilit_amd import device
         from probabilit_amd.distributed import iman_conover_lhs
 
-        Y = iman_conover_lhs(_columns(), np.linalg.cholesky(_target()), N)
+        sp = SPECS[spec]
+        Y = iman_conover_lhs(_columns(sp), np.linalg.cholesky(_target(len(sp))), N, group=dist.group.WORLD)
         np.save(os.path.join(outdir, f"y{rank}.npy"), device.to_host(Y))
     finally:
         dist.destroy_process_group()
@@ -133,15 +189,66 @@ def test_dag_row_sharded_world2_matches_one_process(gpu):
                 np.testing.assert_array_equal(np.load(os.path.join(d, f"correlated{r}_v{j}.npy")), ref[b[r]:b[r + 1]])
 
 
-def test_world2_on_one_gpu_matches_single_call(gpu):
+@pytest.mark.parametrize("spec", sorted(SPECS))
+def test_world2_on_one_gpu_matches_single_call(gpu, spec):
     import torch.multiprocessing as mp
 
     from probabilit_amd.distributed import shard_bounds
 
-    ref = _single_call()
+    ref = _single_call(SPECS[spec])
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(2, _free_port(), d), nprocs=2, join=True, start_method="spawn")
+        mp.start_processes(_worker, args=(2, _free_port(), d, spec), nprocs=2, join=True, start_method="spawn")
         parts = [np.load(os.path.join(d, f"y{r}.npy")) for r in range(2)]
     b = shard_bounds(N, 2)
     for r in range(2):
         np.testing.assert_array_equal(parts[r], ref[:, b[r]:b[r + 1]])
+
+
+def test_rccl_one_rank_forced_collectives(gpu, monkeypatch):
+    """The RCCL branch on the box's one GPU: a one-rank "nccl" (RCCL) communicator with
+    PBH_FORCE_COLLECTIVES=1 runs every collective of the sharded path for real -- the async
+    all-to-alls on the communicator's stream, the side stream that waits for a lane's done
+    event, the work handles' waits -- and the result equals the single call."""
+    import torch.multiprocessing as mp
+
+    ref = _single_call(SPECS["cfg2"])
+    monkeypatch.setenv("PBH_FORCE_COLLECTIVES", "1")
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(1, _free_port(), d, "cfg2", "nccl"), nprocs=1, join=True,
+                           start_method="spawn")
+        part = np.load(os.path.join(d, "y0.npy"))
+    np.testing.assert_array_equal(part, ref)
+
+
+def test_bench_gpus2_rehearsal_matches_one_gpu(gpu):
+    """`bench.py --gpus 2` started without torch.distributed.run launches its two ranks itself
+    (here sharing the box's one GPU over gloo), reports n_gpus 2, and each rank's rows of every
+    column equal the one-process result on the same seed bit for bit (SHA-1 per column)."""
+    import hashlib
+    import json
+    import subprocess
+    import sys
+
+    from probabilit_amd.distributed import shard_bounds
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rows = 2_000_000
+    with tempfile.TemporaryDirectory() as d:
+        cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--rows", str(rows), "--steps", "1",
+               "--warmup", "0", "--no-cpu", "--no-e2e", "--ppf-rows", "0", "--check-out", d]
+        env = dict(os.environ)
+        env.pop("WORLD_SIZE", None)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+        assert r.returncode == 0, r.stderr[-4000:]
+        line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        assert line["n_gpus"] == 2 and line["config"]["rows"] == rows
+        ranks = [json.load(open(os.path.join(d, f"rank{k}.json"))) for k in range(2)]
+    from oracle.pipeline import cfg3_corr, cfg_dists
+    from probabilit_amd.modeling import Distribution, NoOp
+
+    ds = [Distribution(name, **kw) for name, kw in cfg_dists(32)]
+    NoOp(*ds).correlate(*ds, corr_mat=cfg3_corr(32)).sample_device(rows, random_state=ranks[0]["seed"], method="lhs")
+    b = shard_bounds(rows, 2)
+    for k in range(2):
+        want = [hashlib.sha1(x.samples_device[b[k]:b[k + 1]].cpu().numpy().tobytes()).hexdigest() for x in ds]
+        assert ranks[k]["sha1"] == want, f"rank {k}"
