@@ -137,6 +137,8 @@ def main():
         sys.exit(launch_ranks(args.gpus))
 
     import numpy as np
+
+    import probabilit_amd  # noqa: F401  (first: it sets the HIP queue count before the runtime starts)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -8,7 +8,16 @@ All sampling runs in hand-written HIP kernels (libprobabilit_hip.so, C-ABI in
 include/probabilit_hip.h); see DESIGN.md.
 """
 
-from .modeling import (  # noqa: F401
+import os as _os
+
+# The step-4 lanes, the deferred counts' stream, torch's stream and (row-sharded runs) RCCL's
+# stream and the exchange-issue stream run concurrently: more than HIP's default of 4 hardware
+# queues per process, beyond which two streams share a queue and serialise (measured 1.5-4 ms per
+# cfg3 step, profiles/r03).  Read when the HIP runtime initialises, i.e. at the first GPU call:
+# effective when this package is imported first; an explicit setting is kept.
+_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+from .modeling import (  # noqa: F401,E402
     Constant,
     CumulativeDistribution,
     DiscreteDistribution,

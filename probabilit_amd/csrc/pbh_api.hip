@@ -406,9 +406,16 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     }
   } ev_scores, ev_counts;
   ev_counts.wait_on = s;
-  // the last side stream: step 4's lanes use streams 0 .. step4_streams() - 1 (3 by default), so
-  // the counts never queue ahead of a step-4 column
-  hipStream_t side = any_deferred ? step4_side_stream(kStep4MaxStreams - 1) : nullptr;
+  // PBH_COUNTS_STREAM (A/B): the side stream of the deferred counts -- lane 0 (default: the counts
+  // run ahead of lane 0's first column) or the last one (never a step-4 lane with the default 3
+  // lanes, but a 5th stream next to the caller's and the lanes, beyond the runtime's 4 hardware
+  // queues: two streams then share a queue and serialise, measured 4-5 ms per step slower)
+  static const int counts_stream = [] {  // lane 0: 161-162 ms per step against 166 on its own queue (r3 ab1)
+    const char* e = getenv("PBH_COUNTS_STREAM");
+    const int v = e ? atoi(e) : 0;
+    return v < 0 ? 0 : (v >= kStep4MaxStreams ? kStep4MaxStreams - 1 : v);
+  }();
+  hipStream_t side = any_deferred ? step4_side_stream(counts_stream) : nullptr;
   auto launch_counts = [&]() -> int {  // the deferred columns' counts on `side`, after s's work so far
     sync_on_exit.side = true;
     PBH_CHECK_HIP(hipEventCreateWithFlags(&ev_scores.e, hipEventDisableTiming));
@@ -514,14 +521,22 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     step4_gen_carve_shared(L.s4shared, k, sh);
     Step4Lanes lanes(n, L.s4column, nullptr, s);
     sync_on_exit.side = sync_on_exit.side || lanes.ns > 1;
-    st = step4_gen_hist(L.codes, n, L.S, n, n, sh, 0, k, s);
+    st = step4_gen_hist(L.codes, n, nullptr, n, n, sh, 0, k, s);
     if (st) return st;
+    // one readback of the flatness verdicts: the adaptive re-code is launched only for the
+    // columns that need it (the gated kernels would otherwise be dispatched for every column)
+    PBH_CHECK_HIP(hipMemcpyAsync(state.data(), sh.state, (size_t)k * 4, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
     st = lanes.begin();
     if (st) return st;
     for (int c = 0; c < k; ++c) {
       if (!regenerable[c]) continue;
       const int i = lanes.next();
       hipStream_t cs_ = lanes.ss[i];
+      if (state[c]) {
+        st = step4_gen_adapt(L.codes + (int64_t)c * n, n, L.S + (int64_t)c * n, n, n, sh, c, 1, cs_);
+        if (st) return st;
+      }
       st = step4_gen_column(c, L.codes + (int64_t)c * n, L.S + (int64_t)c * n, n, sh, lanes.cb[i], cs_);
       if (st) return st;
       int buf = 0;

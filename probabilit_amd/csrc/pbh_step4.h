@@ -69,6 +69,10 @@ void step4_sync_side_streams();
 // the device (the codes are rewritten in place); state / flags then hold the final verdict.
 int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,
                    int c0, int kk, hipStream_t s);
+// the adaptive re-code alone (after step4_gen_hist without cs): a column's lane runs it, so the
+// rare re-coded column's passes overlap the other lanes; ~6 launches that exit at once otherwise
+int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,
+                    int c0, int kk, hipStream_t s);
 // code passes and bucket finish of column c: (row << 32 | p') pairs in cb.pairs[0], in position
 // order, or (step4_fused) grouped by the top row-placement level
 int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, const Step4Shared& sh,

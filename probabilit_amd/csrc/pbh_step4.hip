@@ -134,6 +134,51 @@ __global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ co
   if (threadIdx.x == 0 && ovf) atomicOr(&state[c], 1);
 }
 
+// The gated re-count of k_hist16 (the adaptive code map's second count): the same counts in four
+// quarters of the 65536 buckets (blockIdx.z), 16-bit packed in 32 KiB of LDS instead of 128 KiB --
+// the gate is only known on the device, so every column's blocks are dispatched, and a no-op block
+// holding 136 KiB of LDS would wait for an almost empty CU; the tile-class counts in quarter 0.
+__global__ __launch_bounds__(1024) void k_hist16_q(const uint32_t* __restrict__ codes, int64_t ld, int64_t n,
+                                                   uint32_t* __restrict__ hist, uint32_t* __restrict__ cls,
+                                                   int32_t* __restrict__ state, const int32_t* __restrict__ gate) {
+  __shared__ uint32_t w[8192];
+  __shared__ uint32_t cw[8 * 256];
+  __shared__ int ovf;
+  const int c = blockIdx.y;
+  if (!gate[c]) return;
+  const uint32_t q = blockIdx.z;
+  const uint32_t* cc = codes + (int64_t)c * ld;
+  for (int i = threadIdx.x; i < 8192; i += 1024) w[i] = 0;
+  for (int i = threadIdx.x; i < 8 * 256; i += 1024) cw[i] = 0;
+  if (threadIdx.x == 0) ovf = 0;
+  __syncthreads();
+  const int64_t chunk = ((n + gridDim.x - 1) / gridDim.x + 3) & ~(int64_t)3;
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  bool bad = false;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 1024) {
+    const uint32_t code = cc[i];
+    const uint32_t b = code >> 16;
+    if (q == 0) atomicAdd(&cw[(((uint32_t)(i / kTile1) & 7u) << 8) | (code >> 24)], 1u);
+    if ((b >> 14) != q) continue;
+    const uint32_t l = b & 16383u, sh = (l & 1u) * 16u;
+    const uint32_t old = atomicAdd(&w[l >> 1], 1u << sh);
+    bad |= ((old >> sh) & 0xFFFFu) == 0xFFFFu;
+  }
+  if (bad) ovf = 1;
+  __syncthreads();
+  uint32_t* hc = hist + (int64_t)c * 65536 + q * 16384;
+  for (int j = threadIdx.x; j < 8192; j += 1024) {
+    const uint32_t v = w[j];
+    if (v & 0xFFFFu) atomicAdd(&hc[2 * j], v & 0xFFFFu);
+    if (v >> 16) atomicAdd(&hc[2 * j + 1], v >> 16);
+  }
+  if (q == 0)
+    for (int j = threadIdx.x; j < 8 * 256; j += 1024)
+      if (cw[j]) atomicAdd(&cls[(int64_t)c * 2048 + j], cw[j]);
+  if (threadIdx.x == 0 && ovf) atomicOr(&state[c], 1);
+}
+
 // One 1024-thread block per column: start[b] = exclusive prefix of the 65536 bucket counts
 // (start[65536] = n), the msd2 tile map (tiles of kTile1 inside every top-byte group: tpre[g]
 // = tiles before group g), and state bit 1 when a bucket exceeds kBucketCap2.
@@ -1395,7 +1440,6 @@ int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs,
   uint32_t* cls = sh.cls + (int64_t)c0 * 2048;
   int32_t* state = sh.state + c0;
   int32_t* flags = sh.flags + c0;
-  int32_t* retry = sh.retry + c0;
   PBH_CHECK_HIP(hipMemsetAsync(hist, 0, (size_t)kk * 65536 * 4, s));
   PBH_CHECK_HIP(hipMemsetAsync(sh.cur1 + c0 * cw, 0, kk * cw * 4, s));
   PBH_CHECK_HIP(hipMemsetAsync(sh.cur2 + (int64_t)c0 * 65536, 0, (size_t)kk * 65536 * 4, s));
@@ -1409,23 +1453,36 @@ int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs,
   int64_t blocks = (n + 65535) / 65536;
   if (blocks > 64) blocks = 64;
   if (blocks < 1) blocks = 1;
-  auto count = [&](const int32_t* gate) -> int {
-    PBH_TIMED(kKHist16, s,
-              hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)kk), dim3(1024), 0, s, codes, ldc, n, hist,
-                                 cls, state, gate));
-    PBH_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)kk), dim3(1024), 0, s, hist, n, sh.start + (int64_t)c0 * 65537,
-                       sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, gate);
-    PBH_CHECK_LAUNCH();
-    return PBH_OK;
-  };
-  int st = count(nullptr);
-  if (st) return st;
+  PBH_TIMED(kKHist16, s,
+            hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)kk), dim3(1024), 0, s, codes, ldc, n, hist,
+                               cls, state, nullptr));
+  PBH_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)kk), dim3(1024), 0, s, hist, n, sh.start + (int64_t)c0 * 65537,
+                     sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, nullptr);
+  PBH_CHECK_LAUNCH();
+  if (!cs) return PBH_OK;
+  return step4_gen_adapt(codes, ldc, cs, ldcs, n, sh, c0, kk, s);
+}
+
+int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,
+                    int c0, int kk, hipStream_t s) {
+  PBH_REQUIRE(c0 >= 0 && kk >= 1 && c0 + kk <= sh.k, "step4_gen_adapt: columns [%d, %d) outside [0, %d)", c0,
+              c0 + kk, sh.k);
   static const bool adapt = [] {
     const char* e = getenv("PBH_ADAPT");  // "0": a column that is not flat goes to the general path
     return !(e && e[0] == '0');
   }();
-  if (!cs || !adapt) return PBH_OK;
+  if (!adapt) return PBH_OK;
+  const int cpad = cur_pad();
+  const size_t cw = (size_t)8 * 256 * cpad;
+  uint32_t* hist = sh.hist + (int64_t)c0 * 65536;
+  uint32_t* cls = sh.cls + (int64_t)c0 * 2048;
+  int32_t* state = sh.state + c0;
+  int32_t* flags = sh.flags + c0;
+  int32_t* retry = sh.retry + c0;
+  int64_t blocks = (n + 65535) / 65536;
+  if (blocks > 64) blocks = 64;
+  if (blocks < 1) blocks = 1;
   // the re-code of the columns that are not flat: every kernel exits at once for the others
   hipLaunchKernelGGL(k_adapt_reset, dim3((unsigned)kk), dim3(1024), 0, s, state, flags, retry, hist,
                      sh.cur1 + c0 * cw, sh.cur2 + (int64_t)c0 * 65536, sh.curF + c0 * cw, cls,
@@ -1442,7 +1499,14 @@ int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs,
   hipLaunchKernelGGL(k_make_codes_adapt, dim3((unsigned)(cb < 1024 ? (cb < 1 ? 1 : cb) : 1024), (unsigned)kk),
                      dim3(256), 0, s, cs, ldcs, n, retry, amap, codes, ldc);
   PBH_CHECK_LAUNCH();
-  return count(retry);
+  PBH_TIMED(kKHist16, s,
+            hipLaunchKernelGGL(k_hist16_q, dim3((unsigned)blocks, (unsigned)kk, 4), dim3(1024), 0, s, codes, ldc, n, hist,
+                               cls, state, retry));
+  PBH_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)kk), dim3(1024), 0, s, hist, n, sh.start + (int64_t)c0 * 65537,
+                     sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, retry);
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
 }
 
 int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, const Step4Shared& sh,

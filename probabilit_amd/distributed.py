@@ -344,14 +344,25 @@ def _exchange(out_list, in_list, group, world, phases, after=None, side_stream=N
         return dist.all_to_all(out_list, in_list, group=group, async_op=True)
 
 
-def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
+class _Redo(Exception):
+    """A deferred tie / inversion count was non-zero: the scores assumed untied are wrong."""
+
+
+def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None, defer=None):
     """Correlate K generated LHS columns of an N-row design to the target whose Cholesky
     factor is P (K x K), returning this rank's rows of the result, shape (K, rows).
 
     columns: list of LHSColumn (same on every rank); flags: optional int32 tensor of K
     non-finite flag words (OR-combined over ranks on return, bits unchanged).  Raises ValueError exactly where
-    ImanConover.__call__ does (rank-correlation matrix not positive definite)."""
-    import torch
+    ImanConover.__call__ does (rank-correlation matrix not positive definite).
+
+    defer (default: on for the HIP phases, PBH_DEFER_COUNTS=0 turns it off): the continuous
+    columns' tie / inversion counts -- an event of probability ~1e-8 per column at N = 1e8 --
+    run on a side stream after step 3, next to the first exchange and the owners' ranking,
+    their scores computed as untied; the summed counts are checked at the end and a non-zero
+    one (on any rank: the sum is global) redoes the call with every count first, as the
+    single-GPU call does (pbh_iman_conover, PBH_DEFER_COUNTS)."""
+    import os
 
     if group is not None or _dist_initialized():
         import torch.distributed as dist
@@ -360,17 +371,31 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
     else:
         world, rank = 1, 0
     phases = phases or HipPhases()
+    if defer is None:
+        defer = isinstance(phases, HipPhases) and os.environ.get("PBH_DEFER_COUNTS", "3") != "0"
     K = len(columns)
     if n <= K:
         raise ValueError(f"The matrix X must have rows > columns. Got shape: {(n, K)}")
     if not 1 <= K <= 128:
         raise ValueError(f"Iman-Conover on the device takes 1 to 128 variables, got {K}")
+    if flags is None:
+        flags = phases.zeros(K, "int32")
+    if defer:
+        try:
+            return _iman_conover_lhs(columns, P, n, group, world, rank, phases, flags, True)
+        except _Redo:
+            flags.zero_()
+    return _iman_conover_lhs(columns, P, n, group, world, rank, phases, flags, False)
+
+
+def _iman_conover_lhs(columns, P, n, group, world, rank, phases, flags, defer):
+    import torch
+
+    K = len(columns)
     rb = shard_bounds(n, world)
     row0, row1 = rb[rank], rb[rank + 1]
     nrows = row1 - row0
     cb = shard_bounds(K, world)
-    if flags is None:
-        flags = phases.zeros(K, "int32")
 
     # ---- step 1: tie / inversion counts of every column's strata in this shard ----------
     # The segment starts one stratum early (row0 - 1) so that the pair across the shard
@@ -379,10 +404,13 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
     seg_t0 = row0 - 1 if first_is_prev else row0
     seg_len = row1 - seg_t0
     disc = [c for c, col in enumerate(columns) if col.dist in DISCRETE]
+    late = [c for c in range(K) if defer and c not in disc]  # counted after step 3
     counts = phases.zeros((K, 2), "int64")
     hcur = phases.zeros(K, "int32")
     heads_buf = phases.empty((max(len(disc), 1), HEADS_CAP), "int32")
     for c, col in enumerate(columns):
+        if c in late:
+            continue
         hb = heads_buf[disc.index(c)] if c in disc else None
         phases.sorted_counts(col, n, seg_t0, seg_len, flags[c:c + 1], counts[c], heads=hb,
                              hcur=hcur[c:c + 1] if hb is not None else None)
@@ -415,13 +443,24 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
     # ---- step 3: correlated scores of the local rows ------------------------------------
     phases.apply(S, L, np.asarray(P, dtype=np.float64))
 
+    # the deferred counts, on a side stream next to the exchanges and the owners' ranking
+    cstream = None
+    if late:
+        dcounts = phases.zeros((K, 2), "int64")
+        if isinstance(phases, HipPhases):
+            cstream = torch.cuda.Stream(device=S.device)
+            cstream.wait_stream(torch.cuda.current_stream(S.device))
+        with torch.cuda.stream(cstream) if cstream is not None else _nullcontext():
+            for c in late:
+                phases.sorted_counts(columns[c], n, seg_t0, seg_len, flags[c:c + 1], dcounts[c])
+
     # ---- step 4: column owners rank their full columns, pipelined -----------------------------
     own = [cb[o + 1] - cb[o] for o in range(world)]
     k_own, m = own[rank], max(own)
-    rows_of = [rb[s + 1] - rb[s] for s in range(world)]
     cs_cols = [phases.empty(n) for _ in range(k_own)]  # owned columns' scores, all rows
     p_cols = [phases.empty(n, "int32") for _ in range(k_own)]  # their sorted positions, all rows
     p_back = phases.empty((K, nrows), "int32")  # this shard's positions in every column
+    Y = phases.empty((K, nrows))
     owned = phases.owned_begin(columns[cb[rank]:cb[rank + 1]], n) if k_own else None
     nothing = phases.empty(0)
     nothing32 = phases.empty(0, "int32")
@@ -436,13 +475,20 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
         recv = [p_back[cb[o] + i] if i < own[o] else nothing32 for o in range(world)]
         return recv, send
 
+    def values(i):  # Y of this shard in every owner's i-th column: sort(X)[p] regenerated
+        for o in range(world):
+            if i < own[o]:
+                c = cb[o] + i
+                phases.values_at(columns[c], n, p_back[c], Y[c])
+
     side = None
     if not _solo(world) and not _staged(group):
         side = torch.cuda.Stream(device=S.device)
         side.wait_stream(torch.cuda.current_stream(S.device))
     try:
         # every scores exchange up front (the communicator runs them in order); then per column:
-        # rank it when its scores are in, send its positions back when its lane is done
+        # rank it when its scores are in, send its positions back when its lane is done, and
+        # regenerate this shard's Y of every owner's i-th column when those positions are in
         cs_work = [_exchange(*cs_lists(i), group, world, phases) for i in range(m)]
         p_work = []
         for i in range(m):
@@ -451,9 +497,10 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
             if i < k_own:
                 done = phases.owned_column(owned, i, cs_cols[i], p_cols[i], phases.ready(owned))
             p_work.append(_exchange(*p_lists(i), group, world, phases, after=done, side_stream=side))
+        for i in range(m):
+            p_work[i].wait()
+            values(i)
         redone = phases.owned_finish(owned) if owned is not None else []
-        for w in p_work:
-            w.wait()
         # a column the fast passes rejected was redone after its positions left: send it again
         again = phases.zeros(max(m, 1), "int32")
         for i in redone:
@@ -462,17 +509,28 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None):
         for i in range(m):
             if again[i]:
                 _exchange(*p_lists(i), group, world, phases).wait()
+                values(i)
     finally:
         if owned is not None:
             phases.owned_end(owned)
     del cs_cols, p_cols, S
 
-    # ---- Y of this shard: sort(X)[p] regenerated from the positions ----------------------
-    Y = phases.empty((K, nrows))
-    for c, col in enumerate(columns):
-        phases.values_at(col, n, p_back[c], Y[c])
+    if late:  # the deferred counts, summed over every rank's segments
+        if cstream is not None:
+            torch.cuda.current_stream(Y.device).wait_stream(cstream)
+        dstats = _all_reduce(dcounts, group, world).cpu().numpy()
+        if dstats.any():
+            raise _Redo()
     _all_reduce_flags(flags, group, world)
     return Y
+
+
+class _nullcontext:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 def _dist_initialized():

@@ -38,7 +38,7 @@ def _columns(spec):
     return [LHSColumn(0, c, d, p) for c, (d, p) in enumerate(spec)]
 
 
-def _worker(rank, world, port, case, outdir, redo=()):
+def _worker(rank, world, port, case, outdir, redo=(), defer=False):
     import torch
     import torch.distributed as dist
 
@@ -52,19 +52,24 @@ def _worker(rank, world, port, case, outdir, redo=()):
         perms, us = design(n, len(spec), seed=3)
         P = np.linalg.cholesky(cfg3_corr(len(spec)))
         flags = torch.zeros(len(spec), dtype=torch.int32)
-        Y = iman_conover_lhs(_columns(spec), P, n, phases=CpuPhases(perms, us, redo=redo if rank == 0 else ()),
-                             flags=flags)
+        # with defer, rank 0's first count of column 0 (continuous in every case) reports a false
+        # tie: the deferred check must redo the whole call on every rank
+        ph = CpuPhases(perms, us, redo=redo if rank == 0 else (), fake_tie=0 if (defer and rank == 0) else None)
+        Y = iman_conover_lhs(_columns(spec), P, n, phases=ph, flags=flags, defer=defer)
         np.save(os.path.join(outdir, f"y{rank}.npy"), Y.numpy())
         np.save(os.path.join(outdir, f"f{rank}.npy"), flags.numpy())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,redo", [(1, ()), (2, ()), (3, ()), (4, ()), (2, (0,)), (3, (1,))])
+@pytest.mark.parametrize("world,redo,defer", [(1, (), False), (2, (), False), (3, (), False), (4, (), False),
+                                              (2, (0,), False), (3, (1,), False), (1, (), True), (3, (), True)])
 @pytest.mark.parametrize("case", sorted(CASES))
-def test_sharded_ic_matches_single_process_oracle(world, redo, case):
+def test_sharded_ic_matches_single_process_oracle(world, redo, defer, case):
     """redo: rank 0 "rejects" its owned column index `redo` on the fast path (garbage positions
-    leave first, the general path's after finish): the re-send must repair every rank's rows."""
+    leave first, the general path's after finish): the re-send must repair every rank's rows.
+    defer: the continuous columns' counts run after step 3; rank 0 reports a false tie in the
+    deferred count, so every rank must redo the call with the counts first."""
     from dist_cpu_phases import column_values, design
     from probabilit_amd.distributed import shard_bounds
 
@@ -74,7 +79,7 @@ def test_sharded_ic_matches_single_process_oracle(world, redo, case):
     X = np.column_stack([column_values(c, perms, us, n) for c in cols])
     ref = iman_conover(X, cfg3_corr(len(spec)))["Y"]
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), case, d, redo), nprocs=world, join=True,
+        mp.start_processes(_worker, args=(world, _free_port(), case, d, redo, defer), nprocs=world, join=True,
                            start_method="spawn")
         parts = [np.load(os.path.join(d, f"y{r}.npy")) for r in range(world)]
         flags = [np.load(os.path.join(d, f"f{r}.npy")).tolist() for r in range(world)]
