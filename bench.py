@@ -211,39 +211,47 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = n * d / (ms_per_step / 1e3) / 1e6  # the whole job: N x d draws per step
 
-    # per-kernel device time inside the timed region (HIP events on the launching stream)
-    import ctypes
+    # per-kernel device time inside the timed region (HIP events on the launching stream; the
+    # step-4 lanes and the deferred counts run concurrently, so these durations are stretched)
+    kernels = read_kernels(lib, n, d, args.steps)
 
-    kernels = {}
-    for kid, name in enumerate(_lib.KERNELS):
-        tot, cnt = ctypes.c_double(), ctypes.c_int64()
-        _lib.check(lib.pbh_timing_read(kid, ctypes.byref(tot), ctypes.byref(cnt)))
-        if cnt.value:
-            avg = tot.value / cnt.value
-            b = kernel_bytes(name, n, d)
-            kernels[name] = {"total_ms_per_step": round(tot.value / args.steps, 3), "launches": cnt.value,
-                             "avg_ms": round(avg, 4), "bytes_per_launch": b,
-                             "GBps": round(b / (avg / 1e3) / 1e9, 1) if b else None}
-    dom = max(kernels, key=lambda k: kernels[k]["total_ms_per_step"])
-    dk = kernels[dom]
+    # the standalone pass (outside the timed region): one more step with every kernel on one
+    # stream in order (pbh_set_serial: one step-4 lane, counts first), so each launch's duration
+    # is its own -- what the committed rocprofv3 1-stream summary measures; the roofline's kernel
+    # and duration come from here
+    lib.pbh_set_serial(1)
+    lib.pbh_timing_reset()
+    lib.pbh_timing_enable(1)
+    barrier()
+    step(args.warmup + args.steps)
+    barrier()
+    lib.pbh_timing_enable(0)
+    lib.pbh_set_serial(0)
+    standalone = read_kernels(lib, n, d, 1)
+    dom = max(standalone, key=lambda k: standalone[k]["total_ms_per_step"])
+    dk = standalone[dom]
     achieved = dk["GBps"] or 0.0
     traffic, traffic_src = pmc_traffic(dom)
+    valu, valu_src = pmc_valu(dom)
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": dom,
-                "avg_launch_ms": dk["avg_ms"], "bytes_per_launch": dk["bytes_per_launch"]}
+                "kernel": dom, "avg_launch_ms": dk["avg_ms"], "bytes_per_launch": dk["bytes_per_launch"],
+                "duration_source": "standalone pass: pbh_set_serial(1), one stream, HIP events",
+                "valu_busy": valu, "valu_source": valu_src}
 
     # whole-step roofline: SURVEY.md §8(d)'s 96 algorithmic bytes per draw over the step time
     # (the N-row job is row-sharded over `world` GPUs: n * d draws in all, against world x the peak)
     pipeline = {"bytes_per_draw": 96, "achieved": round(96 * n * d / (ms_per_step / 1e3) / 1e9, 1),
                 "unit": "GB/s", "peak": HBM_PEAK_GBS * world,
                 "frac": round(96 * n * d / (ms_per_step / 1e3) / 1e9 / (HBM_PEAK_GBS * world), 4),
-                "kernel_time_ms_per_step": round(sum(k["total_ms_per_step"] for k in kernels.values()), 3)}
+                "kernel_time_ms_per_step": round(sum(k["total_ms_per_step"] for k in standalone.values()), 3),
+                "kernel_time_source": "standalone pass (concurrent durations in `kernels` overlap)"}
     copy_peak = hbm_copy_peak(lib) if rank == 0 else None
     if copy_peak:
         pipeline["frac_of_measured_copy"] = round(pipeline["achieved"] / copy_peak["GBps"], 4)
         roofline["frac_of_measured_copy"] = round(achieved / copy_peak["GBps"], 4)
-    e2e = end_to_end(step, ds, n, d, args.warmup + args.steps, barrier) if (world == 1 and not args.no_e2e) else None
+    e2e = end_to_end(root, ds, n, d, args.seed + args.warmup + args.steps, barrier, ms_per_step) \
+        if (world == 1 and not args.no_e2e) else None
 
     sweep = ppf_sweep(lib, base, args.ppf_rows, args.seed) if (args.ppf_rows > 0 and rank == 0) else None
 
@@ -265,10 +273,51 @@ def main():
                                            "out, positions back)") if world > 1 else "single",
                            "devices": torch.cuda.device_count() if world > 1 else 1},
                 "roofline": roofline, "pipeline_roofline": pipeline, "hbm_copy_peak": copy_peak,
-                "end_to_end": e2e, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels}
+                "end_to_end": e2e, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels,
+                "kernels_standalone": standalone}
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def read_kernels(lib, n, d, steps):
+    """Per-kernel HIP-event totals since the last pbh_timing_reset, per step."""
+    import ctypes
+
+    from probabilit_amd import _lib
+
+    kernels = {}
+    for kid, name in enumerate(_lib.KERNELS):
+        tot, cnt = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(lib.pbh_timing_read(kid, ctypes.byref(tot), ctypes.byref(cnt)))
+        if cnt.value:
+            avg = tot.value / cnt.value
+            b = kernel_bytes(name, n, d)
+            kernels[name] = {"total_ms_per_step": round(tot.value / steps, 3), "launches": cnt.value,
+                             "avg_ms": round(avg, 4), "bytes_per_launch": b,
+                             "GBps": round(b / (avg / 1e3) / 1e9, 1) if b else None}
+    return kernels
+
+
+def pmc_valu(kernel):
+    """VALU-busy of `kernel` (the share of SIMD cycles that issued a vector instruction,
+    tools/pmc_valu_summary.py) from the newest committed rocprofv3 VALU pass, dispatch-weighted
+    over the kernel's template variants, or None."""
+    import glob
+
+    def tag(path):
+        m = re.search(r"_r(\d+)", os.path.basename(path))
+        return int(m.group(1)) if m else -1
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_valu_*.json")), key=tag)
+    for f in reversed(files):
+        ks = json.load(open(f)).get("runs", {}).get("bench", {})
+        names = [nm for nm in PMC_NAMES.get(kernel, [kernel]) if nm in ks]
+        disp = sum(ks[nm]["dispatches"] for nm in names)
+        if disp:
+            v = sum(ks[nm]["valu_busy"] * ks[nm]["dispatches"] for nm in names) / disp
+            return round(v, 3), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def ppf_sweep(lib, dists, n, seed, reps=3):
@@ -303,7 +352,8 @@ def ppf_sweep(lib, dists, n, seed, reps=3):
 
 def hbm_copy_peak(lib, nbytes=4 << 30, reps=5):
     """The box's HBM copy ceiling (re-measure with a copy kernel and report it
-    next to the 8 TB/s spec): pbh_hbm_copy over nbytes, read + write bytes / mean launch time."""
+    next to the 8 TB/s spec): the fastest of pbh_hbm_copy's variants over nbytes, read + write
+    bytes / mean launch time."""
     import ctypes
 
     import torch
@@ -314,38 +364,44 @@ def hbm_copy_peak(lib, nbytes=4 << 30, reps=5):
     dst = torch.empty_like(src)
     src.fill_(1)
     kid = _lib.KERNELS.index("k_hbm_copy")
-    _lib.check(lib.pbh_hbm_copy(src.data_ptr(), dst.data_ptr(), nbytes, device.stream()))
-    lib.pbh_timing_reset()
-    lib.pbh_timing_enable(1)
-    for _ in range(reps):
-        _lib.check(lib.pbh_hbm_copy(src.data_ptr(), dst.data_ptr(), nbytes, device.stream()))
-    lib.pbh_timing_enable(0)
-    t, c = ctypes.c_double(), ctypes.c_int64()
-    _lib.check(lib.pbh_timing_read(kid, ctypes.byref(t), ctypes.byref(c)))
-    avg = t.value / max(c.value, 1)
+    per = {}
+    for var in range(5):
+        _lib.check(lib.pbh_hbm_copy(src.data_ptr(), dst.data_ptr(), nbytes, var, device.stream()))
+        lib.pbh_timing_reset()
+        lib.pbh_timing_enable(1)
+        for _ in range(reps):
+            _lib.check(lib.pbh_hbm_copy(src.data_ptr(), dst.data_ptr(), nbytes, var, device.stream()))
+        lib.pbh_timing_enable(0)
+        t, c = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(lib.pbh_timing_read(kid, ctypes.byref(t), ctypes.byref(c)))
+        per[var] = t.value / max(c.value, 1)
     del src, dst
-    return {"kernel": "k_hbm_copy", "bytes_moved": 2 * nbytes, "avg_ms": round(avg, 4),
-            "GBps": round(2 * nbytes / (avg / 1e3) / 1e9, 1), "frac_of_spec": round(2 * nbytes / (avg / 1e3) / 1e9 /
-                                                                                   HBM_PEAK_GBS, 4)}
+    best = min(per, key=per.get)
+    avg = per[best]
+    return {"kernel": "k_hbm_copy", "bytes_moved": 2 * nbytes, "variant": best, "avg_ms": round(avg, 4),
+            "GBps": round(2 * nbytes / (avg / 1e3) / 1e9, 1),
+            "frac_of_spec": round(2 * nbytes / (avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "per_variant_GBps": {v: round(2 * nbytes / (ms / 1e3) / 1e9, 1) for v, ms in per.items()}}
 
 
-def end_to_end(step, ds, n, d, i, barrier):
-    """One more step with every output column handed back as numpy (the reference returns host
-    arrays, modeling.py:582-583,614): the device step plus the D2H of all d columns through
-    `.samples_` (pageable copies), timed together.  A side figure, never `value`."""
+def end_to_end(root, ds, n, d, seed, barrier, device_ms):
+    """The drop-in call end to end: Node.sample() (the reference's API, modeling.py:431) leaves a
+    numpy samples_ on every node (modeling.py:582-583, 614), here all 32 columns handed back in one
+    pipelined batch through the pinned ring (device.to_host_many).  d2h = the total minus the
+    device-resident step time measured above.  A side figure, never `value`."""
     barrier()
     t0 = time.perf_counter()
-    step(i)
-    barrier()
-    t1 = time.perf_counter()
+    root.sample(n, random_state=seed, method="lhs")
     host = [x.samples_ for x in ds]
-    t2 = time.perf_counter()
+    t1 = time.perf_counter()
     nbytes = sum(h.nbytes for h in host)
     del host
-    return {"value": round(n * d / (t2 - t0) / 1e6, 2), "unit": "Msamples/s", "ms": round((t2 - t0) * 1e3, 1),
-            "device_ms": round((t1 - t0) * 1e3, 1), "d2h_ms": round((t2 - t1) * 1e3, 1),
-            "d2h_GBps": round(nbytes / (t2 - t1) / 1e9, 2), "bytes": nbytes,
-            "what": "one step + .samples_ of all columns (numpy, pageable D2H)"}
+    ms = (t1 - t0) * 1e3
+    d2h_ms = max(ms - device_ms, 1e-3)
+    return {"value": round(n * d / (ms / 1e3) / 1e6, 2), "unit": "Msamples/s", "ms": round(ms, 1),
+            "device_ms": round(device_ms, 1), "d2h_ms": round(d2h_ms, 1),
+            "d2h_GBps": round(nbytes / (d2h_ms / 1e3) / 1e9, 2), "bytes": nbytes,
+            "what": "Node.sample() with numpy samples_ on all columns (pinned-ring D2H, 64 MiB chunks)"}
 
 
 def cpu_baseline(n, d):

@@ -455,12 +455,19 @@ int pbh_permcorr_climb(double* xs, double* xo, int64_t n, int32_t k, int64_t ldx
  * recorded on the launching stream; pbh_timing_read returns the summed device time and the
  * launch count of kernel `id` (names via pbh_kernel_name).  Used by bench.py's roofline. */
 int pbh_timing_enable(int on);
+/* Measurement mode (bench.py's standalone pass, the rocprof 1-stream profiles): with on != 0,
+ * pbh_iman_conover runs every kernel on one stream in order -- one step-4 lane, the tie counts
+ * before the scores -- so that each launch's duration is its own, not stretched by concurrent
+ * kernels.  Results are identical either way. */
+int pbh_set_serial(int on);
 int pbh_timing_reset(void);
 const char* pbh_kernel_name(int id);
 int pbh_timing_read(int id, double* total_ms, int64_t* launches);
 /* The box's HBM copy ceiling for bench.py (the measured peak reported beside the 8 TB/s spec):
- * dst = src over `bytes` (16-byte aligned), timed as kernel "k_hbm_copy". */
-int pbh_hbm_copy(const void* src, void* dst, size_t bytes, void* stream);
+ * dst = src over `bytes` (16-byte aligned), timed as kernel "k_hbm_copy".  variant 0: grid-stride
+ * non-temporal 16-byte vectors; 1 / 2: one block per tile of 4 / 8 vectors per lane; 3 / 4: the
+ * same non-temporal.  bench.py reports the fastest. */
+int pbh_hbm_copy(const void* src, void* dst, size_t bytes, int variant, void* stream);
 
 #ifdef __cplusplus
 }

@@ -51,7 +51,8 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_lhs_reference", "pbh_lhs_reference_perms", "pbh_hbm_copy", "pbh_dag_eval",
            "pbh_lhs_sorted_counts", "pbh_sort_heads", "pbh_ic_owned_workspace_size", "pbh_ic_owned_create",
            "pbh_ic_owned_column", "pbh_ic_owned_finish", "pbh_lhs_values_at", "pbh_ic_owned_destroy", "pbh_event_create",
-           "pbh_event_destroy", "pbh_event_record", "pbh_stream_wait_event", "pbh_event_synchronize"]
+           "pbh_event_destroy", "pbh_event_record", "pbh_stream_wait_event", "pbh_event_synchronize",
+           "pbh_set_serial"]
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
@@ -170,7 +171,7 @@ def load():
         "pbh_permcorr_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
         "pbh_lhs_reference_workspace_size": ([i64, ctypes.c_int32, ctypes.POINTER(sz)], i32),
         "pbh_lhs_reference": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, i64, vp, sz, vp], i32),
-        "pbh_hbm_copy": ([vp, vp, sz, vp], i32),
+        "pbh_hbm_copy": ([vp, vp, sz, i32, vp], i32),
         "pbh_dag_eval": ([ctypes.POINTER(DagOp), i32, ctypes.POINTER(DagSource), i32, ctypes.POINTER(vp), i32, i64, i64,
                           vp, vp], i32),
         "pbh_lhs_reference_perms": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, vp], i32),
@@ -189,6 +190,7 @@ def load():
         "pbh_event_record": ([vp, vp], i32),
         "pbh_stream_wait_event": ([vp, vp], i32),
         "pbh_event_synchronize": ([vp], i32),
+        "pbh_set_serial": ([i32], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -250,9 +250,14 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     const char* e = getenv("PBH_DEFER_COUNTS");
     return e ? atoi(e) : 3;
   }();
-  int st = ic_run(a, stream, defer);
+  int st = ic_run(a, stream, g_serial ? 0 : defer);
   if (st == kRedo) st = ic_run(a, stream, 0);
   return st;
+}
+
+extern "C" int pbh_set_serial(int on) {
+  g_serial = on != 0;
+  return PBH_OK;
 }
 
 namespace {

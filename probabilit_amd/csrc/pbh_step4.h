@@ -60,6 +60,7 @@ bool step4_fused();
 // latency-bound kernels (bucket finish, gen_place) overlap another's bandwidth-bound passes
 constexpr int kStep4MaxStreams = 4;
 int step4_streams();
+extern int g_serial;  // pbh_set_serial (measurement mode: one lane, counts not deferred)
 // the side streams of this device, created once (thread-safe) and kept for the process
 hipStream_t step4_side_stream(int i);
 void step4_sync_side_streams();

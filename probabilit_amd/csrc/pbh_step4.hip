@@ -1351,7 +1351,10 @@ void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb) {
   cb.segtp = (uint32_t*)p;
 }
 
+int g_serial = 0;  // pbh_set_serial: one lane, no deferred counts (standalone kernel durations)
+
 int step4_streams() {
+  if (g_serial) return 1;
   static const int v = [] {
     const char* e = getenv("PBH_STEP4_STREAMS");
     int x = e ? atoi(e) : 3;

@@ -46,10 +46,10 @@ void timing_after(int id, hipStream_t s) {
   g_slots[id].stop.push_back(e);
 }
 
-// HBM copy ceiling of the box (bench.py's measured peak next to the 8 TB/s spec): 16-byte
-// non-temporal loads and stores, four in flight per lane, grid-stride over the buffer.
+// HBM copy ceiling of the box (bench.py's measured peak next to the 8 TB/s spec).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// variant 0: grid-stride, 16-byte non-temporal loads and stores, four in flight per lane
 __global__ __launch_bounds__(256) void k_hbm_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n16) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -63,18 +63,56 @@ __global__ __launch_bounds__(256) void k_hbm_copy(const u32x4* __restrict__ src,
   for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
+// variants 1-4: one block per contiguous tile of 256 x U 16-byte vectors (no grid stride: many
+// more blocks than CUs), U loads in flight per lane before the stores; NT: non-temporal
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_hbm_copy_tile(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                       int64_t n16) {
+  const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  u32x4 v[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const int64_t i = base + (int64_t)j * 256;
+    if (i < n16) v[j] = NT ? __builtin_nontemporal_load(src + i) : src[i];
+  }
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const int64_t i = base + (int64_t)j * 256;
+    if (i < n16) {
+      if (NT)
+        __builtin_nontemporal_store(v[j], dst + i);
+      else
+        dst[i] = v[j];
+    }
+  }
+}
+
 }  // namespace pbh
 
 using namespace pbh;
 
-extern "C" int pbh_hbm_copy(const void* src, void* dst, size_t bytes, void* stream) {
+extern "C" int pbh_hbm_copy(const void* src, void* dst, size_t bytes, int variant, void* stream) {
   PBH_REQUIRE(src && dst && bytes % 16 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0,
               "pbh_hbm_copy: 16-byte aligned buffers and size required");
+  PBH_REQUIRE(variant >= 0 && variant <= 4, "pbh_hbm_copy: variant %d outside [0, 4]", variant);
   hipStream_t s = as_stream(stream);
   const int64_t n16 = (int64_t)(bytes / 16);
-  PBH_TIMED(kKHbmCopy, s,
-            hipLaunchKernelGGL(k_hbm_copy, dim3(grid_for(n16, 256, 256 * 16)), dim3(256), 0, s, (const u32x4*)src,
-                               (u32x4*)dst, n16));
+  const auto tiles = [&](int u) { return dim3((unsigned)((n16 + 256 * u - 1) / (256 * u))); };
+  switch (variant) {
+    case 0:
+      PBH_TIMED(kKHbmCopy, s,
+                hipLaunchKernelGGL(k_hbm_copy, dim3(grid_for(n16, 256, 256 * 16)), dim3(256), 0, s, (const u32x4*)src,
+                                   (u32x4*)dst, n16));
+      break;
+    case 1: PBH_TIMED(kKHbmCopy, s, hipLaunchKernelGGL((k_hbm_copy_tile<4, false>), tiles(4), dim3(256), 0, s,
+                                                       (const u32x4*)src, (u32x4*)dst, n16)); break;
+    case 2: PBH_TIMED(kKHbmCopy, s, hipLaunchKernelGGL((k_hbm_copy_tile<8, false>), tiles(8), dim3(256), 0, s,
+                                                       (const u32x4*)src, (u32x4*)dst, n16)); break;
+    case 3: PBH_TIMED(kKHbmCopy, s, hipLaunchKernelGGL((k_hbm_copy_tile<4, true>), tiles(4), dim3(256), 0, s,
+                                                       (const u32x4*)src, (u32x4*)dst, n16)); break;
+    default: PBH_TIMED(kKHbmCopy, s, hipLaunchKernelGGL((k_hbm_copy_tile<8, true>), tiles(8), dim3(256), 0, s,
+                                                        (const u32x4*)src, (u32x4*)dst, n16)); break;
+  }
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }

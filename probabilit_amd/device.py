@@ -64,7 +64,75 @@ def to_device(a):
 
 def to_host(t):
     """Download a device tensor to a fresh numpy array (synchronises the stream)."""
-    return t.detach().cpu().numpy()
+    return to_host_many([t])[0]
+
+
+# The hand-back of samples_ to numpy (modeling.py:582-583, 614: the reference returns host
+# arrays).  A pageable D2H runs at ~8-11 GB/s on the box (the runtime stages it through its own
+# small pinned buffers, one chunk at a time); pinning a fresh destination per call costs ~0.07 s
+# per GB.  Instead: a ring of three 64 MiB pinned buffers kept for the process, DMA of chunk i
+# into one while the host threads copy chunk i - 2 out into the fresh numpy array (first touch
+# included), measured 44-48 GB/s on 4 GiB (tools/d2h_bench.py, profiles/r03/d2h.json).
+_STAGE_BYTES = 64 << 20
+_SMALL_BYTES = 8 << 20  # below this a plain copy is as fast
+_stage = {}
+
+
+def _staging():
+    if not _stage:
+        import concurrent.futures
+
+        torch = _torch()
+        dev = device()
+        _stage["ring"] = [torch.empty(_STAGE_BYTES, dtype=torch.uint8, pin_memory=True) for _ in range(3)]
+        _stage["events"] = [torch.cuda.Event() for _ in range(3)]
+        _stage["stream"] = torch.cuda.Stream(device=dev)
+        _stage["threads"] = max(1, min(16, os.cpu_count() or 1))
+        _stage["pool"] = concurrent.futures.ThreadPoolExecutor(_stage["threads"])
+    return _stage
+
+
+def to_host_many(tensors):
+    """Fresh numpy copies of device tensors, the large ones pipelined through the pinned ring."""
+    torch = _torch()
+    outs = [None] * len(tensors)
+    chunks = []  # (source bytes, destination bytes, lo, hi)
+    for j, t in enumerate(tensors):
+        t = t.detach()
+        nbytes = t.numel() * t.element_size()
+        if nbytes < _SMALL_BYTES or t.dtype == torch.bool or not t.is_contiguous():
+            outs[j] = t.cpu().numpy()
+            continue
+        out = np.empty(tuple(t.shape), dtype=np.dtype(str(t.dtype).replace("torch.", "")))
+        outs[j] = out
+        src = t.reshape(-1).view(torch.uint8)
+        dst = out.reshape(-1).view(np.uint8)
+        for lo in range(0, nbytes, _STAGE_BYTES):
+            chunks.append((src, dst, lo, min(nbytes, lo + _STAGE_BYTES)))
+    if not chunks:
+        return outs
+    st = _staging()
+    ring, evs, stream, pool, nt = st["ring"], st["events"], st["stream"], st["pool"], st["threads"]
+    stream.wait_stream(torch.cuda.current_stream(device()))  # after the producers of the tensors
+
+    def drain(i):
+        src, dst, lo, hi = chunks[i]
+        evs[i % 3].synchronize()
+        buf = ring[i % 3].numpy()
+        step = -(-(hi - lo) // nt)
+        step = (step + 63) // 64 * 64
+        list(pool.map(lambda a: np.copyto(dst[lo + a:min(hi, lo + a + step)], buf[a:min(hi - lo, a + step)]),
+                      range(0, hi - lo, step)))
+
+    with torch.cuda.stream(stream):
+        for i in range(len(chunks) + 2):
+            if i < len(chunks):  # slot i % 3 is free: chunk i - 3 was drained two iterations ago
+                src, dst, lo, hi = chunks[i]
+                ring[i % 3][:hi - lo].copy_(src[lo:hi], non_blocking=True)
+                evs[i % 3].record(stream)
+            if i >= 2:
+                drain(i - 2)
+    return outs  # every chunk was drained: no DMA still reads a source
 
 
 def ptr(t):

@@ -523,6 +523,12 @@ class Node(abc.ABC):
 
         if not to_host:
             return None if self._dev() is None else self.samples_device
+        # the reference leaves numpy samples_ on every node (modeling.py:582-583, 598, 614): hand
+        # them all back in one pipelined batch (device.to_host_many) rather than one by one
+        pending = [nd for nd in set(self.nodes()) if "_smp" in nd.__dict__ and nd.__dict__.get("_host") is None
+                   and nd.__dict__["_smp"] is not None and not isinstance(nd.__dict__["_smp"], _Broadcast)]
+        for nd, host in zip(pending, device.to_host_many([nd.__dict__["_smp"] for nd in pending])):
+            nd.__dict__["_host"] = host
         return self.samples_
 
 
