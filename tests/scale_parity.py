@@ -177,3 +177,46 @@ def gate(cs_ref_cols, y_cols, sx_cols, cs_dev_cols=None, threads=4, log=None):
 
     with ThreadPoolExecutor(max(1, min(threads, k))) as ex:
         return list(ex.map(one, range(k)))
+
+
+def gate_all(n, d, seed, C, threads=8, log=print):
+    """The §8(d) gate over every column (tools/parity_1e8.py, tests/test_gpu_scale.py): the
+    production path on the device keeping S, then on the host E = np.corrcoef(S)
+    (correlation.py:398), L = cholesky(E), D = solve_triangular(L, S.T).T, CS = D @ P.T
+    (:405-414), the reference ranks (:422) and, per column, every row whose device output
+    differs from sort(X[:, k])[idx].  Returns the summary document."""
+    from probabilit_amd import device
+
+    t0 = time.time()
+    Y, S, CS, E_dev, P, gen = run_device(n, d, seed, C)
+    S_host = device.to_host(S)
+    del S
+    E_ref = np.corrcoef(S_host.T, rowvar=False)  # the reference's S is (N, K): S_host.T
+    log(f"[{time.time() - t0:6.1f}s] max |E_dev - E_ref| = {float(np.max(np.abs(E_dev - E_ref))):.3e}")
+    cs_ref = reference_cs(S_host, E_ref, P)
+    del S_host
+    log(f"[{time.time() - t0:6.1f}s] reference CS done")
+
+    def one(j):
+        y = device.to_host(Y[j])
+        csd = device.to_host(CS[j])
+        r = column_gate(j, np.ascontiguousarray(cs_ref[:, j]), y, sorted_x(gen[j], n), csd)
+        r["max_abs_cs_dev_minus_ref"] = float(np.max(np.abs(csd - cs_ref[:, j])))
+        log(r)
+        return r
+
+    with ThreadPoolExecutor(threads) as ex:
+        cols = list(ex.map(one, range(d)))
+    return {"what": "SURVEY.md §8(d) step-4 parity gate: device (production path) vs the reference's "
+                    "corrcoef/cholesky/solve_triangular/@P.T/rankdata on the device scores S",
+            "workload": f"cfg3 (cfg2 set x4), N={n}, d={d}, native LHS seed {seed}, "
+                        "target C = 0.9 corrcoef(A) + 0.1 I",
+            "rows": n, "d": d, "seed": seed,
+            "max_abs_E_dev_minus_ref": float(np.max(np.abs(E_dev - E_ref))),
+            "mismatched_rows_total": sum(c["mismatched_rows"] for c in cols),
+            "swaps_total": sum(c["swaps"] for c in cols),
+            "ties_total": sum(c["ties"] for c in cols),
+            "violations_total": sum(c["violations"] for c in cols),
+            "max_abs_dcs_ref_in_swaps": max(c["max_abs_dcs_ref"] for c in cols),
+            "max_abs_cs_dev_minus_ref": max(c["max_abs_cs_dev_minus_ref"] for c in cols),
+            "seconds": round(time.time() - t0, 1), "columns": cols}

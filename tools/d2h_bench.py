@@ -42,14 +42,36 @@ def main():
     del h
 
     # (c) staging ring of pinned chunks + threaded memcpy into a fresh pageable array
-    for chunk_mb, threads in ((64, 8), (256, 8), (256, 16)):
+    import mmap
+
+    try:
+        out["thp"] = open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip()
+    except OSError:
+        out["thp"] = None
+
+    def huge_empty(m):  # an anonymous mapping advised for transparent huge pages
+        mm = mmap.mmap(-1, m * 8, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+        try:
+            mm.madvise(mmap.MADV_HUGEPAGE)
+        except (AttributeError, OSError):
+            pass
+        return np.frombuffer(mm, dtype=np.float64, count=m)
+
+    for chunk_mb, threads, alloc in ((64, 16, "np"), (64, 16, "huge"), (64, 16, "prefault"), (32, 16, "huge"),
+                                     (128, 16, "huge")):
         chunk = chunk_mb * (1 << 20) // 8
         ring = [torch.empty(chunk, dtype=torch.float64, pin_memory=True) for _ in range(3)]
         evs = [torch.cuda.Event() for _ in range(3)]
         stream = torch.cuda.Stream(device=dev)
         pool = ThreadPoolExecutor(threads)
+        if alloc == "prefault":
+            dst = np.empty(n, dtype=np.float64)
+            dst[:] = 0.0
         t0 = time.perf_counter()
-        dst = np.empty(n, dtype=np.float64)
+        if alloc == "np":
+            dst = np.empty(n, dtype=np.float64)
+        elif alloc == "huge":
+            dst = huge_empty(n)
         nch = (n + chunk - 1) // chunk
 
         def copy_out(i, slot):
@@ -76,7 +98,7 @@ def main():
                     copy_out(j, j % 3)
         t = time.perf_counter() - t0
         assert np.array_equal(dst[:1000], src[:1000].cpu().numpy())
-        out[f"ring_{chunk_mb}MB_{threads}t_GBps"] = rate(t)
+        out[f"ring_{chunk_mb}MB_{threads}t_{alloc}_GBps"] = rate(t)
         pool.shutdown()
         del dst, ring
 
