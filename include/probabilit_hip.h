@@ -221,10 +221,14 @@ int pbh_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col
  * device u32, hcap entries): the run heads -- every t in (t0, t0 + nt) whose value differs from
  * stratum t - 1's, plus t0 itself when t0 == 0 -- unordered, at most hcap written; *hcur_dev
  * (device u32) counts them all.  A shard starting at row0 > 0 passes t0 = row0 - 1, so that the
- * pair across the shard boundary is counted exactly once. */
+ * pair across the shard boundary is counted exactly once.  certify != 0 (continuous columns,
+ * no heads): the tie / inversion certificate instead of the counts -- the inverse CDF evaluated
+ * only at the pairs whose quantile gap its error bound could close (see pbh_ppf.hip); counts
+ * then read non-zero unless the segment is certified free of ties and inversions, and a caller
+ * that sees non-zero recounts exactly. */
 int pbh_lhs_sorted_counts(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist,
                           const double* params_host, int nparams, unsigned long long* counts_dev, uint32_t* heads,
-                          uint32_t* hcur_dev, uint32_t hcap, int32_t* nonfinite_flag, void* stream);
+                          uint32_t* hcur_dev, uint32_t hcap, int32_t* nonfinite_flag, int certify, void* stream);
 /* heads[0 .. nh) in increasing order, nh <= 16384 (the run heads pbh_lhs_sorted_counts appends). */
 int pbh_sort_heads(uint32_t* heads, int64_t nh, void* stream);
 /* Adjacent-pair check of a column: *ties = #(x[t] == x[t+1]), *inversions = #!(x[t] <= x[t+1]).
@@ -456,9 +460,9 @@ int pbh_permcorr_climb(double* xs, double* xo, int64_t n, int32_t k, int64_t ldx
  * launch count of kernel `id` (names via pbh_kernel_name).  Used by bench.py's roofline. */
 int pbh_timing_enable(int on);
 /* Measurement mode (bench.py's standalone pass, the rocprof 1-stream profiles): with on != 0,
- * pbh_iman_conover runs every kernel on one stream in order -- one step-4 lane, the tie counts
- * before the scores -- so that each launch's duration is its own, not stretched by concurrent
- * kernels.  Results are identical either way. */
+ * pbh_iman_conover runs every kernel on the caller's stream in order -- one step-4 lane, the
+ * deferred tie checks in line -- so that each launch's duration is its own, not stretched by
+ * concurrent kernels.  Results are identical either way. */
 int pbh_set_serial(int on);
 int pbh_timing_reset(void);
 const char* pbh_kernel_name(int id);

@@ -177,7 +177,8 @@ def load():
         "pbh_lhs_reference_perms": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, vp], i32),
         "pbh_permcorr_climb": ([vp, vp, i64, ctypes.c_int32, i64, vp, vp, vp, vp, vp, vp, i64, dbl, vp, vp, vp, sz, vp],
                                i32),
-        "pbh_lhs_sorted_counts": ([u64, i64, i64, i64, i32, i32, vp, i32, vp, vp, vp, ctypes.c_uint32, vp, vp], i32),
+        "pbh_lhs_sorted_counts": ([u64, i64, i64, i64, i32, i32, vp, i32, vp, vp, vp, ctypes.c_uint32, vp, i32, vp],
+                                  i32),
         "pbh_sort_heads": ([vp, i64, vp], i32),
         "pbh_ic_owned_workspace_size": ([i64, ctypes.c_int32, ctypes.POINTER(sz)], i32),
         "pbh_ic_owned_create": ([ctypes.POINTER(ICColumn), ctypes.c_int32, i64, vp, sz, ctypes.POINTER(vp), vp], i32),

@@ -7,6 +7,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -250,7 +251,7 @@ extern "C" int pbh_iman_conover(const pbh_ic_args* a, void* stream) {
     const char* e = getenv("PBH_DEFER_COUNTS");
     return e ? atoi(e) : 3;
   }();
-  int st = ic_run(a, stream, g_serial ? 0 : defer);
+  int st = ic_run(a, stream, defer);
   if (st == kRedo) st = ic_run(a, stream, 0);
   return st;
 }
@@ -323,6 +324,24 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
   };
   std::vector<char> deferred(k, 0);
   bool any_deferred = false;
+  // a deferred column's check: the certificate (PBH_CERT=0: the exact counts) -- it can only
+  // confirm "no tie, no inversion"; anything else reads as a count and redoes the call exactly
+  static const bool cert_on = [] {
+    const char* e = getenv("PBH_CERT");
+    return !(e && e[0] == '0');
+  }();
+  auto count_deferred = [&](int c, hipStream_t cs_) -> int {
+    double T = 0.0;
+    uint32_t cap = 0;
+    if (!cert_on || !gen_cert_plan(gens.g[c], n, &T, &cap))  // no bound, or as costly as the count
+      return gen_sorted(gens.g[c], 0, n, nullptr, a->columns[c].nonfinite_flag, L.counts + 2 * c, cs_);
+    uint32_t* list = nullptr;
+    PBH_CHECK_HIP(hipMallocAsync((void**)&list, ((size_t)cap + 64) * 4, cs_));
+    int r = gen_certify(gens.g[c], 0, n, T, list, cap, list + cap, a->columns[c].nonfinite_flag, L.counts + 2 * c,
+                        cs_);
+    PBH_CHECK_HIP(hipFreeAsync(list, cs_));
+    return r;
+  };
   if (a->columns && defer)
     for (int c = 0; c < k; ++c) any_deferred |= (deferred[c] = a->columns[c].dist != PBH_DIST_POISSON) != 0;
   if (a->columns) {
@@ -420,7 +439,8 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     const int v = e ? atoi(e) : 0;
     return v < 0 ? 0 : (v >= kStep4MaxStreams ? kStep4MaxStreams - 1 : v);
   }();
-  hipStream_t side = any_deferred ? step4_side_stream(counts_stream) : nullptr;
+  // (measurement mode, pbh_set_serial: the caller's stream, in order)
+  hipStream_t side = any_deferred ? (g_serial ? s : step4_side_stream(counts_stream)) : nullptr;
   auto launch_counts = [&]() -> int {  // the deferred columns' counts on `side`, after s's work so far
     sync_on_exit.side = true;
     PBH_CHECK_HIP(hipEventCreateWithFlags(&ev_scores.e, hipEventDisableTiming));
@@ -429,7 +449,7 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     PBH_CHECK_HIP(hipStreamWaitEvent(side, ev_scores.e, 0));
     for (int c = 0; c < k; ++c) {
       if (!deferred[c]) continue;
-      int r = gen_sorted(gens.g[c], 0, n, nullptr, a->columns[c].nonfinite_flag, L.counts + 2 * c, side);
+      int r = count_deferred(c, side);
       if (r) return r;
     }
     PBH_CHECK_HIP(hipEventRecord(ev_counts.e, side));
@@ -454,14 +474,14 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     PBH_CHECK_HIP(hipStreamWaitEvent(side, ev_scores.e, 0));
     for (int c = 0; c < k; ++c) {
       if (!deferred[c]) continue;
-      st = gen_sorted(gens.g[c], 0, n, nullptr, a->columns[c].nonfinite_flag, L.counts + 2 * c, side);
+      st = count_deferred(c, side);
       if (st) return st;
     }
     PBH_CHECK_HIP(hipEventRecord(ev_counts.e, side));
   } else if (any_deferred) {  // no side stream: count in order
     for (int c = 0; c < k; ++c) {
       if (!deferred[c]) continue;
-      st = gen_sorted(gens.g[c], 0, n, nullptr, a->columns[c].nonfinite_flag, L.counts + 2 * c, s);
+      st = count_deferred(c, s);
       if (st) return st;
     }
   }

@@ -6,6 +6,8 @@
 //   step 3   pbh_ic_apply                                           (per shard)
 //   step 4   pbh_ic_reorder                                         (per column, on its owner)
 #include <math.h>
+
+#include <algorithm>
 #include <string.h>
 
 #include <vector>
@@ -183,7 +185,7 @@ extern "C" int pbh_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t 
 extern "C" int pbh_lhs_sorted_counts(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist,
                                      const double* params_host, int nparams, unsigned long long* counts,
                                      uint32_t* heads, uint32_t* hcur, uint32_t hcap, int32_t* nonfinite_flag,
-                                     void* stream) {
+                                     int certify, void* stream) {
   PBH_REQUIRE(counts && nparams >= 0 && nparams <= 3 && (nparams == 0 || params_host),
               "pbh_lhs_sorted_counts: bad arguments");
   PBH_REQUIRE(!heads || (hcur && hcap >= 1), "pbh_lhs_sorted_counts: heads need hcur and hcap >= 1");
@@ -194,7 +196,16 @@ extern "C" int pbh_lhs_sorted_counts(uint64_t seed, int64_t n, int64_t t0, int64
   GenColumn* g = nullptr;
   int st = gen_create(seed, n, col, dist, prm, nparams, &g, s);
   if (st != PBH_OK) return st;
-  st = gen_sorted(g, t0, nt, nullptr, nonfinite_flag, counts, s, heads, hcur, heads ? hcap : 0);
+  double T = 0.0;
+  uint32_t cap = 0;
+  if (certify && !heads && gen_cert_plan(g, nt, &T, &cap)) {  // the certificate; else the exact counts
+    uint32_t* list = nullptr;
+    PBH_CHECK_HIP(hipMallocAsync((void**)&list, ((size_t)cap + 64) * 4, s));
+    st = gen_certify(g, t0, nt, T, list, cap, list + cap, nonfinite_flag, counts, s);
+    PBH_CHECK_HIP(hipFreeAsync(list, s));
+  } else {
+    st = gen_sorted(g, t0, nt, nullptr, nonfinite_flag, counts, s, heads, hcur, heads ? hcap : 0);
+  }
   gen_destroy(g, s);  // stream-ordered: the tables are freed after the kernel
   return st;
 }

@@ -4,7 +4,12 @@
 // Roofline: the ppf sweep moves 16 B per draw (read q 8 + write x 8), the fused
 // generator + ppf 8 B per draw (write x only); norm / uniform / expon / triang / lognorm
 // are HBM-bound, gamma (igami) and per-element poisson searches are FP64-VALU-bound.
+#include <array>
+#include <functional>
+#include <map>
+#include <mutex>
 #include <math.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -439,6 +444,85 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_sorted_ppf(uint64_t seed
       if (a) atomicAdd(&counts[0], a);
       if (b) atomicAdd(&counts[1], b);
     }
+  }
+}
+
+// ---------------------------------------------------------------- tie / inversion certificate
+// The deferred tie / inversion check of a continuous column (pbh_api.hip, PBH_DEFER_COUNTS) without
+// evaluating the inverse CDF at every stratum.  Adjacent strata t, t + 1 have quantiles
+// q_t < q_t+1 (the LHS jitter u lies in [0, 1)), and the exact inverse CDF F is strictly increasing
+// on the support, with F(q_t+1) - F(q_t) = dq / f(xi) by the mean value theorem.  The device's F
+// differs from the exact one by at most eps (|loc| + scale |y|) (y the standardised value; eps
+// per family, gen_cert_gap), so the two computed values are strictly ordered whenever
+// dq > 2 eps sup_y f0(y) (|loc| / scale + |y|) =: T.  k_cert_scan lists the pairs with dq <= T (a
+// fraction (T n)^2 / 2 of them: ~1e-3 for norm(0, 1) at N = 1e8) from the quantiles alone (one
+// SplitMix64 per stratum, no inverse CDF); k_cert_eval evaluates only those pairs exactly and
+// counts their ties / inversions, plus both ends of the segment (a non-finite end sets the flag;
+// monotone and finite at both ends means finite throughout).  Any count, a list overflow or a
+// non-finite end is reported as a tie, and the caller redoes the call with the exact counts
+// (k_lhs_sorted_ppf): the certificate can only confirm "no tie, no inversion".
+__global__ __launch_bounds__(kBlock) void k_cert_scan(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
+                                                      double T, uint32_t* __restrict__ list, uint32_t cap,
+                                                      uint32_t* __restrict__ count) {
+  Philox ph(seed);
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t wid0 = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const int64_t iters = (nt + 63 * waves - 1) / (63 * waves);  // waves advance by 63 and overlap by one
+  for (int64_t it = 0; it < iters; ++it) {
+    const int64_t i = (it * waves + wid0) * 63 + lane;
+    const bool valid = i < nt;
+    const double q = valid ? lhs_sorted_quantile(ph, (uint64_t)(t0 + i), col, (uint64_t)n) : 0.0;
+    const double nq = __shfl_down(q, 1, 64);
+    const bool cand = valid && lane < 63 && i + 1 < nt && !(nq - q > T);
+    const uint64_t m = __ballot(cand);
+    if (m) {
+      const int leader = __builtin_ctzll(m);
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+      base = __shfl(base, leader, 64);
+      const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+      const uint32_t slot = base + (uint32_t)__popcll(m & lt);
+      if (cand && slot < cap) list[slot] = (uint32_t)(i);  // offset in the segment
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_cert_eval(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
+                                                      Params prm, PoissonTable pt, const uint32_t* __restrict__ list,
+                                                      uint32_t cap, const uint32_t* __restrict__ count, int32_t* flag,
+                                                      unsigned long long* counts) {
+  Philox ph(seed);
+  auto value = [&](int64_t t) {
+    return ppf_one<D, 0, true>(lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n), prm.val[0], prm.val[1],
+                               prm.val[2], pt);
+  };
+  const uint32_t m = *count;
+  unsigned long long ties = 0, inv = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 2) {  // the segment's ends
+    const double x = value(threadIdx.x == 0 ? t0 : t0 + nt - 1);
+    if (!isfinite(x)) {
+      if (flag) atomicOr(flag, 1);
+      ties += 1;
+    }
+    if (threadIdx.x == 0 && m > cap) ties += 1;  // unlisted candidates: not certified
+  }
+  const uint32_t mm = m < cap ? m : cap;
+  for (uint32_t k = blockIdx.x * kBlock + threadIdx.x; k < mm; k += gridDim.x * kBlock) {
+    const int64_t t = t0 + list[k];
+    const double a = value(t), b = value(t + 1);
+    ties += a == b;
+    inv += !(a <= b);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ties += __shfl_xor(ties, o, 64);
+    inv += __shfl_xor(inv, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && (ties | inv)) {
+    atomicAdd(&counts[0], ties);
+    atomicAdd(&counts[1], inv);
   }
 }
 
@@ -1191,6 +1275,136 @@ int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t*
 #undef PBH_CASE
     default:
       set_error("unsupported distribution id %d", g->dist);
+      return PBH_ERR_UNSUPPORTED;
+  }
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+// T of the certificate (k_cert_scan) for a column's family and scalar parameters, or 0 when it
+// does not apply (discrete, a parameter outside the family's domain, or sup f0 (|loc| / scale + |y|)
+// unbounded).  eps: the assumed bound of the device inverse CDF's error relative to |loc| + scale |y|
+// -- 1e-12 for the closed forms and Cephes' ndtri (errors of a few ulp), 1e-9 for gamma's guided
+// interpolation (checked to 1e-12 per interval when the guide is built) -- 10^3 to 10^4 times the
+// largest difference from scipy measured over 10^6 strata per column at N = 1e8
+// (tests/test_gpu_scale_values.py).  The supremum is taken over a dense grid of y and widened by
+// half for the grid's resolution and for xi between the two strata.
+static double cert_gap(int dist, const double* v);
+
+double gen_cert_gap(const GenColumn* g) {
+  // cached per (family, parameters): the supremum scan costs ~4 ms of host time
+  static std::mutex mu;
+  static std::map<std::array<double, 4>, double> cache;
+  const std::array<double, 4> key = {(double)g->dist, g->prm.val[0], g->prm.val[1], g->prm.val[2]};
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const double T = cert_gap(g->dist, g->prm.val);
+  cache[key] = T;
+  return T;
+}
+
+static double cert_gap(int dist, const double* v) {
+  double loc = 0.0, scale = 1.0, eps = 1e-12;
+  std::function<double(double)> f0;
+  double lo = 0.0, hi = 1.0;
+  bool logy = false;
+  switch (dist) {
+    case PBH_DIST_NORM:
+      loc = v[0], scale = v[1];
+      f0 = [](double y) { return 0.3989422804014327 * exp(-0.5 * y * y); };
+      lo = -40.0, hi = 40.0;
+      break;
+    case PBH_DIST_UNIFORM:
+      loc = v[0], scale = v[1];
+      f0 = [](double) { return 1.0; };
+      break;
+    case PBH_DIST_EXPON:
+      loc = v[0], scale = v[1];
+      f0 = [](double y) { return exp(-y); };
+      hi = 800.0;
+      break;
+    case PBH_DIST_TRIANG: {
+      const double c = v[0];
+      loc = v[1], scale = v[2];
+      if (!(c >= 0.0 && c <= 1.0)) return 0.0;
+      f0 = [c](double y) { return y < c ? 2.0 * y / c : (c < 1.0 ? 2.0 * (1.0 - y) / (1.0 - c) : 0.0); };
+      break;
+    }
+    case PBH_DIST_GAMMA: {
+      const double a = v[0];
+      loc = v[1], scale = v[2], eps = 1e-9;
+      if (!(a > 0.0)) return 0.0;
+      if (a < 1.0 && loc != 0.0) return 0.0;  // f0 unbounded at 0 with |loc| > 0: no finite bound
+      const double lg = lgamma(a);
+      f0 = [a, lg](double y) { return y > 0.0 ? exp((a - 1.0) * log(y) - y - lg) : (a == 1.0 ? 1.0 : 0.0); };
+      lo = 1e-300, hi = 100.0 * (a + 10.0), logy = true;
+      break;
+    }
+    case PBH_DIST_LOGNORM: {
+      const double sg = v[0];
+      loc = v[1], scale = v[2];
+      if (!(sg > 0.0)) return 0.0;
+      eps = 1e-12 * (1.0 + 40.0 * sg);  // exp(s z) amplifies z's error by s |z|
+      f0 = [sg](double y) {
+        if (!(y > 0.0)) return 0.0;
+        const double z = log(y) / sg;
+        return 0.3989422804014327 * exp(-0.5 * z * z) / (sg * y);
+      };
+      lo = 1e-300, hi = 1e300, logy = true;
+      break;
+    }
+    default:
+      return 0.0;
+  }
+  if (!(scale > 0.0) || !isfinite(scale) || !isfinite(loc)) return 0.0;
+  const double L = fabs(loc) / scale;
+  double B = 0.0;
+  const int m = 400000;
+  for (int i = 0; i <= m; ++i) {
+    const double y = logy ? exp(log(lo) + (log(hi) - log(lo)) * i / m) : lo + (hi - lo) * i / m;
+    const double b = f0(y) * (L + fabs(y));
+    if (!isfinite(b)) return 0.0;
+    B = b > B ? b : B;
+  }
+  return 2.0 * eps * B * 1.5;
+}
+
+bool gen_cert_plan(const GenColumn* g, int64_t nt, double* T, uint32_t* cap) {
+  const char* forced = getenv("PBH_CERT_T");  // tests: a given gap, the cost check skipped
+  *T = forced ? atof(forced) : gen_cert_gap(g);
+  if (!(*T > 0.0) || nt < 2) return false;
+  const double n = (double)g->n;
+  const double frac = std::min(1.0, 0.5 * (*T * n) * (*T * n));  // P(gap < T): gap = (1 - u' + u) / n
+  if (!forced && frac > 0.05) return false;  // as costly as counting every stratum
+  *cap = (uint32_t)std::min<double>((double)nt, std::max(65536.0, 8.0 * frac * (double)nt + 4096.0));
+  return true;
+}
+
+int gen_certify(const GenColumn* g, int64_t t0, int64_t nt, double T, uint32_t* list, uint32_t cap, uint32_t* count,
+                int32_t* flag, unsigned long long* counts, hipStream_t s) {
+  PBH_REQUIRE(T > 0.0 && nt >= 1 && t0 >= 0 && t0 + nt <= g->n, "gen_certify: bad arguments");
+  PBH_CHECK_HIP(hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), s));
+  PBH_CHECK_HIP(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_cert_scan, dim3(ppf_grid(nt)), dim3(kBlock), 0, s, g->seed, g->n, t0, nt, g->col, T, list, cap,
+                     count);
+  PBH_CHECK_LAUNCH();
+  switch (g->dist) {
+#define PBH_CASE(D)                                                                                               \
+  case D:                                                                                                         \
+    PBH_TIMED(kKLhsSorted, s,                                                                                     \
+              hipLaunchKernelGGL(k_cert_eval<D>, dim3(512), dim3(kBlock), 0, s, g->seed, g->n, t0, nt, g->col, g->prm, \
+                                 g->pt, list, cap, count, flag, counts));                                         \
+    break;
+    PBH_CASE(PBH_DIST_NORM)
+    PBH_CASE(PBH_DIST_UNIFORM)
+    PBH_CASE(PBH_DIST_EXPON)
+    PBH_CASE(PBH_DIST_LOGNORM)
+    PBH_CASE(PBH_DIST_TRIANG)
+    PBH_CASE(PBH_DIST_GAMMA)
+#undef PBH_CASE
+    default:
+      set_error("gen_certify: distribution %d has no certificate", g->dist);
       return PBH_ERR_UNSUPPORTED;
   }
   PBH_CHECK_LAUNCH();

@@ -94,6 +94,16 @@ void gen_destroy(GenColumn* g, hipStream_t s);
 constexpr int kHeadsCap = 16384;
 int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t* flag, unsigned long long* counts,
                hipStream_t s, uint32_t* heads = nullptr, uint32_t* hcur = nullptr, uint32_t hcap = 0);
+// The tie / inversion certificate of a continuous column's strata [t0, t0 + nt) (k_cert_scan /
+// k_cert_eval, pbh_ppf.hip): counts[0] > 0 unless certified free of ties and inversions (an
+// uncertified column is recounted exactly by the caller).  T = gen_cert_gap(g) > 0 required;
+// list: cap candidate slots, count: one device word.
+double gen_cert_gap(const GenColumn* g);
+// whether the certificate applies to strata segments of nt of column g, with its gap T and list
+// capacity (8 x the expected candidates; false when no bound exists or it would list > 5%)
+bool gen_cert_plan(const GenColumn* g, int64_t nt, double* T, uint32_t* cap);
+int gen_certify(const GenColumn* g, int64_t t0, int64_t nt, double T, uint32_t* list, uint32_t cap, uint32_t* count,
+                int32_t* flag, unsigned long long* counts, hipStream_t s);
 // heads[0 .. nh) in increasing order (nh <= kHeadsCap)
 int sort_heads(uint32_t* heads, int64_t nh, hipStream_t s);
 // y[row * y_rs] = value of stratum p for every pair (row << 32 | p) of `pairs`, grouped by

@@ -70,10 +70,12 @@ def to_host(t):
 # The hand-back of samples_ to numpy (modeling.py:582-583, 614: the reference returns host
 # arrays).  A pageable D2H runs at ~8-11 GB/s on the box (the runtime stages it through its own
 # small pinned buffers, one chunk at a time); pinning a fresh destination per call costs ~0.07 s
-# per GB.  Instead: a ring of three 64 MiB pinned buffers kept for the process, DMA of chunk i
+# per GB.  Instead: a ring of three 128 MiB pinned buffers kept for the process, DMA of chunk i
 # into one while the host threads copy chunk i - 2 out into the fresh numpy array (first touch
-# included), measured 44-48 GB/s on 4 GiB (tools/d2h_bench.py, profiles/r03/d2h.json).
-_STAGE_BYTES = 64 << 20
+# included): 54.7 GB/s on 8 GiB, against 48.5 with 64 MiB chunks, 42 with 32 MiB, and 49.9 with
+# the destination pre-faulted (so page faults are not the limit) (tools/d2h_bench.py,
+# profiles/r03/d2h_r3b.json).
+_STAGE_BYTES = 128 << 20
 _SMALL_BYTES = 8 << 20  # below this a plain copy is as fast
 _stage = {}
 

@@ -108,13 +108,13 @@ class HipPhases:
                        "pbh_stream_wait_event")
 
     # -- step 1 ---------------------------------------------------------------------------
-    def sorted_counts(self, col, n, t0, nt, flag, counts, heads=None, hcur=None):
+    def sorted_counts(self, col, n, t0, nt, flag, counts, heads=None, hcur=None, certify=False):
         prm = (ctypes.c_double * 3)(*col.params)
         _lib.check(self.lib.pbh_lhs_sorted_counts(col.seed, n, t0, nt, col.lhs_col, col.dist, prm, len(col.params),
                                                   counts.data_ptr(), heads.data_ptr() if heads is not None else None,
                                                   hcur.data_ptr() if hcur is not None else None,
                                                   heads.shape[0] if heads is not None else 0, flag.data_ptr(),
-                                                  device.stream()), "pbh_lhs_sorted_counts")
+                                                  int(certify), device.stream()), "pbh_lhs_sorted_counts")
 
     def sort_heads(self, heads):
         _lib.check(self.lib.pbh_sort_heads(heads.data_ptr(), heads.shape[0], device.stream()), "pbh_sort_heads")
@@ -451,8 +451,8 @@ def _iman_conover_lhs(columns, P, n, group, world, rank, phases, flags, defer):
             cstream = torch.cuda.Stream(device=S.device)
             cstream.wait_stream(torch.cuda.current_stream(S.device))
         with torch.cuda.stream(cstream) if cstream is not None else _nullcontext():
-            for c in late:
-                phases.sorted_counts(columns[c], n, seg_t0, seg_len, flags[c:c + 1], dcounts[c])
+            for c in late:  # the certificate: only a non-zero sum (possible tie) redoes with exact counts
+                phases.sorted_counts(columns[c], n, seg_t0, seg_len, flags[c:c + 1], dcounts[c], certify=True)
 
     # ---- step 4: column owners rank their full columns, pipelined -----------------------------
     own = [cb[o + 1] - cb[o] for o in range(world)]

@@ -67,7 +67,7 @@ class CpuPhases:
         return _ppf(col, q)
 
     # -- step 1
-    def sorted_counts(self, col, n, t0, nt, flag, counts, heads=None, hcur=None):
+    def sorted_counts(self, col, n, t0, nt, flag, counts, heads=None, hcur=None, certify=False):
         x = self._sorted(col, n, np.arange(t0, t0 + nt))
         if not np.isfinite(x).all():
             flag |= 1  # the kernels' atomicOr of bit 0

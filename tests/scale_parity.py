@@ -205,8 +205,25 @@ def gate_all(n, d, seed, C, threads=8, log=print):
         log(r)
         return r
 
-    with ThreadPoolExecutor(threads) as ex:
-        cols = list(ex.map(one, range(d)))
+    import threading
+
+    done = []
+    stop = threading.Event()
+
+    def heartbeat():  # a line a minute: long gates are not mistaken for hung runs
+        while not stop.wait(60):
+            log(f"[{time.time() - t0:6.1f}s] {len(done)} of {d} columns gated")
+
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    try:
+        with ThreadPoolExecutor(threads) as ex:
+            cols = []
+            for r in ex.map(one, range(d)):
+                cols.append(r)
+                done.append(r["column"])
+    finally:
+        stop.set()
     return {"what": "SURVEY.md §8(d) step-4 parity gate: device (production path) vs the reference's "
                     "corrcoef/cholesky/solve_triangular/@P.T/rankdata on the device scores S",
             "workload": f"cfg3 (cfg2 set x4), N={n}, d={d}, native LHS seed {seed}, "

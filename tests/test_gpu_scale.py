@@ -59,7 +59,7 @@ def test_cfg3_step4_mismatch_gate_1e8_all_columns(gpu):
 
     from oracle.pipeline import cfg3_corr
 
-    doc = sp.gate_all(100_000_000, 32, 0, cfg3_corr(32), threads=8,
+    doc = sp.gate_all(100_000_000, 32, 0, cfg3_corr(32), threads=16,
                       log=lambda m: print(m if isinstance(m, str) else json.dumps(m), flush=True))
     print(json.dumps({k: v for k, v in doc.items() if k != "columns"}))
     assert doc["violations_total"] == 0, [c for c in doc["columns"] if c["violations"]]

@@ -138,10 +138,11 @@ def test_generated_step4_finish_segments(gpu, monkeypatch, env):
 
 
 def test_deferred_tie_check_redoes_the_call(gpu):
-    """The tie / inversion counts of continuous generated columns run next to steps 1-3 with
-    their scores computed as untied; a column that does tie -- uniform(loc=2**40, scale=1): its
-    ulp (2^-12) spans ~24 strata at n = 1e5 -- fails the check before step 4 and the call is
-    redone with the counts first, so its 'average' ranks and step-4 indices are the oracle's."""
+    """The tie / inversion checks of continuous generated columns run next to steps 1-3 with
+    their scores computed as untied, checked after step 4 (the default PBH_DEFER_COUNTS=3; every
+    mode in tests/test_gpu_certificate.py); a column that does tie -- uniform(loc=2**40, scale=1):
+    its ulp (2^-12) spans ~24 strata at n = 1e5 -- fails the check and the call is redone with the
+    exact counts first, so its 'average' ranks and step-4 indices are the oracle's."""
     dists = [("uniform", {"loc": 2.0**40, "scale": 1.0}), ("norm", {}), ("gamma", {"a": 2.0})]
     C = np.array([[1.0, 0.3, 0.2], [0.3, 1.0, 0.4], [0.2, 0.4, 1.0]])
     n = 100_000

@@ -76,11 +76,11 @@ def main():
         p_back = torch.randint(0, n, (K, nrows), dtype=torch.int64, device=S.device).to(torch.int32)  # valid positions
         Y = ph.empty((K, nrows))
 
-        def counts_phase():
+        def counts_phase():  # discrete: counts + heads; continuous: the (deferred) certificate
             for c, col in enumerate(cols):
                 d = col.dist in DISCRETE
                 ph.sorted_counts(col, n, seg_t0, row1 - seg_t0, flags[c:c + 1], counts[c],
-                                 heads=heads[c] if d else None, hcur=hcur[c:c + 1] if d else None)
+                                 heads=heads[c] if d else None, hcur=hcur[c:c + 1] if d else None, certify=not d)
 
         def scores_phase():
             for c, col in enumerate(cols):
