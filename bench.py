@@ -389,6 +389,8 @@ def end_to_end(root, ds, n, d, seed, barrier, device_ms):
     numpy samples_ on every node (modeling.py:582-583, 614), here all 32 columns handed back in one
     pipelined batch through the pinned ring (device.to_host_many).  d2h = the total minus the
     device-resident step time measured above.  A side figure, never `value`."""
+    from probabilit_amd import device
+
     barrier()
     t0 = time.perf_counter()
     root.sample(n, random_state=seed, method="lhs")
@@ -401,7 +403,8 @@ def end_to_end(root, ds, n, d, seed, barrier, device_ms):
     return {"value": round(n * d / (ms / 1e3) / 1e6, 2), "unit": "Msamples/s", "ms": round(ms, 1),
             "device_ms": round(device_ms, 1), "d2h_ms": round(d2h_ms, 1),
             "d2h_GBps": round(nbytes / (d2h_ms / 1e3) / 1e9, 2), "bytes": nbytes,
-            "what": "Node.sample() with numpy samples_ on all columns (pinned-ring D2H, 64 MiB chunks)"}
+            "what": f"Node.sample() with numpy samples_ on all columns (pinned-ring D2H, "
+                    f"{device.__dict__['_STAGE_BYTES'] >> 20} MiB chunks)"}
 
 
 def cpu_baseline(n, d):

@@ -78,6 +78,7 @@ def to_host(t):
 _STAGE_BYTES = 128 << 20
 _SMALL_BYTES = 8 << 20  # below this a plain copy is as fast
 _stage = {}
+_stage_lock = __import__("threading").Lock()  # one user of the ring at a time (callers may be threads)
 
 
 def _staging():
@@ -113,6 +114,13 @@ def to_host_many(tensors):
             chunks.append((src, dst, lo, min(nbytes, lo + _STAGE_BYTES)))
     if not chunks:
         return outs
+    with _stage_lock:
+        _drain_chunks(chunks)
+    return outs
+
+
+def _drain_chunks(chunks):
+    torch = _torch()
     st = _staging()
     ring, evs, stream, pool, nt = st["ring"], st["events"], st["stream"], st["pool"], st["threads"]
     stream.wait_stream(torch.cuda.current_stream(device()))  # after the producers of the tensors
@@ -134,7 +142,7 @@ def to_host_many(tensors):
                 evs[i % 3].record(stream)
             if i >= 2:
                 drain(i - 2)
-    return outs  # every chunk was drained: no DMA still reads a source
+    # every chunk was drained: no DMA still reads a source
 
 
 def ptr(t):
