@@ -578,6 +578,234 @@ __global__ __launch_bounds__(kT) void k_msd2(const uint32_t* __restrict__ kin, c
   }
 }
 
+// The code passes at 8 waves per SIMD (PBH_MSD_OCC=1, the default): the same passes with fewer
+// live registers.  A slot's LDS position (digit start + rank) replaces its key and rank once the
+// digit starts are known, so the key is dead after the first staging round; the rows round reuses
+// the slots and the destinations.  k_msd1 / k_msd2 need 83-84 VGPRs (5 waves per SIMD); these
+// stay within 64, and with 19 KiB of LDS 8 blocks fit a CU.  Memory-latency-bound passes run
+// faster with more waves in flight.
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8))) void k_msd1o(
+    const uint32_t* __restrict__ codes, int64_t n, const uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ rout, const uint32_t* __restrict__ cstart, int cpad,
+    const int32_t* __restrict__ state) {
+  if (*state) return;
+  __shared__ uint32_t cnt[256], lst[264], gb[256];
+  __shared__ uint32_t sk[kTile1];
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTile1;
+  const int m = (int)((n - base) < kTile1 ? (n - base) : kTile1);
+  cnt[t] = 0;
+  __syncthreads();
+  uint32_t key[kIpt1], slot[kIpt1];
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    key[j] = p < m ? codes[base + p] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) slot[j] = (j * kT + t < m) ? atomicAdd(&cnt[key[j] >> 24], 1u) : 0u;
+  __syncthreads();
+  const uint32_t my = cnt[t];
+  lst[t] = block_excl_scan256(my, lst);
+  uint32_t myb;
+  if (cstart) {
+    const uint32_t xc = blockIdx.x & 7u;
+    myb = my ? cstart[(xc << 8) + t] + atomicAdd(&cur[((xc << 8) + t) * cpad], my) : 0u;
+  } else {
+    myb = my ? start[t << 8] + atomicAdd(&cur[t * cpad], my) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    if (j * kT + t < m) {
+      slot[j] += lst[key[j] >> 24];
+      sk[slot[j]] = key[j];
+    }
+  }
+  gb[t] = myb;
+  __syncthreads();
+  uint32_t dst[kIpt1];
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    if (p < m) {
+      const uint32_t k = sk[p], d = k >> 24;
+      dst[j] = gb[d] + ((uint32_t)p - lst[d]);
+      kout[dst[j]] = k;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j)
+    if (j * kT + t < m) sk[slot[j]] = (uint32_t)(base + j * kT + t);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    if (p < m) rout[dst[j]] = sk[p];
+  }
+}
+
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(7))) void k_msd2o(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin, const uint32_t* __restrict__ start,
+    const uint32_t* __restrict__ tpre, uint32_t* __restrict__ cur, uint16_t* __restrict__ kout,
+    uint32_t* __restrict__ rout, const int32_t* __restrict__ state) {
+  if (*state) return;
+  const uint32_t tile = blockIdx.x;
+  if (tile >= tpre[256]) return;
+  __shared__ uint32_t cnt[256], lst[264], gb[256];
+  __shared__ uint32_t sk[kTile1];
+  __shared__ int gsh;
+  const int t = threadIdx.x;
+  if (t == 0) {  // the group holding this tile: last g with tpre[g] <= tile
+    int lo = 0, hi = 256;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tpre[mid] <= tile)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    while (lo < 255 && tpre[lo + 1] <= tile) ++lo;  // skip empty groups
+    gsh = lo;
+  }
+  cnt[t] = 0;
+  __syncthreads();
+  const int g = gsh;
+  const int64_t gs = start[g << 8], ge = start[(g + 1) << 8];
+  const int64_t base = gs + (int64_t)(tile - tpre[g]) * kTile1;
+  const int m = (int)((ge - base) < kTile1 ? (ge - base) : kTile1);
+  uint32_t key[kIpt1], slot[kIpt1];
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    key[j] = p < m ? kin[base + p] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) slot[j] = (j * kT + t < m) ? atomicAdd(&cnt[(key[j] >> 16) & 255u], 1u) : 0u;
+  __syncthreads();
+  const uint32_t my = cnt[t];
+  lst[t] = block_excl_scan256(my, lst);
+  const uint32_t b = ((uint32_t)g << 8) | (uint32_t)t;
+  const uint32_t myb = my ? start[b] + atomicAdd(&cur[b], my) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    if (j * kT + t < m) {
+      slot[j] += lst[(key[j] >> 16) & 255u];
+      sk[slot[j]] = key[j];
+    }
+  }
+  gb[t] = myb;
+  __syncthreads();
+  uint32_t dst[kIpt1];
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    if (p < m) {
+      const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
+      dst[j] = gb[d] + ((uint32_t)p - lst[d]);
+      kout[dst[j]] = (uint16_t)kk;
+    }
+  }
+  __syncthreads();
+  // the rows are read again here rather than held through the keys round (16 registers)
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    if (p < m) sk[slot[j]] = rin[base + p];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIpt1; ++j) {
+    const int p = j * kT + t;
+    if (p < m) rout[dst[j]] = sk[p];
+  }
+}
+
+// k_msd2o over 512 threads of 8 items (PBH_MSD2_CFG=1): the rows stay in registers through the
+// keys round instead of being read again, still within 64 VGPRs (8 waves per SIMD).
+constexpr int kTW = 512;
+constexpr int kIptW = kTile1 / kTW;
+__global__ __launch_bounds__(kTW) __attribute__((amdgpu_waves_per_eu(8))) void k_msd2w(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin, const uint32_t* __restrict__ start,
+    const uint32_t* __restrict__ tpre, uint32_t* __restrict__ cur, uint16_t* __restrict__ kout,
+    uint32_t* __restrict__ rout, const int32_t* __restrict__ state) {
+  if (*state) return;
+  const uint32_t tile = blockIdx.x;
+  if (tile >= tpre[256]) return;
+  __shared__ uint32_t cnt[256], lst[264], gb[256];
+  __shared__ uint32_t sk[kTile1];
+  __shared__ int gsh;
+  const int t = threadIdx.x;
+  if (t == 0) {  // the group holding this tile: last g with tpre[g] <= tile
+    int lo = 0, hi = 256;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tpre[mid] <= tile)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    while (lo < 255 && tpre[lo + 1] <= tile) ++lo;  // skip empty groups
+    gsh = lo;
+  }
+  if (t < 256) cnt[t] = 0;
+  __syncthreads();
+  const int g = gsh;
+  const int64_t gs = start[g << 8], ge = start[(g + 1) << 8];
+  const int64_t base = gs + (int64_t)(tile - tpre[g]) * kTile1;
+  const int m = (int)((ge - base) < kTile1 ? (ge - base) : kTile1);
+  uint32_t key[kIptW], row[kIptW], slot[kIptW];
+#pragma unroll
+  for (int j = 0; j < kIptW; ++j) {
+    const int p = j * kTW + t;
+    key[j] = p < m ? kin[base + p] : 0u;
+    row[j] = p < m ? rin[base + p] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < kIptW; ++j) slot[j] = (j * kTW + t < m) ? atomicAdd(&cnt[(key[j] >> 16) & 255u], 1u) : 0u;
+  __syncthreads();
+  const uint32_t my = t < 256 ? cnt[t] : 0u;
+  const uint32_t ex = block_excl_scan256(my, lst);  // waves 4-7 add nothing
+  uint32_t myb = 0u;
+  if (t < 256) {
+    lst[t] = ex;
+    const uint32_t b = ((uint32_t)g << 8) | (uint32_t)t;
+    myb = my ? start[b] + atomicAdd(&cur[b], my) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIptW; ++j) {
+    if (j * kTW + t < m) {
+      slot[j] += lst[(key[j] >> 16) & 255u];
+      sk[slot[j]] = key[j];
+    }
+  }
+  if (t < 256) gb[t] = myb;
+  __syncthreads();
+  uint32_t dst[kIptW];
+#pragma unroll
+  for (int j = 0; j < kIptW; ++j) {
+    const int p = j * kTW + t;
+    if (p < m) {
+      const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
+      dst[j] = gb[d] + ((uint32_t)p - lst[d]);
+      kout[dst[j]] = (uint16_t)kk;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIptW; ++j)
+    if (j * kTW + t < m) sk[slot[j]] = row[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIptW; ++j) {
+    const int p = j * kTW + t;
+    if (p < m) rout[dst[j]] = sk[p];
+  }
+}
+
 // ---------------------------------------------------------------- bucket finish
 // One wave per top-16 bucket: the low 16 bits and rows in registers (32 items per lane), a
 // non-stable LDS-atomic pass on the low byte and a stable ballot-ranked pass on the high byte
@@ -1089,6 +1317,194 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   if (t == 0 && bad) atomicOr(flags, 1);
 }
 
+// The counting finish over 512 threads (PBH_FINISH_CFG=29, the default): k_finish_ah's work with
+// 4 items of each bucket per thread instead of 8, so it fits 64 VGPRs and 8 waves per SIMD (the
+// 256-thread kernel needs ~100-120 VGPRs: 4 waves), which hides its latency far better (r3 A/B:
+// 23-24 against 28-30 ms per step).  The bin loop counts by code alone and marks the members of
+// runs of equal codes; a second loop orders each run by CS value.  With Q the run members' CS
+// values are first loaded together into an LDS queue (one round trip per bucket instead of one
+// per item; a bucket whose runs hold more than kFQCap items reads the rest from global memory):
+// faster standalone, but the default without it measured ~2 ms per step faster in the pipeline.
+constexpr int kFQCap = 512;
+
+template <int BINS>
+union FinishQLds {
+  struct {
+    uint32_t cnt[BINS + 1];
+    uint16_t key[kBucketCap2];
+    uint16_t qi[kBucketCap2];  // a run member's queue slot, by its position in the bin order
+    uint32_t row[kBucketCap2];
+    double qx[kFQCap];
+  } a;
+  uint64_t sv[2 * kBucketCap2];
+};
+
+// NT threads per block (256: 8 items of each bucket per thread, 4 waves per SIMD; 512: 4 items, 8)
+// Q = false: no queue, the run members read the CS values of their run from global memory in
+// pass 2 (as k_finish_ah does in its one loop)
+template <int BINS, int NT, bool Q = true>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 8 : 4))) void k_finish_q(
+    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ rows, const double* __restrict__ x,
+    const uint32_t* __restrict__ start, int s_top, uint32_t* __restrict__ gcur, int cpad, uint64_t* __restrict__ out,
+    int32_t* __restrict__ flags, const int32_t* __restrict__ state) {
+  if (*state) return;
+  constexpr int FB = 2;
+  constexpr int kShift = 16 - __builtin_ctz(BINS);
+  constexpr int kPer = BINS / NT;
+  constexpr int kIt = kBucketCap2 / NT;  // items of a bucket per thread
+  __shared__ FinishQLds<BINS> L;
+  __shared__ uint32_t gcnt[256], goff[264], gbase[256];
+  __shared__ int bad;
+  __shared__ uint32_t nq;
+  const int t = threadIdx.x;
+  if (t == 0) bad = 0;
+  if (t < 256) gcnt[t] = 0;
+  uint32_t kk[FB][kIt], rr[FB][kIt], grk[FB * kIt];
+  int64_t s0[FB];
+  int l0[FB];
+#pragma unroll
+  for (int bb = 0; bb < FB; ++bb) {
+    const int bkt = blockIdx.x * FB + bb;
+    s0[bb] = start[bkt];
+    l0[bb] = (int)((int64_t)start[bkt + 1] - s0[bb]);
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+      const int p = j * NT + t;
+      kk[bb][j] = p < l0[bb] ? (uint32_t)keys[s0[bb] + p] : 0u;
+      rr[bb][j] = p < l0[bb] ? rows[s0[bb] + p] : 0u;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int bb = 0; bb < FB; ++bb)
+#pragma unroll
+    for (int j = 0; j < kIt; ++j)
+      grk[bb * kIt + j] = (j * NT + t < l0[bb]) ? atomicAdd(&gcnt[rr[bb][j] >> s_top], 1u) : 0u;
+  __syncthreads();
+  const uint32_t my = t < 256 ? gcnt[t] : 0u;
+  const uint32_t gex = block_excl_scan256(my, goff);  // waves past 4 add nothing
+  if (t < 256) goff[t] = gex;
+  const uint32_t mybase = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * cpad], my)) : 0u;
+  uint64_t pr[FB * kIt];
+  int total = 0;
+#pragma unroll
+  for (int bb = 0; bb < FB; ++bb) {
+    const int64_t s = s0[bb];
+    const int len = l0[bb];
+    for (int i = t; i <= BINS; i += NT) L.a.cnt[i] = 0;
+    if (t == 0) nq = 0;
+    __syncthreads();
+    uint32_t rk[kIt];
+#pragma unroll
+    for (int j = 0; j < kIt; ++j)
+      rk[j] = (j * NT + t < len) ? atomicAdd(&L.a.cnt[kk[bb][j] >> kShift], 1u) : 0u;
+    __syncthreads();
+    uint32_t cb[kPer], sum = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      cb[q] = L.a.cnt[kPer * t + q];
+      sum += cb[q];
+    }
+    uint32_t run = block_excl_scan256(sum, goff);  // scratch goff[256..259]; goff[0..255] kept
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      L.a.cnt[kPer * t + q] = run;
+      run += cb[q];
+    }
+    if (t == NT - 1) L.a.cnt[BINS] = run;
+    __syncthreads();
+    uint32_t pos[kIt];
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+      if (j * NT + t < len) {
+        pos[j] = L.a.cnt[kk[bb][j] >> kShift] + rk[j];
+        L.a.key[pos[j]] = (uint16_t)kk[bb][j];
+        L.a.row[pos[j]] = rr[bb][j];
+      }
+    }
+    __syncthreads();
+    // pass 1: the bin's items by code alone; members of runs of equal codes are marked
+    uint32_t lt[kIt], runs = 0;
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+      lt[j] = 0;
+      if (j * NT + t >= len) continue;
+      const uint32_t kj = kk[bb][j];
+      const uint32_t bs = L.a.cnt[kj >> kShift], be = L.a.cnt[(kj >> kShift) + 1];
+      if (be - bs > 1) {
+        if (be - bs > (uint32_t)kBinCap) bad = 1;
+        bool member = false;
+        for (uint32_t m = bs; m < be; ++m) {
+          const uint32_t km = L.a.key[m];
+          lt[j] += km < kj;
+          member |= km == kj && m != pos[j];
+        }
+        runs |= (uint32_t)member << j;
+      }
+      lt[j] += bs;
+    }
+    // the run members' CS values: queue slots, then every load issued before any is waited on
+    uint32_t slot[kIt];
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) slot[j] = kFQCap;
+    if constexpr (Q) {
+#pragma unroll
+      for (int j = 0; j < kIt; ++j) {
+        if ((runs >> j) & 1u) {
+          slot[j] = atomicAdd(&nq, 1u);
+          L.a.qi[pos[j]] = (uint16_t)(slot[j] < (uint32_t)kFQCap ? slot[j] : 0xFFFFu);
+        }
+      }
+      double v[kIt];
+#pragma unroll
+      for (int j = 0; j < kIt; ++j) v[j] = slot[j] < (uint32_t)kFQCap ? x[rr[bb][j]] : 0.0;
+#pragma unroll
+      for (int j = 0; j < kIt; ++j)
+        if (slot[j] < (uint32_t)kFQCap) L.a.qx[slot[j]] = v[j];
+      __syncthreads();
+    }
+    // pass 2: a run member counts the smaller / equal CS values of its run (from LDS)
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+      const int sl = bb * kIt + j;
+      if (j * NT + t >= len) {
+        pr[sl] = ~0ull;
+        continue;
+      }
+      uint32_t eq = 0;
+      if ((runs >> j) & 1u) {
+        const uint32_t kj = kk[bb][j];
+        const uint32_t bs = L.a.cnt[kj >> kShift], be = L.a.cnt[(kj >> kShift) + 1];
+        const double xv = slot[j] < (uint32_t)kFQCap ? L.a.qx[slot[j]] : x[rr[bb][j]];
+        for (uint32_t m = bs; m < be; ++m) {
+          if (L.a.key[m] != kj || m == pos[j]) continue;
+          const uint32_t qm = Q ? L.a.qi[m] : 0xFFFFu;
+          const double xm = qm < (uint32_t)kFQCap ? L.a.qx[qm] : x[L.a.row[m]];
+          lt[j] += xm < xv;
+          eq += xm == xv;
+        }
+      }
+      const uint32_t p = (uint32_t)s + lt[j] + eq / 2;
+      pr[sl] = ((uint64_t)rr[bb][j] << 32) | (uint64_t)p;
+    }
+    total += len;
+    __syncthreads();
+  }
+  if (t < 256) gbase[t] = mybase;
+  __syncthreads();
+#pragma unroll
+  for (int sl = 0; sl < FB * kIt; ++sl)
+    if (pr[sl] != ~0ull) L.sv[goff[(uint32_t)(pr[sl] >> (32 + s_top))] + grk[sl]] = pr[sl];
+  __syncthreads();
+  for (int p = t; p < total; p += NT) {
+    const uint64_t v2 = L.sv[p];
+    const uint32_t g = (uint32_t)(v2 >> (32 + s_top));
+    out[gbase[g] + ((uint32_t)p - goff[g])] = v2;
+  }
+  __syncthreads();
+  if (t == 0 && bad) atomicOr(flags, 1);
+}
+
 // ---------------------------------------------------------------- row placement passes
 // Input grouped by row >> s_in (closed-form groups: rows are a permutation of [0, n), so group
 // g occupies positions [g << s_in, ...)); tiles of kTileP never straddle a group.  Digit =
@@ -1214,6 +1630,79 @@ __global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ i
         const uint32_t d = (uint32_t)(x >> (32 + s_out)) - g0;
         out[gb[d] + ((uint32_t)p - lst[d])] = x;
       }
+    }
+  }
+}
+
+// k_place_msd at 8 waves per SIMD (PBH_MSD_OCC=1, closed-form groups): the same 4096-pair tile
+// over 512 threads of 8 pairs each (k_place_msd<true>: 256 threads of 16, 100 VGPRs, 4 waves per
+// SIMD).  The low halves are staged first and read back in position order, then the high halves
+// (rows), which give the destination; the pair is written whole.
+constexpr int kTO = 512;
+constexpr int kIptO = kTileP / kTO;
+__global__ __launch_bounds__(kTO) __attribute__((amdgpu_waves_per_eu(8))) void k_place_msdo(
+    const uint64_t* __restrict__ in, int64_t n, int s_out, uint32_t* __restrict__ cur, uint64_t* __restrict__ out,
+    const int32_t* __restrict__ state) {
+  if (state && *state) return;
+  __shared__ uint32_t cnt[256], lst[264], gb[256];
+  __shared__ uint32_t sh32[kTileP];
+  __shared__ uint32_t gfirst;
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTileP;
+  const int m = (int)((n - base) < kTileP ? (n - base) : kTileP);
+  if (t < 256) cnt[t] = 0;
+  if (t == 0) gfirst = 0xFFFFFFFFu;
+  __syncthreads();
+  uint32_t hi[kIptO], lo[kIptO], slot[kIptO];
+#pragma unroll
+  for (int j = 0; j < kIptO; ++j) {
+    const int p = j * kTO + t;
+    const uint64_t v = p < m ? in[base + p] : 0ull;
+    hi[j] = (uint32_t)(v >> 32);
+    lo[j] = (uint32_t)v;
+  }
+  uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+  for (int j = 0; j < kIptO; ++j)
+    if (j * kTO + t < m) mn = min(mn, hi[j] >> s_out);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor(mn, o, 64));
+  if ((t & 63) == 0) atomicMin(&gfirst, mn);
+  __syncthreads();
+  const uint32_t g0 = gfirst;
+#pragma unroll
+  for (int j = 0; j < kIptO; ++j) slot[j] = (j * kTO + t < m) ? atomicAdd(&cnt[(hi[j] >> s_out) - g0], 1u) : 0u;
+  __syncthreads();
+  const uint32_t my = t < 256 ? cnt[t] : 0u;
+  const uint32_t ex = block_excl_scan256(my, lst);  // waves 4-7 add nothing (lst[256..263] scratch)
+  uint32_t myb = 0u;
+  if (t < 256) {
+    lst[t] = ex;
+    myb = my ? (uint32_t)(((uint64_t)(g0 + t) << s_out) + atomicAdd(&cur[g0 + t], my)) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIptO; ++j) {
+    if (j * kTO + t < m) {
+      slot[j] += lst[(hi[j] >> s_out) - g0];
+      sh32[slot[j]] = lo[j];
+    }
+  }
+  if (t < 256) gb[t] = myb;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIptO; ++j) lo[j] = sh32[j * kTO + t];  // low halves in position order
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIptO; ++j)
+    if (j * kTO + t < m) sh32[slot[j]] = hi[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIptO; ++j) {
+    const int p = j * kTO + t;
+    if (p < m) {
+      const uint32_t h = sh32[p], d = (h >> s_out) - g0;
+      out[gb[d] + ((uint32_t)p - lst[d])] = ((uint64_t)h << 32) | lo[j];
     }
   }
 }
@@ -1385,6 +1874,16 @@ void step4_sync_side_streams() {
   }
 }
 
+// PBH_MSD_OCC=0: the code passes and the row-placement passes at their earlier register use
+// (5 / 4 waves per SIMD) instead of k_msd1o / k_msd2o / k_place_msdo (8)
+static bool msd_occ() {
+  static const bool v = [] {
+    const char* e = getenv("PBH_MSD_OCC");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 bool step4_fused() {
   static const bool v = [] {
     const char* e = getenv("PBH_STEP4_FUSED");  // "0": position-order finish + every placement level
@@ -1526,7 +2025,24 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     const char* e = getenv("PBH_MSD_SPLIT");
     return !(e && e[0] == '0');
   }();
-  if (split) {
+  if (msd_occ()) {
+    PBH_TIMED(kKMsd1, s,
+              hipLaunchKernelGGL(k_msd1o, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
+                                 sh.cur1 + (int64_t)c * 8 * 256 * cur_pad(), cb.keys32, cb.rows1, cst, cur_pad(), state));
+    PBH_CHECK_LAUNCH();
+    static const int msd2_cfg = [] {  // PBH_MSD2_CFG: 1 = k_msd2w (512 threads), 0 = k_msd2o
+      const char* e = getenv("PBH_MSD2_CFG");
+      return e ? atoi(e) : 1;
+    }();
+    if (msd2_cfg == 1)
+      PBH_TIMED(kKMsd2, s,
+                hipLaunchKernelGGL(k_msd2w, dim3((unsigned)(t1 + 256)), dim3(kTW), 0, s, cb.keys32, cb.rows1, start,
+                                   sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
+    else
+      PBH_TIMED(kKMsd2, s,
+                hipLaunchKernelGGL(k_msd2o, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
+                                   sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
+  } else if (split) {
     PBH_TIMED(kKMsd1, s,
               hipLaunchKernelGGL(k_msd1<true>, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
                                  sh.cur1 + (int64_t)c * 8 * 256 * cur_pad(), cb.keys32, cb.rows1, cst, cur_pad(), state));
@@ -1548,12 +2064,14 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     int shifts[4];
     const int nl = place_levels(n, shifts);
     const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
-    // PBH_FINISH_CFG (A/B measurements): 26 (default) / 25 / 24 = k_finish_ah (2 buckets per block,
-    // cursor adds hoisted) with 1024 / 2048 / 4096 bins; otherwise k_finish_fused with
+    // PBH_FINISH_CFG (A/B measurements, profiles/r03/README_ab.md): 29 (default) = k_finish_q over
+    // 512 threads, 1024 bins, the run members' CS values read in pass 2; 28 = the same with those
+    // reads queued through LDS; 30 = queued, 2048 bins; 27 = queued, 256 threads; 26 / 25 / 24 = k_finish_ah (2 buckets per block, cursor adds hoisted) with 1024 /
+    // 2048 / 4096 bins; otherwise k_finish_fused with
     // <buckets per block><log2 bins - 10>, 23 = with prefetch
     static const int cfg = [] {
       const char* e = getenv("PBH_FINISH_CFG");
-      return e ? atoi(e) : 26;
+      return e ? atoi(e) : 29;
     }();
     uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
     const int cpad = cur_pad();
@@ -1567,6 +2085,42 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
             hipLaunchKernelGGL((k_finish_fused<FB, BINS>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16, cb.rows2, cs, \
                                start, s_top, gc, cpad, segcap, cb.pairs[0], sh.flags + c, state))
     switch (cfg) {
+      case 27:
+        if (!segcap) {
+          PBH_TIMED(kKFinish, s,
+                    hipLaunchKernelGGL((k_finish_q<1024, 256>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
+                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
+          break;
+        }
+        PBH_FIN(2, 4096);
+        break;
+      case 28:
+        if (!segcap) {
+          PBH_TIMED(kKFinish, s,
+                    hipLaunchKernelGGL((k_finish_q<1024, 512>), dim3(65536 / 2), dim3(512), 0, s, cb.keys16, cb.rows2, cs,
+                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
+          break;
+        }
+        PBH_FIN(2, 4096);
+        break;
+      case 29:
+        if (!segcap) {
+          PBH_TIMED(kKFinish, s,
+                    hipLaunchKernelGGL((k_finish_q<1024, 512, false>), dim3(65536 / 2), dim3(512), 0, s, cb.keys16, cb.rows2,
+                                       cs, start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
+          break;
+        }
+        PBH_FIN(2, 4096);
+        break;
+      case 30:
+        if (!segcap) {
+          PBH_TIMED(kKFinish, s,
+                    hipLaunchKernelGGL((k_finish_q<2048, 512>), dim3(65536 / 2), dim3(512), 0, s, cb.keys16, cb.rows2, cs,
+                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
+          break;
+        }
+        PBH_FIN(2, 4096);
+        break;
       case 11: PBH_FIN(1, 2048); break;
       case 12: PBH_FIN(1, 4096); break;
       case 21: PBH_FIN(2, 2048); break;
@@ -1638,7 +2192,11 @@ int step4_gen_place_passes(int c, int64_t n, const Step4Shared& sh, const Step4C
       return !(e && e[0] == '0');
     }();
     const uint32_t* segp = sg ? cb.segtp : nullptr;
-    if (split)
+    if (!sg && msd_occ())
+      PBH_TIMED(kKPlaceMsd, s,
+                hipLaunchKernelGGL(k_place_msdo, dim3((unsigned)grid), dim3(kTO), 0, s, cb.pairs[cur], n, shifts[l], cr,
+                                   cb.pairs[cur ^ 1], state));
+    else if (split)
       PBH_TIMED(kKPlaceMsd, s,
                 hipLaunchKernelGGL(k_place_msd<true>, dim3((unsigned)grid), dim3(kT), 0, s, cb.pairs[cur], n, shifts[l],
                                    cr, cb.pairs[cur ^ 1], state, segp, segcur, cpad, segcap, nseg));
