@@ -62,11 +62,13 @@ PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k
              "k_code_runs": ["k_code_buckets", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
              "k_apply": ["k_apply_mfma", "k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"],
              "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"],
-             "k_finish": ["k_finish_ah<2048>", "k_finish_ah<1024>", "k_finish_ah<4096>", "k_finish_fused<2, 4096>", "k_finish_fused<2, 4096, false>",
+             "k_finish": ["k_finish_q<1024, 512, false>", "k_finish_q<1024, 512, true>", "k_finish_q<2048, 512, true>",
+                          "k_finish_q<1024, 256, true>", "k_finish_ah<2048>", "k_finish_ah<1024>", "k_finish_ah<4096>", "k_finish_fused<2, 4096>", "k_finish_fused<2, 4096, false>",
                           "k_finish_fused<2, 4096, true>", "k_finish_fused<1, 4096>", "k_finish_fused<2, 2048>",
                           "k_finish_fused<1, 2048>", "k_finish_fused<4, 2048>", "k_finish_fused<4, 4096>", "k_finish"],
-             "k_msd1": ["k_msd1<true>", "k_msd1<false>", "k_msd1"], "k_msd2": ["k_msd2<true>", "k_msd2<false>", "k_msd2"],
-             "k_place_msd": ["k_place_msd<true>", "k_place_msd<false>", "k_place_msd"],
+             "k_msd1": ["k_msd1o", "k_msd1<true>", "k_msd1<false>", "k_msd1"],
+             "k_msd2": ["k_msd2w", "k_msd2o", "k_msd2<true>", "k_msd2<false>", "k_msd2"],
+             "k_place_msd": ["k_place_msdo", "k_place_msd<true>", "k_place_msd<false>", "k_place_msd"],
              "k_hist16": ["k_hist16"],
              # one timing id over every variant that ran (the cfg3 set: norm, lognorm, triang,
              # uniform, expon, gamma, poisson): traffic = their dispatch-weighted mean

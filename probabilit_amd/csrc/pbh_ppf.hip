@@ -724,6 +724,201 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
   }
 }
 
+// gamma with a window of the guide table in LDS: a column of n strata draws its quantiles from
+// [~1 / n, 1 - ~1 / n], i.e. w = log(q / (1 - q)) within about +-log n, a third of the table's
+// [-80, 40] at n = 1e8 (1280 nodes: 40 KiB next to the 32 KiB block).  Two 512-thread workgroups
+// per CU then take the place of one 1024-thread one (k_place_gen_gamma), so one workgroup's
+// barriers and loads overlap the other's arithmetic.  The interpolation is guide_interp's
+// arithmetic on the same node values, so every value is bit-identical; an item whose interval
+// lies outside the window (a quantile within 1 / (4 n) of 0 or 1) goes to the slow queue, which
+// evaluates ppf_one with the global table (the same function and values as gamma_ppf_lds).
+constexpr int kGWBlock = 512;
+constexpr int kGWin = 1280;  // window nodes of the step-4 placement
+
+// nodes [*j0, *j0 + *jn) of the guide cover w in [-wl, wl]; false when more than cap nodes
+// PBH_GAMMA_WIN=0: the whole table in LDS, one 1024-thread workgroup per CU
+bool gamma_win_on() {
+  static const bool on = [] {
+    const char* e = getenv("PBH_GAMMA_WIN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool gamma_window_w(double wl, const sf::GammaGuide& T, int cap, int* j0, int* jn) {
+  const int lo = (int)floor((-wl - T.z0) * T.inv_h) - 1, hi = (int)ceil((wl - T.z0) * T.inv_h) + 2;
+  *j0 = lo < 0 ? 0 : lo;
+  const int h = hi > T.m ? T.m : hi;
+  *jn = h - *j0;
+  return *jn >= 2 && *jn <= cap;
+}
+
+bool gamma_window(int64_t n, const sf::GammaGuide& T, int* j0, int* jn) {
+  return gamma_window_w(log(4.0 * (double)n), T, kGWin, j0, jn);  // q in [1 / (4 n), 1 - 1 / (4 n)]
+}
+
+// The ppf sweep's gamma (q read from memory, any value): the window |w| <= 36, i.e. q within
+// [2.3e-16, 1 - 2.3e-16] -- every 53-bit uniform but the few nearest 0 and 1 -- 2310 nodes, 72 KiB,
+// so two 512-thread workgroups fit a CU instead of one 1024-thread workgroup with the whole 120 KiB
+// table (k_ppf_gamma_lds).  Same arithmetic on the same node values; items outside the window
+// (and every other slow case) take ppf_one with the global table.
+constexpr int kGSWin = 2320;
+constexpr double kGSWinW = 36.0;
+
+__global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_ppf_gamma_w(
+    const double* __restrict__ q, int64_t q_stride, int64_t n, Params prm, PoissonTable pt, double* __restrict__ out,
+    int32_t* flag, int j0, int jn) {
+  __shared__ double win[4 * kGSWin];
+  constexpr int kPer = 8, kTile = kPer * kGWBlock, kQCap = 2048;
+  __shared__ uint16_t slowq[kQCap];
+  __shared__ int nslow;
+  const sf::GammaGuide& G = pt.guide;
+  for (int k = threadIdx.x; k < 4 * jn; k += kGWBlock) {
+    const int a = k / jn, i = k - a * jn;
+    win[a * kGSWin + i] = G.y[(int64_t)a * G.m + j0 + i];
+  }
+  const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
+  const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
+  for (int64_t base = (int64_t)blockIdx.x * kTile; base < n; base += (int64_t)gridDim.x * kTile) {
+    if (threadIdx.x == 0) nslow = 0;
+    __syncthreads();
+    double qv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = base + j * kGWBlock + threadIdx.x;
+      qv[j] = i < n ? q[i * q_stride] : 0.5;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = base + j * kGWBlock + threadIdx.x;
+      if (i >= n) continue;
+      bool fast = cond0 && qv[j] > 0.0 && qv[j] < 1.0;
+      double v = 0.0;
+      if (fast) {
+        const double w = log(qv[j] / (1.0 - qv[j]));
+        const double u = (w - G.z0) * G.inv_h;
+        fast = u >= 0.0 && u < (double)(G.m - 1);
+        if (fast) {
+          const int jj = (int)u;
+          const int jl = jj - j0;
+          fast = jl >= 0 && jl < jn - 1;
+          if (fast) {
+            const double yy = sf::guide_interp_arr(win, win + kGSWin, win + 2 * kGSWin, G.h, jl, u - (double)jj);
+            fast = yy >= -680.0 && yy <= 700.0 && win[3 * kGSWin + jl] != 0.0;
+            if (fast) v = exp(yy) * scale + loc;
+          }
+        }
+      }
+      if (fast) {
+        out[i] = v;
+        flag_nonfinite(flag, !isfinite(v));
+      } else {
+        const int slot = atomicAdd(&nslow, 1);
+        if (slot < kQCap) slowq[slot] = (uint16_t)(j * kGWBlock + threadIdx.x);
+      }
+    }
+    __syncthreads();
+    const int ns = nslow;
+    const int nd = ns <= kQCap ? ns : kTile;  // queue overflow: the whole tile again
+    for (int t = threadIdx.x; t < nd; t += kGWBlock) {
+      const int64_t i = base + (ns <= kQCap ? slowq[t] : t);
+      if (i >= n) continue;
+      const double x = ppf_one<PBH_DIST_GAMMA>(q[i * q_stride], prm.val[0], prm.val[1], prm.val[2], pt);
+      out[i] = x;
+      flag_nonfinite(flag, !isfinite(x));
+    }
+  }
+}
+
+template <bool BYROW = false>
+__global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_place_gen_gamma_w(const uint64_t* __restrict__ pairs,
+                                                                const uint32_t* __restrict__ pidx, int64_t rows,
+                                                                int64_t n, uint64_t seed, uint32_t col, Params prm,
+                                                                PoissonTable pt, double* __restrict__ y, int64_t y_rs,
+                                                                int32_t* __restrict__ idx,
+                                                                const int32_t* __restrict__ state, int j0, int jn) {
+  if (state && *state) return;
+  __shared__ double win[4 * kGWin];  // y, d1, d2, ok of nodes j0 .. j0 + jn - 1
+  __shared__ double buf[kGenRows];
+  constexpr int kQCap = 2048;
+  __shared__ uint16_t slowq[kQCap];
+  __shared__ int nslow;
+  const sf::GammaGuide& G = pt.guide;
+  for (int k = threadIdx.x; k < 4 * jn; k += kGWBlock) {
+    const int a = k / jn, i = k - a * jn;
+    win[a * kGWin + i] = G.y[(int64_t)a * G.m + j0 + i];  // the four global arrays are contiguous
+  }
+  __syncthreads();
+  Philox ph(seed);
+  const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
+  const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
+  constexpr int kPer = kGenRows / kGWBlock;
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
+    if (threadIdx.x == 0) nslow = 0;
+    __syncthreads();
+    uint64_t pr[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int p = j * kGWBlock + threadIdx.x;
+      if constexpr (BYROW)
+        pr[j] = p < cnt ? ((uint64_t)(r0 + p) << 32) | pidx[r0 + p] : ~0ull;
+      else
+        pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const bool valid = pr[j] != ~0ull;
+      const double q = lhs_sorted_quantile(ph, (uint64_t)(uint32_t)pr[j], col, (uint64_t)n);
+      // igami_guided's interpolation branch, operation for operation, on the window
+      bool fast = valid && cond0 && q > 0.0 && q < 1.0;
+      double v = 0.0;
+      if (fast) {
+        const double w = log(q / (1.0 - q));
+        const double u = (w - G.z0) * G.inv_h;
+        fast = u >= 0.0 && u < (double)(G.m - 1);
+        if (fast) {
+          const int jj = (int)u;
+          const int jl = jj - j0;
+          fast = jl >= 0 && jl < jn - 1;
+          if (fast) {
+            const double yy = sf::guide_interp_arr(win, win + kGWin, win + 2 * kGWin, G.h, jl, u - (double)jj);
+            fast = yy >= -680.0 && yy <= 700.0 && win[3 * kGWin + jl] != 0.0;
+            if (fast) v = exp(yy) * scale + loc;
+          }
+        }
+      }
+      if (valid) {
+        const int64_t row = (int64_t)(pr[j] >> 32);
+        if (!BYROW && idx) idx[row] = (int32_t)(uint32_t)pr[j];
+        if (fast) {
+          buf[row - r0] = v;
+        } else {
+          const int slot = atomicAdd(&nslow, 1);
+          if (slot < kQCap) slowq[slot] = (uint16_t)(j * kGWBlock + threadIdx.x);
+        }
+      }
+    }
+    __syncthreads();
+    const int ns = nslow;
+    const int nd = ns <= kQCap ? ns : cnt;  // queue overflow: recompute the whole block
+    for (int i = threadIdx.x; i < nd; i += kGWBlock) {
+      const int p = ns <= kQCap ? slowq[i] : i;
+      const uint64_t prr = BYROW ? ((uint64_t)(r0 + p) << 32) | pidx[r0 + p] : pairs[r0 + p];
+      buf[(int64_t)(prr >> 32) - r0] = ppf_one<PBH_DIST_GAMMA>(
+          lhs_sorted_quantile(ph, (uint64_t)(uint32_t)prr, col, (uint64_t)n), prm.val[0], prm.val[1], prm.val[2], pt);
+    }
+    __syncthreads();
+    if (y_rs == 1) {
+      for (int p = threadIdx.x; p < cnt; p += kGWBlock) y[r0 + p] = buf[p];
+    } else {
+      for (int p = threadIdx.x; p < cnt; p += kGWBlock) y[(r0 + p) * y_rs] = buf[p];
+    }
+    __syncthreads();
+  }
+}
+
 // poisson with the CDF table + guide in (dynamic) LDS
 template <bool BYROW = false>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_poisson(const uint64_t* __restrict__ pairs,
@@ -1080,6 +1275,13 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
   const bool streamable = light && qs == 1 && !prm.ptr[0] && !prm.ptr[1] && !prm.ptr[2] &&
                           ((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0 && stream_enabled();
   dim3 gv(grid_for(n, kVTile, 256 * 8));
+  int j0 = 0, jn = 0;
+  if (gamma_win_on() && gamma_lds_ok(dist, prm, pt) && gamma_window_w(kGSWinW, pt.guide, kGSWin, &j0, &jn)) {
+    PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_gamma_w, dim3(grid_for(n, 8 * kGWBlock, 512)), dim3(kGWBlock), 0, s,
+                                           q, qs, n, prm, pt, out, flag, j0, jn));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
   if (gamma_lds_ok(dist, prm, pt)) {
     PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_gamma_lds, dim3(gamma_lds_grid(n)), dim3(kGBlock), 0, s, q, qs, n,
                                            prm, pt, out, flag));
@@ -1446,6 +1648,15 @@ static int place_launch(const GenColumn* g, const uint64_t* pairs, const uint32_
   const int64_t n = g->n;
   const int64_t blocks = (rows + kGenRows - 1) / kGenRows;
   if (blocks <= 0) return PBH_OK;
+  int j0 = 0, jn = 0;
+  if (gamma_win_on() && gamma_lds_ok(g->dist, g->prm, g->pt) && gamma_window(n, g->pt.guide, &j0, &jn)) {
+    PBH_TIMED(kKPlaceGen, s,
+              hipLaunchKernelGGL(k_place_gen_gamma_w<BYROW>, dim3((unsigned)(blocks < 512 ? blocks : 512)),
+                                 dim3(kGWBlock), 0, s, pairs, pidx, rows, n, g->seed, g->col, g->prm, g->pt, y, y_rs,
+                                 idx, state, j0, jn));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
   if (gamma_lds_ok(g->dist, g->prm, g->pt)) {
     PBH_TIMED(kKPlaceGen, s,
               hipLaunchKernelGGL(k_place_gen_gamma<BYROW>, dim3((unsigned)(blocks < 256 ? blocks : 256)), dim3(kGBlock),

@@ -646,85 +646,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8))) void k_
   }
 }
 
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(7))) void k_msd2o(
-    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin, const uint32_t* __restrict__ start,
-    const uint32_t* __restrict__ tpre, uint32_t* __restrict__ cur, uint16_t* __restrict__ kout,
-    uint32_t* __restrict__ rout, const int32_t* __restrict__ state) {
-  if (*state) return;
-  const uint32_t tile = blockIdx.x;
-  if (tile >= tpre[256]) return;
-  __shared__ uint32_t cnt[256], lst[264], gb[256];
-  __shared__ uint32_t sk[kTile1];
-  __shared__ int gsh;
-  const int t = threadIdx.x;
-  if (t == 0) {  // the group holding this tile: last g with tpre[g] <= tile
-    int lo = 0, hi = 256;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (tpre[mid] <= tile)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    while (lo < 255 && tpre[lo + 1] <= tile) ++lo;  // skip empty groups
-    gsh = lo;
-  }
-  cnt[t] = 0;
-  __syncthreads();
-  const int g = gsh;
-  const int64_t gs = start[g << 8], ge = start[(g + 1) << 8];
-  const int64_t base = gs + (int64_t)(tile - tpre[g]) * kTile1;
-  const int m = (int)((ge - base) < kTile1 ? (ge - base) : kTile1);
-  uint32_t key[kIpt1], slot[kIpt1];
-#pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    key[j] = p < m ? kin[base + p] : 0u;
-  }
-#pragma unroll
-  for (int j = 0; j < kIpt1; ++j) slot[j] = (j * kT + t < m) ? atomicAdd(&cnt[(key[j] >> 16) & 255u], 1u) : 0u;
-  __syncthreads();
-  const uint32_t my = cnt[t];
-  lst[t] = block_excl_scan256(my, lst);
-  const uint32_t b = ((uint32_t)g << 8) | (uint32_t)t;
-  const uint32_t myb = my ? start[b] + atomicAdd(&cur[b], my) : 0u;
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    if (j * kT + t < m) {
-      slot[j] += lst[(key[j] >> 16) & 255u];
-      sk[slot[j]] = key[j];
-    }
-  }
-  gb[t] = myb;
-  __syncthreads();
-  uint32_t dst[kIpt1];
-#pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    if (p < m) {
-      const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
-      dst[j] = gb[d] + ((uint32_t)p - lst[d]);
-      kout[dst[j]] = (uint16_t)kk;
-    }
-  }
-  __syncthreads();
-  // the rows are read again here rather than held through the keys round (16 registers)
-#pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    if (p < m) sk[slot[j]] = rin[base + p];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    if (p < m) rout[dst[j]] = sk[p];
-  }
-}
-
-// k_msd2o over 512 threads of 8 items (PBH_MSD2_CFG=1): the rows stay in registers through the
-// keys round instead of being read again, still within 64 VGPRs (8 waves per SIMD).
+// msd2 over 512 threads of 8 items: the rows stay in registers through the keys round, within
+// 64 VGPRs (8 waves per SIMD; the 256-thread form with 16 items needs 72 VGPRs, or the rows read
+// twice, and measured 15.5 against 14.7 ms per step).
 constexpr int kTW = 512;
 constexpr int kIptW = kTile1 / kTW;
 __global__ __launch_bounds__(kTW) __attribute__((amdgpu_waves_per_eu(8))) void k_msd2w(
@@ -1043,8 +967,9 @@ union FinishLds {
 };
 
 // FB buckets per block (staging FB * kBucketCap2 pairs); BINS counting bins on the top
-// log2(BINS) of the 16 low code bits
-template <int FB, int BINS, bool PF = false>  // PF: the next bucket's keys / rows loaded ahead
+// log2(BINS) of the 16 low code bits.  Kept for the segmented XCD-class output (PBH_FINISH_XCD=1);
+// the closed-form layout takes k_finish_q.
+template <int FB, int BINS>
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_finish_fused(const uint16_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ rows,
                                                      const double* __restrict__ x,
@@ -1065,7 +990,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   uint64_t pr[FB * kFIpt];
   uint32_t grk[FB * kFIpt];
   int total = 0;
-  uint32_t kn[kFIpt], rn[kFIpt];
   auto load = [&](int bkt, uint32_t* kk, uint32_t* rr) {
     const int64_t s0 = start[bkt];
     const int l0 = (int)((int64_t)start[bkt + 1] - s0);
@@ -1076,7 +1000,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       rr[j] = p < l0 ? rows[s0 + p] : 0u;
     }
   };
-  if (PF) load(blockIdx.x * FB, kn, rn);
 #pragma unroll
   for (int bb = 0; bb < FB; ++bb) {
     const int bkt = blockIdx.x * FB + bb;
@@ -1084,16 +1007,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const int len = (int)((int64_t)start[bkt + 1] - s);  // <= kBucketCap2 (k_hist16_scan)
     for (int i = t; i <= BINS; i += kT) L.a.cnt[i] = 0;
     uint32_t k[kFIpt], r[kFIpt], rk[kFIpt];
-    if (PF) {
-#pragma unroll
-      for (int j = 0; j < kFIpt; ++j) {
-        k[j] = kn[j];
-        r[j] = rn[j];
-      }
-      if (bb + 1 < FB) load(bkt + 1, kn, rn);
-    } else {
-      load(bkt, k, r);
-    }
+    load(bkt, k, r);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kFIpt; ++j) rk[j] = (j * kT + t < len) ? atomicAdd(&L.a.cnt[k[j] >> kShift], 1u) : 0u;
@@ -1187,136 +1101,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   if (t == 0 && bad) atomicOr(flags, 1);
 }
 
-// The same finish with the group-cursor atomics hoisted (PBH_FINISH_CFG=24): both buckets' rows
-// are loaded first, their row groups counted and the global cursor adds issued before the
-// buckets are worked on, so the adds' round trip overlaps the bucket work instead of ending the
-// block.  Closed-form group layout only.
-template <int BINS>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_finish_ah(
-    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ rows, const double* __restrict__ x,
-    const uint32_t* __restrict__ start, int s_top, uint32_t* __restrict__ gcur, int cpad, uint64_t* __restrict__ out,
-    int32_t* __restrict__ flags, const int32_t* __restrict__ state) {
-  if (*state) return;
-  constexpr int FB = 2;
-  constexpr int kShift = 16 - __builtin_ctz(BINS);
-  constexpr int kPer = BINS / kT;
-  __shared__ FinishLds<FB, BINS> L;
-  __shared__ uint32_t gcnt[256], goff[264], gbase[256];
-  __shared__ int bad;
-  const int t = threadIdx.x;
-  if (t == 0) bad = 0;
-  gcnt[t] = 0;
-  uint32_t kk[FB][kFIpt], rr[FB][kFIpt], grk[FB * kFIpt];
-  int64_t s0[FB];
-  int l0[FB];
-#pragma unroll
-  for (int bb = 0; bb < FB; ++bb) {
-    const int bkt = blockIdx.x * FB + bb;
-    s0[bb] = start[bkt];
-    l0[bb] = (int)((int64_t)start[bkt + 1] - s0[bb]);
-#pragma unroll
-    for (int j = 0; j < kFIpt; ++j) {
-      const int p = j * kT + t;
-      kk[bb][j] = p < l0[bb] ? (uint32_t)keys[s0[bb] + p] : 0u;
-      rr[bb][j] = p < l0[bb] ? rows[s0[bb] + p] : 0u;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int bb = 0; bb < FB; ++bb)
-#pragma unroll
-    for (int j = 0; j < kFIpt; ++j)
-      grk[bb * kFIpt + j] = (j * kT + t < l0[bb]) ? atomicAdd(&gcnt[rr[bb][j] >> s_top], 1u) : 0u;
-  __syncthreads();
-  const uint32_t my = gcnt[t];
-  goff[t] = block_excl_scan256(my, goff);
-  const uint32_t mybase = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * cpad], my)) : 0u;
-  uint64_t pr[FB * kFIpt];
-  int total = 0;
-#pragma unroll
-  for (int bb = 0; bb < FB; ++bb) {
-    const int64_t s = s0[bb];
-    const int len = l0[bb];
-    for (int i = t; i <= BINS; i += kT) L.a.cnt[i] = 0;
-    __syncthreads();
-    uint32_t rk[kFIpt];
-#pragma unroll
-    for (int j = 0; j < kFIpt; ++j)
-      rk[j] = (j * kT + t < len) ? atomicAdd(&L.a.cnt[kk[bb][j] >> kShift], 1u) : 0u;
-    __syncthreads();
-    uint32_t cb[kPer], sum = 0;
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-      cb[q] = L.a.cnt[kPer * t + q];
-      sum += cb[q];
-    }
-    uint32_t run = block_excl_scan256(sum, goff);  // scratch goff[256..259]; goff[0..255] kept
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-      L.a.cnt[kPer * t + q] = run;
-      run += cb[q];
-    }
-    if (t == kT - 1) L.a.cnt[BINS] = run;
-    __syncthreads();
-    uint32_t pos[kFIpt];
-#pragma unroll
-    for (int j = 0; j < kFIpt; ++j) {
-      if (j * kT + t < len) {
-        pos[j] = L.a.cnt[kk[bb][j] >> kShift] + rk[j];
-        L.a.key[pos[j]] = (uint16_t)kk[bb][j];
-        L.a.row[pos[j]] = rr[bb][j];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kFIpt; ++j) {
-      const int slot = bb * kFIpt + j;
-      if (j * kT + t >= len) {
-        pr[slot] = ~0ull;
-        continue;
-      }
-      const uint32_t kj = kk[bb][j];
-      const uint32_t bs = L.a.cnt[kj >> kShift], be = L.a.cnt[(kj >> kShift) + 1];
-      uint32_t lt = 0, eq = 0;
-      if (be - bs > 1) {
-        if (be - bs > (uint32_t)kBinCap) bad = 1;
-        bool have = false;
-        double xv = 0.0;
-        for (uint32_t m = bs; m < be; ++m) {
-          const uint32_t km = L.a.key[m];
-          lt += km < kj;
-          if (km == kj && m != pos[j]) {
-            if (!have) {
-              xv = x[rr[bb][j]];
-              have = true;
-            }
-            const double xm = x[L.a.row[m]];
-            lt += xm < xv;
-            eq += xm == xv;
-          }
-        }
-      }
-      const uint32_t p = (uint32_t)s + bs + lt + eq / 2;
-      pr[slot] = ((uint64_t)rr[bb][j] << 32) | (uint64_t)p;
-    }
-    total += len;
-    __syncthreads();
-  }
-  gbase[t] = mybase;
-  __syncthreads();
-#pragma unroll
-  for (int slot = 0; slot < FB * kFIpt; ++slot)
-    if (pr[slot] != ~0ull) L.sv[goff[(uint32_t)(pr[slot] >> (32 + s_top))] + grk[slot]] = pr[slot];
-  __syncthreads();
-  for (int p = t; p < total; p += kT) {
-    const uint64_t v = L.sv[p];
-    const uint32_t g = (uint32_t)(v >> (32 + s_top));
-    out[gbase[g] + ((uint32_t)p - goff[g])] = v;
-  }
-  __syncthreads();
-  if (t == 0 && bad) atomicOr(flags, 1);
-}
-
 // The counting finish over 512 threads (PBH_FINISH_CFG=29, the default): k_finish_ah's work with
 // 4 items of each bucket per thread instead of 8, so it fits 64 VGPRs and 8 waves per SIMD (the
 // 256-thread kernel needs ~100-120 VGPRs: 4 waves), which hides its latency far better (r3 A/B:
@@ -1327,7 +1111,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // faster standalone, but the default without it measured ~2 ms per step faster in the pipeline.
 constexpr int kFQCap = 512;
 
-template <int BINS>
+template <int BINS, int FB>
 union FinishQLds {
   struct {
     uint32_t cnt[BINS + 1];
@@ -1336,7 +1120,7 @@ union FinishQLds {
     uint32_t row[kBucketCap2];
     double qx[kFQCap];
   } a;
-  uint64_t sv[2 * kBucketCap2];
+  uint64_t sv[FB * kBucketCap2];
 };
 
 // NT threads per block (256: 8 items of each bucket per thread, 4 waves per SIMD; 512: 4 items, 8)
@@ -1348,11 +1132,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
     const uint32_t* __restrict__ start, int s_top, uint32_t* __restrict__ gcur, int cpad, uint64_t* __restrict__ out,
     int32_t* __restrict__ flags, const int32_t* __restrict__ state) {
   if (*state) return;
-  constexpr int FB = 2;
+  constexpr int FB = 2;  // buckets per block (one per block measured 24 -> 42 ms per step)
   constexpr int kShift = 16 - __builtin_ctz(BINS);
   constexpr int kPer = BINS / NT;
   constexpr int kIt = kBucketCap2 / NT;  // items of a bucket per thread
-  __shared__ FinishQLds<BINS> L;
+  __shared__ FinishQLds<BINS, FB> L;
   __shared__ uint32_t gcnt[256], goff[264], gbase[256];
   __shared__ int bad;
   __shared__ uint32_t nq;
@@ -1892,6 +1676,7 @@ bool step4_fused() {
   return v;
 }
 
+
 // MSD levels of the row placement: shifts from kGenPlaceShift up, at most 8 bits per level
 static int place_levels(int64_t n, int* shifts) {
   int bits = 0;
@@ -2001,9 +1786,9 @@ int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs
   hipLaunchKernelGGL(k_make_codes_adapt, dim3((unsigned)(cb < 1024 ? (cb < 1 ? 1 : cb) : 1024), (unsigned)kk),
                      dim3(256), 0, s, cs, ldcs, n, retry, amap, codes, ldc);
   PBH_CHECK_LAUNCH();
-  PBH_TIMED(kKHist16, s,
-            hipLaunchKernelGGL(k_hist16_q, dim3((unsigned)blocks, (unsigned)kk, 4), dim3(1024), 0, s, codes, ldc, n, hist,
-                               cls, state, retry));
+  // (not timed as k_hist16: a re-count of one column, where k_hist16's bytes per launch are all of them)
+  hipLaunchKernelGGL(k_hist16_q, dim3((unsigned)blocks, (unsigned)kk, 4), dim3(1024), 0, s, codes, ldc, n, hist, cls,
+                     state, retry);
   PBH_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)kk), dim3(1024), 0, s, hist, n, sh.start + (int64_t)c0 * 65537,
                      sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, retry);
@@ -2030,18 +1815,9 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
               hipLaunchKernelGGL(k_msd1o, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
                                  sh.cur1 + (int64_t)c * 8 * 256 * cur_pad(), cb.keys32, cb.rows1, cst, cur_pad(), state));
     PBH_CHECK_LAUNCH();
-    static const int msd2_cfg = [] {  // PBH_MSD2_CFG: 1 = k_msd2w (512 threads), 0 = k_msd2o
-      const char* e = getenv("PBH_MSD2_CFG");
-      return e ? atoi(e) : 1;
-    }();
-    if (msd2_cfg == 1)
-      PBH_TIMED(kKMsd2, s,
-                hipLaunchKernelGGL(k_msd2w, dim3((unsigned)(t1 + 256)), dim3(kTW), 0, s, cb.keys32, cb.rows1, start,
-                                   sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
-    else
-      PBH_TIMED(kKMsd2, s,
-                hipLaunchKernelGGL(k_msd2o, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
-                                   sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
+    PBH_TIMED(kKMsd2, s,
+              hipLaunchKernelGGL(k_msd2w, dim3((unsigned)(t1 + 256)), dim3(kTW), 0, s, cb.keys32, cb.rows1, start,
+                                 sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
   } else if (split) {
     PBH_TIMED(kKMsd1, s,
               hipLaunchKernelGGL(k_msd1<true>, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
@@ -2066,9 +1842,8 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
     // PBH_FINISH_CFG (A/B measurements, profiles/r03/README_ab.md): 29 (default) = k_finish_q over
     // 512 threads, 1024 bins, the run members' CS values read in pass 2; 28 = the same with those
-    // reads queued through LDS; 30 = queued, 2048 bins; 27 = queued, 256 threads; 26 / 25 / 24 = k_finish_ah (2 buckets per block, cursor adds hoisted) with 1024 /
-    // 2048 / 4096 bins; otherwise k_finish_fused with
-    // <buckets per block><log2 bins - 10>, 23 = with prefetch
+    // reads queued through LDS; 30 = queued, 2048 bins; 26 = 256 threads (round 2's k_finish_ah).
+    // The segmented XCD-class output (PBH_FINISH_XCD=1) always takes k_finish_fused.
     static const int cfg = [] {
       const char* e = getenv("PBH_FINISH_CFG");
       return e ? atoi(e) : 29;
@@ -2076,86 +1851,23 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
     const int cpad = cur_pad();
     const uint32_t segcap = fin_segcap(n);
-#define PBH_FIN2(FB, BINS)                                                                                        \
-  PBH_TIMED(kKFinish, s,                                                                                          \
-            hipLaunchKernelGGL((k_finish_fused<FB, BINS, true>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16,     \
-                               cb.rows2, cs, start, s_top, gc, cpad, segcap, cb.pairs[0], sh.flags + c, state))
-#define PBH_FIN(FB, BINS)                                                                                         \
-  PBH_TIMED(kKFinish, s,                                                                                          \
-            hipLaunchKernelGGL((k_finish_fused<FB, BINS>), dim3(65536 / FB), dim3(kT), 0, s, cb.keys16, cb.rows2, cs, \
-                               start, s_top, gc, cpad, segcap, cb.pairs[0], sh.flags + c, state))
-    switch (cfg) {
-      case 27:
-        if (!segcap) {
-          PBH_TIMED(kKFinish, s,
-                    hipLaunchKernelGGL((k_finish_q<1024, 256>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
-                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
-          break;
-        }
-        PBH_FIN(2, 4096);
-        break;
-      case 28:
-        if (!segcap) {
-          PBH_TIMED(kKFinish, s,
-                    hipLaunchKernelGGL((k_finish_q<1024, 512>), dim3(65536 / 2), dim3(512), 0, s, cb.keys16, cb.rows2, cs,
-                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
-          break;
-        }
-        PBH_FIN(2, 4096);
-        break;
-      case 29:
-        if (!segcap) {
-          PBH_TIMED(kKFinish, s,
-                    hipLaunchKernelGGL((k_finish_q<1024, 512, false>), dim3(65536 / 2), dim3(512), 0, s, cb.keys16, cb.rows2,
-                                       cs, start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
-          break;
-        }
-        PBH_FIN(2, 4096);
-        break;
-      case 30:
-        if (!segcap) {
-          PBH_TIMED(kKFinish, s,
-                    hipLaunchKernelGGL((k_finish_q<2048, 512>), dim3(65536 / 2), dim3(512), 0, s, cb.keys16, cb.rows2, cs,
-                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
-          break;
-        }
-        PBH_FIN(2, 4096);
-        break;
-      case 11: PBH_FIN(1, 2048); break;
-      case 12: PBH_FIN(1, 4096); break;
-      case 21: PBH_FIN(2, 2048); break;
-      case 23: PBH_FIN2(2, 4096); break;
-      case 26:
-        if (!segcap) {
-          PBH_TIMED(kKFinish, s,
-                    hipLaunchKernelGGL((k_finish_ah<1024>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
-                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
-          break;
-        }
-        PBH_FIN(2, 4096);
-        break;
-      case 25:
-        if (!segcap) {
-          PBH_TIMED(kKFinish, s,
-                    hipLaunchKernelGGL((k_finish_ah<2048>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
-                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
-          break;
-        }
-        PBH_FIN(2, 4096);
-        break;
-      case 24:
-        if (!segcap) {
-          PBH_TIMED(kKFinish, s,
-                    hipLaunchKernelGGL((k_finish_ah<4096>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
-                                       start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state));
-          break;
-        }
-        PBH_FIN(2, 4096);
-        break;
-      default: PBH_FIN(2, 4096); break;
+#define PBH_FINQ(BINS, NT, Q)                                                                                    \
+  PBH_TIMED(kKFinish, s,                                                                                         \
+            hipLaunchKernelGGL((k_finish_q<BINS, NT, Q>), dim3(65536 / 2), dim3(NT), 0, s, cb.keys16, cb.rows2, cs, \
+                               start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state))
+    if (segcap) {
+      PBH_TIMED(kKFinish, s,
+                hipLaunchKernelGGL((k_finish_fused<2, 4096>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
+                                   start, s_top, gc, cpad, segcap, cb.pairs[0], sh.flags + c, state));
+    } else {
+      switch (cfg) {
+        case 26: PBH_FINQ(1024, 256, false); break;
+        case 28: PBH_FINQ(1024, 512, true); break;
+        case 30: PBH_FINQ(2048, 512, true); break;
+        default: PBH_FINQ(1024, 512, false); break;
+      }
     }
-#undef PBH_FIN
-#undef PBH_FIN2
+#undef PBH_FINQ
   } else {
     PBH_TIMED(kKFinish, s,
               hipLaunchKernelGGL(k_finish, dim3(65536 / kBFWaves), dim3(64 * kBFWaves), 0, s, cb.keys16, cb.rows2, cs,

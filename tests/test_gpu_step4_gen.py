@@ -151,3 +151,67 @@ def test_deferred_tie_check_redoes_the_call(gpu):
     assert len(np.unique(ref["Y"][:, 0])) < n // 10  # the column does tie
     np.testing.assert_array_equal(idx, ref["idx"])
     assert_close(Y, ref["Y"], rtol=1e-10, what="deferred tie check")
+
+
+_VARIANT_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})
+from probabilit_amd import device
+from test_gpu_step4_gen import _debug_run
+out = _debug_run({n}, {dists!r}, {seed}, np.array({C!r}))
+for k, v in out.items():
+    np.save({d!r} + "/" + k + ".npy", v)
+"""
+
+
+def _debug_run(n, dists, seed, C):
+    """Y, idx, S and E of the generated-column path (debug outputs of pbh_iman_conover)."""
+    import ctypes
+
+    from probabilit_amd import _lib, device, qmc
+    from probabilit_amd.correlation import ImanConover
+    from probabilit_amd.modeling import Distribution
+
+    d = len(dists)
+    inst = ImanConover().set_target(C)
+    flags = device.zeros(d, "int32")
+    cols = []
+    for j, (nm, kw) in enumerate(dists):
+        v = Distribution(nm, **kw)
+        params = [float(p) for p in v._params(n)]
+        cols.append(_lib.ICColumn(qmc.seed_from(seed), j, _lib.DIST_IDS[nm], (ctypes.c_double * 3)(*params),
+                                  len(params), flags.data_ptr() + 4 * j))
+    dbg = {"idx": device.empty((d, n), "int32"), "S": device.empty((d, n), "float64"), "E": np.zeros((d, d))}
+    Y = inst._transform_generated(cols, n, debug=dbg)
+    return {"Y": device.to_host(Y).T, "idx": device.to_host(dbg["idx"]).T, "S": device.to_host(dbg["S"]).T,
+            "E": dbg["E"].copy()}
+
+
+@pytest.mark.timeout(900)
+def test_step4_variants_match_the_oracle(gpu, tmp_path):
+    """Every A/B switch of the generated-column path, each in its own process (they are read
+    once): the round-2 code passes and 256-thread finish (PBH_MSD_OCC=0, PBH_FINISH_CFG=26), the
+    queued finish (28, 30), the whole gamma table in LDS (PBH_GAMMA_WIN=0) -- step-4 indices equal
+    to the oracle's and the outputs within 1e-10."""
+    import os
+    import subprocess
+    import sys
+
+    from oracle.pipeline import cfg3_corr, cfg_dists
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n, d, seed = 300_001, 8, 31
+    dists, C = cfg_dists(d), cfg3_corr(d)
+    ref = _oracle(n, dists, seed, C)
+    for env in ({"PBH_MSD_OCC": "0", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"}, {"PBH_FINISH_CFG": "30"},
+                {"PBH_GAMMA_WIN": "0"}):
+        dd = tmp_path / "_".join(f"{k}{v}" for k, v in env.items())
+        dd.mkdir()
+        script = _VARIANT_SCRIPT.format(root=root, tests=os.path.join(root, "tests"), d=str(dd), n=n, dists=dists,
+                                      seed=seed, C=C.tolist())
+        r = subprocess.run([sys.executable, "-c", script], env={**os.environ, **env}, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, (env, r.stderr[-3000:])
+        np.testing.assert_array_equal(np.load(dd / "idx.npy"), ref["idx"], err_msg=str(env))
+        assert_close(np.load(dd / "Y.npy"), ref["Y"], rtol=1e-10, what=str(env))
