@@ -537,8 +537,10 @@ __global__ void k_transform_matrix(const double* __restrict__ L, const double* _
   }
 }
 
-constexpr int AM_ROWS = 64;  // rows per wave tile
-
+// AM_ROWS rows per wave tile: 64 (2 waves per SIMD: 218 registers with the prefetch, 80 KiB of
+// LDS) or 32 (PBH_APPLY_ROWS=32: half the prefetch registers and half the LDS tile, 3 waves per
+// SIMD; each store instruction writes two columns' 256-byte halves)
+template <int AM_ROWS>
 __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int64_t n, int k, int64_t ld,
                                                    const double* __restrict__ M, uint32_t* __restrict__ codes,
                                                    int64_t ldc, CodeMap cm) {
@@ -601,10 +603,11 @@ __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int6
     }
     if ((bt + gridDim.x) * 4 < tiles) load(bt + gridDim.x);
     __syncthreads();
-    const int64_t r = r0 + lane;
+    const int rl = lane % AM_ROWS, c0 = lane / AM_ROWS;  // row in the tile, first column
+    const int64_t r = r0 + rl;
     if (tw < tiles && r < n) {
-      for (int c = 0; c < k; ++c) {
-        const double v = tl[lane * 33 + c];
+      for (int c = c0; c < k; c += 64 / AM_ROWS) {
+        const double v = tl[rl * 33 + c];
         S[(int64_t)c * ld + r] = v;
         if (codes) codes[(int64_t)c * ldc + r] = code_of(v, cm);
       }
@@ -743,10 +746,18 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
     PBH_CHECK_HIP(hipMallocAsync((void**)&M, 32 * 32 * sizeof(double), s));
     hipLaunchKernelGGL(k_transform_matrix, dim3(1), dim3(64), 0, s, L, inv_diag, P, k, M);
     PBH_CHECK_LAUNCH();
-    const int64_t tiles = (n + AM_ROWS - 1) / AM_ROWS;
+    static const int rows = [] {
+      const char* e = getenv("PBH_APPLY_ROWS");
+      return e && atoi(e) == 32 ? 32 : 64;
+    }();
+    const int64_t tiles = (n + rows - 1) / rows;
     const unsigned gb = (unsigned)((tiles + 3) / 4 < 8192 ? (tiles + 3) / 4 : 8192);
-    PBH_TIMED(kKApply, s,
-              hipLaunchKernelGGL(k_apply_mfma, dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc, c));
+    if (rows == 32)
+      PBH_TIMED(kKApply, s,
+                hipLaunchKernelGGL(k_apply_mfma<32>, dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc, c));
+    else
+      PBH_TIMED(kKApply, s,
+                hipLaunchKernelGGL(k_apply_mfma<64>, dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc, c));
     PBH_CHECK_LAUNCH();
     PBH_CHECK_HIP(hipFreeAsync(M, s));
     return PBH_OK;

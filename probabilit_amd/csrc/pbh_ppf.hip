@@ -757,79 +757,6 @@ bool gamma_window(int64_t n, const sf::GammaGuide& T, int* j0, int* jn) {
   return gamma_window_w(log(4.0 * (double)n), T, kGWin, j0, jn);  // q in [1 / (4 n), 1 - 1 / (4 n)]
 }
 
-// The ppf sweep's gamma (q read from memory, any value): the window |w| <= 36, i.e. q within
-// [2.3e-16, 1 - 2.3e-16] -- every 53-bit uniform but the few nearest 0 and 1 -- 2310 nodes, 72 KiB,
-// so two 512-thread workgroups fit a CU instead of one 1024-thread workgroup with the whole 120 KiB
-// table (k_ppf_gamma_lds).  Same arithmetic on the same node values; items outside the window
-// (and every other slow case) take ppf_one with the global table.
-constexpr int kGSWin = 2320;
-constexpr double kGSWinW = 36.0;
-
-__global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_ppf_gamma_w(
-    const double* __restrict__ q, int64_t q_stride, int64_t n, Params prm, PoissonTable pt, double* __restrict__ out,
-    int32_t* flag, int j0, int jn) {
-  __shared__ double win[4 * kGSWin];
-  constexpr int kPer = 8, kTile = kPer * kGWBlock, kQCap = 2048;
-  __shared__ uint16_t slowq[kQCap];
-  __shared__ int nslow;
-  const sf::GammaGuide& G = pt.guide;
-  for (int k = threadIdx.x; k < 4 * jn; k += kGWBlock) {
-    const int a = k / jn, i = k - a * jn;
-    win[a * kGSWin + i] = G.y[(int64_t)a * G.m + j0 + i];
-  }
-  const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
-  const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
-  for (int64_t base = (int64_t)blockIdx.x * kTile; base < n; base += (int64_t)gridDim.x * kTile) {
-    if (threadIdx.x == 0) nslow = 0;
-    __syncthreads();
-    double qv[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int64_t i = base + j * kGWBlock + threadIdx.x;
-      qv[j] = i < n ? q[i * q_stride] : 0.5;
-    }
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int64_t i = base + j * kGWBlock + threadIdx.x;
-      if (i >= n) continue;
-      bool fast = cond0 && qv[j] > 0.0 && qv[j] < 1.0;
-      double v = 0.0;
-      if (fast) {
-        const double w = log(qv[j] / (1.0 - qv[j]));
-        const double u = (w - G.z0) * G.inv_h;
-        fast = u >= 0.0 && u < (double)(G.m - 1);
-        if (fast) {
-          const int jj = (int)u;
-          const int jl = jj - j0;
-          fast = jl >= 0 && jl < jn - 1;
-          if (fast) {
-            const double yy = sf::guide_interp_arr(win, win + kGSWin, win + 2 * kGSWin, G.h, jl, u - (double)jj);
-            fast = yy >= -680.0 && yy <= 700.0 && win[3 * kGSWin + jl] != 0.0;
-            if (fast) v = exp(yy) * scale + loc;
-          }
-        }
-      }
-      if (fast) {
-        out[i] = v;
-        flag_nonfinite(flag, !isfinite(v));
-      } else {
-        const int slot = atomicAdd(&nslow, 1);
-        if (slot < kQCap) slowq[slot] = (uint16_t)(j * kGWBlock + threadIdx.x);
-      }
-    }
-    __syncthreads();
-    const int ns = nslow;
-    const int nd = ns <= kQCap ? ns : kTile;  // queue overflow: the whole tile again
-    for (int t = threadIdx.x; t < nd; t += kGWBlock) {
-      const int64_t i = base + (ns <= kQCap ? slowq[t] : t);
-      if (i >= n) continue;
-      const double x = ppf_one<PBH_DIST_GAMMA>(q[i * q_stride], prm.val[0], prm.val[1], prm.val[2], pt);
-      out[i] = x;
-      flag_nonfinite(flag, !isfinite(x));
-    }
-  }
-}
-
 template <bool BYROW = false>
 __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_place_gen_gamma_w(const uint64_t* __restrict__ pairs,
                                                                 const uint32_t* __restrict__ pidx, int64_t rows,
@@ -1275,13 +1202,6 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
   const bool streamable = light && qs == 1 && !prm.ptr[0] && !prm.ptr[1] && !prm.ptr[2] &&
                           ((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0 && stream_enabled();
   dim3 gv(grid_for(n, kVTile, 256 * 8));
-  int j0 = 0, jn = 0;
-  if (gamma_win_on() && gamma_lds_ok(dist, prm, pt) && gamma_window_w(kGSWinW, pt.guide, kGSWin, &j0, &jn)) {
-    PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_gamma_w, dim3(grid_for(n, 8 * kGWBlock, 512)), dim3(kGWBlock), 0, s,
-                                           q, qs, n, prm, pt, out, flag, j0, jn));
-    PBH_CHECK_LAUNCH();
-    return PBH_OK;
-  }
   if (gamma_lds_ok(dist, prm, pt)) {
     PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_gamma_lds, dim3(gamma_lds_grid(n)), dim3(kGBlock), 0, s, q, qs, n,
                                            prm, pt, out, flag));

@@ -1678,11 +1678,19 @@ bool step4_fused() {
 
 
 // MSD levels of the row placement: shifts from kGenPlaceShift up, at most 8 bits per level
+// PBH_PLACE_TOP=1: with two levels, the top one (the finish's scatter) takes 8 bits and the MSD
+// pass the rest (at N = 1e8: 191 groups of 2^19 rows, 128 digits per placement tile) instead of
+// the MSD pass taking 8 (96 groups of 2^20, 256 digits)
 static int place_levels(int64_t n, int* shifts) {
+  static const bool top = [] {
+    const char* e = getenv("PBH_PLACE_TOP");
+    return e && e[0] == '1';
+  }();
   int bits = 0;
   while (((int64_t)1 << bits) < n) ++bits;
   int nl = 0;
   for (int sh = kGenPlaceShift; sh < bits; sh += 8) shifts[nl++] = sh;
+  if (top && nl == 2 && bits - 8 > shifts[0]) shifts[1] = bits - 8;
   return nl;
 }
 
