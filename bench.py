@@ -66,14 +66,16 @@ PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k
                           "k_finish_q<1024, 256, true>", "k_finish_ah<2048>", "k_finish_ah<1024>", "k_finish_ah<4096>", "k_finish_fused<2, 4096>", "k_finish_fused<2, 4096, false>",
                           "k_finish_fused<2, 4096, true>", "k_finish_fused<1, 4096>", "k_finish_fused<2, 2048>",
                           "k_finish_fused<1, 2048>", "k_finish_fused<4, 2048>", "k_finish_fused<4, 4096>", "k_finish"],
-             "k_msd1": ["k_msd1o", "k_msd1<true>", "k_msd1<false>", "k_msd1"],
-             "k_msd2": ["k_msd2w", "k_msd2o", "k_msd2<true>", "k_msd2<false>", "k_msd2"],
+             "k_msd1": ["k_msd1x<1024, 8>", "k_msd1x<256, 16>", "k_msd1o", "k_msd1<true>", "k_msd1<false>", "k_msd1"],
+             "k_msd2": ["k_msd2x<1024, 8>", "k_msd2x<512, 8>", "k_msd2w", "k_msd2o", "k_msd2<true>", "k_msd2<false>",
+                        "k_msd2"],
              "k_place_msd": ["k_place_msdo", "k_place_msd<true>", "k_place_msd<false>", "k_place_msd"],
              "k_hist16": ["k_hist16"],
              # one timing id over every variant that ran (the cfg3 set: norm, lognorm, triang,
              # uniform, expon, gamma, poisson): traffic = their dispatch-weighted mean
              "k_place_gen": ["k_place_gen<0>", "k_place_gen<1>", "k_place_gen<2>", "k_place_gen<3>", "k_place_gen<4>",
                              "k_place_gen_direct<0>", "k_place_gen_direct<3>", "k_place_gen_gamma",
+                             "k_place_gen_gamma_w<false>",
                              "k_place_gen_poisson"],
              "k_lhs_sorted_ppf": ["k_lhs_sorted_ppf<0>", "k_lhs_sorted_ppf<1>", "k_lhs_sorted_ppf<2>",
                                   "k_lhs_sorted_ppf<3>", "k_lhs_sorted_ppf<4>", "k_lhs_sorted_ppf<5>",

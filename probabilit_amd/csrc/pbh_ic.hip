@@ -537,9 +537,9 @@ __global__ void k_transform_matrix(const double* __restrict__ L, const double* _
   }
 }
 
-// AM_ROWS rows per wave tile: 64 (2 waves per SIMD: 218 registers with the prefetch, 80 KiB of
-// LDS) or 32 (PBH_APPLY_ROWS=32: half the prefetch registers and half the LDS tile, 3 waves per
-// SIMD; each store instruction writes two columns' 256-byte halves)
+// AM_ROWS rows per wave tile: 32 (default: 148 registers with the prefetch and 46 KiB of LDS, 3
+// waves per SIMD; each store instruction writes two columns' 256-byte halves) or 64
+// (PBH_APPLY_ROWS=64: 218 registers and 80 KiB, 2 waves per SIMD)
 template <int AM_ROWS>
 __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int64_t n, int k, int64_t ld,
                                                    const double* __restrict__ M, uint32_t* __restrict__ codes,
@@ -746,9 +746,9 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
     PBH_CHECK_HIP(hipMallocAsync((void**)&M, 32 * 32 * sizeof(double), s));
     hipLaunchKernelGGL(k_transform_matrix, dim3(1), dim3(64), 0, s, L, inv_diag, P, k, M);
     PBH_CHECK_LAUNCH();
-    static const int rows = [] {
+    static const int rows = [] {  // 32 (default): 15.1 against 15.3-15.7 ms per step with 64
       const char* e = getenv("PBH_APPLY_ROWS");
-      return e && atoi(e) == 32 ? 32 : 64;
+      return e && atoi(e) == 64 ? 64 : 32;
     }();
     const int64_t tiles = (n + rows - 1) / rows;
     const unsigned gb = (unsigned)((tiles + 3) / 4 < 8192 ? (tiles + 3) / 4 : 8192);

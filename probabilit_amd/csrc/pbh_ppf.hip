@@ -729,9 +729,14 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
 // [-80, 40] at n = 1e8 (1280 nodes: 40 KiB next to the 32 KiB block).  Two 512-thread workgroups
 // per CU then take the place of one 1024-thread one (k_place_gen_gamma), so one workgroup's
 // barriers and loads overlap the other's arithmetic.  The interpolation is guide_interp's
-// arithmetic on the same node values, so every value is bit-identical; an item whose interval
-// lies outside the window (a quantile within 1 / (4 n) of 0 or 1) goes to the slow queue, which
-// evaluates ppf_one with the global table (the same function and values as gamma_ppf_lds).
+// arithmetic on the same node values, so every value is bit-identical.  An item the window
+// cannot interpolate (its interval outside the window -- a quantile within 1 / (4 n) of 0 or 1 --
+// or an interval without the midpoint check, q at 0 or 1, invalid parameters) is appended to a
+// global list instead, and k_place_gen_gamma_slow evaluates the list with ppf_one and the global
+// table (the same function and values as gamma_ppf_lds) after the placement: igami's iteration
+// is not in this kernel at all, whose registers it would otherwise size (80+ VGPRs of spills on
+// the hot path, 0.4 GB of scratch traffic per launch).  A list that overflows (a shape whose guide
+// leaves many intervals unchecked) makes the second kernel evaluate every row of the column.
 constexpr int kGWBlock = 512;
 constexpr int kGWin = 1280;  // window nodes of the step-4 placement
 
@@ -763,13 +768,11 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
                                                                 int64_t n, uint64_t seed, uint32_t col, Params prm,
                                                                 PoissonTable pt, double* __restrict__ y, int64_t y_rs,
                                                                 int32_t* __restrict__ idx,
-                                                                const int32_t* __restrict__ state, int j0, int jn) {
+                                                                const int32_t* __restrict__ state, int j0, int jn,
+                                                                unsigned long long* __restrict__ slow, uint32_t cap) {
   if (state && *state) return;
   __shared__ double win[4 * kGWin];  // y, d1, d2, ok of nodes j0 .. j0 + jn - 1
   __shared__ double buf[kGenRows];
-  constexpr int kQCap = 2048;
-  __shared__ uint16_t slowq[kQCap];
-  __shared__ int nslow;
   const sf::GammaGuide& G = pt.guide;
   for (int k = threadIdx.x; k < 4 * jn; k += kGWBlock) {
     const int a = k / jn, i = k - a * jn;
@@ -783,8 +786,6 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
   for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
     const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
-    if (threadIdx.x == 0) nslow = 0;
-    __syncthreads();
     uint64_t pr[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -819,22 +820,12 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
       if (valid) {
         const int64_t row = (int64_t)(pr[j] >> 32);
         if (!BYROW && idx) idx[row] = (int32_t)(uint32_t)pr[j];
-        if (fast) {
-          buf[row - r0] = v;
-        } else {
-          const int slot = atomicAdd(&nslow, 1);
-          if (slot < kQCap) slowq[slot] = (uint16_t)(j * kGWBlock + threadIdx.x);
+        buf[row - r0] = v;  // a slow item's value is written again by k_place_gen_gamma_slow
+        if (!fast) {
+          const unsigned long long k = atomicAdd(&slow[0], 1ull);
+          if (k < cap) slow[1 + k] = pr[j];
         }
       }
-    }
-    __syncthreads();
-    const int ns = nslow;
-    const int nd = ns <= kQCap ? ns : cnt;  // queue overflow: recompute the whole block
-    for (int i = threadIdx.x; i < nd; i += kGWBlock) {
-      const int p = ns <= kQCap ? slowq[i] : i;
-      const uint64_t prr = BYROW ? ((uint64_t)(r0 + p) << 32) | pidx[r0 + p] : pairs[r0 + p];
-      buf[(int64_t)(prr >> 32) - r0] = ppf_one<PBH_DIST_GAMMA>(
-          lhs_sorted_quantile(ph, (uint64_t)(uint32_t)prr, col, (uint64_t)n), prm.val[0], prm.val[1], prm.val[2], pt);
     }
     __syncthreads();
     if (y_rs == 1) {
@@ -843,6 +834,35 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
       for (int p = threadIdx.x; p < cnt; p += kGWBlock) y[(r0 + p) * y_rs] = buf[p];
     }
     __syncthreads();
+  }
+}
+
+// The window kernel's slow list: y[row] = ppf_one (igami with the global guide) for every listed
+// (row << 32 | p), or, when the list overflowed, for every row of the column
+template <bool BYROW = false>
+__global__ __launch_bounds__(256) void k_place_gen_gamma_slow(const uint64_t* __restrict__ pairs,
+                                                              const uint32_t* __restrict__ pidx, int64_t rows, int64_t n,
+                                                              uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
+                                                              double* __restrict__ y, int64_t y_rs,
+                                                              const int32_t* __restrict__ state,
+                                                              const unsigned long long* __restrict__ slow,
+                                                              uint32_t cap) {
+  if (state && *state) return;
+  Philox ph(seed);
+  const unsigned long long count = slow[0];
+  const bool all = count > cap;
+  const int64_t m = all ? rows : (int64_t)count;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (int64_t)gridDim.x * 256) {
+    uint64_t pr;
+    if (!all)
+      pr = slow[1 + i];
+    else if constexpr (BYROW)
+      pr = ((uint64_t)i << 32) | pidx[i];
+    else
+      pr = pairs[i];
+    const int64_t row = (int64_t)(pr >> 32);
+    y[row * y_rs] = ppf_one<PBH_DIST_GAMMA>(lhs_sorted_quantile(ph, (uint64_t)(uint32_t)pr, col, (uint64_t)n),
+                                            prm.val[0], prm.val[1], prm.val[2], pt);
   }
 }
 
@@ -959,6 +979,8 @@ __device__ __forceinline__ double run_average_rank(const uint32_t* __restrict__ 
   return (double)(s + 1) + (double)(e - s) / 2.0;
 }
 
+constexpr int64_t kLdsHeads = 4096;  // run heads staged in LDS by k_perm_scores (16 KiB)
+
 // Van der Waerden scores of an LHS column, rows [row0, row0 + nrows), in row order: the rank
 // of row r is pi(r) + 1 (untied), or the run average of stratum pi(r) (heads != NULL), so
 // S[r] = ndtri(rank / (n + 1)) (correlation.py:394-395) without sorting anything.  Ranks of
@@ -972,10 +994,16 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
   __shared__ TailQueue tq;
   __shared__ double res[kCTile];
   __shared__ double sh[kBlock / 64];
+  extern __shared__ uint32_t lheads[];  // a tied column's run heads (dynamic LDS; 0 bytes otherwise)
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
   const double np1 = (double)(n + 1);
   double sum = 0.0;
+  if (heads && nheads <= kLdsHeads) {  // the binary search reads LDS instead of L1/L2
+    for (int64_t i = threadIdx.x; i < nheads; i += kBlock) lheads[i] = heads[i];
+    __syncthreads();
+    heads = lheads;
+  }
   for (int64_t base = (int64_t)blockIdx.x * kCTile; base < nrows; base += (int64_t)gridDim.x * kCTile) {
     if (threadIdx.x == 0) tq.count = 0;
     __syncthreads();
@@ -1393,6 +1421,69 @@ void gen_destroy(GenColumn* g, hipStream_t s) {
   delete g;
 }
 
+// The counts and run heads of a poisson column's strata [t0, t0 + nt) without evaluating every
+// stratum: q_t = (t + 1 - u_t) / n increases strictly with t and the poisson ppf is monotone in q,
+// so the values are non-decreasing and a run boundary is the first stratum whose value reaches
+// some integer k.  One thread per k in (value(t0), value(t0 + nt - 1)] binary-searches it with
+// the same value() k_lhs_sorted_ppf evaluates (the same SplitMix64 jitter, the same CDF table
+// and comparisons), so the heads, the tie count (nt - 1 - #heads) and the inversion count (0)
+// equal that kernel's exactly, from ~30 evaluations per distinct value instead of nt.  The host
+// takes this path only when the last value is finite and the values span at most kDiscreteSpan.
+constexpr int kDiscreteSpan = 4096;
+
+__global__ __launch_bounds__(256) void k_discrete_heads(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
+                                                        Params prm, PoissonTable pt, int32_t* flag,
+                                                        unsigned long long* counts, uint32_t* __restrict__ heads,
+                                                        uint32_t* __restrict__ hcur, uint32_t hcap) {
+  __shared__ uint32_t b[kDiscreteSpan];
+  __shared__ int span, bad;
+  __shared__ double vlo;
+  __shared__ uint32_t found;
+  Philox ph(seed);
+  auto value = [&](int64_t t) {
+    const double q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
+    return ppf_one<PBH_DIST_POISSON, 0, true>(q, prm.val[0], prm.val[1], prm.val[2], pt);
+  };
+  if (threadIdx.x == 0) {
+    const double a = value(t0), z = value(t0 + nt - 1);
+    vlo = a;
+    found = 0;
+    // not the case this kernel covers (non-finite or non-integer ends, too many values): the
+    // caller checked the parameters, so this is a guard; the counts then say "not certified"
+    bad = !(isfinite(a) && isfinite(z) && a == floor(a) && z == floor(z) && z >= a && z - a <= kDiscreteSpan);
+    span = bad ? 0 : (int)(z - a);
+    if (bad) {
+      flag_nonfinite(flag, !isfinite(a) || !isfinite(z));
+      atomicAdd(&counts[1], 1ull);  // read as an inversion: the caller redoes the column exactly
+    }
+  }
+  __syncthreads();
+  const int m = span;
+  for (int i = threadIdx.x; i < m; i += 256) {  // k = vlo + 1 + i
+    const double k = vlo + 1.0 + (double)i;
+    int64_t lo = t0, hi = t0 + nt - 1;  // value(lo) < k <= value(hi)
+    while (hi - lo > 1) {
+      const int64_t mid = lo + ((hi - lo) >> 1);
+      if (value(mid) >= k)
+        hi = mid;
+      else
+        lo = mid;
+    }
+    b[i] = (uint32_t)hi;
+  }
+  __syncthreads();
+  uint32_t mine = 0;
+  for (int i = threadIdx.x; i < m; i += 256) {
+    if (i > 0 && b[i] == b[i - 1]) continue;  // a value no stratum takes: the same boundary
+    const uint32_t slot = atomicAdd(hcur, 1u);
+    if (slot < hcap) heads[slot] = b[i];
+    ++mine;
+  }
+  if (mine) atomicAdd(&found, mine);
+  __syncthreads();
+  if (threadIdx.x == 0 && !bad) atomicAdd(&counts[0], (unsigned long long)(nt - 1 - (int64_t)found));
+}
+
 int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t* flag, unsigned long long* counts,
                hipStream_t s, uint32_t* heads, uint32_t* hcur, uint32_t hcap) {
   const int64_t n = g->n;
@@ -1408,6 +1499,19 @@ int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t*
     PBH_CHECK_HIP(hipMemsetAsync(hcur, 0, sizeof(uint32_t), s));
   }
   if (nt == 0) return PBH_OK;
+  static const bool fast_heads = [] {  // PBH_DISCRETE_SCAN=1: evaluate every stratum
+    const char* e = getenv("PBH_DISCRETE_SCAN");
+    return !(e && e[0] == '1');
+  }();
+  const double mu = g->prm.val[0];
+  if (fast_heads && g->dist == PBH_DIST_POISSON && counts && heads && !out && nt >= 2 && g->pt.cdf &&
+      isfinite(mu) && mu > 0.0 && mu + 40.0 * sqrt(mu) + 100.0 < (double)kDiscreteSpan) {
+    PBH_TIMED(kKLhsSorted, s,
+              hipLaunchKernelGGL(k_discrete_heads, dim3(1), dim3(256), 0, s, g->seed, n, t0, nt, g->col, g->prm, g->pt,
+                                 flag, counts, heads, hcur, hcap));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
   dim3 gr(ppf_grid(nt)), b(kBlock);
   switch (g->dist) {
 #define PBH_CASE(D)                                                                                            \
@@ -1570,11 +1674,20 @@ static int place_launch(const GenColumn* g, const uint64_t* pairs, const uint32_
   if (blocks <= 0) return PBH_OK;
   int j0 = 0, jn = 0;
   if (gamma_win_on() && gamma_lds_ok(g->dist, g->prm, g->pt) && gamma_window(n, g->pt.guide, &j0, &jn)) {
+    // the slow list: a counter and cap entries (stream-ordered, freed after the second kernel)
+    const uint32_t cap = (uint32_t)(rows / 64 + 1024 < (1 << 20) ? rows / 64 + 1024 : (1 << 20));
+    unsigned long long* slow = nullptr;
+    PBH_CHECK_HIP(hipMallocAsync((void**)&slow, ((size_t)cap + 1) * 8, s));
+    PBH_CHECK_HIP(hipMemsetAsync(slow, 0, 8, s));
     PBH_TIMED(kKPlaceGen, s,
               hipLaunchKernelGGL(k_place_gen_gamma_w<BYROW>, dim3((unsigned)(blocks < 512 ? blocks : 512)),
                                  dim3(kGWBlock), 0, s, pairs, pidx, rows, n, g->seed, g->col, g->prm, g->pt, y, y_rs,
-                                 idx, state, j0, jn));
+                                 idx, state, j0, jn, slow, cap));
     PBH_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_place_gen_gamma_slow<BYROW>, dim3(1024), dim3(256), 0, s, pairs, pidx, rows, n, g->seed,
+                       g->col, g->prm, g->pt, y, y_rs, state, slow, cap);
+    PBH_CHECK_LAUNCH();
+    PBH_CHECK_HIP(hipFreeAsync(slow, s));
     return PBH_OK;
   }
   if (gamma_lds_ok(g->dist, g->prm, g->pt)) {
@@ -1661,8 +1774,9 @@ int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, 
   PBH_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "perm_scores: rows outside [0, n)");
   if (nrows == 0) return PBH_OK;
   PBH_TIMED(kKPermScores, s,
-            hipLaunchKernelGGL(k_perm_scores, dim3(compact_grid(nrows)), dim3(kBlock), 0, s, seed, n, (uint32_t)col, row0,
-                               nrows, heads, nheads, S, partial));
+            hipLaunchKernelGGL(k_perm_scores, dim3(compact_grid(nrows)), dim3(kBlock),
+                               heads && nheads <= kLdsHeads ? (size_t)nheads * 4 : 0, s, seed, n, (uint32_t)col,
+                               row0, nrows, heads, nheads, S, partial));
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }

@@ -35,11 +35,6 @@ namespace pbh {
 namespace {
 
 constexpr int kT = 256;
-#ifndef PBH_MSD_IPT
-#define PBH_MSD_IPT 16
-#endif
-constexpr int kIpt1 = PBH_MSD_IPT;
-constexpr int kTile1 = kT * kIpt1;  // msd1 / msd2 tiles: 8192 items
 constexpr int kIptP = 16;
 constexpr int kTileP = kT * kIptP;  // placement tiles: 4096 pairs (divides every group size 2^s >= 2^12)
 constexpr int kBucketCap2 = 2048;   // items per top-16 bucket a wave can finish
@@ -58,7 +53,7 @@ static int cur_pad() {
   return v;
 }
 
-__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh /* >= 260 */) {
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh /* >= 256 + waves */) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t x = v;
 #pragma unroll
@@ -80,12 +75,13 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh 
 // one block (a spike: a discrete-dominated correlated score) sets the column's state bit 0,
 // which routes it to the general path; so does a bucket above kBucketCap2 (k_hist16_scan).
 //
-// It also counts, per column, the top code byte of every tile class x = (row / kTile1) mod 8
-// (cls[x][byte]): k_msd1 tile i runs as block i, and blocks b and b + 8 share an XCD, so the
-// code pass gives each class its own cursors and sub-ranges (see k_msd1).
+// It also counts, per column, the top code byte of every tile class x = (row >> tlog) mod 8
+// (cls[x][byte]; 2^tlog = msd1's tile): k_msd1x tile i runs as block i, and blocks b and b + 8
+// share an XCD, so the code pass gives each class its own cursors and sub-ranges (see k_msd1x).
 __global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ codes, int64_t ld, int64_t n,
                                                  uint32_t* __restrict__ hist, uint32_t* __restrict__ cls,
-                                                 int32_t* __restrict__ state, const int32_t* __restrict__ gate) {
+                                                 int32_t* __restrict__ state, const int32_t* __restrict__ gate,
+                                                 int tlog) {
   __shared__ uint32_t w[32768];
   __shared__ uint32_t cw[8 * 256];
   __shared__ int ovf;
@@ -104,7 +100,7 @@ __global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ co
     const uint32_t b = code >> 16, sh = (b & 1u) * 16u;
     const uint32_t old = atomicAdd(&w[b >> 1], 1u << sh);
     bad |= ((old >> sh) & 0xFFFFu) == 0xFFFFu;
-    atomicAdd(&cw[(((uint32_t)(row / kTile1) & 7u) << 8) | (code >> 24)], 1u);
+    atomicAdd(&cw[(((uint32_t)(row >> tlog) & 7u) << 8) | (code >> 24)], 1u);
   };
   if ((((uintptr_t)(cc + lo)) & 15) == 0) {
     const int64_t n4 = (hi - lo) / 4;
@@ -140,7 +136,8 @@ __global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ co
 // holding 136 KiB of LDS would wait for an almost empty CU; the tile-class counts in quarter 0.
 __global__ __launch_bounds__(1024) void k_hist16_q(const uint32_t* __restrict__ codes, int64_t ld, int64_t n,
                                                    uint32_t* __restrict__ hist, uint32_t* __restrict__ cls,
-                                                   int32_t* __restrict__ state, const int32_t* __restrict__ gate) {
+                                                   int32_t* __restrict__ state, const int32_t* __restrict__ gate,
+                                                   int tlog) {
   __shared__ uint32_t w[8192];
   __shared__ uint32_t cw[8 * 256];
   __shared__ int ovf;
@@ -159,7 +156,7 @@ __global__ __launch_bounds__(1024) void k_hist16_q(const uint32_t* __restrict__ 
   for (int64_t i = lo + threadIdx.x; i < hi; i += 1024) {
     const uint32_t code = cc[i];
     const uint32_t b = code >> 16;
-    if (q == 0) atomicAdd(&cw[(((uint32_t)(i / kTile1) & 7u) << 8) | (code >> 24)], 1u);
+    if (q == 0) atomicAdd(&cw[(((uint32_t)(i >> tlog) & 7u) << 8) | (code >> 24)], 1u);
     if ((b >> 14) != q) continue;
     const uint32_t l = b & 16383u, sh = (l & 1u) * 16u;
     const uint32_t old = atomicAdd(&w[l >> 1], 1u << sh);
@@ -180,14 +177,14 @@ __global__ __launch_bounds__(1024) void k_hist16_q(const uint32_t* __restrict__ 
 }
 
 // One 1024-thread block per column: start[b] = exclusive prefix of the 65536 bucket counts
-// (start[65536] = n), the msd2 tile map (tiles of kTile1 inside every top-byte group: tpre[g]
+// (start[65536] = n), the msd2 tile map (tiles of 2^tlog inside every top-byte group: tpre[g]
 // = tiles before group g), and state bit 1 when a bucket exceeds kBucketCap2.
 // cstart[x][g] = start of top byte g + the counts of classes < x in it (k_msd1's sub-ranges).
 __global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict__ hist, int64_t n,
                                                       uint32_t* __restrict__ start, uint32_t* __restrict__ tpre,
                                                       const uint32_t* __restrict__ cls, uint32_t* __restrict__ cstart,
                                                       int32_t* __restrict__ state, int32_t* __restrict__ flags,
-                                                      const int32_t* __restrict__ gate) {
+                                                      const int32_t* __restrict__ gate, int tlog) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t gsize[256];
   __shared__ uint32_t gstart[256];
@@ -238,7 +235,7 @@ __global__ __launch_bounds__(1024) void k_hist16_scan(const uint32_t* __restrict
     uint32_t acc = 0;
     for (int g = 0; g < 256; ++g) {
       tpre[(int64_t)c * 257 + g] = acc;
-      acc += (gsize[g] + kTile1 - 1) / kTile1;
+      acc += (gsize[g] + (1u << tlog) - 1) >> tlog;
     }
     tpre[(int64_t)c * 257 + 256] = acc;
     if (big) atomicOr(&state[c], 2);
@@ -380,254 +377,72 @@ __global__ __launch_bounds__(256) void k_make_codes_adapt(const double* __restri
 }
 
 // ---------------------------------------------------------------- code passes
-// msd1: tile = kTile1 consecutive rows; digit = top code byte.
-// SPLIT: one 32-bit staging array, used twice (keys, then rows): 32 KiB of LDS per block instead
-// of 64, so 4 blocks per CU instead of 2, for two more barriers.
-// XCD: the block's tile class x = blockIdx.x mod 8 appends to its own sub-range of every top-byte
+// msd1: tiles of NT x IPT consecutive rows; digit = top code byte.  msd2: tiles of the same size
+// inside each top-byte group (tile map tpre); digit = code byte 2; destination = the group's
+// top-16 bucket (g << 8 | digit); writes the low 16 code bits.
+//
+// Both stage through one 32-bit LDS array, used twice (codes, then rows).  A slot's LDS position
+// (digit start + rank) replaces its code and rank once the digit starts are known, so the code is
+// dead after the first staging round and the rows round reuses the slots and the destinations:
+// every configuration stays within 64 VGPRs, 8 waves per SIMD (round 2's 256-thread kernels held
+// code, rank and destination at once: 83-84 VGPRs, 5 waves, msd1 16.4 against 11 ms per step).
+// PBH_MSD_TILE picks the tile: 8192 rows over 1024 threads (default: a tile's run for one digit is
+// 32 items, 128 bytes of codes) or 4096 over 256 (msd1) / 512 (msd2) threads (64-byte runs).
+// XCD: msd1's tile class x = blockIdx.x mod 8 appends to its own sub-range of every top-byte
 // group through its own cursor (cstart, cur + x * 256): 1/8 of the tiles contend on a cursor,
-// and the runs of one sub-range are all written from one XCD (its L2 merges the lines).
-template <bool SPLIT>
-__global__ __launch_bounds__(kT) void k_msd1(const uint32_t* __restrict__ codes, int64_t n,
-                                             const uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
-                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ rout,
-                                             const uint32_t* __restrict__ cstart, int cpad,
-                                             const int32_t* __restrict__ state) {
-  if (*state) return;  // uniform: this column takes the general path
-  __shared__ uint32_t cnt[256], lst[264], gb[256];
-  __shared__ uint32_t sk[kTile1], sr[SPLIT ? 1 : kTile1];
-  const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kTile1;
-  const int m = (int)((n - base) < kTile1 ? (n - base) : kTile1);
-  cnt[t] = 0;
-  __syncthreads();
-  uint32_t key[kIpt1], rk[kIpt1];
-#pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    key[j] = p < m ? codes[base + p] : 0u;
-    rk[j] = p < m ? atomicAdd(&cnt[key[j] >> 24], 1u) : 0u;
-  }
-  __syncthreads();
-  const uint32_t my = cnt[t];
-  const uint32_t ex = block_excl_scan256(my, lst);
-  lst[t] = ex;
-  // the cursor add's round trip overlaps the first LDS scatter: its result is stored to gb only
-  // after that scatter (the barrier that follows publishes it)
-  uint32_t myb;
-  if (cstart) {
-    const uint32_t xc = blockIdx.x & 7u;
-    myb = my ? cstart[(xc << 8) + t] + atomicAdd(&cur[((xc << 8) + t) * cpad], my) : 0u;
-  } else {
-    myb = my ? start[t << 8] + atomicAdd(&cur[t * cpad], my) : 0u;
-  }
-  __syncthreads();
-  if constexpr (SPLIT) {
-    uint32_t dst[kIpt1];  // where slot p = j * kT + t's key goes, kept for the rows round
-#pragma unroll
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) sk[lst[key[j] >> 24] + rk[j]] = key[j];
-    }
-    gb[t] = myb;
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) {
-        const uint32_t k = sk[p], d = k >> 24;
-        dst[j] = gb[d] + ((uint32_t)p - lst[d]);
-        kout[dst[j]] = k;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) sk[lst[key[j] >> 24] + rk[j]] = (uint32_t)(base + p);
-    }
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) rout[dst[j]] = sk[p];
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) {
-        const uint32_t q = lst[key[j] >> 24] + rk[j];
-        sk[q] = key[j];
-        sr[q] = (uint32_t)(base + p);
-      }
-    }
-    gb[t] = myb;
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) {
-        const uint32_t k = sk[p], d = k >> 24;
-        const uint32_t o = gb[d] + ((uint32_t)p - lst[d]);
-        kout[o] = k;
-        rout[o] = sr[p];
-      }
-    }
-  }
-}
-
-// msd2: tiles of kTile1 inside each top-byte group (tile map tpre); digit = code byte 2; the
-// destination is the group's top-16 bucket (g << 8 | digit).  Writes the low 16 code bits.
-template <bool SPLIT>
-__global__ __launch_bounds__(kT) void k_msd2(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin,
-                                             const uint32_t* __restrict__ start, const uint32_t* __restrict__ tpre,
-                                             uint32_t* __restrict__ cur, uint16_t* __restrict__ kout,
-                                             uint32_t* __restrict__ rout, const int32_t* __restrict__ state) {
-  if (*state) return;
-  const uint32_t tile = blockIdx.x;
-  if (tile >= tpre[256]) return;
-  __shared__ uint32_t cnt[256], lst[264], gb[256];
-  __shared__ uint32_t sk[kTile1], sr[SPLIT ? 1 : kTile1];
-  __shared__ int gsh;
-  const int t = threadIdx.x;
-  if (t == 0) {  // the group holding this tile: last g with tpre[g] <= tile
-    int lo = 0, hi = 256;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (tpre[mid] <= tile)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    while (lo < 255 && tpre[lo + 1] <= tile) ++lo;  // skip empty groups
-    gsh = lo;
-  }
-  cnt[t] = 0;
-  __syncthreads();
-  const int g = gsh;
-  const int64_t gs = start[g << 8], ge = start[(g + 1) << 8];
-  const int64_t base = gs + (int64_t)(tile - tpre[g]) * kTile1;
-  const int m = (int)((ge - base) < kTile1 ? (ge - base) : kTile1);
-  uint32_t key[kIpt1], row[kIpt1], rk[kIpt1];
-#pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
-    key[j] = p < m ? kin[base + p] : 0u;
-    row[j] = p < m ? rin[base + p] : 0u;
-    rk[j] = p < m ? atomicAdd(&cnt[(key[j] >> 16) & 255u], 1u) : 0u;
-  }
-  __syncthreads();
-  const uint32_t my = cnt[t];
-  const uint32_t ex = block_excl_scan256(my, lst);
-  lst[t] = ex;
-  const uint32_t b = ((uint32_t)g << 8) | (uint32_t)t;
-  const uint32_t myb = my ? start[b] + atomicAdd(&cur[b], my) : 0u;  // stored after the first scatter
-  __syncthreads();
-  if constexpr (SPLIT) {
-    uint32_t dst[kIpt1];
-#pragma unroll
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) sk[lst[(key[j] >> 16) & 255u] + rk[j]] = key[j];
-    }
-    gb[t] = myb;
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) {
-        const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
-        dst[j] = gb[d] + ((uint32_t)p - lst[d]);
-        kout[dst[j]] = (uint16_t)kk;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) sk[lst[(key[j] >> 16) & 255u] + rk[j]] = row[j];
-    }
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) rout[dst[j]] = sk[p];
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) {
-        const uint32_t q = lst[(key[j] >> 16) & 255u] + rk[j];
-        sk[q] = key[j];
-        sr[q] = row[j];
-      }
-    }
-    gb[t] = myb;
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < kIpt1; ++j) {
-      const int p = j * kT + t;
-      if (p < m) {
-        const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
-        const uint32_t o = gb[d] + ((uint32_t)p - lst[d]);
-        kout[o] = (uint16_t)kk;
-        rout[o] = sr[p];
-      }
-    }
-  }
-}
-
-// The code passes at 8 waves per SIMD (PBH_MSD_OCC=1, the default): the same passes with fewer
-// live registers.  A slot's LDS position (digit start + rank) replaces its key and rank once the
-// digit starts are known, so the key is dead after the first staging round; the rows round reuses
-// the slots and the destinations.  k_msd1 / k_msd2 need 83-84 VGPRs (5 waves per SIMD); these
-// stay within 64, and with 19 KiB of LDS 8 blocks fit a CU.  Memory-latency-bound passes run
-// faster with more waves in flight.
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8))) void k_msd1o(
+// and the runs of one sub-range are all written from one XCD (its L2 merges the lines); k_hist16
+// counts the classes with the same tile size.
+template <int NT, int IPT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8))) void k_msd1x(
     const uint32_t* __restrict__ codes, int64_t n, const uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ rout, const uint32_t* __restrict__ cstart, int cpad,
     const int32_t* __restrict__ state) {
-  if (*state) return;
-  __shared__ uint32_t cnt[256], lst[264], gb[256];
-  __shared__ uint32_t sk[kTile1];
+  constexpr int kTile = NT * IPT;
+  if (*state) return;  // uniform: this column takes the general path
+  __shared__ uint32_t cnt[256], lst[256 + NT / 64], gb[256];
+  __shared__ uint32_t sk[kTile];
   const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kTile1;
-  const int m = (int)((n - base) < kTile1 ? (n - base) : kTile1);
-  cnt[t] = 0;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int m = (int)((n - base) < kTile ? (n - base) : kTile);
+  if (t < 256) cnt[t] = 0;
   __syncthreads();
-  uint32_t key[kIpt1], slot[kIpt1];
+  uint32_t key[IPT], slot[IPT];
 #pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
+  for (int j = 0; j < IPT; ++j) {
+    const int p = j * NT + t;
     key[j] = p < m ? codes[base + p] : 0u;
   }
 #pragma unroll
-  for (int j = 0; j < kIpt1; ++j) slot[j] = (j * kT + t < m) ? atomicAdd(&cnt[key[j] >> 24], 1u) : 0u;
+  for (int j = 0; j < IPT; ++j) slot[j] = (j * NT + t < m) ? atomicAdd(&cnt[key[j] >> 24], 1u) : 0u;
   __syncthreads();
-  const uint32_t my = cnt[t];
-  lst[t] = block_excl_scan256(my, lst);
-  uint32_t myb;
-  if (cstart) {
-    const uint32_t xc = blockIdx.x & 7u;
-    myb = my ? cstart[(xc << 8) + t] + atomicAdd(&cur[((xc << 8) + t) * cpad], my) : 0u;
-  } else {
-    myb = my ? start[t << 8] + atomicAdd(&cur[t * cpad], my) : 0u;
+  const uint32_t my = t < 256 ? cnt[t] : 0u;
+  const uint32_t ex = block_excl_scan256(my, lst);  // waves past the fourth add nothing
+  // the cursor add's round trip overlaps the first LDS scatter: its result is stored to gb only
+  // after that scatter (the barrier that follows publishes it)
+  uint32_t myb = 0u;
+  if (t < 256) {
+    lst[t] = ex;
+    if (cstart) {
+      const uint32_t xc = blockIdx.x & 7u;
+      myb = my ? cstart[(xc << 8) + t] + atomicAdd(&cur[((xc << 8) + t) * cpad], my) : 0u;
+    } else {
+      myb = my ? start[t << 8] + atomicAdd(&cur[t * cpad], my) : 0u;
+    }
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    if (j * kT + t < m) {
+  for (int j = 0; j < IPT; ++j) {
+    if (j * NT + t < m) {
       slot[j] += lst[key[j] >> 24];
       sk[slot[j]] = key[j];
     }
   }
-  gb[t] = myb;
+  if (t < 256) gb[t] = myb;
   __syncthreads();
-  uint32_t dst[kIpt1];
+  uint32_t dst[IPT];
 #pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
+  for (int j = 0; j < IPT; ++j) {
+    const int p = j * NT + t;
     if (p < m) {
       const uint32_t k = sk[p], d = k >> 24;
       dst[j] = gb[d] + ((uint32_t)p - lst[d]);
@@ -636,30 +451,27 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8))) void k_
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kIpt1; ++j)
-    if (j * kT + t < m) sk[slot[j]] = (uint32_t)(base + j * kT + t);
+  for (int j = 0; j < IPT; ++j)
+    if (j * NT + t < m) sk[slot[j]] = (uint32_t)(base + j * NT + t);
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kIpt1; ++j) {
-    const int p = j * kT + t;
+  for (int j = 0; j < IPT; ++j) {
+    const int p = j * NT + t;
     if (p < m) rout[dst[j]] = sk[p];
   }
 }
 
-// msd2 over 512 threads of 8 items: the rows stay in registers through the keys round, within
-// 64 VGPRs (8 waves per SIMD; the 256-thread form with 16 items needs 72 VGPRs, or the rows read
-// twice, and measured 15.5 against 14.7 ms per step).
-constexpr int kTW = 512;
-constexpr int kIptW = kTile1 / kTW;
-__global__ __launch_bounds__(kTW) __attribute__((amdgpu_waves_per_eu(8))) void k_msd2w(
+template <int NT, int IPT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8))) void k_msd2x(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin, const uint32_t* __restrict__ start,
     const uint32_t* __restrict__ tpre, uint32_t* __restrict__ cur, uint16_t* __restrict__ kout,
     uint32_t* __restrict__ rout, const int32_t* __restrict__ state) {
+  constexpr int kTile = NT * IPT;
   if (*state) return;
   const uint32_t tile = blockIdx.x;
   if (tile >= tpre[256]) return;
-  __shared__ uint32_t cnt[256], lst[264], gb[256];
-  __shared__ uint32_t sk[kTile1];
+  __shared__ uint32_t cnt[256], lst[256 + NT / 64], gb[256];
+  __shared__ uint32_t sk[kTile];
   __shared__ int gsh;
   const int t = threadIdx.x;
   if (t == 0) {  // the group holding this tile: last g with tpre[g] <= tile
@@ -678,20 +490,20 @@ __global__ __launch_bounds__(kTW) __attribute__((amdgpu_waves_per_eu(8))) void k
   __syncthreads();
   const int g = gsh;
   const int64_t gs = start[g << 8], ge = start[(g + 1) << 8];
-  const int64_t base = gs + (int64_t)(tile - tpre[g]) * kTile1;
-  const int m = (int)((ge - base) < kTile1 ? (ge - base) : kTile1);
-  uint32_t key[kIptW], row[kIptW], slot[kIptW];
+  const int64_t base = gs + (int64_t)(tile - tpre[g]) * kTile;
+  const int m = (int)((ge - base) < kTile ? (ge - base) : kTile);
+  uint32_t key[IPT], row[IPT], slot[IPT];
 #pragma unroll
-  for (int j = 0; j < kIptW; ++j) {
-    const int p = j * kTW + t;
+  for (int j = 0; j < IPT; ++j) {
+    const int p = j * NT + t;
     key[j] = p < m ? kin[base + p] : 0u;
     row[j] = p < m ? rin[base + p] : 0u;
   }
 #pragma unroll
-  for (int j = 0; j < kIptW; ++j) slot[j] = (j * kTW + t < m) ? atomicAdd(&cnt[(key[j] >> 16) & 255u], 1u) : 0u;
+  for (int j = 0; j < IPT; ++j) slot[j] = (j * NT + t < m) ? atomicAdd(&cnt[(key[j] >> 16) & 255u], 1u) : 0u;
   __syncthreads();
   const uint32_t my = t < 256 ? cnt[t] : 0u;
-  const uint32_t ex = block_excl_scan256(my, lst);  // waves 4-7 add nothing
+  const uint32_t ex = block_excl_scan256(my, lst);
   uint32_t myb = 0u;
   if (t < 256) {
     lst[t] = ex;
@@ -700,18 +512,18 @@ __global__ __launch_bounds__(kTW) __attribute__((amdgpu_waves_per_eu(8))) void k
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kIptW; ++j) {
-    if (j * kTW + t < m) {
+  for (int j = 0; j < IPT; ++j) {
+    if (j * NT + t < m) {
       slot[j] += lst[(key[j] >> 16) & 255u];
       sk[slot[j]] = key[j];
     }
   }
   if (t < 256) gb[t] = myb;
   __syncthreads();
-  uint32_t dst[kIptW];
+  uint32_t dst[IPT];
 #pragma unroll
-  for (int j = 0; j < kIptW; ++j) {
-    const int p = j * kTW + t;
+  for (int j = 0; j < IPT; ++j) {
+    const int p = j * NT + t;
     if (p < m) {
       const uint32_t kk = sk[p], d = (kk >> 16) & 255u;
       dst[j] = gb[d] + ((uint32_t)p - lst[d]);
@@ -720,12 +532,12 @@ __global__ __launch_bounds__(kTW) __attribute__((amdgpu_waves_per_eu(8))) void k
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kIptW; ++j)
-    if (j * kTW + t < m) sk[slot[j]] = row[j];
+  for (int j = 0; j < IPT; ++j)
+    if (j * NT + t < m) sk[slot[j]] = row[j];
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kIptW; ++j) {
-    const int p = j * kTW + t;
+  for (int j = 0; j < IPT; ++j) {
+    const int p = j * NT + t;
     if (p < m) rout[dst[j]] = sk[p];
   }
 }
@@ -1658,12 +1470,11 @@ void step4_sync_side_streams() {
   }
 }
 
-// PBH_MSD_OCC=0: the code passes and the row-placement passes at their earlier register use
-// (5 / 4 waves per SIMD) instead of k_msd1o / k_msd2o / k_place_msdo (8)
-static bool msd_occ() {
-  static const bool v = [] {
-    const char* e = getenv("PBH_MSD_OCC");
-    return !(e && e[0] == '0');
+// PBH_MSD_TILE: the code passes' tile, 8192 rows (default) or 4096 (k_msd1x / k_msd2x)
+static int msd_tile_log() {
+  static const int v = [] {
+    const char* e = getenv("PBH_MSD_TILE");
+    return e && atoi(e) == 4096 ? 12 : 13;
   }();
   return v;
 }
@@ -1678,13 +1489,14 @@ bool step4_fused() {
 
 
 // MSD levels of the row placement: shifts from kGenPlaceShift up, at most 8 bits per level
-// PBH_PLACE_TOP=1: with two levels, the top one (the finish's scatter) takes 8 bits and the MSD
-// pass the rest (at N = 1e8: 191 groups of 2^19 rows, 128 digits per placement tile) instead of
-// the MSD pass taking 8 (96 groups of 2^20, 256 digits)
+// With two levels the top one (the finish's scatter) takes 8 bits and the MSD pass the rest (at
+// N = 1e8: 191 groups of 2^19 rows, 128 digits per placement tile, 32-item runs: place_msd 13.2 ->
+// 11.3 ms per step, the finish +0.5); PBH_PLACE_TOP=0: the MSD pass takes 8 (96 groups of 2^20,
+// 256 digits)
 static int place_levels(int64_t n, int* shifts) {
   static const bool top = [] {
     const char* e = getenv("PBH_PLACE_TOP");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   int bits = 0;
   while (((int64_t)1 << bits) < n) ++bits;
@@ -1750,10 +1562,11 @@ int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs,
   if (blocks < 1) blocks = 1;
   PBH_TIMED(kKHist16, s,
             hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)kk), dim3(1024), 0, s, codes, ldc, n, hist,
-                               cls, state, nullptr));
+                               cls, state, nullptr, msd_tile_log()));
   PBH_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)kk), dim3(1024), 0, s, hist, n, sh.start + (int64_t)c0 * 65537,
-                     sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, nullptr);
+                     sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, nullptr,
+                     msd_tile_log());
   PBH_CHECK_LAUNCH();
   if (!cs) return PBH_OK;
   return step4_gen_adapt(codes, ldc, cs, ldcs, n, sh, c0, kk, s);
@@ -1796,10 +1609,11 @@ int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs
   PBH_CHECK_LAUNCH();
   // (not timed as k_hist16: a re-count of one column, where k_hist16's bytes per launch are all of them)
   hipLaunchKernelGGL(k_hist16_q, dim3((unsigned)blocks, (unsigned)kk, 4), dim3(1024), 0, s, codes, ldc, n, hist, cls,
-                     state, retry);
+                     state, retry, msd_tile_log());
   PBH_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)kk), dim3(1024), 0, s, hist, n, sh.start + (int64_t)c0 * 65537,
-                     sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, retry);
+                     sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, retry,
+                     msd_tile_log());
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
@@ -1808,40 +1622,32 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
                      const Step4Column& cb, hipStream_t s) {
   const uint32_t* start = sh.start + (int64_t)c * 65537;
   const int32_t* state = sh.state + c;
-  const int64_t t1 = (n + kTile1 - 1) / kTile1;
+  const int tlog = msd_tile_log();
+  const int64_t t1 = (n + ((int64_t)1 << tlog) - 1) >> tlog;
   static const bool xcd = [] {  // PBH_MSD1_XCD=0: one cursor per top byte for every tile
     const char* e = getenv("PBH_MSD1_XCD");
     return !(e && e[0] == '0');
   }();
   const uint32_t* cst = xcd ? sh.cstart + (int64_t)c * 2048 : nullptr;
-  static const bool split = [] {  // PBH_MSD_SPLIT=0: keys and rows staged together (64 KiB)
-    const char* e = getenv("PBH_MSD_SPLIT");
-    return !(e && e[0] == '0');
-  }();
-  if (msd_occ()) {
+  uint32_t* cur1 = sh.cur1 + (int64_t)c * 8 * 256 * cur_pad();
+  uint32_t* cur2 = sh.cur2 + (int64_t)c * 65536;
+  const uint32_t* tp = sh.tpre + (int64_t)c * 257;
+  if (tlog == 13) {
     PBH_TIMED(kKMsd1, s,
-              hipLaunchKernelGGL(k_msd1o, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
-                                 sh.cur1 + (int64_t)c * 8 * 256 * cur_pad(), cb.keys32, cb.rows1, cst, cur_pad(), state));
+              hipLaunchKernelGGL((k_msd1x<1024, 8>), dim3((unsigned)t1), dim3(1024), 0, s, codes, n, start, cur1,
+                                 cb.keys32, cb.rows1, cst, cur_pad(), state));
     PBH_CHECK_LAUNCH();
     PBH_TIMED(kKMsd2, s,
-              hipLaunchKernelGGL(k_msd2w, dim3((unsigned)(t1 + 256)), dim3(kTW), 0, s, cb.keys32, cb.rows1, start,
-                                 sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
-  } else if (split) {
-    PBH_TIMED(kKMsd1, s,
-              hipLaunchKernelGGL(k_msd1<true>, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
-                                 sh.cur1 + (int64_t)c * 8 * 256 * cur_pad(), cb.keys32, cb.rows1, cst, cur_pad(), state));
-    PBH_CHECK_LAUNCH();
-    PBH_TIMED(kKMsd2, s,
-              hipLaunchKernelGGL(k_msd2<true>, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
-                                 sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
+              hipLaunchKernelGGL((k_msd2x<1024, 8>), dim3((unsigned)(t1 + 256)), dim3(1024), 0, s, cb.keys32, cb.rows1,
+                                 start, tp, cur2, cb.keys16, cb.rows2, state));
   } else {
     PBH_TIMED(kKMsd1, s,
-              hipLaunchKernelGGL(k_msd1<false>, dim3((unsigned)t1), dim3(kT), 0, s, codes, n, start,
-                                 sh.cur1 + (int64_t)c * 8 * 256 * cur_pad(), cb.keys32, cb.rows1, cst, cur_pad(), state));
+              hipLaunchKernelGGL((k_msd1x<256, 16>), dim3((unsigned)t1), dim3(256), 0, s, codes, n, start, cur1,
+                                 cb.keys32, cb.rows1, cst, cur_pad(), state));
     PBH_CHECK_LAUNCH();
     PBH_TIMED(kKMsd2, s,
-              hipLaunchKernelGGL(k_msd2<false>, dim3((unsigned)(t1 + 256)), dim3(kT), 0, s, cb.keys32, cb.rows1, start,
-                                 sh.tpre + (int64_t)c * 257, sh.cur2 + (int64_t)c * 65536, cb.keys16, cb.rows2, state));
+              hipLaunchKernelGGL((k_msd2x<512, 8>), dim3((unsigned)(t1 + 256)), dim3(512), 0, s, cb.keys32, cb.rows1,
+                                 start, tp, cur2, cb.keys16, cb.rows2, state));
   }
   PBH_CHECK_LAUNCH();
   if (step4_fused()) {
@@ -1912,7 +1718,7 @@ int step4_gen_place_passes(int c, int64_t n, const Step4Shared& sh, const Step4C
       return !(e && e[0] == '0');
     }();
     const uint32_t* segp = sg ? cb.segtp : nullptr;
-    if (!sg && msd_occ())
+    if (!sg)  // 8 waves per SIMD (k_place_msd<true>: 4; 13.4 against 13.1 ms per step)
       PBH_TIMED(kKPlaceMsd, s,
                 hipLaunchKernelGGL(k_place_msdo, dim3((unsigned)grid), dim3(kTO), 0, s, cb.pairs[cur], n, shifts[l], cr,
                                    cb.pairs[cur ^ 1], state));

@@ -105,3 +105,41 @@ def test_every_deferral_mode_matches_the_oracle(gpu, tmp_path):
         for tag, ref in refs.items():
             np.testing.assert_array_equal(np.load(d / f"{tag}_i.npy"), ref["idx"], err_msg=json.dumps(env))
             assert_close(np.load(d / f"{tag}_y.npy"), ref["Y"], rtol=1e-10, what=f"{env} {tag}")
+
+
+_HEADS_SCRIPT = r"""
+import ctypes, json, sys
+import numpy as np
+sys.path.insert(0, {root!r})
+from probabilit_amd import _lib, device
+out = {{}}
+lib = _lib.load()
+for mu, n, t0, nt in {cases!r}:
+    counts, flag = device.zeros(2, "int64"), device.zeros(1, "int32")
+    heads, hcur = device.zeros(16384, "int32"), device.zeros(1, "int32")
+    _lib.check(lib.pbh_lhs_sorted_counts(11, n, t0, nt, 3, _lib.DIST_IDS["poisson"], (ctypes.c_double * 3)(mu, 0.0, 1.0),
+                                         3, counts.data_ptr(), heads.data_ptr(), hcur.data_ptr(), 16384, flag.data_ptr(),
+                                         0, device.stream()))
+    h = int(device.to_host(hcur)[0])
+    out[f"{{mu}}_{{n}}_{{t0}}"] = {{"counts": device.to_host(counts).tolist(), "flag": int(device.to_host(flag)[0]),
+                                   "heads": sorted(device.to_host(heads)[:min(h, 16384)].tolist()), "hcur": h}}
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.timeout(300)
+def test_poisson_boundary_search_equals_the_scan(gpu):
+    """A poisson column's tie count and run heads from the boundary search (k_discrete_heads: one
+    binary search per distinct value) equal the stratum-by-stratum scan's (PBH_DISCRETE_SCAN=1,
+    its own process) exactly: whole columns and shard segments (t0 = row0 - 1), mu 4 / 30 / 400."""
+    cases = [(4.0, 10_000_000, 0, 10_000_000), (30.0, 10_000_000, 0, 10_000_000), (400.0, 3_000_001, 0, 3_000_001),
+             (30.0, 10_000_000, 3_333_332, 3_333_334), (4.0, 1000, 0, 1000), (400.0, 50, 0, 50)]
+    res = []
+    for env in ({}, {"PBH_DISCRETE_SCAN": "1"}):
+        r = subprocess.run([sys.executable, "-c", _HEADS_SCRIPT.format(root=ROOT, cases=cases)],
+                           env={**os.environ, **env}, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, (env, r.stderr[-3000:])
+        res.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert res[0] == res[1]
+    for k, v in res[0].items():
+        assert v["counts"][1] == 0 and v["flag"] == 0, (k, v)

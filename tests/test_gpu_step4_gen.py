@@ -191,9 +191,11 @@ def _debug_run(n, dists, seed, C):
 @pytest.mark.timeout(900)
 def test_step4_variants_match_the_oracle(gpu, tmp_path):
     """Every A/B switch of the generated-column path, each in its own process (they are read
-    once): the round-2 code passes and 256-thread finish (PBH_MSD_OCC=0, PBH_FINISH_CFG=26), the
-    queued finish (28, 30), the whole gamma table in LDS (PBH_GAMMA_WIN=0) -- step-4 indices equal
-    to the oracle's and the outputs within 1e-10."""
+    once): 4096-row code-pass tiles (PBH_MSD_TILE=4096), the 256-thread finish (PBH_FINISH_CFG=26),
+    the queued finish (28, 30), the whole gamma table in LDS (PBH_GAMMA_WIN=0), the top-heavy
+    placement levels' other split (PBH_PLACE_TOP=0), 64-row step-3 tiles (PBH_APPLY_ROWS=64), the poisson run
+    heads from every stratum instead of the boundary search (PBH_DISCRETE_SCAN=1) -- step-4
+    indices equal to the oracle's and the outputs within 1e-10."""
     import os
     import subprocess
     import sys
@@ -204,8 +206,9 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     n, d, seed = 300_001, 8, 31
     dists, C = cfg_dists(d), cfg3_corr(d)
     ref = _oracle(n, dists, seed, C)
-    for env in ({"PBH_MSD_OCC": "0", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"}, {"PBH_FINISH_CFG": "30"},
-                {"PBH_GAMMA_WIN": "0"}):
+    for env in ({"PBH_MSD_TILE": "4096", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"},
+                {"PBH_FINISH_CFG": "30"}, {"PBH_GAMMA_WIN": "0"}, {"PBH_PLACE_TOP": "0"}, {"PBH_APPLY_ROWS": "64"},
+                {"PBH_DISCRETE_SCAN": "1"}):
         dd = tmp_path / "_".join(f"{k}{v}" for k, v in env.items())
         dd.mkdir()
         script = _VARIANT_SCRIPT.format(root=root, tests=os.path.join(root, "tests"), d=str(dd), n=n, dists=dists,
@@ -215,3 +218,18 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
         assert r.returncode == 0, (env, r.stderr[-3000:])
         np.testing.assert_array_equal(np.load(dd / "idx.npy"), ref["idx"], err_msg=str(env))
         assert_close(np.load(dd / "Y.npy"), ref["Y"], rtol=1e-10, what=str(env))
+
+
+@pytest.mark.parametrize("shape", [0.1, 0.25])
+def test_gamma_placement_slow_list(gpu, shape):
+    """Small gamma shapes leave guide intervals without the midpoint check (coverage is complete
+    only for a >= 0.3), so the step-4 placement sends many items to the slow list that
+    k_place_gen_gamma_slow evaluates after the windowed kernel (with a = 0.1 more than the list
+    holds at this N: the second kernel then evaluates every row).  Indices and values equal the
+    oracle's."""
+    dists = [("gamma", {"a": shape}), ("norm", {}), ("gamma", {"a": shape, "scale": 2.0})]
+    C = np.array([[1.0, 0.4, 0.2], [0.4, 1.0, 0.3], [0.2, 0.3, 1.0]])
+    Y, idx = _run(200_003, dists, 41, C)
+    ref = _oracle(200_003, dists, 41, C)
+    np.testing.assert_array_equal(idx, ref["idx"])
+    assert_close(Y, ref["Y"], rtol=1e-10, what=f"gamma(a={shape}) placement")
