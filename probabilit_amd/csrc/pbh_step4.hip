@@ -1596,7 +1596,9 @@ int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs
                      sh.cur1 + c0 * cw, sh.cur2 + (int64_t)c0 * 65536, sh.curF + c0 * cw, cls,
                      sh.seghist + (int64_t)c0 * kAdaptSegments, cpad);
   PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_seg_hist, dim3(64, (unsigned)kk), dim3(1024), 0, s, cs, ldcs, n, retry,
+  // one column (a lane's re-code, kk = 1): enough blocks to fill the chip; all columns: 64 each
+  const unsigned sblocks = kk == 1 ? 512u : 64u;
+  hipLaunchKernelGGL(k_seg_hist, dim3(sblocks, (unsigned)kk), dim3(1024), 0, s, cs, ldcs, n, retry,
                      sh.seghist + (int64_t)c0 * kAdaptSegments);
   PBH_CHECK_LAUNCH();
   uint32_t* amap = sh.amap + (int64_t)c0 * kAdaptMapWords;
@@ -1607,9 +1609,18 @@ int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs
   hipLaunchKernelGGL(k_make_codes_adapt, dim3((unsigned)(cb < 1024 ? (cb < 1 ? 1 : cb) : 1024), (unsigned)kk),
                      dim3(256), 0, s, cs, ldcs, n, retry, amap, codes, ldc);
   PBH_CHECK_LAUNCH();
-  // (not timed as k_hist16: a re-count of one column, where k_hist16's bytes per launch are all of them)
-  hipLaunchKernelGGL(k_hist16_q, dim3((unsigned)blocks, (unsigned)kk, 4), dim3(1024), 0, s, codes, ldc, n, hist, cls,
-                     state, retry, msd_tile_log());
+  // (not timed as k_hist16: a re-count, where k_hist16's bytes per launch are all the columns.)
+  // One column: the full-LDS count (the column read once; k_hist16_q's four quarters read it four
+  // times), on as many blocks as k_hist16 gives a column (each flushes ~64 K counters with global
+  // atomics); several: k_hist16_q, whose no-op blocks for the columns that need no re-count hold
+  // 32 KiB instead of 136 (the gate is only known on the device)
+  if (kk == 1) {
+    hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, 1), dim3(1024), 0, s, codes, ldc, n, hist, cls, state, retry,
+                       msd_tile_log());
+  } else {
+    hipLaunchKernelGGL(k_hist16_q, dim3((unsigned)blocks, (unsigned)kk, 4), dim3(1024), 0, s, codes, ldc, n, hist, cls,
+                       state, retry, msd_tile_log());
+  }
   PBH_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)kk), dim3(1024), 0, s, hist, n, sh.start + (int64_t)c0 * 65537,
                      sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, retry,
@@ -1657,6 +1668,8 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     // PBH_FINISH_CFG (A/B measurements, profiles/r03/README_ab.md): 29 (default) = k_finish_q over
     // 512 threads, 1024 bins, the run members' CS values read in pass 2; 28 = the same with those
     // reads queued through LDS; 30 = queued, 2048 bins; 26 = 256 threads (round 2's k_finish_ah).
+    // (Both buckets' phases merged into one pass, ~10 barriers instead of ~21: 23.7-24.1 against
+    // 24.1-24.3 ms per step, within run-to-run noise; not kept.)
     // The segmented XCD-class output (PBH_FINISH_XCD=1) always takes k_finish_fused.
     static const int cfg = [] {
       const char* e = getenv("PBH_FINISH_CFG");

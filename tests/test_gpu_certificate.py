@@ -117,8 +117,8 @@ lib = _lib.load()
 for mu, n, t0, nt in {cases!r}:
     counts, flag = device.zeros(2, "int64"), device.zeros(1, "int32")
     heads, hcur = device.zeros(16384, "int32"), device.zeros(1, "int32")
-    _lib.check(lib.pbh_lhs_sorted_counts(11, n, t0, nt, 3, _lib.DIST_IDS["poisson"], (ctypes.c_double * 3)(mu, 0.0, 1.0),
-                                         3, counts.data_ptr(), heads.data_ptr(), hcur.data_ptr(), 16384, flag.data_ptr(),
+    _lib.check(lib.pbh_lhs_sorted_counts(11, n, t0, nt, 3, _lib.DIST_IDS["poisson"], (ctypes.c_double * 3)(mu, 0.0, 0.0),
+                                         2, counts.data_ptr(), heads.data_ptr(), hcur.data_ptr(), 16384, flag.data_ptr(),
                                          0, device.stream()))
     h = int(device.to_host(hcur)[0])
     out[f"{{mu}}_{{n}}_{{t0}}"] = {{"counts": device.to_host(counts).tolist(), "flag": int(device.to_host(flag)[0]),

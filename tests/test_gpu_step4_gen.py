@@ -192,10 +192,10 @@ def _debug_run(n, dists, seed, C):
 def test_step4_variants_match_the_oracle(gpu, tmp_path):
     """Every A/B switch of the generated-column path, each in its own process (they are read
     once): 4096-row code-pass tiles (PBH_MSD_TILE=4096), the 256-thread finish (PBH_FINISH_CFG=26),
-    the queued finish (28, 30), the whole gamma table in LDS (PBH_GAMMA_WIN=0), the top-heavy
-    placement levels' other split (PBH_PLACE_TOP=0), 64-row step-3 tiles (PBH_APPLY_ROWS=64), the poisson run
-    heads from every stratum instead of the boundary search (PBH_DISCRETE_SCAN=1) -- step-4
-    indices equal to the oracle's and the outputs within 1e-10."""
+    the queued finish (28, 30), the whole gamma table in LDS
+    (PBH_GAMMA_WIN=0), the placement levels' other split (PBH_PLACE_TOP=0), 64-row step-3 tiles
+    (PBH_APPLY_ROWS=64), the poisson run heads from every stratum instead of the boundary search
+    (PBH_DISCRETE_SCAN=1) -- step-4 indices equal to the oracle's and the outputs within 1e-10."""
     import os
     import subprocess
     import sys

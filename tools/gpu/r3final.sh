@@ -24,4 +24,10 @@ PY
 cd /tmp && export TMPDIR=/tmp
 PBH_STEP4_STREAMS=1 PBH_DEFER_COUNTS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_${TAG}_1s -o bench --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-e2e --ppf-rows 0 > $R/gpurun_out/${TAG}_prof_bench.json 2> $R/gpurun_out/${TAG}_prof.err
 rc=$?; echo "prof exit $rc"; [ $rc -eq 0 ] || exit $rc
-bash $R/tools/gpu/pmc.sh $TAG
+bash $R/tools/gpu/pmc.sh $TAG || exit $?
+if [ "$3" == "full" ]; then
+  cd $R
+  timeout -k 10 300 python tools/bench_configs.py > gpurun_out/${TAG}_configs.json 2> gpurun_out/${TAG}_configs.err
+  rc=$?; echo "configs exit $rc"; [ $rc -eq 0 ] || exit $rc
+  bash $R/tools/gpu/pmc_valu.sh ${TAG}_valu
+fi
