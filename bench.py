@@ -82,17 +82,21 @@ PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k
                                   "k_lhs_sorted_ppf<6>"]}
 
 
+def _profile_tag(path):
+    """Order of committed profiles, newest last (mtimes do not survive a checkout): the round
+    directory profiles/r<RR>/, then the pass tag of the file name (`_r77`, `_r3m` < `_r3p`)."""
+    d = re.search(r"r(\d+)$", os.path.basename(os.path.dirname(path)))
+    m = re.search(r"_r(\d+)([a-z]*)", os.path.basename(path))
+    return (int(d.group(1)) if d else -1, int(m.group(1)) if m else -1, m.group(2) if m else "")
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/r*/pmc_traffic_*.json, written by tools/gpu/pmc.sh + tools/pmc_summary.py:
     2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
     import glob
 
-    def tag(path):  # newest = highest pass number in pmc_traffic_r<NN>.json (mtimes do not survive a checkout)
-        m = re.search(r"_r(\d+)", os.path.basename(path))
-        return int(m.group(1)) if m else -1
-
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_*.json")), key=tag)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_*.json")), key=_profile_tag)
     if not files:
         return None, None
     ks = json.load(open(files[-1]))["kernels"]
@@ -309,11 +313,7 @@ def pmc_valu(kernel):
     over the kernel's template variants, or None."""
     import glob
 
-    def tag(path):
-        m = re.search(r"_r(\d+)", os.path.basename(path))
-        return int(m.group(1)) if m else -1
-
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_valu_*.json")), key=tag)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_valu_*.json")), key=_profile_tag)
     for f in reversed(files):
         ks = json.load(open(f)).get("runs", {}).get("bench", {})
         names = [nm for nm in PMC_NAMES.get(kernel, [kernel]) if nm in ks]
