@@ -217,7 +217,7 @@ PBH_DI double gamma_ppf_lds(double q, const Params& prm, const PoissonTable& pt,
 // (gamma_ppf_lds), so that the hot loops carry no igami code.
 PBH_DI bool gamma_fast(double q, const sf::GammaGuide& T, double scale, double loc, bool cond0, double* v) {
   if (!(cond0 && q > 0.0 && q < 1.0)) return false;
-  const double w = log(q / (1.0 - q));
+  const double w = sf::log_tab(q / (1.0 - q));
   const double u = (w - T.z0) * T.inv_h;
   if (!(u >= 0.0 && u < (double)(T.m - 1))) return false;
   const int j = (int)u;
@@ -684,7 +684,7 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
       bool fast = valid && cond0 && q > 0.0 && q < 1.0;
       double v = 0.0;
       if (fast) {
-        const double w = log(q / (1.0 - q));
+        const double w = sf::log_tab(q / (1.0 - q));
         const double u = (w - T.z0) * T.inv_h;
         fast = u >= 0.0 && u < (double)(T.m - 1);
         if (fast) {
@@ -803,7 +803,7 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
       bool fast = valid && cond0 && q > 0.0 && q < 1.0;
       double v = 0.0;
       if (fast) {
-        const double w = log(q / (1.0 - q));
+        const double w = sf::log_tab(q / (1.0 - q));
         const double u = (w - G.z0) * G.inv_h;
         fast = u >= 0.0 && u < (double)(G.m - 1);
         if (fast) {

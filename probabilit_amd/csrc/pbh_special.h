@@ -53,6 +53,56 @@ PBH_HD inline double p1evl(double x, const double* c, int n) {
   return a;
 }
 
+// ---------------------------------------------------------------- table-driven log
+#include "pbh_log_table.inc"
+
+// Natural log for the hot ppf paths (ndtri's tail, the gamma guide's log-odds): ~40 VALU
+// instructions against ~115 for the device math library's double-double log.  x = 2^k z,
+// z in [0.6875, 1.375) split into 128 subintervals (tools/gen_log_table.py):
+//   log x = k ln2 + log c + log1p(r),  r = z / c - 1 (c = 1 next to 1),  |r| <= 2^-7,
+// with r exact as a double-double (Dekker product by fma), k ln2 + log c + r summed exactly
+// (Fast2Sum, then TwoSum) and log1p(r) - r as its Taylor
+// series to r^9 (truncation < 2^-63 relative).  The result is the rounded sum plus an error
+// below 2^-60 relative, so it is the correctly rounded log except within ~0.01 ulp of a
+// rounding midpoint: it agrees with glibc's log (what scipy's Cephes calls) on all but ~1e-4
+// of inputs, where glibc's (0.52-ulp) result is the misrounded one, and is never more than
+// 1 ulp from it (tests/test_special_host.py).
+// Branch-free, so that it adds no divergent path or second code body: subnormal arguments are
+// scaled by 2^54 first; zero, negative, infinite and NaN arguments are patched at the end
+// (-inf, NaN, +inf, NaN as the math library's log gives).
+PBH_HD inline double log_tab(double x) {
+  const bool sub = x < 0x1.0p-1022;
+  const uint64_t ix = __builtin_bit_cast(uint64_t, sub ? x * 0x1.0p54 : x);
+  const uint64_t tmp = ix - 0x3fe6000000000000ull;
+  const int i = (int)((tmp >> 45) & 127u);
+  const double kd = (double)(((int64_t)tmp >> 52) - (sub ? 54 : 0));
+  const double z = __builtin_bit_cast(double, ix - (tmp & 0xfff0000000000000ull));
+  const double invc = pbh_log_tab[i][0], lch = pbh_log_tab[i][1], lcl = pbh_log_tab[i][2];
+  const double ph = z * invc;
+  const double pl = fma(z, invc, -ph);  // z invc = ph + pl exactly
+  const double rh = ph - 1.0;           // exact: ph in [0.99, 1.01]
+  const double r = rh + pl;
+  const double rl = (rh - r) + pl;      // r + rl = z invc - 1 exactly (|rh| >= |pl| or rh = 0)
+  const double t1 = kd * kLogTabLn2Hi;  // exact: ln2hi has 42 significant bits
+  const double w = t1 + lch;            // |t1| >= ln 2 > |log c| unless k = 0
+  const double e1 = (t1 - w) + lch;
+  const double s = w + r;
+  const double bv = s - w;
+  const double e2 = (w - (s - bv)) + (r - bv);
+  double p = 1.0 / 9.0;
+  p = fma(p, r, -1.0 / 8.0);
+  p = fma(p, r, 1.0 / 7.0);
+  p = fma(p, r, -1.0 / 6.0);
+  p = fma(p, r, 1.0 / 5.0);
+  p = fma(p, r, -1.0 / 4.0);
+  p = fma(p, r, 1.0 / 3.0);
+  p = fma(p, r, -0.5);
+  const double lo = fma(r * r, p, fma(kd, kLogTabLn2Lo, lcl + e1)) + (e2 + rl);
+  const double v = s + lo;
+  if (x > 0.0 && x < kInf) return v;
+  return x == 0.0 ? -kInf : x == kInf ? kInf : kNaN;
+}
+
 // ---------------------------------------------------------------- inverse normal CDF
 constexpr double kNdtriExpM2 = 0.13533528323661269189;  // exp(-2): ndtri's centre / tail split
 
@@ -104,8 +154,8 @@ PBH_HD inline double ndtri_tail(double y0) {
     y = 1.0 - y;
     negate = false;
   }
-  double x = sqrt(-2.0 * log(y));
-  const double x0 = x - log(x) / x;
+  double x = sqrt(-2.0 * log_tab(y));
+  const double x0 = x - log_tab(x) / x;
   const double z = 1.0 / x;
   double x1;
   if (x < 8.0)
@@ -812,7 +862,7 @@ PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const G
     double x = 0.0;
     bool halley = false, slow = !(p > 0.0 && p < 1.0);
     if (!slow) {
-      const double w = log(p / (1.0 - p));
+      const double w = log_tab(p / (1.0 - p));
       double u = (w - T.z0) * T.inv_h;
       slow = !(u >= 0.0 && u < (double)(T.m - 1));
       if (!slow) {
@@ -828,7 +878,7 @@ PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const G
     return (slow || halley) ? igami_guided_fallback(a, p, x, halley, g->lga, g->lg1pa, g->lanczos) : x;
   } else {
     if (!(p > 0.0 && p < 1.0)) return igami(a, p);
-    const double w = log(p / (1.0 - p));
+    const double w = log_tab(p / (1.0 - p));
     double u = (w - T.z0) * T.inv_h;
     if (!(u >= 0.0 && u < (double)(T.m - 1))) return igami(a, p);
     int j = (int)u;

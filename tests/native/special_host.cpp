@@ -10,6 +10,32 @@ using namespace pbh;
 
 extern "C" {
 
+void sfh_log_tab(const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sf::log_tab(x[i]);
+}
+
+// log_tab against the C library's log (glibc: what scipy's Cephes calls) on n points
+// x = lo * (hi / lo)^u, u from a 64-bit LCG: counts[0] differing results, counts[1] results more
+// than 1 ulp apart.
+void sfh_log_tab_vs_libm(double lo, double hi, long n, unsigned long long seed, long* counts) {
+  long diff = 0, far = 0;
+  const double lr = log(hi / lo);
+  for (long i = 0; i < n; ++i) {
+    seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+    const double u = (double)(seed >> 11) * 0x1.0p-53;
+    const double x = lo * exp(lr * u);
+    const double a = sf::log_tab(x), b = log(x);
+    if (a != b) {
+      ++diff;
+      const long long ia = (long long)__builtin_bit_cast(unsigned long long, a);
+      const long long ib = (long long)__builtin_bit_cast(unsigned long long, b);
+      if (ia - ib > 1 || ib - ia > 1) ++far;
+    }
+  }
+  counts[0] = diff;
+  counts[1] = far;
+}
+
 void sfh_ndtri(const double* q, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = sf::ndtri(q[i]);
 }
