@@ -51,6 +51,8 @@ bool stream_enabled() {  // PBH_PPF_STREAM=0 selects the plain grid-stride k_ppf
 
 unsigned compact_grid(int64_t n) { return grid_for(n, kCTile, 256 * 8); }
 
+bool scalar_params(const Params& prm) { return !prm.ptr[0] && !prm.ptr[1] && !prm.ptr[2]; }
+
 bool compaction_enabled() {
   static const bool on = [] {
     const char* e = getenv("PBH_COMPACT");
@@ -60,19 +62,31 @@ bool compaction_enabled() {
 }
 
 // k_ppf / k_lhs_ppf for D in {norm, lognorm} with tail compaction.  Q(i) gives the quantile of
-// tile item i (a strided load, or the fused LHS generator).
-template <int D, class Q>
-PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm, const PoissonTable& pt, double* __restrict__ out,
-                          int32_t* flag, TailQueue& tq, double* res) {
+// tile item i (a strided load, or the fused LHS generator).  SC: every parameter is a scalar
+// (no per-row arrays), read once into registers -- with per-item Params::at the norm sweep
+// measured 0.78-0.90 ms per 1e8 against 0.60-0.71 (tools/microbench_ppf_c.hip).
+template <int D, bool SC, class Q>
+PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm_in, const PoissonTable& pt,
+                          double* __restrict__ out, int32_t* flag, TailQueue& tq, double* res) {
+  Params prm = prm_in;
+  if constexpr (SC) prm.ptr[0] = prm.ptr[1] = prm.ptr[2] = nullptr;  // at() folds to the scalars
   for (int64_t base = (int64_t)blockIdx.x * kCTile; base < n; base += (int64_t)gridDim.x * kCTile) {
     if (threadIdx.x == 0) tq.count = 0;
     __syncthreads();
+    // every quantile of the tile first: the loads are issued together, not one per round trip
+    // (interleaved with tail_push's LDS atomics they were serialised: 0.82 -> 0.60 ms per 1e8)
+    double qa[kCIpt];
+#pragma unroll
+    for (int j = 0; j < kCIpt; ++j) {
+      const int64_t i = base + j * kBlock + threadIdx.x;
+      qa[j] = i < n ? qof(i) : 0.5;
+    }
 #pragma unroll
     for (int j = 0; j < kCIpt; ++j) {
       const int p = j * kBlock + threadIdx.x;
       const int64_t i = base + p;
       const bool valid = i < n;
-      const double qv = valid ? qof(i) : 0.5;
+      const double qv = qa[j];
       const bool tail = valid && sf::ndtri_takes_tail(qv);
       if (valid && !tail) res[p] = ppf_one<D, 1>(qv, prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
       tail_push(tq, tail, qv, p);
@@ -96,13 +110,13 @@ PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm, const Pois
   }
 }
 
-template <int D>
+template <int D, bool SC>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_c(const double* __restrict__ q, int64_t q_stride, int64_t n,
                                                   Params prm, PoissonTable pt, double* __restrict__ out,
                                                   int32_t* flag) {
   __shared__ TailQueue tq;
   __shared__ double res[kCTile];
-  ppf_compacted<D>(n, [&](int64_t i) { return q[i * q_stride]; }, prm, pt, out, flag, tq, res);
+  ppf_compacted<D, SC>(n, [&](int64_t i) { return q[i * q_stride]; }, prm, pt, out, flag, tq, res);
 }
 
 template <int D>
@@ -176,7 +190,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf(uint64_t seed, int64
   }
 }
 
-template <int D>
+template <int D, bool SC>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_c(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
                                                       uint32_t col, Params prm, PoissonTable pt,
                                                       double* __restrict__ out, int32_t* flag) {
@@ -184,7 +198,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_c(uint64_t seed, int
   __shared__ double res[kCTile];
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
-  ppf_compacted<D>(nrows, [&](int64_t i) { return lhs_quantile(ph, fp, (uint64_t)(row0 + i), col); }, prm, pt, out,
+  ppf_compacted<D, SC>(nrows, [&](int64_t i) { return lhs_quantile(ph, fp, (uint64_t)(row0 + i), col); }, prm, pt, out,
                    flag, tq, res);
 }
 
@@ -322,10 +336,25 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_poisson_lds(const double
                                                             double* __restrict__ out, int32_t* flag) {
   extern __shared__ double plds[];
   const PoissonTable T = stage_poisson(pt, plds);
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-    const double x = ppf_one<PBH_DIST_POISSON>(q[i * q_stride], prm.val[0], prm.val[1], prm.val[2], T);
-    out[i] = x;
-    flag_nonfinite(flag, !isfinite(x));
+  // 4 items per thread per step, their loads issued together (4 independent chains, as in
+  // k_place_gen_poisson)
+  constexpr int kPer = 4;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock * kPer; b < n; b += (int64_t)gridDim.x * kBlock * kPer) {
+    double qv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = b + j * kBlock + threadIdx.x;
+      qv[j] = i < n ? q[i * q_stride] : 0.5;
+    }
+    double x[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) x[j] = ppf_one<PBH_DIST_POISSON>(qv[j], prm.val[0], prm.val[1], prm.val[2], T);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = b + j * kBlock + threadIdx.x;
+      if (i < n) out[i] = x[j];
+      flag_nonfinite(flag, i < n && !isfinite(x[j]));
+    }
   }
 }
 
@@ -594,6 +623,13 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
         if (threadIdx.x == 0) tq[0].count = 0;
         __syncthreads();
       }
+      // every pair of the tile first (loads issued together; see ppf_compacted)
+      uint64_t pa[kCIpt];
+#pragma unroll
+      for (int j = 0; j < kCIpt; ++j) {
+        const int p = h + j * kBlock + threadIdx.x;
+        pa[j] = p >= cnt ? 0ull : BYROW ? (uint64_t)pidx[r0 + p] : pairs[r0 + p];
+      }
 #pragma unroll
       for (int j = 0; j < kCIpt; ++j) {
         const int p = h + j * kBlock + threadIdx.x;
@@ -603,10 +639,10 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
         if (valid) {
           uint32_t t;
           if constexpr (BYROW) {
-            t = pidx[r0 + p];
+            t = (uint32_t)pa[j];
             off = p;
           } else {
-            const uint64_t pr = pairs[r0 + p];
+            const uint64_t pr = pa[j];
             t = (uint32_t)pr;
             const int64_t row = (int64_t)(pr >> 32);
             if (idx) idx[row] = (int32_t)t;
@@ -1191,7 +1227,7 @@ struct SobolCol {
   double scale;
 };
 
-template <int D>
+template <int D, bool SC>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_sobol_ppf_c(SobolCol sc, int64_t row0, int64_t nrows, Params prm,
                                                                PoissonTable pt, double* __restrict__ out,
                                                                int32_t* flag) {
@@ -1200,7 +1236,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_sobol_ppf_c(SobolCol sc, int
   __shared__ uint32_t T[1024];
   build_sobol_tables(sc.sv, T);
   __syncthreads();
-  ppf_compacted<D>(nrows, [&](int64_t i) { return (double)sobol_point(T, sc.shift, (uint64_t)(row0 + i)) * sc.scale; },
+  ppf_compacted<D, SC>(nrows, [&](int64_t i) { return (double)sobol_point(T, sc.shift, (uint64_t)(row0 + i)) * sc.scale; },
                    prm, pt, out, flag, tq, res);
 }
 
@@ -1246,8 +1282,8 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
 #define PBH_CASE(D) \
   case D:           \
     if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
-      PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_c<D>, dim3(compact_grid(n)), b, 0, s, q, qs, n, prm, pt, out,  \
-                                             flag));                                                            \
+      PBH_TIMED(kKPpf, s, hipLaunchKernelGGL((scalar_params(prm) ? k_ppf_c<D, true> : k_ppf_c<D, false>),            \
+                                             dim3(compact_grid(n)), b, 0, s, q, qs, n, prm, pt, out, flag));    \
     else if (streamable)                                                                                        \
       PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_v<D>, gv, b, 0, s, q, n, prm, pt, out, flag));               \
     else                                                                                                        \
@@ -1289,8 +1325,9 @@ int launch_lhs_ppf(int dist, uint64_t seed, int64_t n, int64_t row0, int64_t nro
   case D:           \
     if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
       PBH_TIMED(kKLhsPpf, s,                                                                                    \
-                hipLaunchKernelGGL(k_lhs_ppf_c<D>, dim3(compact_grid(nrows)), b, 0, s, seed, n, row0, nrows, col, \
-                                   prm, pt, out, flag));                                                        \
+                hipLaunchKernelGGL((scalar_params(prm) ? k_lhs_ppf_c<D, true> : k_lhs_ppf_c<D, false>),            \
+                                   dim3(compact_grid(nrows)), b, 0, s, seed, n, row0, nrows, col, prm, pt, out, \
+                                   flag));                                                                      \
     else                                                                                                        \
       PBH_TIMED(kKLhsPpf, s,                                                                                    \
                 hipLaunchKernelGGL(k_lhs_ppf<D>, g, b, 0, s, seed, n, row0, nrows, col, prm, pt, out, flag));   \
@@ -1927,8 +1964,9 @@ extern "C" int pbh_sobol_ppf(const uint32_t* sv_host, const uint32_t* shift_host
   case D:                                                                                                         \
     if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                                    \
       PBH_TIMED(kKPpf, s,                                                                                         \
-                hipLaunchKernelGGL(k_sobol_ppf_c<D>, dim3(compact_grid(nrows)), b, 0, s, sc, row0, nrows, prm, pt, \
-                                   out, nonfinite_flag));                                                         \
+                hipLaunchKernelGGL((scalar_params(prm) ? k_sobol_ppf_c<D, true> : k_sobol_ppf_c<D, false>),         \
+                                   dim3(compact_grid(nrows)), b, 0, s, sc, row0, nrows, prm, pt, out,             \
+                                   nonfinite_flag));                                                              \
     else                                                                                                          \
       PBH_TIMED(kKPpf, s,                                                                                         \
                 hipLaunchKernelGGL(k_sobol_ppf<D>, g, b, 0, s, sc, row0, nrows, prm, pt, out, nonfinite_flag));  \

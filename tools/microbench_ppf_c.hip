@@ -165,6 +165,64 @@ __global__ KATTR(W) void k_norm(const double* __restrict__ q, int64_t n, double*
   }
 }
 
+// the production k_ppf_c<norm> body (pbh_ppf.hip ppf_compacted) with its Params / flag arguments;
+// FLAG = false drops the per-item non-finite flag
+// VAR 0: per-item Params::at; 1: scalars in registers (runtime loc / scale); 2: scalars, no
+// cond0 / q edge checks (the centre formula times scale plus loc); 3: compile-time loc 0, scale 1
+template <bool FLAG, int VAR = 0>
+__global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void k_prod(const double* __restrict__ q,
+                                                                                     int64_t n, Params prm_in,
+                                                                                     PoissonTable pt,
+                                                                                     double* __restrict__ out,
+                                                                                     int32_t* flag) {
+  Params prm = prm_in;
+  if (VAR >= 1) prm.ptr[0] = prm.ptr[1] = prm.ptr[2] = nullptr;
+  if (VAR == 3) {
+    prm.val[0] = 0.0;
+    prm.val[1] = 1.0;
+  }
+  __shared__ TailQueue tq;
+  __shared__ double res[kCTile];
+  for (int64_t base = (int64_t)blockIdx.x * kCTile; base < n; base += (int64_t)gridDim.x * kCTile) {
+    if (threadIdx.x == 0) tq.count = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kCIpt; ++j) {
+      const int p = j * kB + threadIdx.x;
+      const int64_t i = base + p;
+      const bool valid = i < n;
+      const double qv = valid ? q[i] : 0.5;
+      const bool tail = valid && sf::ndtri_takes_tail(qv);
+      if (valid && !tail) {
+        if (VAR == 2)
+          res[p] = sf::ndtri_centre(qv) * prm.val[1] + prm.val[0];
+        else
+          res[p] = ppf_one<PBH_DIST_NORM, 1>(qv, prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
+      }
+      tail_push(tq, tail, qv, p);
+    }
+    __syncthreads();
+    const int T = tq.count;
+    for (int t = threadIdx.x; t < T; t += kB) {
+      const int p = tq.pos[t];
+      const int64_t i = base + p;
+      if (VAR == 2)
+        res[p] = sf::ndtri_tail(tq.arg[t]) * prm.val[1] + prm.val[0];
+      else
+        res[p] = ppf_one<PBH_DIST_NORM, 2>(tq.arg[t], prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kCIpt; ++j) {
+      const int p = j * kB + threadIdx.x;
+      const int64_t i = base + p;
+      const double x = i < n ? res[p] : 0.0;
+      if (i < n) out[i] = x;
+      if (FLAG) flag_nonfinite(flag, !isfinite(x));
+    }
+  }
+}
+
 // wave-private tiles: each wave owns 64 x IPT items, queues its tail items in its own LDS slice
 // and drains them itself (no block barrier); centre results stored from registers; the next
 // tile's quantiles are loaded before the drain when PF.
@@ -303,16 +361,39 @@ int main() {
   hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, q, n);
   hipLaunchKernelGGL(k_ref, dim3(8192), dim3(256), 0, 0, q, n, ref);
   hipDeviceSynchronize();
-  for (int g : {2048, 8192}) {
-    run<3, 8, 0>("copy ipt8", q, out, ref, n, bad, g);
-    run<4, 8, 0>("centre-all ipt8", q, out, ref, n, bad, g);
-    run<5, 8, 4>("base ipt8 w4, libm log", q, out, ref, n, bad, g);
-    run<0, 8, 4>("base ipt8 w4 (production)", q, out, ref, n, bad, g);
-    run<6, 8, 4>("base ipt8 w4 drain x2", q, out, ref, n, bad, g);
-    run<6, 8, 2>("base ipt8 w2 drain x2", q, out, ref, n, bad, g);
-    run<6, 4, 4>("base ipt4 w4 drain x2", q, out, ref, n, bad, g);
-    run<6, 16, 4>("base ipt16 w4 drain x2", q, out, ref, n, bad, g);
-    run_wave<8, 6, true>("wave ipt8 w6 pf", q, out, ref, n, bad, g);
+  int32_t* flag;
+  hipMalloc(&flag, 4);
+  hipMemset(flag, 0, 4);
+  Params prm{};
+  prm.val[0] = 0.0;
+  prm.val[1] = 1.0;
+  for (int rep = 0; rep < 2; ++rep) {
+    for (int g : {2048, 8192}) {
+      run<0, 8, 4>("base ipt8 w4 (replica)", q, out, ref, n, bad, g);
+      for (int f = 0; f < 6; ++f) {
+        hipEvent_t a, b;
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+        hipEventRecord(a);
+        for (int r = 0; r < 10; ++r) {
+          switch (f) {
+            case 0: hipLaunchKernelGGL((k_prod<true, 0>), dim3(g), dim3(kB), 0, 0, q, n, prm, PoissonTable{}, out, flag); break;
+            case 1: hipLaunchKernelGGL((k_prod<true, 1>), dim3(g), dim3(kB), 0, 0, q, n, prm, PoissonTable{}, out, flag); break;
+            case 2: hipLaunchKernelGGL((k_prod<false, 1>), dim3(g), dim3(kB), 0, 0, q, n, prm, PoissonTable{}, out, flag); break;
+            case 3: hipLaunchKernelGGL((k_prod<true, 2>), dim3(g), dim3(kB), 0, 0, q, n, prm, PoissonTable{}, out, flag); break;
+            case 4: hipLaunchKernelGGL((k_prod<false, 2>), dim3(g), dim3(kB), 0, 0, q, n, prm, PoissonTable{}, out, flag); break;
+            default: hipLaunchKernelGGL((k_prod<false, 3>), dim3(g), dim3(kB), 0, 0, q, n, prm, PoissonTable{}, out, flag); break;
+          }
+        }
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        const char* nm[6] = {"prod: at(), flag", "prod: scalars, flag", "prod: scalars", "prod: bare ndtri, flag",
+                             "prod: bare ndtri", "prod: const 0/1"};
+        printf("%-28s grid %7d  %.4f ms\n", nm[f], g, ms / 10);
+      }
+    }
   }
   return 0;
 }
