@@ -70,7 +70,7 @@ PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k
              "k_msd2": ["k_msd2x<1024, 8>", "k_msd2x<512, 8>", "k_msd2w", "k_msd2o", "k_msd2<true>", "k_msd2<false>",
                         "k_msd2"],
              "k_place_msd": ["k_place_msdo", "k_place_msd<true>", "k_place_msd<false>", "k_place_msd"],
-             "k_hist16": ["k_hist16"],
+             "k_hist16": ["k_hist16", "k_hist16c"],
              # one timing id over every variant that ran (the cfg3 set: norm, lognorm, triang,
              # uniform, expon, gamma, poisson): traffic = their dispatch-weighted mean
              "k_place_gen": ["k_place_gen<0>", "k_place_gen<1>", "k_place_gen<2>", "k_place_gen<3>", "k_place_gen<4>",

@@ -70,6 +70,7 @@ PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm_in, const P
                           double* __restrict__ out, int32_t* flag, TailQueue& tq, double* res) {
   Params prm = prm_in;
   if constexpr (SC) prm.ptr[0] = prm.ptr[1] = prm.ptr[2] = nullptr;  // at() folds to the scalars
+  bool bad = false;  // a non-finite output, flagged once per thread at the end
   for (int64_t base = (int64_t)blockIdx.x * kCTile; base < n; base += (int64_t)gridDim.x * kCTile) {
     if (threadIdx.x == 0) tq.count = 0;
     __syncthreads();
@@ -105,9 +106,10 @@ PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm_in, const P
       const int64_t i = base + p;
       const double x = i < n ? res[p] : 0.0;
       if (i < n) out[i] = x;
-      flag_nonfinite(flag, !isfinite(x));
+      bad |= !isfinite(x);
     }
   }
+  flag_nonfinite(flag, bad);
 }
 
 template <int D, bool SC>
@@ -251,6 +253,7 @@ __global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restr
   const sf::GammaGuide T = stage_guide(pt.guide, lds);
   const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
   const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
+  bool bad = false;  // a non-finite output, flagged once per thread at the end
   for (int64_t base = (int64_t)blockIdx.x * kTile; base < n; base += (int64_t)gridDim.x * kTile) {
     if (threadIdx.x == 0) nslow = 0;
     __syncthreads();
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restr
       double v;
       if (gamma_fast(qv[j], T, scale, loc, cond0, &v)) {
         out[i] = v;
-        flag_nonfinite(flag, !isfinite(v));
+        bad |= !isfinite(v);
       } else {
         const int slot = atomicAdd(&nslow, 1);
         if (slot < kQCap) slowq[slot] = (uint16_t)(j * kGBlock + threadIdx.x);
@@ -281,9 +284,10 @@ __global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restr
       if (i >= n) continue;
       const double x = gamma_ppf_lds(q[i * q_stride], prm, pt, T);
       out[i] = x;
-      flag_nonfinite(flag, !isfinite(x));
+      bad |= !isfinite(x);
     }
   }
+  flag_nonfinite(flag, bad);
 }
 
 __global__ __launch_bounds__(kGBlock) void k_lhs_ppf_gamma_lds(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
@@ -339,6 +343,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_poisson_lds(const double
   // 4 items per thread per step, their loads issued together (4 independent chains, as in
   // k_place_gen_poisson)
   constexpr int kPer = 4;
+  bool bad = false;  // a non-finite output, flagged once per thread at the end
   for (int64_t b = (int64_t)blockIdx.x * kBlock * kPer; b < n; b += (int64_t)gridDim.x * kBlock * kPer) {
     double qv[kPer];
 #pragma unroll
@@ -353,9 +358,10 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_poisson_lds(const double
     for (int j = 0; j < kPer; ++j) {
       const int64_t i = b + j * kBlock + threadIdx.x;
       if (i < n) out[i] = x[j];
-      flag_nonfinite(flag, i < n && !isfinite(x[j]));
+      bad |= i < n && !isfinite(x[j]);
     }
   }
+  flag_nonfinite(flag, bad);
 }
 
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_poisson_lds(uint64_t seed, int64_t n, int64_t row0,
@@ -1283,7 +1289,8 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
   case D:           \
     if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
       PBH_TIMED(kKPpf, s, hipLaunchKernelGGL((scalar_params(prm) ? k_ppf_c<D, true> : k_ppf_c<D, false>),            \
-                                             dim3(compact_grid(n)), b, 0, s, q, qs, n, prm, pt, out, flag));    \
+                                             dim3(grid_for(n, kCTile, 8192)), b, 0, s, q, qs, n, prm, pt, out,  \
+                                             flag));                                                            \
     else if (streamable)                                                                                        \
       PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_v<D>, gv, b, 0, s, q, n, prm, pt, out, flag));               \
     else                                                                                                        \

@@ -130,6 +130,89 @@ __global__ __launch_bounds__(1024) void k_hist16(const uint32_t* __restrict__ co
   if (threadIdx.x == 0 && ovf) atomicOr(&state[c], 1);
 }
 
+// k_hist16 in class-major order (gridDim.x a multiple of 8, the default 64 blocks per column): block
+// b counts only tiles of class x = b mod 8 (a contiguous share of them), so its tile-class top-byte
+// counts are the sums of its own 65536 counters over each top byte -- formed once at the flush
+// instead of one more LDS atomic per code (half of the kernel's atomics) -- and each thread keeps
+// four 16-byte loads in flight.  Same counts as k_hist16.
+__global__ __launch_bounds__(1024) void k_hist16c(const uint32_t* __restrict__ codes, int64_t ld, int64_t n,
+                                                  uint32_t* __restrict__ hist, uint32_t* __restrict__ cls,
+                                                  int32_t* __restrict__ state, const int32_t* __restrict__ gate,
+                                                  int tlog) {
+  __shared__ uint32_t w[32768];
+  __shared__ uint32_t cw[256];
+  __shared__ int ovf;
+  const int c = blockIdx.y;
+  if (gate && !gate[c]) return;
+  const uint32_t* cc = codes + (int64_t)c * ld;
+  for (int i = threadIdx.x; i < 32768; i += 1024) w[i] = 0;
+  if (threadIdx.x < 256) cw[threadIdx.x] = 0;
+  if (threadIdx.x == 0) ovf = 0;
+  __syncthreads();
+  const int x = blockIdx.x & 7, sub = blockIdx.x >> 3, nsub = gridDim.x >> 3;
+  const int64_t T = (int64_t)1 << tlog;
+  const int64_t ntiles = (n + T - 1) >> tlog;
+  const int64_t nct = ntiles > x ? (ntiles - x + 7) >> 3 : 0;  // tiles of class x
+  const int64_t j0 = nct * sub / nsub, j1 = nct * (sub + 1) / nsub;
+  bool bad = false;
+  auto add = [&](uint32_t code) {
+    const uint32_t b = code >> 16, sh = (b & 1u) * 16u;
+    const uint32_t old = atomicAdd(&w[b >> 1], 1u << sh);
+    bad |= ((old >> sh) & 0xFFFFu) == 0xFFFFu;
+  };
+  // the full tiles as one stream of 16-byte units: unit u -> tile x + 8 (j0 + u / q4), offset u % q4
+  const bool partial_last = (n & (T - 1)) != 0 && j1 > j0 && x + 8 * (j1 - 1) == ntiles - 1;
+  const int64_t jf = partial_last ? j1 - 1 : j1;  // full tiles [j0, jf)
+  const int64_t q4 = T >> 2;
+  if ((((uintptr_t)cc) & 15) == 0 && tlog >= 2) {
+    const uint4* v4 = reinterpret_cast<const uint4*>(cc);
+    const int64_t units = (jf - j0) * q4;
+    for (int64_t u0 = threadIdx.x; u0 < units; u0 += 4 * 1024) {
+      uint4 v[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int64_t u = u0 + m * 1024;
+        if (u < units) {
+          const int64_t j = j0 + (u >> (tlog - 2));  // q4 = 2^(tlog - 2) units per tile
+          v[m] = v4[((x + 8 * j) << (tlog - 2)) + (u & (q4 - 1))];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        if (u0 + m * 1024 < units) {
+          add(v[m].x);
+          add(v[m].y);
+          add(v[m].z);
+          add(v[m].w);
+        }
+      }
+    }
+  } else {
+    for (int64_t j = j0; j < jf; ++j)
+      for (int64_t i = threadIdx.x; i < T; i += 1024) add(cc[((x + 8 * j) << tlog) + i]);
+  }
+  if (partial_last) {
+    const int64_t r0 = (x + 8 * (j1 - 1)) << tlog;
+    for (int64_t i = r0 + threadIdx.x; i < n; i += 1024) add(cc[i]);
+  }
+  if (bad) ovf = 1;
+  __syncthreads();
+  uint32_t* hc = hist + (int64_t)c * 65536;
+  for (int j = threadIdx.x; j < 32768; j += 1024) {
+    const uint32_t v = w[j];
+    if (v & 0xFFFFu) atomicAdd(&hc[2 * j], v & 0xFFFFu);
+    if (v >> 16) atomicAdd(&hc[2 * j + 1], v >> 16);
+    // the top byte of the counters in word j is j >> 7; a wave's 64 words share it
+    uint32_t sum = (v & 0xFFFFu) + (v >> 16);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(&cw[j >> 7], sum);
+  }
+  __syncthreads();
+  if (threadIdx.x < 256 && cw[threadIdx.x]) atomicAdd(&cls[(int64_t)c * 2048 + (x << 8) + threadIdx.x], cw[threadIdx.x]);
+  if (threadIdx.x == 0 && ovf) atomicOr(&state[c], 1);
+}
+
 // The gated re-count of k_hist16 (the adaptive code map's second count): the same counts in four
 // quarters of the 65536 buckets (blockIdx.z), 16-bit packed in 32 KiB of LDS instead of 128 KiB --
 // the gate is only known on the device, so every column's blocks are dispatched, and a no-op block
@@ -1471,6 +1554,14 @@ void step4_sync_side_streams() {
 }
 
 // PBH_MSD_TILE: the code passes' tile, 8192 rows (default) or 4096 (k_msd1x / k_msd2x)
+static bool hist_class_major() {  // PBH_HIST_CLASS=0: k_hist16 (one more LDS atomic per code) everywhere
+  static const bool on = [] {
+    const char* e = getenv("PBH_HIST_CLASS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static int msd_tile_log() {
   static const int v = [] {
     const char* e = getenv("PBH_MSD_TILE");
@@ -1560,9 +1651,15 @@ int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs,
   int64_t blocks = (n + 65535) / 65536;
   if (blocks > 64) blocks = 64;
   if (blocks < 1) blocks = 1;
-  PBH_TIMED(kKHist16, s,
-            hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)kk), dim3(1024), 0, s, codes, ldc, n, hist,
-                               cls, state, nullptr, msd_tile_log()));
+  if (blocks >= 8) blocks &= ~(int64_t)7;  // k_hist16c: 8 tile classes
+  if (blocks % 8 == 0 && hist_class_major())
+    PBH_TIMED(kKHist16, s,
+              hipLaunchKernelGGL(k_hist16c, dim3((unsigned)blocks, (unsigned)kk), dim3(1024), 0, s, codes, ldc, n,
+                                 hist, cls, state, nullptr, msd_tile_log()));
+  else
+    PBH_TIMED(kKHist16, s,
+              hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, (unsigned)kk), dim3(1024), 0, s, codes, ldc, n, hist,
+                                 cls, state, nullptr, msd_tile_log()));
   PBH_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_hist16_scan, dim3((unsigned)kk), dim3(1024), 0, s, hist, n, sh.start + (int64_t)c0 * 65537,
                      sh.tpre + (int64_t)c0 * 257, cls, sh.cstart + (int64_t)c0 * 2048, state, flags, nullptr,
@@ -1591,6 +1688,7 @@ int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs
   int64_t blocks = (n + 65535) / 65536;
   if (blocks > 64) blocks = 64;
   if (blocks < 1) blocks = 1;
+  if (blocks >= 8) blocks &= ~(int64_t)7;  // k_hist16c: 8 tile classes
   // the re-code of the columns that are not flat: every kernel exits at once for the others
   hipLaunchKernelGGL(k_adapt_reset, dim3((unsigned)kk), dim3(1024), 0, s, state, flags, retry, hist,
                      sh.cur1 + c0 * cw, sh.cur2 + (int64_t)c0 * 65536, sh.curF + c0 * cw, cls,
@@ -1615,8 +1713,12 @@ int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs
   // atomics); several: k_hist16_q, whose no-op blocks for the columns that need no re-count hold
   // 32 KiB instead of 136 (the gate is only known on the device)
   if (kk == 1) {
-    hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, 1), dim3(1024), 0, s, codes, ldc, n, hist, cls, state, retry,
-                       msd_tile_log());
+    if (blocks % 8 == 0 && hist_class_major())
+      hipLaunchKernelGGL(k_hist16c, dim3((unsigned)blocks, 1), dim3(1024), 0, s, codes, ldc, n, hist, cls, state,
+                         retry, msd_tile_log());
+    else
+      hipLaunchKernelGGL(k_hist16, dim3((unsigned)blocks, 1), dim3(1024), 0, s, codes, ldc, n, hist, cls, state, retry,
+                         msd_tile_log());
   } else {
     hipLaunchKernelGGL(k_hist16_q, dim3((unsigned)blocks, (unsigned)kk, 4), dim3(1024), 0, s, codes, ldc, n, hist, cls,
                        state, retry, msd_tile_log());

@@ -195,7 +195,9 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     the queued finish (28, 30), the whole gamma table in LDS
     (PBH_GAMMA_WIN=0), the placement levels' other split (PBH_PLACE_TOP=0), 64-row step-3 tiles
     (PBH_APPLY_ROWS=64), the poisson run heads from every stratum instead of the boundary search
-    (PBH_DISCRETE_SCAN=1) -- step-4 indices equal to the oracle's and the outputs within 1e-10."""
+    (PBH_DISCRETE_SCAN=1), the code histogram with the tile-class counts per code (PBH_HIST_CLASS=0)
+    -- step-4 indices equal to the oracle's and the outputs within 1e-10.  600 001 rows: 8 histogram
+    blocks per column, so the default takes the class-major k_hist16c."""
     import os
     import subprocess
     import sys
@@ -203,10 +205,10 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     from oracle.pipeline import cfg3_corr, cfg_dists
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    n, d, seed = 300_001, 8, 31
+    n, d, seed = 600_001, 8, 31
     dists, C = cfg_dists(d), cfg3_corr(d)
     ref = _oracle(n, dists, seed, C)
-    for env in ({"PBH_MSD_TILE": "4096", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"},
+    for env in ({"PBH_HIST_CLASS": "0"}, {"PBH_MSD_TILE": "4096", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"},
                 {"PBH_FINISH_CFG": "30"}, {"PBH_GAMMA_WIN": "0"}, {"PBH_PLACE_TOP": "0"}, {"PBH_APPLY_ROWS": "64"},
                 {"PBH_DISCRETE_SCAN": "1"}):
         dd = tmp_path / "_".join(f"{k}{v}" for k, v in env.items())
