@@ -239,7 +239,7 @@ PBH_DI bool gamma_fast(double q, const sf::GammaGuide& T, double scale, double l
   const int j = (int)u;
   const double y = sf::guide_interp(T, j, u - (double)j);
   if (!(y >= -680.0 && y <= 700.0 && T.ok[j] != 0.0)) return false;
-  *v = exp(y) * scale + loc;
+  *v = sf::exp_tab(y) * scale + loc;
   return true;
 }
 
@@ -733,7 +733,7 @@ __global__ __launch_bounds__(kGBlock) void k_place_gen_gamma(const uint64_t* __r
           const int jj = (int)u;
           const double yy = sf::guide_interp(T, jj, u - (double)jj);
           fast = yy >= -680.0 && yy <= 700.0 && T.ok[jj] != 0.0;
-          if (fast) v = exp(yy) * scale + loc;
+          if (fast) v = sf::exp_tab(yy) * scale + loc;
         }
       }
       if (valid) {
@@ -855,7 +855,7 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
           if (fast) {
             const double yy = sf::guide_interp_arr(win, win + kGWin, win + 2 * kGWin, G.h, jl, u - (double)jj);
             fast = yy >= -680.0 && yy <= 700.0 && win[3 * kGWin + jl] != 0.0;
-            if (fast) v = exp(yy) * scale + loc;
+            if (fast) v = sf::exp_tab(yy) * scale + loc;
           }
         }
       }

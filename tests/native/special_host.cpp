@@ -36,6 +36,28 @@ void sfh_log_tab_vs_libm(double lo, double hi, long n, unsigned long long seed, 
   counts[1] = far;
 }
 
+void sfh_exp_tab(const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sf::exp_tab(x[i]);
+}
+
+// exp_tab against the C library's exp on n uniform points of [lo, hi): counts as sfh_log_tab_vs_libm
+void sfh_exp_tab_vs_libm(double lo, double hi, long n, unsigned long long seed, long* counts) {
+  long diff = 0, far = 0;
+  for (long i = 0; i < n; ++i) {
+    seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+    const double y = lo + (hi - lo) * ((double)(seed >> 11) * 0x1.0p-53);
+    const double a = sf::exp_tab(y), b = exp(y);
+    if (a != b) {
+      ++diff;
+      const long long ia = (long long)__builtin_bit_cast(unsigned long long, a);
+      const long long ib = (long long)__builtin_bit_cast(unsigned long long, b);
+      if (ia - ib > 1 || ib - ia > 1) ++far;
+    }
+  }
+  counts[0] = diff;
+  counts[1] = far;
+}
+
 void sfh_ndtri(const double* q, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = sf::ndtri(q[i]);
 }
