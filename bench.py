@@ -324,6 +324,12 @@ def pmc_valu(kernel):
     return None, None
 
 
+# the sweep kernel each cfg2 distribution takes (pbh_ppf.hip launch_ppf), for its VALU-busy figure
+SWEEP_KERNELS = {"norm": "k_ppf_c<0, true>", "lognorm": "k_ppf_c<3, true>", "gamma": "k_ppf_gamma_lds",
+                 "poisson": "k_ppf_poisson_lds", "triang": "k_ppf_v<4>", "uniform": "k_ppf_v<1>",
+                 "expon": "k_ppf_v<2>"}
+
+
 def ppf_sweep(lib, dists, n, seed, reps=3):
     """Side measurement for the north_star's "ppf sweep" roofline (16 B/draw, read
     q 8 + write x 8, at the sample_from_quantiles boundary): pbh_ppf over one HBM-resident
@@ -347,7 +353,15 @@ def ppf_sweep(lib, dists, n, seed, reps=3):
         t, c = ctypes.c_double(), ctypes.c_int64()
         _lib.check(lib.pbh_timing_read(kid, ctypes.byref(t), ctypes.byref(c)))
         avg = t.value / max(c.value, 1)
-        per[f"{name}{kw}"] = {"ms": round(avg, 4), "GBps": round(16 * n / (avg / 1e3) / 1e9, 1)}
+        ent = {"ms": round(avg, 4), "GBps": round(16 * n / (avg / 1e3) / 1e9, 1)}
+        kname = SWEEP_KERNELS.get(name)
+        if kname:  # issue-level bound next to the bandwidth (committed rocprofv3 VALU pass)
+            valu, src = pmc_valu(kname)
+            if valu is not None:
+                bound = ("HBM" if ent["GBps"] >= 0.6 * HBM_PEAK_GBS else "VALU" if valu >= 0.7
+                         else "latency (VALU-busy < 0.7, < 0.6 of HBM)")
+                ent.update({"kernel": kname, "valu_busy": valu, "valu_source": src, "bound": bound})
+        per[f"{name}{kw}"] = ent
         tot_ms += avg
         tot_b += 16 * n
     gbps = tot_b / (tot_ms / 1e3) / 1e9
