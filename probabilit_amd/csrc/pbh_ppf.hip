@@ -254,14 +254,29 @@ __global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restr
   const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
   const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
   bool bad = false;  // a non-finite output, flagged once per thread at the end
-  for (int64_t base = (int64_t)blockIdx.x * kTile; base < n; base += (int64_t)gridDim.x * kTile) {
+  // one workgroup per CU: nothing else on the CU hides a tile's load latency, so the next tile's
+  // quantiles are loaded while this one is evaluated (register prefetch)
+  const int64_t step = (int64_t)gridDim.x * kTile;
+  double qn[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t i = (int64_t)blockIdx.x * kTile + j * kGBlock + threadIdx.x;
+    qn[j] = i < n ? q[i * q_stride] : 0.5;
+  }
+  for (int64_t base = (int64_t)blockIdx.x * kTile; base < n; base += step) {
     if (threadIdx.x == 0) nslow = 0;
     __syncthreads();
     double qv[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
+#ifndef PBH_NO_PREFETCH
+      qv[j] = qn[j];
+      const int64_t i = base + step + j * kGBlock + threadIdx.x;
+      qn[j] = i < n ? q[i * q_stride] : 0.5;
+#else
       const int64_t i = base + j * kGBlock + threadIdx.x;
       qv[j] = i < n ? q[i * q_stride] : 0.5;
+#endif
     }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -825,10 +840,10 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
   const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
   const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
   constexpr int kPer = kGenRows / kGWBlock;
-  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
+  // the next block's pairs are loaded while this one is evaluated (register prefetch)
+  auto load = [&](int64_t b, uint64_t* pr) {
     const int64_t r0 = b << kGenPlaceShift;
-    const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
-    uint64_t pr[kPer];
+    const int cnt = r0 < rows ? (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows) : 0;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int p = j * kGWBlock + threadIdx.x;
@@ -837,6 +852,20 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
       else
         pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
     }
+  };
+  uint64_t pn[kPer];
+  load(blockIdx.x, pn);
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
+    uint64_t pr[kPer];
+#ifndef PBH_NO_PREFETCH
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) pr[j] = pn[j];
+    load(b + gridDim.x, pn);
+#else
+    load(b, pr);
+#endif
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const bool valid = pr[j] != ~0ull;
