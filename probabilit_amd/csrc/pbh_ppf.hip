@@ -67,7 +67,8 @@ bool compaction_enabled() {
 // measured 0.78-0.90 ms per 1e8 against 0.60-0.71 (tools/microbench_ppf_c.hip).
 template <int D, bool SC, class Q>
 PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm_in, const PoissonTable& pt,
-                          double* __restrict__ out, int32_t* flag, TailQueue& tq, double* res) {
+                          double* __restrict__ out, int32_t* flag, TailQueue& tq, double* res,
+                          const double* lt = nullptr) {
   Params prm = prm_in;
   if constexpr (SC) prm.ptr[0] = prm.ptr[1] = prm.ptr[2] = nullptr;  // at() folds to the scalars
   bool bad = false;  // a non-finite output, flagged once per thread at the end
@@ -97,7 +98,7 @@ PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm_in, const P
     for (int t = threadIdx.x; t < T; t += kBlock) {
       const int p = tq.pos[t];
       const int64_t i = base + p;
-      res[p] = ppf_one<D, 2>(tq.arg[t], prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
+      res[p] = ppf_one<D, 2>(tq.arg[t], prm.at(0, i), prm.at(1, i), prm.at(2, i), pt, lt);
     }
     __syncthreads();
 #pragma unroll
@@ -118,7 +119,9 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_c(const double* __restri
                                                   int32_t* flag) {
   __shared__ TailQueue tq;
   __shared__ double res[kCTile];
-  ppf_compacted<D, SC>(n, [&](int64_t i) { return q[i * q_stride]; }, prm, pt, out, flag, tq, res);
+  __shared__ double lt[kLog3N];
+  stage_log3(lt);  // (ppf_compacted's first barrier follows)
+  ppf_compacted<D, SC>(n, [&](int64_t i) { return q[i * q_stride]; }, prm, pt, out, flag, tq, res, lt);
 }
 
 template <int D>
@@ -231,25 +234,46 @@ PBH_DI double gamma_ppf_lds(double q, const Params& prm, const PoissonTable& pt,
 // igami_guided's interpolation branch and ppf_one's gamma wrapper, operation for operation:
 // true and *v = the value when the element needs no iteration; false sends it to the slow queue
 // (gamma_ppf_lds), so that the hot loops carry no igami code.
-PBH_DI bool gamma_fast(double q, const sf::GammaGuide& T, double scale, double loc, bool cond0, double* v) {
+// ltab / etab: the log and exp tables staged in LDS (stage_logexp)
+PBH_DI bool gamma_fast(double q, const sf::GammaGuide& T, double scale, double loc, bool cond0, double* v,
+                       const double* ltab, const double* etab) {
   if (!(cond0 && q > 0.0 && q < 1.0)) return false;
-  const double w = sf::log_tab(q / (1.0 - q));
+  const double w = sf::log_tab_at(q / (1.0 - q), ltab);
   const double u = (w - T.z0) * T.inv_h;
   if (!(u >= 0.0 && u < (double)(T.m - 1))) return false;
   const int j = (int)u;
   const double y = sf::guide_interp(T, j, u - (double)j);
   if (!(y >= -680.0 && y <= 700.0 && T.ok[j] != 0.0)) return false;
-  *v = sf::exp_tab(y) * scale + loc;
+  *v = sf::exp_tab_at(y, etab) * scale + loc;
   return true;
+}
+
+// sf::log_tab's and sf::exp_tab's tables copied into LDS (4 KiB + 2 KiB): their entries are picked
+// per lane, so a wave's load from the global copy touches up to 32 / 16 cache lines
+constexpr int kLogTabN = 128 * 4, kExpTabN = 128 * 2;
+PBH_DI void stage_logexp(double*& ltab, double*& etab) {
+#ifdef PBH_NO_LDS_LOGEXP  // A/B build: the global tables
+  ltab = const_cast<double*>(&sf::pbh_log_tab[0][0]);
+  etab = const_cast<double*>(&sf::pbh_exp_tab[0][0]);
+#else
+  for (int k = threadIdx.x; k < kLogTabN; k += blockDim.x) ltab[k] = (&sf::pbh_log_tab[0][0])[k];
+  for (int k = threadIdx.x; k < kExpTabN; k += blockDim.x) etab[k] = (&sf::pbh_exp_tab[0][0])[k];
+#endif
 }
 
 __global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restrict__ q, int64_t q_stride, int64_t n,
                                                            Params prm, PoissonTable pt, double* __restrict__ out,
                                                            int32_t* flag) {
   __shared__ double lds[kGTable];
-  constexpr int kPer = 4, kTile = kPer * kGBlock, kQCap = 2048;
+#ifndef PBH_GAMMA_SWEEP_PER
+#define PBH_GAMMA_SWEEP_PER 4
+#endif
+  constexpr int kPer = PBH_GAMMA_SWEEP_PER, kTile = kPer * kGBlock, kQCap = 2048;
   __shared__ uint16_t slowq[kQCap];
   __shared__ int nslow;
+  __shared__ double ltab_s[kLogTabN], etab_s[kExpTabN];
+  double *ltab = ltab_s, *etab = etab_s;
+  stage_logexp(ltab, etab);  // (stage_guide's barrier follows)
   const sf::GammaGuide T = stage_guide(pt.guide, lds);
   const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
   const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
@@ -283,7 +307,7 @@ __global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restr
       const int64_t i = base + j * kGBlock + threadIdx.x;
       if (i >= n) continue;
       double v;
-      if (gamma_fast(qv[j], T, scale, loc, cond0, &v)) {
+      if (gamma_fast(qv[j], T, scale, loc, cond0, &v, ltab, etab)) {
         out[i] = v;
         bad |= !isfinite(v);
       } else {
@@ -830,6 +854,9 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
   if (state && *state) return;
   __shared__ double win[4 * kGWin];  // y, d1, d2, ok of nodes j0 .. j0 + jn - 1
   __shared__ double buf[kGenRows];
+  __shared__ double ltab_s[kLogTabN], etab_s[kExpTabN];
+  double *ltab = ltab_s, *etab = etab_s;
+  stage_logexp(ltab, etab);  // (the window's barrier follows)
   const sf::GammaGuide& G = pt.guide;
   for (int k = threadIdx.x; k < 4 * jn; k += kGWBlock) {
     const int a = k / jn, i = k - a * jn;
@@ -874,7 +901,7 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
       bool fast = valid && cond0 && q > 0.0 && q < 1.0;
       double v = 0.0;
       if (fast) {
-        const double w = sf::log_tab(q / (1.0 - q));
+        const double w = sf::log_tab_at(q / (1.0 - q), ltab);
         const double u = (w - G.z0) * G.inv_h;
         fast = u >= 0.0 && u < (double)(G.m - 1);
         if (fast) {
@@ -884,7 +911,7 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
           if (fast) {
             const double yy = sf::guide_interp_arr(win, win + kGWin, win + 2 * kGWin, G.h, jl, u - (double)jj);
             fast = yy >= -680.0 && yy <= 700.0 && win[3 * kGWin + jl] != 0.0;
-            if (fast) v = sf::exp_tab(yy) * scale + loc;
+            if (fast) v = sf::exp_tab_at(yy, etab) * scale + loc;
           }
         }
       }
@@ -1106,7 +1133,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
     }
     __syncthreads();
     const int T = tq.count;
-    for (int t = threadIdx.x; t < T; t += kBlock) res[tq.pos[t]] = sf::ndtri_tail(tq.arg[t]);
+    for (int t = threadIdx.x; t < T; t += kBlock) res[tq.pos[t]] = sf::ndtri_tail(tq.arg[t]);  // (an LDS copy of the log table measured 1 ms per step slower here)
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kCIpt; ++j) {

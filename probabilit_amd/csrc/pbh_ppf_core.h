@@ -61,12 +61,27 @@ PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
   return (double)(t.k_lo + lo);
 }
 
+// log_tab's table staged in LDS without its padding column (3 KiB): ndtri's tail reads two random
+// entries per draw, up to 32 cache lines per wave load from the global copy
+constexpr int kLog3N = 128 * 3;
+PBH_DI void stage_log3(double* lt) {
+  for (int k = threadIdx.x; k < kLog3N; k += blockDim.x) lt[k] = (&sf::pbh_log_tab[0][0])[4 * (k / 3) + k % 3];
+}
+PBH_DI double tail_of(double q, const double* lt) {
+#ifdef PBH_NO_LDS_LOGEXP  // A/B build: the global table
+  return sf::ndtri_tail(q);
+#else
+  return lt ? sf::ndtri_tail_at<3>(q, lt) : sf::ndtri_tail(q);
+#endif
+}
+
 // ppf of one element for distribution D; p = (shape..., loc, scale) already resolved.
 // PART selects ndtri's branch for norm / lognorm (0: ndtri, 1: ndtri_centre, 2: ndtri_tail),
 // for the compacted kernels that know which one an element takes.
 // COLD_GAMMA: igami_guided's fallbacks as a call (see igami_guided)
+// lt: for PART 2, log_tab's table in LDS with entry stride 3 (stage_log3), else the global table
 template <int D, int PART = 0, bool COLD_GAMMA = false>
-PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTable& pt) {
+PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTable& pt, const double* lt = nullptr) {
   if constexpr (D == PBH_DIST_POISSON) {
     double mu = p0, loc = p1;
     bool cond0 = (mu >= 0.0) && (loc == loc);
@@ -100,13 +115,13 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
     if (!(q > 0.0 && q < 1.0)) return kNaN;
     double x;
     if constexpr (D == PBH_DIST_NORM) {
-      x = PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q);
+      x = PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? tail_of(q, lt) : sf::ndtri(q);
     } else if constexpr (D == PBH_DIST_UNIFORM) {
       x = q;
     } else if constexpr (D == PBH_DIST_EXPON) {
       x = -sf::log1p_(-q);  // scipy expon._ppf: -sc.log1p(-q), the Cephes log1p
     } else if constexpr (D == PBH_DIST_LOGNORM) {
-      x = exp(shape * (PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? sf::ndtri_tail(q) : sf::ndtri(q)));
+      x = exp(shape * (PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? tail_of(q, lt) : sf::ndtri(q)));
     } else if constexpr (D == PBH_DIST_TRIANG) {
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));

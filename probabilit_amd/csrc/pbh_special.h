@@ -70,14 +70,17 @@ PBH_HD inline double p1evl(double x, const double* c, int n) {
 // Branch-free, so that it adds no divergent path or second code body: subnormal arguments are
 // scaled by 2^54 first; zero, negative, infinite and NaN arguments are patched at the end
 // (-inf, NaN, +inf, NaN as the math library's log gives).
-PBH_HD inline double log_tab(double x) {
+// tab: pbh_log_tab (flat, 4 doubles per entry) wherever it lives -- a kernel may stage it in LDS
+// (random entries per lane: 64 scattered cache lines per load otherwise); same values, same result
+template <int S = 4>  // entry stride of tab: 4 (the global table) or 3 (an LDS copy without the padding)
+PBH_HD inline double log_tab_at(double x, const double* __restrict__ tab) {
   const bool sub = x < 0x1.0p-1022;
   const uint64_t ix = __builtin_bit_cast(uint64_t, sub ? x * 0x1.0p54 : x);
   const uint64_t tmp = ix - 0x3fe6000000000000ull;
   const int i = (int)((tmp >> 45) & 127u);
   const double kd = (double)(((int64_t)tmp >> 52) - (sub ? 54 : 0));
   const double z = __builtin_bit_cast(double, ix - (tmp & 0xfff0000000000000ull));
-  const double invc = pbh_log_tab[i][0], lch = pbh_log_tab[i][1], lcl = pbh_log_tab[i][2];
+  const double invc = tab[S * i], lch = tab[S * i + 1], lcl = tab[S * i + 2];
   const double ph = z * invc;
   const double pl = fma(z, invc, -ph);  // z invc = ph + pl exactly
   const double rh = ph - 1.0;           // exact: ph in [0.99, 1.01]
@@ -102,6 +105,7 @@ PBH_HD inline double log_tab(double x) {
   if (x > 0.0 && x < kInf) return v;
   return x == 0.0 ? -kInf : x == kInf ? kInf : kNaN;
 }
+PBH_HD inline double log_tab(double x) { return log_tab_at(x, &pbh_log_tab[0][0]); }
 
 // e^y for y in [-700, 700] (the gamma guide's interpolated log x; its callers check the range):
 // y = (k / 128) ln2 + r, |r| <= ln2 / 256, r exact to ~2^-60 (k ln2hi exact, Sterbenz),
@@ -109,12 +113,12 @@ PBH_HD inline double log_tab(double x) {
 // (truncation < 2^-60): ~25 VALU instructions against ~42 for the math library's exp; within
 // 0.52 ulp, equal to glibc's exp on all but ~1e-3 of arguments (tests/test_special_host.py).  The
 // gamma guide's interpolated log x it exponentiates is itself accurate to ~1e-12 only.
-PBH_HD inline double exp_tab(double y) {
+PBH_HD inline double exp_tab_at(double y, const double* __restrict__ tab /* pbh_exp_tab, flat */) {
   const double kd = __builtin_rint(y * kExpTabInvLn2N);
   const double r = (y - kd * kExpTabLn2HiN) - kd * kExpTabLn2LoN;
   const int ki = (int)kd;
   const int j = ki & 127, e = ki >> 7;  // arithmetic shift: floor(k / 128)
-  const double th = pbh_exp_tab[j][0], tl = pbh_exp_tab[j][1];
+  const double th = tab[2 * j], tl = tab[2 * j + 1];
   double p = 1.0 / 120.0;
   p = fma(p, r, 1.0 / 24.0);
   p = fma(p, r, 1.0 / 6.0);
@@ -123,6 +127,7 @@ PBH_HD inline double exp_tab(double y) {
   const double v = th + fma(th, em1, tl);
   return __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, v) + ((uint64_t)(int64_t)e << 52));
 }
+PBH_HD inline double exp_tab(double y) { return exp_tab_at(y, &pbh_exp_tab[0][0]); }
 
 // ---------------------------------------------------------------- inverse normal CDF
 constexpr double kNdtriExpM2 = 0.13533528323661269189;  // exp(-2): ndtri's centre / tail split
@@ -153,8 +158,10 @@ PBH_HD inline double ndtri_centre(double y0) {
   return x * kSqrt2Pi;
 }
 
-// Tail: ndtri_takes_tail(y0).
-PBH_HD inline double ndtri_tail(double y0) {
+// Tail: ndtri_takes_tail(y0).  LT: log_tab's table and its stride (a kernel's LDS copy), or the
+// global table.
+template <int S = 4>
+PBH_HD inline double ndtri_tail_at(double y0, const double* __restrict__ lt) {
   // z = sqrt(-2 log y) in [2, 8)
   const double P1[9] = {4.05544892305962419923e0, 3.15251094599893866154e1, 5.71628192246421288162e1,
                         4.40805073893200834700e1, 1.46849561928858024014e1, 2.18663306850790267539e0,
@@ -175,8 +182,8 @@ PBH_HD inline double ndtri_tail(double y0) {
     y = 1.0 - y;
     negate = false;
   }
-  double x = sqrt(-2.0 * log_tab(y));
-  const double x0 = x - log_tab(x) / x;
+  double x = sqrt(-2.0 * log_tab_at<S>(y, lt));
+  const double x0 = x - log_tab_at<S>(x, lt) / x;
   const double z = 1.0 / x;
   double x1;
   if (x < 8.0)
@@ -186,6 +193,7 @@ PBH_HD inline double ndtri_tail(double y0) {
   x = x0 - x1;
   return negate ? -x : x;
 }
+PBH_HD inline double ndtri_tail(double y0) { return ndtri_tail_at(y0, &pbh_log_tab[0][0]); }
 
 // Cephes ndtri (scipy.special.ndtri): Phi^-1(y0).
 PBH_HD inline double ndtri(double y0) {
