@@ -45,7 +45,24 @@ typedef enum pbh_dist {
   PBH_DIST_BETA = 7,    /* params: a, b, loc, scale           I_x(a, b) = q (Boost ibeta_inv) */
   PBH_DIST_TRUNCNORM = 8, /* params: a, b, loc, scale         truncnorm._ppf (log space)     */
   PBH_DIST_BINOM = 9,   /* params: n, p, loc (discrete)       smallest k: bdtr(k, n, p) >= q */
-  PBH_DIST_BERNOULLI = 10 /* params: p, loc (discrete)        binom with n = 1               */
+  PBH_DIST_BERNOULLI = 10, /* params: p, loc (discrete)       binom with n = 1               */
+  /* closed-form scipy _ppf bodies (scipy 1.15 stats/_continuous_distns.py), params: shapes,
+   * loc, scale; any other scipy.stats name the reference's getattr(stats, distr) would take
+   * (modeling.py:805-807) has no kernel */
+  PBH_DIST_WEIBULL_MIN = 11, /* c                                pow(-log1p(-q), 1/c)           */
+  PBH_DIST_WEIBULL_MAX = 12, /* c                                -pow(-log(q), 1/c)             */
+  PBH_DIST_LOGISTIC = 13,    /*                                  logit(q)                       */
+  PBH_DIST_CAUCHY = 14,      /*                                  Boost cauchy quantile          */
+  PBH_DIST_LAPLACE = 15,     /*                                  +-log(2 min(q, 1 - q))         */
+  PBH_DIST_GUMBEL_R = 16,    /*                                  -log(-log(q))                  */
+  PBH_DIST_GUMBEL_L = 17,    /*                                  log(-log1p(-q))                */
+  PBH_DIST_PARETO = 18,      /* b                                pow(1 - q, -1/b)               */
+  PBH_DIST_LOGUNIFORM = 19,  /* a, b   (also scipy's reciprocal) exp(log a + q (log b - log a)) */
+  PBH_DIST_RAYLEIGH = 20,    /*                                  sqrt(-2 log1p(-q))             */
+  PBH_DIST_LOMAX = 21,       /* c                                expm1(-log1p(-q) / c)          */
+  PBH_DIST_GENEXTREME = 22,  /* c                                -expm1(-c x) / c, x = gumbel_r */
+  PBH_DIST_GOMPERTZ = 23,    /* c                                log1p(-log1p(-q) / c)          */
+  PBH_DIST_CHI2 = 24         /* df                               2 gammaincinv(df / 2, q)       */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

@@ -17,7 +17,9 @@ OK, ERR_INVALID, ERR_HIP, ERR_NOT_PD, ERR_NONFINITE, ERR_WORKSPACE, ERR_UNSUPPOR
 
 # pbh_dist
 DIST_IDS = {"norm": 0, "uniform": 1, "expon": 2, "lognorm": 3, "triang": 4, "gamma": 5, "poisson": 6, "beta": 7,
-            "truncnorm": 8, "binom": 9, "bernoulli": 10}
+            "truncnorm": 8, "binom": 9, "bernoulli": 10, "weibull_min": 11, "weibull_max": 12, "logistic": 13,
+            "cauchy": 14, "laplace": 15, "gumbel_r": 16, "gumbel_l": 17, "pareto": 18, "loguniform": 19,
+            "reciprocal": 19, "rayleigh": 20, "lomax": 21, "genextreme": 22, "gompertz": 23, "chi2": 24}
 
 # pbh_table_kind
 TABLE_INTERP, TABLE_QUANTILE, TABLE_SEARCH = 0, 1, 2

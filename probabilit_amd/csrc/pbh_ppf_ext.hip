@@ -8,6 +8,9 @@
 //   binom      scipy _binom_ppf (Boost quantile, integer_round_up): smallest k in [0, n] with
 //              bdtr(k, n, p) >= q, bdtr = Cephes incbet(n - k, k + 1, 1 - p)
 //   bernoulli  binom with n = 1
+//   weibull_min ... chi2 (PBH_DIST_WEIBULL_MIN..CHI2): scipy's closed-form _ppf bodies, one
+//              expression each (closed_ppf01), with rv_continuous.ppf's edges: q == 0 / 1 give
+//              the support ends, invalid shapes or scale <= 0 give NaN; chi2 = 2 igami(df / 2, q)
 // Parity is to floating-point tolerance (1e-10 relative; discrete outputs exact): scipy's
 // beta / binom bodies are Boost's and log_ndtr is Faddeeva's, so the restatements here are
 // accurate to a few ulp of the exact function, not bit copies.  FP64-VALU bound.
@@ -31,6 +34,74 @@ struct Params4 {
   __device__ __forceinline__ double at(int j, int64_t i) const { return ptr[j] ? ptr[j][i] : val[j]; }
 };
 
+constexpr bool is_closed(int d) { return d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_CHI2; }
+
+constexpr int closed_shapes(int d) {
+  return d == PBH_DIST_LOGUNIFORM ? 2
+         : (d == PBH_DIST_WEIBULL_MIN || d == PBH_DIST_WEIBULL_MAX || d == PBH_DIST_PARETO || d == PBH_DIST_LOMAX ||
+            d == PBH_DIST_GENEXTREME || d == PBH_DIST_GOMPERTZ || d == PBH_DIST_CHI2)
+             ? 1
+             : 0;
+}
+
+// _argcheck and the support [_a, _b] of scipy's class (rv_continuous default: every shape > 0)
+template <int D>
+__device__ __forceinline__ bool closed_support(double s0, double s1, double& lo, double& hi) {
+  constexpr double inf = sf::kInf;
+  lo = -inf;
+  hi = inf;
+  if constexpr (D == PBH_DIST_WEIBULL_MIN || D == PBH_DIST_RAYLEIGH || D == PBH_DIST_LOMAX ||
+                D == PBH_DIST_GOMPERTZ || D == PBH_DIST_CHI2)
+    lo = 0.0;
+  if constexpr (D == PBH_DIST_WEIBULL_MAX) hi = 0.0;
+  if constexpr (D == PBH_DIST_PARETO) lo = 1.0;
+  if constexpr (D == PBH_DIST_LOGUNIFORM) {  // loguniform._get_support = (a, b), _argcheck a > 0, b > a
+    lo = s0;
+    hi = s1;
+    return s0 > 0.0 && s1 > s0;
+  }
+  if constexpr (D == PBH_DIST_GENEXTREME) {  // _argcheck isfinite(c); support from the sign of c
+    constexpr double tiny = 2.2250738585072014e-308;  // np.finfo(float).tiny
+    if (s0 > 0.0) hi = 1.0 / fmax(s0, tiny);
+    if (s0 < 0.0) lo = 1.0 / fmin(s0, -tiny);
+    return isfinite(s0);
+  }
+  if constexpr (closed_shapes(D) == 1) return s0 > 0.0;
+  return true;
+}
+
+// scipy _ppf for 0 < q < 1
+template <int D>
+__device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
+  if constexpr (D == PBH_DIST_WEIBULL_MIN) return pow(-log1p(-q), 1.0 / s0);
+  if constexpr (D == PBH_DIST_WEIBULL_MAX) return -pow(-log(q), 1.0 / s0);
+  if constexpr (D == PBH_DIST_LOGISTIC) {  // scipy special logit: log1p form on [0.3, 0.65]
+    if (q < 0.3 || q > 0.65) return log(q / (1.0 - q));
+    const double s = 2.0 * (q - 0.5);
+    return log1p(s) - log1p(-s);
+  }
+  if constexpr (D == PBH_DIST_CAUCHY) {  // Boost cauchy quantile: P in (-0.5, 0.5], -1 / tan(pi P)
+    double p = q - floor(q);
+    if (p > 0.5) p = p - 1.0;
+    if (p == 0.5) return 0.0;
+    return -1.0 / tan(sf::kPi * p);
+  }
+  if constexpr (D == PBH_DIST_LAPLACE) return q > 0.5 ? -log(2.0 * (1.0 - q)) : log(2.0 * q);
+  if constexpr (D == PBH_DIST_GUMBEL_R) return -log(-log(q));
+  if constexpr (D == PBH_DIST_GUMBEL_L) return log(-log1p(-q));
+  if constexpr (D == PBH_DIST_PARETO) return pow(1.0 - q, -1.0 / s0);
+  if constexpr (D == PBH_DIST_LOGUNIFORM) return exp(log(s0) + q * (log(s1) - log(s0)));
+  if constexpr (D == PBH_DIST_RAYLEIGH) return sqrt(-2.0 * log1p(-q));
+  if constexpr (D == PBH_DIST_LOMAX) return expm1(-log1p(-q) / s0);
+  if constexpr (D == PBH_DIST_GENEXTREME) {
+    const double x = -log(-log(q));
+    return (x == x && s0 != 0.0) ? -expm1(-s0 * x) / s0 : x;
+  }
+  if constexpr (D == PBH_DIST_GOMPERTZ) return log1p(-1.0 / s0 * log1p(-q));
+  if constexpr (D == PBH_DIST_CHI2) return 2.0 * sf::igami(s0 / 2.0, q);
+  return sf::kNaN;
+}
+
 template <int D>
 __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_t i) {
   constexpr double inf = sf::kInf, nan = sf::kNaN;
@@ -43,6 +114,16 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
     if (!ok || !(q >= 0.0 && q <= 1.0)) return nan;
     if (q == 1.0) return n + loc;
     return sfx::binom_ppf01(q, n, pp) + loc;
+  } else if constexpr (is_closed(D)) {
+    constexpr int S = closed_shapes(D);
+    const double s0 = S > 0 ? p.at(0, i) : 0.0, s1 = S > 1 ? p.at(1, i) : 0.0;
+    const double loc = p.at(S, i), scale = p.at(S + 1, i);
+    double lo, hi;
+    const bool ok = closed_support<D>(s0, s1, lo, hi) && scale > 0.0 && loc == loc;
+    if (!ok || !(q >= 0.0 && q <= 1.0)) return nan;
+    if (q == 0.0) return lo * scale + loc;
+    if (q == 1.0) return hi * scale + loc;
+    return closed_ppf01<D>(q, s0, s1) * scale + loc;
   } else {
     const double a = p.at(0, i), b = p.at(1, i), loc = p.at(2, i), scale = p.at(3, i);
     bool ok = scale > 0.0 && loc == loc;
@@ -91,7 +172,10 @@ __global__ __launch_bounds__(256) void k_lhs_column(uint64_t seed, int64_t n, in
 
 int ppf_ext(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_param* params, int nparams, double* out,
             int32_t* flag, hipStream_t s) {
-  const int want = dist == PBH_DIST_BERNOULLI ? 2 : (dist == PBH_DIST_BINOM ? 3 : 4);
+  const int want = dist == PBH_DIST_BERNOULLI ? 2
+                   : dist == PBH_DIST_BINOM   ? 3
+                   : is_closed(dist)          ? closed_shapes(dist) + 2
+                                              : 4;
   PBH_REQUIRE(nparams == want && params, "ppf: distribution %d takes %d parameters, got %d", dist, want, nparams);
   Params4 prm{};
   for (int j = 0; j < nparams; ++j) {
@@ -114,6 +198,62 @@ int ppf_ext(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_pa
     case PBH_DIST_BERNOULLI:
       PBH_TIMED(kKPpf, s,
                 hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_BERNOULLI>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_WEIBULL_MIN:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_WEIBULL_MIN>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_WEIBULL_MAX:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_WEIBULL_MAX>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_LOGISTIC:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_LOGISTIC>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_CAUCHY:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_CAUCHY>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_LAPLACE:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_LAPLACE>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_GUMBEL_R:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_GUMBEL_R>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_GUMBEL_L:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_GUMBEL_L>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_PARETO:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_PARETO>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_LOGUNIFORM:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_LOGUNIFORM>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_RAYLEIGH:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_RAYLEIGH>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_LOMAX:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_LOMAX>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_GENEXTREME:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_GENEXTREME>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_GOMPERTZ:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_GOMPERTZ>, g, b, 0, s, q, q_stride, n, prm, out, flag));
+      break;
+    case PBH_DIST_CHI2:
+      PBH_TIMED(kKPpf, s,
+                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_CHI2>, g, b, 0, s, q, q_stride, n, prm, out, flag));
       break;
     default:
       set_error("ppf: unknown distribution id %d", dist);

@@ -589,7 +589,10 @@ class AbstractDistribution(Node, OverloadMixin, abc.ABC):
 # then loc (and scale for continuous ones) -- scipy's rv_generic._parse_args.
 _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "triang": ("c",),
                 "gamma": ("a",), "poisson": ("mu",), "beta": ("a", "b"), "truncnorm": ("a", "b"),
-                "binom": ("n", "p"), "bernoulli": ("p",)}
+                "binom": ("n", "p"), "bernoulli": ("p",), "weibull_min": ("c",), "weibull_max": ("c",),
+                "logistic": (), "cauchy": (), "laplace": (), "gumbel_r": (), "gumbel_l": (), "pareto": ("b",),
+                "loguniform": ("a", "b"), "reciprocal": ("a", "b"), "rayleigh": (), "lomax": ("c",),
+                "genextreme": ("c",), "gompertz": ("c",), "chi2": ("df",)}
 _DISCRETE = {"poisson", "binom", "bernoulli"}
 # distributions with a fused native-LHS + inverse-CDF kernel (and the Iman-Conover fast path)
 _FUSED_LHS = {"norm", "uniform", "expon", "lognorm", "triang", "gamma", "poisson"}
