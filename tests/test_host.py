@@ -110,6 +110,25 @@ def test_scipy_parameter_parsing():
         _parse_scipy_args("norm", (1,), {"loc": 1})
 
 
+def test_distribution_table_matches_header_and_scipy():
+    """Every supported name: an id in include/probabilit_hip.h's pbh_dist enum, and scipy's own
+    shape names in scipy's order (the reference's getattr(stats, distr), modeling.py:805-807)."""
+    import re
+
+    import scipy.stats
+
+    from probabilit_amd import _lib
+    from probabilit_amd.modeling import _DIST_SHAPES
+
+    text = open(f"{ROOT}/include/probabilit_hip.h").read()
+    enum = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"PBH_DIST_(\w+) = (\d+)", text)}
+    for name, shapes in _DIST_SHAPES.items():
+        assert _lib.DIST_IDS[name] == enum.get(name, enum.get("loguniform") if name == "reciprocal" else None), name
+        sc = getattr(scipy.stats, name).shapes
+        assert (tuple(x.strip() for x in sc.split(",")) if sc else ()) == shapes, name
+    assert sorted(set(_lib.DIST_IDS.values())) == sorted(enum.values())
+
+
 def test_numpy_result_dtypes():
     from probabilit_amd.modeling import _canonical, _numpy_result
 
