@@ -540,7 +540,8 @@ __global__ void k_transform_matrix(const double* __restrict__ L, const double* _
 // AM_ROWS rows per wave tile: 32 (default: 148 registers with the prefetch and 46 KiB of LDS, 3
 // waves per SIMD; each store instruction writes two columns' 256-byte halves) or 64
 // (PBH_APPLY_ROWS=64: 218 registers and 80 KiB, 2 waves per SIMD)
-template <int AM_ROWS>
+// NT: non-temporal loads of S and stores of CS and the codes (PBH_APPLY_NT=1; streaming, no reuse)
+template <int AM_ROWS, bool NT = false>
 __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int64_t n, int k, int64_t ld,
                                                    const double* __restrict__ M, uint32_t* __restrict__ codes,
                                                    int64_t ldc, CodeMap cm) {
@@ -575,7 +576,9 @@ __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int6
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const int c = 4 * s + q;
-        pa[rb][s] = (tw < tiles && c < k && r < n) ? S[(int64_t)c * ld + r] : 0.0;
+        pa[rb][s] = (tw < tiles && c < k && r < n)
+                        ? (NT ? __builtin_nontemporal_load(&S[(int64_t)c * ld + r]) : S[(int64_t)c * ld + r])
+                        : 0.0;
       }
     }
   };
@@ -608,8 +611,13 @@ __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int6
     if (tw < tiles && r < n) {
       for (int c = c0; c < k; c += 64 / AM_ROWS) {
         const double v = tl[rl * 33 + c];
-        S[(int64_t)c * ld + r] = v;
-        if (codes) codes[(int64_t)c * ldc + r] = code_of(v, cm);
+        if constexpr (NT) {
+          __builtin_nontemporal_store(v, &S[(int64_t)c * ld + r]);
+          if (codes) __builtin_nontemporal_store(code_of(v, cm), &codes[(int64_t)c * ldc + r]);
+        } else {
+          S[(int64_t)c * ld + r] = v;
+          if (codes) codes[(int64_t)c * ldc + r] = code_of(v, cm);
+        }
       }
     }
     __syncthreads();
@@ -752,7 +760,15 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
     }();
     const int64_t tiles = (n + rows - 1) / rows;
     const unsigned gb = (unsigned)((tiles + 3) / 4 < 8192 ? (tiles + 3) / 4 : 8192);
-    if (rows == 32)
+    static const bool nt = [] {
+      const char* e = getenv("PBH_APPLY_NT");
+      return e && atoi(e) == 1;
+    }();
+    if (rows == 32 && nt)
+      PBH_TIMED(kKApply, s,
+                hipLaunchKernelGGL((k_apply_mfma<32, true>), dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc,
+                                   c));
+    else if (rows == 32)
       PBH_TIMED(kKApply, s,
                 hipLaunchKernelGGL(k_apply_mfma<32>, dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc, c));
     else
