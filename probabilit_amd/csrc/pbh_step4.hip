@@ -1648,8 +1648,13 @@ int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs,
   // >= 64 K codes per block and at most 64 blocks per column: every block flushes its non-empty
   // counters with global atomics (~64 K each), which the PMC pass counted as ~2 GB of writes at
   // 256 blocks per column (pmc_traffic_r72_ck1.json)
+  static const int64_t cap = [] {  // PBH_HIST_BLOCKS: blocks per column (fewer: fewer flush atomics)
+    const char* e = getenv("PBH_HIST_BLOCKS");
+    const int64_t v = e ? atoll(e) : 64;
+    return v >= 8 && v <= 256 ? v : 64;
+  }();
   int64_t blocks = (n + 65535) / 65536;
-  if (blocks > 64) blocks = 64;
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   if (blocks >= 8) blocks &= ~(int64_t)7;  // k_hist16c: 8 tile classes
   if (blocks % 8 == 0 && hist_class_major())
