@@ -624,6 +624,96 @@ __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int6
   }
 }
 
+// Paired-row variant (PBH_APPLY_W2=1): 32-row wave tiles as in k_apply_mfma<32>, but each lane
+// loads and stores two consecutive rows of a column with one 16-byte access (codes: 8 bytes), so
+// a tile takes half the memory instructions.  The even rows of the tile feed the first 16-row
+// MFMA block and the odd rows the second; the LDS transpose puts them back in row order.
+// Needs ld, ldc even and S / codes 16- / 8-byte aligned (checked on the host).
+__global__ __launch_bounds__(256) void k_apply_mfma_w2(double* __restrict__ S, int64_t n, int k, int64_t ld,
+                                                       const double* __restrict__ M, uint32_t* __restrict__ codes,
+                                                       int64_t ldc, CodeMap cm) {
+  constexpr int R = 32;
+  __shared__ double tile[4][R * 33];
+  __shared__ uint32_t cbase[kCodeSegments + 1];
+  __shared__ double cscale[kCodeSegments];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* tl = tile[w];
+  if (codes) {
+    for (int j = threadIdx.x; j <= cm.m; j += 256) cbase[j] = cm.base[j];
+    for (int j = threadIdx.x; j < cm.m; j += 256) cscale[j] = cm.scale[j];
+    cm.base = cbase;
+    cm.scale = cscale;
+  }
+  __syncthreads();
+  const int q = lane >> 4, m16 = lane & 15;
+  double b[8][2];
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int J = 0; J < 2; ++J) b[s][J] = M[(4 * s + q) * 32 + 16 * J + m16];
+  const int64_t tiles = (n + R - 1) / R;
+  double pa[2][8];  // [row parity][s]: rows r0 + 2 m16 (+1) of column 4 s + q
+  auto load = [&](int64_t bt) {
+    const int64_t tw = bt * 4 + w;
+    const int64_t r = tw * R + 2 * m16;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int c = 4 * s + q;
+      double2 v = {0.0, 0.0};
+      if (tw < tiles && c < k) {
+        const double* src = &S[(int64_t)c * ld + r];
+        if (r + 1 < n) {
+          v = *(const double2*)src;
+        } else if (r < n) {
+          v.x = src[0];
+        }
+      }
+      pa[0][s] = v.x;
+      pa[1][s] = v.y;
+    }
+  };
+  if ((int64_t)blockIdx.x * 4 < tiles) load(blockIdx.x);
+  for (int64_t bt = blockIdx.x; bt * 4 < tiles; bt += gridDim.x) {
+    const int64_t tw = bt * 4 + w;
+    const int64_t r0 = tw * R;
+    if (tw < tiles) {
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        f64x4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[par][s], b[s][0], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[par][s], b[s][1], c1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = 2 * (q + 4 * g) + par;  // MFMA row i = q + 4 g is tile row 2 i + parity
+          tl[row * 33 + m16] = c0[g];
+          tl[row * 33 + 16 + m16] = c1[g];
+        }
+      }
+    }
+    if ((bt + gridDim.x) * 4 < tiles) load(bt + gridDim.x);
+    __syncthreads();
+    const int rp = lane & 15, c0 = lane >> 4;  // rows 2 rp, 2 rp + 1; first column
+    const int64_t r = r0 + 2 * rp;
+    if (tw < tiles && r < n) {
+      for (int c = c0; c < k; c += 4) {
+        const double v0 = tl[(2 * rp) * 33 + c], v1 = tl[(2 * rp + 1) * 33 + c];
+        double* dst = &S[(int64_t)c * ld + r];
+        if (r + 1 < n) {
+          *(double2*)dst = double2{v0, v1};
+          if (codes) *(uint2*)&codes[(int64_t)c * ldc + r] = uint2{code_of(v0, cm), code_of(v1, cm)};
+        } else {
+          dst[0] = v0;
+          if (codes) codes[(int64_t)c * ldc + r] = code_of(v0, cm);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 size_t tie_workspace_bytes(int64_t n) {
@@ -764,7 +854,16 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
       const char* e = getenv("PBH_APPLY_NT");
       return e && atoi(e) == 1;
     }();
-    if (rows == 32 && nt)
+    static const bool w2 = [] {
+      const char* e = getenv("PBH_APPLY_W2");
+      return e && atoi(e) == 1;
+    }();
+    const bool w2_ok = w2 && rows == 32 && ld % 2 == 0 && ((uintptr_t)S & 15) == 0 &&
+                       (!codes || (ldc % 2 == 0 && ((uintptr_t)codes & 7) == 0));
+    if (w2_ok)
+      PBH_TIMED(kKApply, s,
+                hipLaunchKernelGGL(k_apply_mfma_w2, dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc, c));
+    else if (rows == 32 && nt)
       PBH_TIMED(kKApply, s,
                 hipLaunchKernelGGL((k_apply_mfma<32, true>), dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc,
                                    c));
