@@ -162,3 +162,27 @@ def test_closed_form_composite_and_sample(gpu):
     ref_b = scipy.stats.weibull_min(c=scipy.stats.uniform(loc=1, scale=2).ppf(qq[:, 0])).ppf(qq[:, 1])
     ok_a = np.allclose(s, ref_a, rtol=1e-10, atol=1e-13)
     assert ok_a or np.allclose(s, ref_b, rtol=1e-10, atol=1e-13)
+
+
+def test_closed_form_correlated_iman_conover(gpu):
+    """Closed-form distributions under ImanConover through Node.sample (modeling.py:571-583): the
+    correlated samples equal the oracle's Iman-Conover (correlation.py:388-425 restated) applied to
+    the same graph's uncorrelated samples (same random_state, same column assignment)."""
+    from oracle.ic import iman_conover
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.modeling import NoOp
+
+    C = np.array([[1.0, 0.5, -0.3], [0.5, 1.0, 0.2], [-0.3, 0.2, 1.0]])
+
+    def graph():
+        ds = [D("weibull_min", c=1.5), D("logistic", loc=2.0), D("gumbel_r", scale=0.5)]
+        return ds, NoOp(*ds)
+
+    n = 20_000
+    ds, sink = graph()
+    sink.sample(n, random_state=11)
+    X = np.column_stack([d.samples_ for d in ds])
+    ds, sink = graph()
+    sink.correlate(*ds, corr_mat=C).sample(n, random_state=11)
+    Y = np.column_stack([d.samples_ for d in ds])
+    assert_close(Y, iman_conover(X, C)["Y"], rtol=1e-12, what="closed-form Iman-Conover")
