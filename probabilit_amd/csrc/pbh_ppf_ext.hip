@@ -150,28 +150,66 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(256) void k_ppf_ext(const double* __restrict__ q, int64_t q_stride, int64_t n, Params4 prm,
-                                                 double* __restrict__ out, int32_t* flag) {
+// one kernel for the swept column (q[i * q_stride]) and the fused native-LHS column (LHS: the
+// quantile of row row0 + i generated in registers, 8 B per draw instead of 16)
+struct LhsCol {
+  uint64_t seed;
+  int64_t n, row0;
+  uint32_t col;
+};
+
+template <int D, bool LHS>
+__global__ __launch_bounds__(256) void k_ppf_ext(const double* __restrict__ q, int64_t q_stride, LhsCol lc, int64_t n,
+                                                 Params4 prm, double* __restrict__ out, int32_t* flag) {
+  Philox ph(lc.seed);
+  FeistelPerm fp(ph, (uint64_t)(LHS ? lc.n : 1), lc.col);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const double x = ppf_ext_one<D>(q[i * q_stride], prm, i);
+    const double qi = LHS ? lhs_quantile(ph, fp, (uint64_t)(lc.row0 + i), lc.col) : q[i * q_stride];
+    const double x = ppf_ext_one<D>(qi, prm, i);
     out[i] = x;
     flag_nonfinite(flag, !isfinite(x));
   }
 }
 
-__global__ __launch_bounds__(256) void k_lhs_column(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, uint32_t col,
-                                                    double* __restrict__ q) {
-  Philox ph(seed);
-  FeistelPerm fp(ph, (uint64_t)n, col);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * 256)
-    q[i] = lhs_quantile(ph, fp, (uint64_t)(row0 + i), col);
+template <int D>
+struct DistTag {
+  static constexpr int value = D;
+};
+
+// f(DistTag<D>{}) for the distribution ids handled here; false for any other id
+template <class F>
+bool dispatch_ext(int dist, F&& f) {
+  switch (dist) {
+#define PBH_EXT(D) \
+  case D:          \
+    f(DistTag<D>{}); \
+    return true;
+    PBH_EXT(PBH_DIST_BETA)
+    PBH_EXT(PBH_DIST_TRUNCNORM)
+    PBH_EXT(PBH_DIST_BINOM)
+    PBH_EXT(PBH_DIST_BERNOULLI)
+    PBH_EXT(PBH_DIST_WEIBULL_MIN)
+    PBH_EXT(PBH_DIST_WEIBULL_MAX)
+    PBH_EXT(PBH_DIST_LOGISTIC)
+    PBH_EXT(PBH_DIST_CAUCHY)
+    PBH_EXT(PBH_DIST_LAPLACE)
+    PBH_EXT(PBH_DIST_GUMBEL_R)
+    PBH_EXT(PBH_DIST_GUMBEL_L)
+    PBH_EXT(PBH_DIST_PARETO)
+    PBH_EXT(PBH_DIST_LOGUNIFORM)
+    PBH_EXT(PBH_DIST_RAYLEIGH)
+    PBH_EXT(PBH_DIST_LOMAX)
+    PBH_EXT(PBH_DIST_GENEXTREME)
+    PBH_EXT(PBH_DIST_GOMPERTZ)
+    PBH_EXT(PBH_DIST_CHI2)
+#undef PBH_EXT
+    default:
+      return false;
+  }
 }
 
-}  // namespace
-
-int ppf_ext(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_param* params, int nparams, double* out,
-            int32_t* flag, hipStream_t s) {
+int launch_ext(int dist, const double* q, int64_t q_stride, const LhsCol* lc, int64_t n, const pbh_param* params,
+               int nparams, double* out, int32_t* flag, hipStream_t s) {
   const int want = dist == PBH_DIST_BERNOULLI ? 2
                    : dist == PBH_DIST_BINOM   ? 3
                    : is_closed(dist)          ? closed_shapes(dist) + 2
@@ -184,97 +222,34 @@ int ppf_ext(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_pa
   }
   if (n == 0) return PBH_OK;
   dim3 g(grid_for(n, 256, 16384)), b(256);
-  switch (dist) {
-    case PBH_DIST_BETA:
-      PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_BETA>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_TRUNCNORM:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_TRUNCNORM>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_BINOM:
-      PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_BINOM>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_BERNOULLI:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_BERNOULLI>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_WEIBULL_MIN:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_WEIBULL_MIN>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_WEIBULL_MAX:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_WEIBULL_MAX>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_LOGISTIC:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_LOGISTIC>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_CAUCHY:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_CAUCHY>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_LAPLACE:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_LAPLACE>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_GUMBEL_R:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_GUMBEL_R>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_GUMBEL_L:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_GUMBEL_L>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_PARETO:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_PARETO>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_LOGUNIFORM:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_LOGUNIFORM>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_RAYLEIGH:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_RAYLEIGH>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_LOMAX:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_LOMAX>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_GENEXTREME:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_GENEXTREME>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_GOMPERTZ:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_GOMPERTZ>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    case PBH_DIST_CHI2:
-      PBH_TIMED(kKPpf, s,
-                hipLaunchKernelGGL(k_ppf_ext<PBH_DIST_CHI2>, g, b, 0, s, q, q_stride, n, prm, out, flag));
-      break;
-    default:
-      set_error("ppf: unknown distribution id %d", dist);
-      return PBH_ERR_UNSUPPORTED;
+  const LhsCol l = lc ? *lc : LhsCol{0, 1, 0, 0};
+  const bool known = dispatch_ext(dist, [&](auto tag) {
+    constexpr int D = decltype(tag)::value;
+    if (lc)
+      PBH_TIMED(kKLhsPpf, s, hipLaunchKernelGGL((k_ppf_ext<D, true>), g, b, 0, s, q, q_stride, l, n, prm, out, flag));
+    else
+      PBH_TIMED(kKPpf, s, hipLaunchKernelGGL((k_ppf_ext<D, false>), g, b, 0, s, q, q_stride, l, n, prm, out, flag));
+  });
+  if (!known) {
+    set_error("ppf: unknown distribution id %d", dist);
+    return PBH_ERR_UNSUPPORTED;
   }
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
 
-// Fused-LHS entry for these distributions: the native LHS column is written to a stream-ordered
-// temporary, then swept (16 B per draw instead of 8).
+}  // namespace
+
+int ppf_ext(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_param* params, int nparams, double* out,
+            int32_t* flag, hipStream_t s) {
+  return launch_ext(dist, q, q_stride, nullptr, n, params, nparams, out, flag, s);
+}
+
+// Fused-LHS entry for these distributions: the native LHS quantile is generated in the ppf kernel
 int lhs_ppf_ext(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col, int dist, const pbh_param* params,
                 int nparams, double* out, int32_t* flag, hipStream_t s) {
-  double* q = nullptr;
-  PBH_CHECK_HIP(hipMallocAsync((void**)&q, (size_t)nrows * 8, s));
-  hipLaunchKernelGGL(k_lhs_column, dim3(grid_for(nrows, 256, 16384)), dim3(256), 0, s, seed, n, row0, nrows,
-                     (uint32_t)col, q);
-  PBH_CHECK_LAUNCH();
-  int st = ppf_ext(dist, q, 1, nrows, params, nparams, out, flag, s);
-  PBH_CHECK_HIP(hipFreeAsync(q, s));
-  return st;
+  const LhsCol lc{seed, n, row0, (uint32_t)col};
+  return launch_ext(dist, nullptr, 0, &lc, nrows, params, nparams, out, flag, s);
 }
 
 }  // namespace pbh

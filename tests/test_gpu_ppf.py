@@ -104,15 +104,21 @@ def test_ppf_random_sweep(gpu, name, kw):
 
 
 def test_fused_lhs_ppf_equals_two_pass(gpu):
-    """pbh_lhs_ppf (q never stored) is bit-identical to pbh_fill_lhs + pbh_ppf."""
+    """pbh_lhs_ppf (q never stored) is bit-identical to pbh_fill_lhs + pbh_ppf, for the base
+    set and the pbh_ppf_ext distributions (the LHS quantile generated inside k_ppf_ext), with a
+    row offset too."""
     from probabilit_amd import native
 
     n = 100_003
-    for col, (name, kw) in enumerate([("norm", {}), ("gamma", {"a": 2.0}), ("poisson", {"mu": 4.0})]):
+    for col, (name, kw) in enumerate([("norm", {}), ("gamma", {"a": 2.0}), ("poisson", {"mu": 4.0}),
+                                      ("beta", {"a": 3.4, "b": 2.6}), ("binom", {"n": 20, "p": 0.3}),
+                                      ("weibull_min", {"c": 1.5}), ("loguniform", {"a": 0.5, "b": 8.0}),
+                                      ("chi2", {"df": 3.0})]):
         fused = native.lhs_ppf(name, 1234, n, col, **kw)
         q = native.fill_lhs(1234, n, col + 1)[:, col]
         two = native.ppf(name, q, **kw)
         np.testing.assert_array_equal(fused, two)
+        np.testing.assert_array_equal(native.lhs_ppf(name, 1234, n, col, row0=777, nrows=5000, **kw), two[777:5777])
 
 
 def test_ppf_empty_and_nan(gpu):
