@@ -157,11 +157,10 @@ def test_closed_form_composite_and_sample(gpu):
                      rtol=1e-10, atol=1e-13, what=f"Node.sample {name}")
     s = D("weibull_min", c=D("uniform", loc=1, scale=2)).sample(2000, random_state=4)
     qq = np.random.RandomState(4).random((2000, 2))
-    # column order: the reference numbers distribution nodes in its own traversal order
-    ref_a = scipy.stats.weibull_min(c=scipy.stats.uniform(loc=1, scale=2).ppf(qq[:, 1])).ppf(qq[:, 0])
-    ref_b = scipy.stats.weibull_min(c=scipy.stats.uniform(loc=1, scale=2).ppf(qq[:, 0])).ppf(qq[:, 1])
-    ok_a = np.allclose(s, ref_a, rtol=1e-10, atol=1e-13)
-    assert ok_a or np.allclose(s, ref_b, rtol=1e-10, atol=1e-13)
+    # column order: ISNs take quantile columns in _id order, so the parameter
+    # node uniform (created first) takes column 0 and weibull_min column 1
+    ref = scipy.stats.weibull_min(c=scipy.stats.uniform(loc=1, scale=2).ppf(qq[:, 0])).ppf(qq[:, 1])
+    assert_close(s, ref, rtol=1e-10, atol=1e-13, what="composite weibull_min column order")
 
 
 def test_closed_form_correlated_iman_conover(gpu):
@@ -186,3 +185,61 @@ def test_closed_form_correlated_iman_conover(gpu):
     sink.correlate(*ds, corr_mat=C).sample(n, random_state=11)
     Y = np.column_stack([d.samples_ for d in ds])
     assert_close(Y, iman_conover(X, C)["Y"], rtol=1e-12, what="closed-form Iman-Conover")
+
+
+# the fused native-LHS inverse CDF of the extended distributions (pbh_lhs_ppf -> k_ppf_ext with
+# the generator inside the kernel): Node.sample(method="lhs") and row-offset windows against
+# scipy's ppf on the same native-LHS quantiles (native.fill_lhs, the two-pass form)
+_LHS_EXT = [("beta", dict(a=3.4, b=2.6, loc=0, scale=10)), ("beta", dict(a=0.5, b=0.5)),
+            ("beta", dict(a=7.0, b=5.0, loc=-1.0, scale=3.0)), ("truncnorm", dict(a=-1.0, b=1.0, loc=2.0, scale=0.5)),
+            ("truncnorm", dict(a=3.0, b=3.3)), ("binom", dict(n=20, p=0.3)), ("binom", dict(n=1000, p=0.7, loc=2)),
+            ("bernoulli", dict(p=0.25))] + [c for c in _CLOSED[:30]]
+
+
+@pytest.mark.parametrize("name,kw", _LHS_EXT)
+def test_fused_lhs_ext_vs_scipy(gpu, name, kw):
+    import scipy.stats
+
+    from probabilit_amd import native
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.qmc import seed_from
+
+    n, s = 40_000, 21
+    q = native.fill_lhs(seed_from(s), n, 1)[:, 0]
+    with np.errstate(all="ignore"):
+        ref = getattr(scipy.stats, name)(**kw).ppf(q)
+    got = D(name, **kw).sample(n, method="lhs", random_state=s)
+    if name in ("binom", "bernoulli"):
+        np.testing.assert_array_equal(got, ref)
+    else:
+        assert_close(got, ref, rtol=1e-10, atol=1e-13, what=f"LHS {name} {kw}")
+    # a window [row0, row0 + rows) of a 3-column design, column 2
+    row0, rows = 12_345, 9_999
+    q3 = native.fill_lhs(77, n, 3, row0=row0, nrows=rows)[:, 2]
+    with np.errstate(all="ignore"):
+        ref3 = getattr(scipy.stats, name)(**kw).ppf(q3)
+    got3 = native.lhs_ppf(name, 77, n, 2, row0=row0, nrows=rows, **kw)
+    if name in ("binom", "bernoulli"):
+        np.testing.assert_array_equal(got3, ref3)
+    else:
+        assert_close(got3, ref3, rtol=1e-10, atol=1e-13, what=f"LHS window {name} {kw}")
+
+
+def test_fused_lhs_pert_composite(gpu):
+    """PERT (the reference's headline constructor, distributions.py:78-94 -> beta) with a
+    composite mode under method="lhs": parameters per row, ISN columns in _id order."""
+    import scipy.stats
+
+    from probabilit_amd import distributions as dists
+    from probabilit_amd import native
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.qmc import seed_from
+
+    n, s = 30_000, 5
+    x = dists.PERT(0, 6, 10).sample(n, method="lhs", random_state=s)
+    q = native.fill_lhs(seed_from(s), n, 1)[:, 0]
+    assert_close(x, scipy.stats.beta(a=3.4, b=2.6, loc=0, scale=10).ppf(q), what="PERT LHS")
+    y = D("beta", a=D("uniform", loc=1, scale=3), b=2.0).sample(n, method="lhs", random_state=s)
+    q2 = native.fill_lhs(seed_from(s), n, 2)
+    a = scipy.stats.uniform(loc=1, scale=3).ppf(q2[:, 0])
+    assert_close(y, scipy.stats.beta(a=a, b=2.0).ppf(q2[:, 1]), what="composite beta LHS")

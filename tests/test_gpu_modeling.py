@@ -189,8 +189,9 @@ def test_non_finite_raises(gpu):
 def test_unsupported_distribution_fails_loudly(gpu):
     from probabilit_amd.modeling import Distribution
 
-    with pytest.raises(NotImplementedError):
-        Distribution("weibull_min", c=2).sample(10, random_state=0)
+    # a scipy name with no device kernel: the message names the supported set
+    with pytest.raises(NotImplementedError, match=r"no native inverse-CDF kernel.*'weibull_min'"):
+        Distribution("johnsonsu", a=1.0, b=2.0).sample(10, random_state=0)
     with pytest.raises(AttributeError):
         Distribution("no_such_distribution").sample(10, random_state=0)
 
