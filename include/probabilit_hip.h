@@ -194,7 +194,7 @@ typedef struct pbh_ic_column {
   uint64_t seed;
   int32_t lhs_col;
   int32_t dist;
-  double params[3];
+  double params[4];
   int32_t nparams;
   int32_t* nonfinite_flag;
 } pbh_ic_column;

@@ -76,7 +76,7 @@ class Operand(ctypes.Structure):
 
 class ICColumn(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("lhs_col", ctypes.c_int32), ("dist", ctypes.c_int32),
-                ("params", ctypes.c_double * 3), ("nparams", ctypes.c_int32), ("nonfinite_flag", ctypes.c_void_p)]
+                ("params", ctypes.c_double * 4), ("nparams", ctypes.c_int32), ("nonfinite_flag", ctypes.c_void_p)]
 
 
 class ICArgs(ctypes.Structure):

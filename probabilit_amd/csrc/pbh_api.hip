@@ -343,18 +343,18 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     return r;
   };
   if (a->columns && defer)
-    for (int c = 0; c < k; ++c) any_deferred |= (deferred[c] = a->columns[c].dist != PBH_DIST_POISSON) != 0;
+    for (int c = 0; c < k; ++c) any_deferred |= (deferred[c] = !gen_discrete(a->columns[c].dist)) != 0;
   if (a->columns) {
     for (int c = 0; c < k; ++c) {
       const pbh_ic_column& g = a->columns[c];
-      pbh_param prm[3];
-      for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
+      pbh_param prm[4];
+      for (int j = 0; j < 4; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
       st = gen_create(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, &gens.g[c], s);
       if (st) return st;
       if (deferred[c]) continue;  // counted next to steps 1-3 (below)
       // run heads only for a discrete column (few runs); a continuous one ties rarely, if ever,
       // and would append every stratum
-      const bool discrete = g.dist == PBH_DIST_POISSON;
+      const bool discrete = gen_discrete(g.dist);
       st = gen_sorted(gens.g[c], 0, n, nullptr, g.nonfinite_flag, L.counts + 2 * c, s,
                       discrete ? L.heads_all + (int64_t)c * kHeadsCap : nullptr, discrete ? L.hcur + c : nullptr,
                       discrete ? kHeadsCap : 0);
@@ -373,8 +373,8 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     if (a->columns) {
       // generated LHS column: sorted order straight from the inverse permutation
       const pbh_ic_column& g = a->columns[c];
-      pbh_param prm[3];
-      for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
+      pbh_param prm[4];
+      for (int j = 0; j < 4; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
       const unsigned long long* cnt = cnt_host.data() + 2 * c;
       if (cnt[1] == 0) {
         uint32_t* heads = nullptr;
@@ -386,7 +386,7 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
             const int64_t v = e ? atoll(e) : kHeadsCap;
             return v < 1 ? 1 : (v > kHeadsCap ? (int64_t)kHeadsCap : v);
           }();
-          if (a->columns[c].dist == PBH_DIST_POISSON && nheads <= cap) {  // appended heads, put in order
+          if (gen_discrete(a->columns[c].dist) && nheads <= cap) {  // appended heads, put in order
             heads = L.heads_all + (int64_t)c * kHeadsCap;
             st = sort_heads(heads, nheads, s);
           } else {  // too many distinct values for the list: from the materialised column
@@ -713,8 +713,8 @@ extern "C" int pbh_ic_owned_create(const pbh_ic_column* columns, int32_t m, int6
   int st = reorder_carve(lay.reorder, n, h->rw, s);
   for (int i = 0; st == PBH_OK && i < m; ++i) {
     const pbh_ic_column& g = columns[i];
-    pbh_param prm[3];
-    for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
+    pbh_param prm[4];
+    for (int j = 0; j < 4; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
     st = gen_create(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, &h->gens[i], s);
   }
   if (st == PBH_OK) {

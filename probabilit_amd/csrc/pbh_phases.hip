@@ -175,9 +175,9 @@ using namespace pbh;
 extern "C" int pbh_lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist,
                                   const double* params_host, int nparams, double* out, int32_t* nonfinite_flag,
                                   void* stream) {
-  PBH_REQUIRE(out != nullptr && nparams >= 0 && nparams <= 3 && (nparams == 0 || params_host),
+  PBH_REQUIRE(out != nullptr && nparams >= 0 && nparams <= 4 && (nparams == 0 || params_host),
               "pbh_lhs_sorted_ppf: bad arguments");
-  pbh_param prm[3];
+  pbh_param prm[4];
   for (int j = 0; j < nparams; ++j) prm[j] = pbh_param{nullptr, params_host[j]};
   return lhs_sorted_ppf(seed, n, t0, nt, col, dist, prm, nparams, out, nonfinite_flag, as_stream(stream));
 }
@@ -186,12 +186,12 @@ extern "C" int pbh_lhs_sorted_counts(uint64_t seed, int64_t n, int64_t t0, int64
                                      const double* params_host, int nparams, unsigned long long* counts,
                                      uint32_t* heads, uint32_t* hcur, uint32_t hcap, int32_t* nonfinite_flag,
                                      int certify, void* stream) {
-  PBH_REQUIRE(counts && nparams >= 0 && nparams <= 3 && (nparams == 0 || params_host),
+  PBH_REQUIRE(counts && nparams >= 0 && nparams <= 4 && (nparams == 0 || params_host),
               "pbh_lhs_sorted_counts: bad arguments");
   PBH_REQUIRE(!heads || (hcur && hcap >= 1), "pbh_lhs_sorted_counts: heads need hcur and hcap >= 1");
   PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "pbh_lhs_sorted_counts: n out of range");
   hipStream_t s = as_stream(stream);
-  pbh_param prm[3];
+  pbh_param prm[4];
   for (int j = 0; j < nparams; ++j) prm[j] = pbh_param{nullptr, params_host[j]};
   GenColumn* g = nullptr;
   int st = gen_create(seed, n, col, dist, prm, nparams, &g, s);
@@ -216,8 +216,8 @@ extern "C" int pbh_lhs_values_at(const pbh_ic_column* column, int64_t n, const u
   PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "pbh_lhs_values_at: n out of range");
   if (m == 0) return PBH_OK;
   hipStream_t s = as_stream(stream);
-  pbh_param prm[3];
-  for (int j = 0; j < 3; ++j) prm[j] = pbh_param{nullptr, column->params[j]};
+  pbh_param prm[4];
+  for (int j = 0; j < 4; ++j) prm[j] = pbh_param{nullptr, column->params[j]};
   GenColumn* g = nullptr;
   int st = gen_create(column->seed, n, column->lhs_col, column->dist, prm, column->nparams, &g, s);
   if (st != PBH_OK) return st;

@@ -1495,6 +1495,8 @@ struct GenColumn {
   Params prm;
   PoissonTable pt;
   double* table;
+  bool ext;        // an extended distribution (pbh_ppf_ext.hip): its kernels take xval
+  double xval[4];
 };
 
 int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* params, int nparams, GenColumn** out,
@@ -1506,6 +1508,17 @@ int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* par
   g->n = n;
   g->col = (uint32_t)col;
   g->dist = dist;
+  if (const int want = ext_nparams(dist); want >= 0) {
+    if (nparams != want || (nparams && !params)) {
+      delete g;
+      set_error("distribution %d expects %d parameters, got %d", dist, want, nparams);
+      return PBH_ERR_INVALID;
+    }
+    g->ext = true;
+    for (int j = 0; j < nparams; ++j) g->xval[j] = params[j].value;
+    *out = g;
+    return PBH_OK;
+  }
   int st = with_params(dist, params, nparams, g->prm, g->pt, &g->table, s);
   if (st != PBH_OK) {
     delete g;
@@ -1599,6 +1612,8 @@ int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t*
     PBH_CHECK_HIP(hipMemsetAsync(hcur, 0, sizeof(uint32_t), s));
   }
   if (nt == 0) return PBH_OK;
+  if (g->ext)
+    return ext_gen_sorted(g->seed, n, g->col, g->dist, g->xval, t0, nt, out, flag, counts, heads, hcur, hcap, s);
   static const bool fast_heads = [] {  // PBH_DISCRETE_SCAN=1: evaluate every stratum
     const char* e = getenv("PBH_DISCRETE_SCAN");
     return !(e && e[0] == '1');
@@ -1770,6 +1785,9 @@ template <bool BYROW>
 static int place_launch(const GenColumn* g, const uint64_t* pairs, const uint32_t* pidx, int64_t rows, double* y,
                         int64_t y_rs, int32_t* idx, const int32_t* state, hipStream_t s) {
   const int64_t n = g->n;
+  if (g->ext)
+    return ext_gen_place(g->seed, n, g->col, g->dist, g->xval, pairs, BYROW ? pidx : nullptr, rows, y, y_rs, idx, state,
+                         s);
   const int64_t blocks = (rows + kGenRows - 1) / kGenRows;
   if (blocks <= 0) return PBH_OK;
   int j0 = 0, jn = 0;

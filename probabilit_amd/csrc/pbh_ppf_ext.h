@@ -11,4 +11,19 @@ int ppf_ext(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_pa
 int lhs_ppf_ext(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col, int dist, const pbh_param* params,
                 int nparams, double* out, int32_t* flag, hipStream_t s);
 
+// Generated columns of these distributions (the Iman-Conover fast path; scalar parameters `val`,
+// ext_nparams(dist) of them).  ext_nparams is -1 for an id outside this set.
+int ext_nparams(int dist);
+bool ext_is_discrete(int dist);  // binom, bernoulli: sorted columns with runs of equal values
+// the column in stratum order over [t0, t0 + nt): values (out, optional), tie / inversion counts
+// (counts[2], device, optional), run heads appended at heads[*hcur] (< hcap written)
+int ext_gen_sorted(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, int64_t t0, int64_t nt,
+                   double* out, int32_t* flag, unsigned long long* counts, uint32_t* heads, uint32_t* hcur,
+                   uint32_t hcap, hipStream_t s);
+// step 4's placement: y[row * y_rs] = value(p) for the (row << 32 | p) pairs, or (pidx != NULL)
+// y[i * y_rs] = value(pidx[i]) for i < rows
+int ext_gen_place(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, const uint64_t* pairs,
+                  const uint32_t* pidx, int64_t rows, double* y, int64_t y_rs, int32_t* idx, const int32_t* state,
+                  hipStream_t s);
+
 }  // namespace pbh

@@ -21,6 +21,7 @@
 #include "pbh_rng.h"
 #include "pbh_special.h"
 #include "pbh_special_ext.h"
+#include "pbh_step4.h"
 #include "pbh_timing.h"
 
 namespace pbh {
@@ -238,7 +239,248 @@ int launch_ext(int dist, const double* q, int64_t q_stride, const LhsCol* lc, in
   return PBH_OK;
 }
 
+// ---------------------------------------------------------------- generated columns
+// The Iman-Conover fast path for these distributions (pbh_api.hip ic_run, pbh_ic_owned_*): the
+// column in stratum order, value(t) = ppf(lhs_sorted_quantile(t)) -- the quantile of the row
+// pi^-1(t), so bit-identical to k_ppf_ext<D, true>'s value for that row -- counted for ties and
+// inversions without being stored, and regenerated by step 4's last pass at the sorted position p
+// of every row (Y[row] = sort(X)[p]).  The same roles k_lhs_sorted_ppf / k_discrete_heads /
+// k_place_gen play for the base set (pbh_ppf.hip).
+template <int D>
+__device__ __forceinline__ double gen_value(const Philox& ph, int64_t t, uint32_t col, int64_t n, const Params4& p) {
+  return ppf_ext_one<D>(lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n), p, 0);
+}
+
+// out[i] = value(t0 + i) (out may be NULL); counts[0] += #ties, counts[1] += #inversions over the
+// pairs inside the segment; heads: every run head t + 1 (x[t] != x[t + 1]) appended at heads[*hcur].
+// Waves advance by 63 strata and overlap by one, so every pair meets inside one wave.
+template <int D>
+__global__ __launch_bounds__(256) void k_ext_sorted(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
+                                                    Params4 prm, double* __restrict__ out, int32_t* flag,
+                                                    unsigned long long* counts, uint32_t* __restrict__ heads,
+                                                    uint32_t* __restrict__ hcur, uint32_t hcap) {
+  __shared__ unsigned long long sh[2][4];
+  Philox ph(seed);
+  const int lane = threadIdx.x & 63;
+  unsigned long long ties = 0, inv = 0;
+  const int64_t waves = (int64_t)gridDim.x * 4;
+  const int64_t wid0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t iters = (nt + 63 * waves - 1) / (63 * waves);
+  for (int64_t it = 0; it < iters; ++it) {
+    const int64_t i = (it * waves + wid0) * 63 + lane;
+    const bool valid = i < nt;
+    double x = 0.0;
+    if (valid) {
+      x = gen_value<D>(ph, t0 + i, col, n, prm);
+      if (out && lane < 63) out[i] = x;
+    }
+    flag_nonfinite(flag, valid && lane < 63 && !isfinite(x));
+    const double nx = __shfl_down(x, 1, 64);
+    const bool has_next = valid && lane < 63 && i + 1 < nt;
+    ties += has_next && x == nx;
+    inv += has_next && !(x <= nx);
+    if (heads) {
+      const bool hd = has_next && x != nx;
+      const uint64_t m = __ballot(hd);
+      if (m) {
+        const int leader = __builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(hcur, (uint32_t)__popcll(m));
+        base = __shfl(base, leader, 64);
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const uint32_t slot = base + (uint32_t)__popcll(m & lt);
+        if (hd && slot < hcap) heads[slot] = (uint32_t)(t0 + i + 1);
+      }
+    }
+  }
+  if (!counts) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ties += __shfl_xor(ties, o, 64);
+    inv += __shfl_xor(inv, o, 64);
+  }
+  if (lane == 0) {
+    sh[0][threadIdx.x >> 6] = ties;
+    sh[1][threadIdx.x >> 6] = inv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long a = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+    const unsigned long long b = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+    if (a) atomicAdd(&counts[0], a);
+    if (b) atomicAdd(&counts[1], b);
+  }
+}
+
+// binom / bernoulli: the run heads of strata [t0, t0 + nt) by one binary search per integer value
+// k in (value(t0), value(t0 + nt - 1)] (the strata's quantiles increase strictly and the ppf is
+// monotone, so a run boundary is the first stratum whose value reaches k): the heads, the tie count
+// nt - 1 - #heads and the inversion count 0 equal k_ext_sorted's, from ~30 evaluations per value
+// instead of nt (as k_discrete_heads does for poisson).  Ends that are not finite integers within
+// kDiscreteSpan of each other are reported as an inversion: the caller then counts exactly.
+constexpr int kExtDiscreteSpan = 4096;
+
+template <int D>
+__global__ __launch_bounds__(256) void k_ext_discrete_heads(uint64_t seed, int64_t n, int64_t t0, int64_t nt,
+                                                            uint32_t col, Params4 prm, int32_t* flag,
+                                                            unsigned long long* counts, uint32_t* __restrict__ heads,
+                                                            uint32_t* __restrict__ hcur, uint32_t hcap) {
+  __shared__ uint32_t b[kExtDiscreteSpan];
+  __shared__ int span, bad;
+  __shared__ double vlo;
+  __shared__ uint32_t found;
+  Philox ph(seed);
+  if (threadIdx.x == 0) {
+    const double a = gen_value<D>(ph, t0, col, n, prm), z = gen_value<D>(ph, t0 + nt - 1, col, n, prm);
+    vlo = a;
+    found = 0;
+    bad = !(isfinite(a) && isfinite(z) && a == floor(a) && z == floor(z) && z >= a && z - a <= kExtDiscreteSpan);
+    span = bad ? 0 : (int)(z - a);
+    if (bad) {
+      flag_nonfinite(flag, !isfinite(a) || !isfinite(z));
+      atomicAdd(&counts[1], 1ull);
+    }
+  }
+  __syncthreads();
+  const int m = span;
+  for (int i = threadIdx.x; i < m; i += 256) {
+    const double k = vlo + 1.0 + (double)i;
+    int64_t lo = t0, hi = t0 + nt - 1;  // value(lo) < k <= value(hi)
+    while (hi - lo > 1) {
+      const int64_t mid = lo + ((hi - lo) >> 1);
+      if (gen_value<D>(ph, mid, col, n, prm) >= k)
+        hi = mid;
+      else
+        lo = mid;
+    }
+    b[i] = (uint32_t)hi;
+  }
+  __syncthreads();
+  uint32_t mine = 0;
+  for (int i = threadIdx.x; i < m; i += 256) {
+    if (i > 0 && b[i] == b[i - 1]) continue;  // a value no stratum takes
+    const uint32_t slot = atomicAdd(hcur, 1u);
+    if (slot < hcap) heads[slot] = b[i];
+    ++mine;
+  }
+  if (mine) atomicAdd(&found, mine);
+  __syncthreads();
+  if (threadIdx.x == 0 && !bad) atomicAdd(&counts[0], (unsigned long long)(nt - 1 - (int64_t)found));
+}
+
+// Step 4's last pass: Y[row] = value(p) for the (row << 32 | p) pairs of every block of
+// kGenRows consecutive rows, assembled in LDS and written contiguously (BYROW: row r0 + i itself
+// with stratum pidx[r0 + i], the row owner's half of a row-sharded step 4).
+constexpr int kExtGenRows = 1 << kGenPlaceShift;
+
+template <int D, bool BYROW>
+__global__ __launch_bounds__(256) void k_ext_place(const uint64_t* __restrict__ pairs,
+                                                   const uint32_t* __restrict__ pidx, int64_t rows, int64_t n,
+                                                   uint64_t seed, uint32_t col, Params4 prm, double* __restrict__ y,
+                                                   int64_t y_rs, int32_t* __restrict__ idx,
+                                                   const int32_t* __restrict__ state) {
+  if (state && *state) return;
+  __shared__ double buf[kExtGenRows];
+  Philox ph(seed);
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((rows - r0) < kExtGenRows ? (rows - r0) : kExtGenRows);
+    for (int p = threadIdx.x; p < cnt; p += 256) {
+      uint32_t t;
+      int off;
+      if constexpr (BYROW) {
+        t = pidx[r0 + p];
+        off = p;
+      } else {
+        const uint64_t pr = pairs[r0 + p];
+        t = (uint32_t)pr;
+        const int64_t row = (int64_t)(pr >> 32);
+        if (idx) idx[row] = (int32_t)t;
+        off = (int)(row - r0);
+      }
+      buf[off] = gen_value<D>(ph, (int64_t)t, col, n, prm);
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < cnt; p += 256) y[(r0 + p) * y_rs] = buf[p];
+    __syncthreads();
+  }
+}
+
+Params4 scalar_params(const double* val, int np) {
+  Params4 p{};
+  for (int j = 0; j < 4; ++j) p.val[j] = j < np ? val[j] : 0.0;
+  return p;
+}
+
 }  // namespace
+
+int ext_nparams(int dist) {
+  if (dist == PBH_DIST_BERNOULLI) return 2;
+  if (dist == PBH_DIST_BINOM) return 3;
+  if (dist == PBH_DIST_BETA || dist == PBH_DIST_TRUNCNORM) return 4;
+  if (is_closed(dist)) return closed_shapes(dist) + 2;
+  return -1;
+}
+
+bool ext_is_discrete(int dist) { return dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI; }
+
+int ext_gen_sorted(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, int64_t t0, int64_t nt,
+                   double* out, int32_t* flag, unsigned long long* counts, uint32_t* heads, uint32_t* hcur,
+                   uint32_t hcap, hipStream_t s) {
+  const int np = ext_nparams(dist);
+  PBH_REQUIRE(np >= 0, "ext_gen_sorted: distribution %d is not an extended one", dist);
+  if (nt == 0) return PBH_OK;
+  const Params4 prm = scalar_params(val, np);
+  // binom / bernoulli, counts and heads only: the binary-search heads when the values span few
+  // integers (n + 1 at most); the kernel reports anything else as an inversion
+  if (ext_is_discrete(dist) && counts && heads && !out && nt >= 2) {
+    const double nn = dist == PBH_DIST_BINOM ? val[0] : 1.0;
+    if (nn >= 0.0 && nn + 1.0 < (double)kExtDiscreteSpan) {
+      const bool known = dispatch_ext(dist, [&](auto tag) {
+        constexpr int D = decltype(tag)::value;
+        if constexpr (D == PBH_DIST_BINOM || D == PBH_DIST_BERNOULLI)
+          PBH_TIMED(kKLhsSorted, s,
+                    hipLaunchKernelGGL(k_ext_discrete_heads<D>, dim3(1), dim3(256), 0, s, seed, n, t0, nt, col, prm,
+                                       flag, counts, heads, hcur, hcap));
+      });
+      (void)known;
+      PBH_CHECK_LAUNCH();
+      return PBH_OK;
+    }
+  }
+  const dim3 g(grid_for(nt, 256 * 63 / 64 + 1, 8192)), b(256);
+  dispatch_ext(dist, [&](auto tag) {
+    constexpr int D = decltype(tag)::value;
+    PBH_TIMED(kKLhsSorted, s,
+              hipLaunchKernelGGL(k_ext_sorted<D>, g, b, 0, s, seed, n, t0, nt, col, prm, out, flag, counts, heads, hcur,
+                                 hcap));
+  });
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int ext_gen_place(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, const uint64_t* pairs,
+                  const uint32_t* pidx, int64_t rows, double* y, int64_t y_rs, int32_t* idx, const int32_t* state,
+                  hipStream_t s) {
+  const int np = ext_nparams(dist);
+  PBH_REQUIRE(np >= 0, "ext_gen_place: distribution %d is not an extended one", dist);
+  const int64_t blocks = (rows + kExtGenRows - 1) / kExtGenRows;
+  if (blocks <= 0) return PBH_OK;
+  const Params4 prm = scalar_params(val, np);
+  const dim3 g((unsigned)(blocks < 256 * 8 ? blocks : 256 * 8)), b(256);
+  dispatch_ext(dist, [&](auto tag) {
+    constexpr int D = decltype(tag)::value;
+    if (pidx)
+      hipLaunchKernelGGL((k_ext_place<D, true>), g, b, 0, s, pairs, pidx, rows, n, seed, col, prm, y, y_rs, idx,
+                         state);
+    else
+      PBH_TIMED(kKPlaceGen, s,
+                hipLaunchKernelGGL((k_ext_place<D, false>), g, b, 0, s, pairs, pidx, rows, n, seed, col, prm, y, y_rs,
+                                   idx, state));
+  });
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
 
 int ppf_ext(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_param* params, int nparams, double* out,
             int32_t* flag, hipStream_t s) {

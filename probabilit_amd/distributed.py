@@ -39,7 +39,7 @@ import numpy as np
 from . import _lib, device
 
 HEADS_CAP = 16384  # run heads a discrete column's shard may append (kHeadsCap, pbh_step4.h)
-DISCRETE = {_lib.DIST_IDS["poisson"]}  # the generated distributions whose sorted column has runs
+DISCRETE = {_lib.DIST_IDS[d] for d in ("poisson", "binom", "bernoulli")}  # sorted columns with runs
 
 
 def shard_bounds(n, world):
@@ -57,7 +57,7 @@ class LHSColumn:
         self.params = [float(p) for p in params]
 
     def ic_column(self):
-        return _lib.ICColumn(self.seed, self.lhs_col, self.dist, (ctypes.c_double * 3)(*self.params),
+        return _lib.ICColumn(self.seed, self.lhs_col, self.dist, (ctypes.c_double * 4)(*self.params),
                              len(self.params), None)
 
 
@@ -109,7 +109,7 @@ class HipPhases:
 
     # -- step 1 ---------------------------------------------------------------------------
     def sorted_counts(self, col, n, t0, nt, flag, counts, heads=None, hcur=None, certify=False):
-        prm = (ctypes.c_double * 3)(*col.params)
+        prm = (ctypes.c_double * 4)(*col.params)
         _lib.check(self.lib.pbh_lhs_sorted_counts(col.seed, n, t0, nt, col.lhs_col, col.dist, prm, len(col.params),
                                                   counts.data_ptr(), heads.data_ptr() if heads is not None else None,
                                                   hcur.data_ptr() if hcur is not None else None,
@@ -123,7 +123,7 @@ class HipPhases:
         """Run heads of strata [t0, t0 + nt) from the materialised segment (the rare fallback:
         a continuous column that ties, or a discrete one with more heads than HEADS_CAP)."""
         out = device.empty(max(nt, 1))
-        prm = (ctypes.c_double * 3)(*col.params)
+        prm = (ctypes.c_double * 4)(*col.params)
         _lib.check(self.lib.pbh_lhs_sorted_ppf(col.seed, n, t0, nt, col.lhs_col, col.dist, prm, len(col.params),
                                                out.data_ptr(), flag.data_ptr(), device.stream()),
                    "pbh_lhs_sorted_ppf")

@@ -472,7 +472,7 @@ class Node(abc.ABC):
                     for var in all_variables:
                         _, seed, n_total, col, _ = deferred[var]
                         params = [float(p) for p in var._params(size)]
-                        cols.append(_lib.ICColumn(seed, col, _lib.DIST_IDS[var.distr], (ctypes.c_double * 3)(*params),
+                        cols.append(_lib.ICColumn(seed, col, _lib.DIST_IDS[var.distr], (ctypes.c_double * 4)(*params),
                                                   len(params), ev.flag_ptr(var)))
                     Y = inst._transform_generated(cols, size)
                     for j, var in enumerate(all_variables):
@@ -594,8 +594,10 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "loguniform": ("a", "b"), "reciprocal": ("a", "b"), "rayleigh": (), "lomax": ("c",),
                 "genextreme": ("c",), "gompertz": ("c",), "chi2": ("df",)}
 _DISCRETE = {"poisson", "binom", "bernoulli"}
-# distributions with a fused native-LHS + inverse-CDF kernel (and the Iman-Conover fast path)
-_FUSED_LHS = {"norm", "uniform", "expon", "lognorm", "triang", "gamma", "poisson"}
+# distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so
+# that Iman-Conover takes them as generated columns (pbh_ppf.hip k_lhs_sorted_ppf / k_place_gen;
+# the extended set pbh_ppf_ext.hip k_ext_sorted / k_ext_place): every distribution with a kernel
+_FUSED_LHS = set(_DIST_SHAPES)
 
 
 def _parse_scipy_args(name, args, kwargs):

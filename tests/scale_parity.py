@@ -30,7 +30,7 @@ def cfg3_generated(n, d, seed, C):
     cols = []
     for j, v in enumerate(ds):
         params = [float(p) for p in v._params(n)]
-        cols.append(_lib.ICColumn(s, j, _lib.DIST_IDS[v.distr], (ctypes.c_double * 3)(*params), len(params),
+        cols.append(_lib.ICColumn(s, j, _lib.DIST_IDS[v.distr], (ctypes.c_double * 4)(*params), len(params),
                                   flags.data_ptr() + 4 * j))
     return inst, cols, flags
 

@@ -40,7 +40,7 @@ def _single_call(spec=SPEC):
     from probabilit_amd.correlation import ImanConover
 
     flags = device.zeros(len(spec), "int32")
-    cols = [_lib.ICColumn(SEED, c, d, (ctypes.c_double * 3)(*p), len(p), flags.data_ptr() + 4 * c)
+    cols = [_lib.ICColumn(SEED, c, d, (ctypes.c_double * 4)(*p), len(p), flags.data_ptr() + 4 * c)
             for c, (d, p) in enumerate(spec)]
     Y = ImanConover().set_target(_target(len(spec)))._transform_generated(cols, N)
     return device.to_host(Y)
@@ -79,7 +79,7 @@ def test_owned_columns_values_and_positions(gpu):
     cols = _columns(sp)
     lib = _lib.load()
     flags = device.zeros(len(sp), "int32")
-    icc = [_lib.ICColumn(SEED, c, d, (ctypes.c_double * 3)(*p), len(p), flags.data_ptr() + 4 * c)
+    icc = [_lib.ICColumn(SEED, c, d, (ctypes.c_double * 4)(*p), len(p), flags.data_ptr() + 4 * c)
            for c, (d, p) in enumerate(sp)]
     inst = ImanConover().set_target(_target(len(sp)))
     CS = device.empty((len(sp), N))

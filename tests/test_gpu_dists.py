@@ -243,3 +243,45 @@ def test_fused_lhs_pert_composite(gpu):
     q2 = native.fill_lhs(seed_from(s), n, 2)
     a = scipy.stats.uniform(loc=1, scale=3).ppf(q2[:, 0])
     assert_close(y, scipy.stats.beta(a=a, b=2.0).ppf(q2[:, 1]), what="composite beta LHS")
+
+
+def _ext_graph(kind):
+    from probabilit_amd import distributions as dists
+    from probabilit_amd.modeling import Distribution as D
+
+    if kind == "pert":
+        return [dists.PERT(0, 6, 10), dists.PERT(1, 2, 9, gamma=10), dists.PERT(-3, 0, 1), dists.PERT(5, 6, 7)]
+    if kind == "discrete":
+        return [D("binom", n=20, p=0.3), D("bernoulli", p=0.25), D("binom", n=1000, p=0.7, loc=2), D("norm")]
+    return [D("truncnorm", a=-1.0, b=2.0, loc=1.0), D("weibull_min", c=1.7), D("logistic", loc=2.0),
+            D("gumbel_r", scale=0.5), D("chi2", df=5.5), D("beta", 0.5, 0.5), D("lomax", c=1.88), D("gamma", a=2.0)]
+
+
+@pytest.mark.parametrize("kind,n", [("pert", 50_000), ("discrete", 40_000), ("mixed", 30_001)])
+def test_ext_generated_iman_conover(gpu, kind, n):
+    """Extended distributions (PERT -> beta, truncnorm, binom, bernoulli, closed forms) correlated
+    with method="lhs" go through the generated-column fast path (stratum-ordered generator + step-4
+    regeneration, pbh_ppf_ext.hip): bit-identical to the general path fed the same native-LHS
+    quantiles (sample_from_quantiles, X materialised and sorted), and that equals the oracle's
+    Iman-Conover (correlation.py:388-425 restated) of the same uncorrelated samples."""
+    from oracle.ic import iman_conover
+    from probabilit_amd import native
+    from probabilit_amd.modeling import NoOp
+    from probabilit_amd.qmc import seed_from
+
+    d = len(_ext_graph(kind))
+    rng = np.random.default_rng(d)
+    A = rng.normal(size=(d, d + 2))
+    C = np.corrcoef(A)
+    ds = _ext_graph(kind)
+    root = NoOp(*ds).correlate(*ds, corr_mat=C)
+    root.sample(n, random_state=9, method="lhs")
+    fast = np.column_stack([x.samples_ for x in ds])
+    q = native.fill_lhs(seed_from(9), n, d)
+    root.sample_from_quantiles(q)
+    general = np.column_stack([x.samples_ for x in ds])
+    np.testing.assert_array_equal(fast, general)
+    ds = _ext_graph(kind)
+    NoOp(*ds).sample_from_quantiles(q)
+    X = np.column_stack([x.samples_ for x in ds])
+    np.testing.assert_array_equal(fast, iman_conover(X, C)["Y"])

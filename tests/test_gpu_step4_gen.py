@@ -25,7 +25,7 @@ def _run(n, dists, seed, C, debug_idx=True):
     for j, (nm, kw) in enumerate(dists):
         v = Distribution(nm, **kw)
         params = [float(p) for p in v._params(n)]
-        cols.append(_lib.ICColumn(qmc.seed_from(seed), j, _lib.DIST_IDS[nm], (ctypes.c_double * 3)(*params),
+        cols.append(_lib.ICColumn(qmc.seed_from(seed), j, _lib.DIST_IDS[nm], (ctypes.c_double * 4)(*params),
                                   len(params), flags.data_ptr() + 4 * j))
     dbg = {"idx": device.empty((d, n), "int32")} if debug_idx else None
     Y = inst._transform_generated(cols, n, debug=dbg)
@@ -180,7 +180,7 @@ def _debug_run(n, dists, seed, C):
     for j, (nm, kw) in enumerate(dists):
         v = Distribution(nm, **kw)
         params = [float(p) for p in v._params(n)]
-        cols.append(_lib.ICColumn(qmc.seed_from(seed), j, _lib.DIST_IDS[nm], (ctypes.c_double * 3)(*params),
+        cols.append(_lib.ICColumn(qmc.seed_from(seed), j, _lib.DIST_IDS[nm], (ctypes.c_double * 4)(*params),
                                   len(params), flags.data_ptr() + 4 * j))
     dbg = {"idx": device.empty((d, n), "int32"), "S": device.empty((d, n), "float64"), "E": np.zeros((d, d))}
     Y = inst._transform_generated(cols, n, debug=dbg)

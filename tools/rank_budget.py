@@ -44,7 +44,7 @@ def main():
     cols = [LHSColumn(7, c, _lib.DIST_IDS[name], [float(x) for x in _parse_scipy_args(name, (), kw)])
             for c, (name, kw) in enumerate(cfg_dists(K))]
     flags = device.zeros(K, "int32")
-    icc = [_lib.ICColumn(7, c, col.dist, (ctypes.c_double * 3)(*col.params), len(col.params),
+    icc = [_lib.ICColumn(7, c, col.dist, (ctypes.c_double * 4)(*col.params), len(col.params),
                          flags.data_ptr() + 4 * c) for c, col in enumerate(cols)]
     CS = device.empty((K, n))
     ImanConover().set_target(C)._transform_generated(icc, n, debug={"CS": CS})
