@@ -44,12 +44,13 @@ def ppf(name, q, return_device=False, **params):
     return out if return_device else device.to_host(out)
 
 
-def lhs_ppf(name, seed, n, col, row0=0, nrows=None, return_device=False, **params):
-    """Fused native-LHS column `col` pushed through ppf (pbh_lhs_ppf)."""
-    nrows = n - row0 if nrows is None else nrows
+def lhs_ppf(name, seed, n_total, col, row0=0, nrows=None, return_device=False, **params):
+    """Fused native-LHS column `col` of an n_total-row design pushed through ppf (pbh_lhs_ppf).
+    (n_total, not n: binom's shape parameter is called n.)"""
+    nrows = n_total - row0 if nrows is None else nrows
     arr, keep = _params(name, nrows, params)
     out = device.empty(nrows)
-    _lib.check(_lib.load().pbh_lhs_ppf(seed, n, row0, nrows, col, _lib.DIST_IDS[name], arr, len(arr),
+    _lib.check(_lib.load().pbh_lhs_ppf(seed, n_total, row0, nrows, col, _lib.DIST_IDS[name], arr, len(arr),
                                        out.data_ptr(), None, device.stream()), "pbh_lhs_ppf")
     del keep
     return out if return_device else device.to_host(out)
