@@ -107,6 +107,46 @@ PBH_HD inline double log_tab_at(double x, const double* __restrict__ tab) {
 }
 PBH_HD inline double log_tab(double x) { return log_tab_at(x, &pbh_log_tab[0][0]); }
 
+// log_tab_at for x known to be positive, normal and finite: the same operations without the
+// subnormal scaling and the special-value patch (their selects), so the same result.
+template <int S = 4>
+PBH_HD inline double log_tab_pos_at(double x, const double* __restrict__ tab) {
+  const uint64_t ix = __builtin_bit_cast(uint64_t, x);
+  const uint64_t tmp = ix - 0x3fe6000000000000ull;
+  const int i = (int)((tmp >> 45) & 127u);
+  const double kd = (double)((int64_t)tmp >> 52);
+  const double z = __builtin_bit_cast(double, ix - (tmp & 0xfff0000000000000ull));
+  const double invc = tab[S * i], lch = tab[S * i + 1], lcl = tab[S * i + 2];
+  const double ph = z * invc;
+  const double pl = fma(z, invc, -ph);
+  const double rh = ph - 1.0;
+  const double r = rh + pl;
+  const double rl = (rh - r) + pl;
+  const double t1 = kd * kLogTabLn2Hi;
+  const double w = t1 + lch;
+  const double e1 = (t1 - w) + lch;
+  const double s = w + r;
+  const double bv = s - w;
+  const double e2 = (w - (s - bv)) + (r - bv);
+  double p = 1.0 / 9.0;
+  p = fma(p, r, -1.0 / 8.0);
+  p = fma(p, r, 1.0 / 7.0);
+  p = fma(p, r, -1.0 / 6.0);
+  p = fma(p, r, 1.0 / 5.0);
+  p = fma(p, r, -1.0 / 4.0);
+  p = fma(p, r, 1.0 / 3.0);
+  p = fma(p, r, -0.5);
+  const double lo = fma(r * r, p, fma(kd, kLogTabLn2Lo, lcl + e1)) + (e2 + rl);
+  return s + lo;
+}
+
+// the general log_tab_at as a real call: a kernel's rare path (a subnormal argument), kept out of
+// the common path's code so that it is neither if-converted into it nor merged with it
+template <int S = 4>
+__attribute__((noinline)) PBH_HD inline double log_tab_cold(double x, const double* __restrict__ tab) {
+  return log_tab_at<S>(x, tab);
+}
+
 // e^y for y in [-700, 700] (the gamma guide's interpolated log x; its callers check the range):
 // y = (k / 128) ln2 + r, |r| <= ln2 / 256, r exact to ~2^-60 (k ln2hi exact, Sterbenz),
 // e^y = 2^(k >> 7) (T + T expm1(r)), T = 2^((k & 127) / 128) as a double-double and expm1(r) to r^5
@@ -159,37 +199,52 @@ PBH_HD inline double ndtri_centre(double y0) {
 }
 
 // Tail: ndtri_takes_tail(y0).  LT: log_tab's table and its stride (a kernel's LDS copy), or the
-// global table.
-template <int S = 4>
-PBH_HD inline double ndtri_tail_at(double y0, const double* __restrict__ lt) {
-  // z = sqrt(-2 log y) in [2, 8)
+// global table.  The second rational (z = sqrt(-2 log y) >= 8, i.e. y < exp(-32)) and the log of
+// a subnormal y are real calls: with them inline the compiler if-converted the branch on x < 8
+// into a per-lane select of every coefficient (~200 of the tail's ~420 instructions); now a wave
+// with no such lane runs one polynomial pair with scalar coefficients.  Same operations per lane.
+PBH_HD inline double ndtri_tail_near(double z) {  // x in [2, 8)
   const double P1[9] = {4.05544892305962419923e0, 3.15251094599893866154e1, 5.71628192246421288162e1,
                         4.40805073893200834700e1, 1.46849561928858024014e1, 2.18663306850790267539e0,
                         -1.40256079171354495875e-1, -3.50424626827848203418e-2, -8.57456785154685413611e-4};
   const double Q1[8] = {1.57799883256466749731e1, 4.53907635128879210584e1, 4.13172038254672030440e1,
                         1.50425385692907503408e1, 2.50464946208309415979e0, -1.42182922854787788574e-1,
                         -3.80806407691578277194e-2, -9.33259480895457427372e-4};
-  // z in [8, 64)
+  return z * polevl(z, P1, 8) / p1evl(z, Q1, 8);
+}
+__attribute__((noinline)) PBH_HD inline double ndtri_tail_far(double z) {  // x in [8, 64)
   const double P2[9] = {3.23774891776946035970e0, 6.91522889068984211695e0, 3.93881025292474443415e0,
                         1.33303460815807542389e0, 2.01485389549179081538e-1, 1.23716634817820021358e-2,
                         3.01581553508235416007e-4, 2.65806974686737550832e-6, 6.23974539184983293730e-9};
   const double Q2[8] = {6.02427039364742014255e0, 3.67983563856160859403e0, 1.37702099489081330271e0,
                         2.16236993594496635890e-1, 1.34204006088543189037e-2, 3.28014464682127739104e-4,
                         2.89247864745380683936e-6, 6.79019408009981274425e-9};
+  return z * polevl(z, P2, 8) / p1evl(z, Q2, 8);
+}
+
+template <int S = 4>
+PBH_HD inline double ndtri_tail_at(double y0, const double* __restrict__ lt) {
   bool negate = true;
   double y = y0;
   if (y > (1.0 - kNdtriExpM2)) {
     y = 1.0 - y;
     negate = false;
   }
-  double x = sqrt(-2.0 * log_tab_at<S>(y, lt));
-  const double x0 = x - log_tab_at<S>(x, lt) / x;
+  // y in (0, exp(-2)]: log y is finite and x = sqrt(-2 log y) lies in [2, 39), so log x needs no
+  // special-value handling, and log y only for a subnormal y
+  double ly;
+  if (y >= 0x1.0p-1022)
+    ly = log_tab_pos_at<S>(y, lt);
+  else
+    ly = log_tab_cold<S>(y, lt);
+  double x = sqrt(-2.0 * ly);
+  const double x0 = x - log_tab_pos_at<S>(x, lt) / x;
   const double z = 1.0 / x;
   double x1;
   if (x < 8.0)
-    x1 = z * polevl(z, P1, 8) / p1evl(z, Q1, 8);
+    x1 = ndtri_tail_near(z);
   else
-    x1 = z * polevl(z, P2, 8) / p1evl(z, Q2, 8);
+    x1 = ndtri_tail_far(z);
   x = x0 - x1;
   return negate ? -x : x;
 }

@@ -23,6 +23,10 @@ SPECS = {
     # a leading poisson column: its correlated score IS its tied scores (runs of equal codes beyond
     # the finish), so the owner's fast passes reject it and the general path redoes it
     "tied_first": [(6, [4.0, 0.0]), (0, [0.0, 1.0]), (5, [2.0, 0.0, 1.0]), (4, [0.3, 0.0, 1.0])],
+    # extended distributions (pbh_ppf_ext.hip generated columns): PERT's beta, binom / bernoulli
+    # run heads by binary search in every shard, truncnorm and a closed form
+    "ext": [(7, [3.4, 2.6, 0.0, 10.0]), (9, [20.0, 0.3, 0.0]), (0, [0.0, 1.0]), (10, [0.25, 0.0]),
+            (8, [-1.0, 2.0, 1.0, 1.0]), (11, [1.7, 0.0, 1.0])],
 }
 SPEC = SPECS["cfg2"]
 N = 300_007
@@ -138,6 +142,12 @@ def _dag(kind):
     if kind == "correlated":
         ds = [Distribution(name, **kw) for name, kw in cfg_dists(8)]
         return NoOp(*ds).correlate(*ds, corr_mat=_target()), "lhs"
+    if kind == "ext":  # PERT, binom, bernoulli, a closed form: generated columns too
+        from probabilit_amd import distributions as dists
+
+        ds = [dists.PERT(0, 6, 10), Distribution("binom", n=20, p=0.3), Distribution("bernoulli", p=0.25),
+              Distribution("weibull_min", c=1.7), dists.PERT(1, 2, 9, gamma=10)]
+        return NoOp(*ds).correlate(*ds, corr_mat=_target(len(ds))), "lhs"
     r = 0
     for _ in range(20):  # README mutual-fund loop (BASELINE config 5)
         r = r * Distribution("norm", loc=1.11, scale=0.15) + 1200
@@ -152,7 +162,7 @@ def _dag_worker(rank, world, port, outdir):
     try:
         from probabilit_amd import device
 
-        for kind in ("correlated", "fund"):
+        for kind in ("correlated", "fund", "ext"):
             root, method = _dag(kind)
             out = root.sample_device(1 << 16, random_state=7, method=method, group=dist.group.WORLD)
             if kind == "fund":
@@ -173,20 +183,21 @@ def test_dag_row_sharded_world2_matches_one_process(gpu):
 
     n = 1 << 16
     refs = {}
-    for kind in ("correlated", "fund"):
+    for kind in ("correlated", "fund", "ext"):
         root, method = _dag(kind)
         out = root.sample(n, random_state=7, method=method)
         if kind == "fund":
             refs[kind] = out
         else:
-            refs["vars"] = [d.samples_ for d in root.get_parents()]
+            refs[kind] = [d.samples_ for d in root.get_parents()]
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_dag_worker, args=(2, _free_port(), d), nprocs=2, join=True, start_method="spawn")
         b = shard_bounds(n, 2)
         for r in range(2):
             np.testing.assert_array_equal(np.load(os.path.join(d, f"fund{r}.npy")), refs["fund"][b[r]:b[r + 1]])
-            for j, ref in enumerate(refs["vars"]):
-                np.testing.assert_array_equal(np.load(os.path.join(d, f"correlated{r}_v{j}.npy")), ref[b[r]:b[r + 1]])
+            for kind in ("correlated", "ext"):
+                for j, ref in enumerate(refs[kind]):
+                    np.testing.assert_array_equal(np.load(os.path.join(d, f"{kind}{r}_v{j}.npy")), ref[b[r]:b[r + 1]])
 
 
 @pytest.mark.parametrize("spec", sorted(SPECS))
