@@ -231,6 +231,13 @@ PBH_DI double gamma_ppf_lds(double q, const Params& prm, const PoissonTable& pt,
   return ppf_one<PBH_DIST_GAMMA>(q, prm.val[0], prm.val[1], prm.val[2], local);
 }
 
+// the same as a real call: a kernel's slow drain (igami's iteration inline sized the sweep kernel's
+// registers and spilled into its hot loop)
+__attribute__((noinline)) __device__ double gamma_ppf_lds_cold(double q, const Params& prm, const PoissonTable& pt,
+                                                                const sf::GammaGuide& T) {
+  return gamma_ppf_lds(q, prm, pt, T);
+}
+
 // igami_guided's interpolation branch and ppf_one's gamma wrapper, operation for operation:
 // true and *v = the value when the element needs no iteration; false sends it to the slow queue
 // (gamma_ppf_lds), so that the hot loops carry no igami code.
@@ -238,7 +245,7 @@ PBH_DI double gamma_ppf_lds(double q, const Params& prm, const PoissonTable& pt,
 PBH_DI bool gamma_fast(double q, const sf::GammaGuide& T, double scale, double loc, bool cond0, double* v,
                        const double* ltab, const double* etab) {
   if (!(cond0 && q > 0.0 && q < 1.0)) return false;
-  const double w = sf::log_tab_at(q / (1.0 - q), ltab);
+  const double w = sf::log_odds_at(q, ltab);
   const double u = (w - T.z0) * T.inv_h;
   if (!(u >= 0.0 && u < (double)(T.m - 1))) return false;
   const int j = (int)u;
@@ -321,7 +328,7 @@ __global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restr
     for (int t = threadIdx.x; t < nd; t += kGBlock) {
       const int64_t i = base + (ns <= kQCap ? slowq[t] : t);
       if (i >= n) continue;
-      const double x = gamma_ppf_lds(q[i * q_stride], prm, pt, T);
+      const double x = gamma_ppf_lds_cold(q[i * q_stride], prm, pt, T);
       out[i] = x;
       bad |= !isfinite(x);
     }
@@ -901,7 +908,7 @@ __global__ __launch_bounds__(kGWBlock) __attribute__((amdgpu_waves_per_eu(4))) v
       bool fast = valid && cond0 && q > 0.0 && q < 1.0;
       double v = 0.0;
       if (fast) {
-        const double w = sf::log_tab_at(q / (1.0 - q), ltab);
+        const double w = sf::log_odds_at(q, ltab);
         const double u = (w - G.z0) * G.inv_h;
         fast = u >= 0.0 && u < (double)(G.m - 1);
         if (fast) {

@@ -169,6 +169,15 @@ PBH_HD inline double exp_tab_at(double y, const double* __restrict__ tab /* pbh_
 }
 PBH_HD inline double exp_tab(double y) { return exp_tab_at(y, &pbh_exp_tab[0][0]); }
 
+// log(p / (1 - p)) for p in (0, 1) (the gamma guide's log-odds): the ratio is positive and
+// finite, so log_tab_pos_at unless it is subnormal (a call).  Same value as log_tab_at.
+template <int S = 4>
+PBH_HD inline double log_odds_at(double p, const double* __restrict__ tab) {
+  const double r = p / (1.0 - p);
+  if (r >= 0x1.0p-1022) return log_tab_pos_at<S>(r, tab);
+  return log_tab_cold<S>(r, tab);
+}
+
 // ---------------------------------------------------------------- inverse normal CDF
 constexpr double kNdtriExpM2 = 0.13533528323661269189;  // exp(-2): ndtri's centre / tail split
 
@@ -946,7 +955,7 @@ PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const G
     double x = 0.0;
     bool halley = false, slow = !(p > 0.0 && p < 1.0);
     if (!slow) {
-      const double w = log_tab(p / (1.0 - p));
+      const double w = log_odds_at(p, &pbh_log_tab[0][0]);
       double u = (w - T.z0) * T.inv_h;
       slow = !(u >= 0.0 && u < (double)(T.m - 1));
       if (!slow) {
@@ -962,7 +971,7 @@ PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const G
     return (slow || halley) ? igami_guided_fallback(a, p, x, halley, g->lga, g->lg1pa, g->lanczos) : x;
   } else {
     if (!(p > 0.0 && p < 1.0)) return igami(a, p);
-    const double w = log_tab(p / (1.0 - p));
+    const double w = log_odds_at(p, &pbh_log_tab[0][0]);
     double u = (w - T.z0) * T.inv_h;
     if (!(u >= 0.0 && u < (double)(T.m - 1))) return igami(a, p);
     int j = (int)u;
