@@ -14,8 +14,25 @@ import os as _os
 # stream and the exchange-issue stream run concurrently: more than HIP's default of 4 hardware
 # queues per process, beyond which two streams share a queue and serialise (measured 1.5-4 ms per
 # cfg3 step, profiles/r03).  Read when the HIP runtime initialises, i.e. at the first GPU call:
-# effective when this package is imported first; an explicit setting is kept.
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# effective when this package is imported before anything initialises HIP (import it before the
+# first torch.cuda call); an explicit setting is kept.  Child processes inherit the variable.
+def _hw_queues():
+    import sys
+
+    if "GPU_MAX_HW_QUEUES" in _os.environ:
+        return
+    _os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    torch = sys.modules.get("torch")  # never imported here: only asks whether HIP is already up
+    if torch is not None and torch.cuda.is_initialized():
+        import warnings
+
+        warnings.warn("probabilit_amd was imported after the HIP runtime started: GPU_MAX_HW_QUEUES=8 has no "
+                      "effect in this process, so its concurrent streams share HIP's default 4 hardware queues "
+                      "(slower, same results); import probabilit_amd first or export GPU_MAX_HW_QUEUES=8",
+                      RuntimeWarning, stacklevel=3)
+
+
+_hw_queues()
 
 from .modeling import (  # noqa: F401,E402
     Constant,

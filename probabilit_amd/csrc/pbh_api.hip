@@ -85,7 +85,7 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* codes = c.take((size_t)n * k * 4);
   void* colpart = c.take((size_t)k * perm_scores_blocks(n) * 8);
   void* s4s = c.take(step4_gen_shared_bytes(k));
-  void* s4c = c.take(step4_gen_column_bytes(n) * step4_streams());
+  void* s4c = c.take(step4_gen_column_bytes(n) * step4_lanes_configured());
   void* hall = c.take((size_t)k * kHeadsCap * 4);
   void* hcur = c.take((size_t)k * 4);
   if (carve) {
@@ -669,8 +669,8 @@ size_t owned_bytes(int64_t n, int m, void* base, OwnedLayout* o) {
   Carver c(base);
   OwnedLayout l;
   l.shared = c.take(step4_gen_shared_bytes(m));
-  l.lanes = c.take(step4_gen_column_bytes(n) * kStep4MaxStreams);
-  l.codes = c.take(align256((size_t)n * 4) * kStep4MaxStreams);
+  l.lanes = c.take(step4_gen_column_bytes(n) * step4_lanes_configured());
+  l.codes = c.take(align256((size_t)n * 4) * step4_lanes_configured());
   l.reorder = c.take(reorder_ws_bytes(n));
   l.tmp = c.take((size_t)n * 8);
   l.tmp2 = c.take((size_t)n * 8);

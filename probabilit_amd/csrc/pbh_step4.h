@@ -59,7 +59,8 @@ bool step4_fused();
 // most kStep4MaxStreams), each with its own Step4Column staging, so that one column's VALU- or
 // latency-bound kernels (bucket finish, gen_place) overlap another's bandwidth-bound passes
 constexpr int kStep4MaxStreams = 4;
-int step4_streams();
+int step4_streams();            // lanes in use now (1 in the serial measurement mode)
+int step4_lanes_configured();   // lanes a workspace is sized for (>= step4_streams() always)
 extern int g_serial;  // pbh_set_serial (measurement mode: one lane, counts not deferred)
 // the side streams of this device, created once (thread-safe) and kept for the process
 hipStream_t step4_side_stream(int i);

@@ -1521,8 +1521,7 @@ void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb) {
 
 int g_serial = 0;  // pbh_set_serial: one lane, no deferred counts (standalone kernel durations)
 
-int step4_streams() {
-  if (g_serial) return 1;
+int step4_lanes_configured() {  // PBH_STEP4_STREAMS (default 3): the workspaces hold this many lanes
   static const int v = [] {
     const char* e = getenv("PBH_STEP4_STREAMS");
     int x = e ? atoi(e) : 3;
@@ -1530,6 +1529,8 @@ int step4_streams() {
   }();
   return v;
 }
+
+int step4_streams() { return g_serial ? 1 : step4_lanes_configured(); }
 
 hipStream_t step4_side_stream(int i) {
   // created once per device and kept for the life of the process (non-blocking: no implicit

@@ -380,12 +380,20 @@ def iman_conover_lhs(columns, P, n, group=None, phases=None, flags=None, defer=N
         raise ValueError(f"Iman-Conover on the device takes 1 to 128 variables, got {K}")
     if flags is None:
         flags = phases.zeros(K, "int32")
+    # every attempt flags into a scratch word per column; the caller's words are OR-ed with the
+    # attempt that stands, so bits set before the call are kept and a redone attempt's are not doubled
     if defer:
+        scratch = phases.zeros(K, "int32")
         try:
-            return _iman_conover_lhs(columns, P, n, group, world, rank, phases, flags, True)
+            Y = _iman_conover_lhs(columns, P, n, group, world, rank, phases, scratch, True)
+            flags |= scratch
+            return Y
         except _Redo:
-            flags.zero_()
-    return _iman_conover_lhs(columns, P, n, group, world, rank, phases, flags, False)
+            pass
+    scratch = phases.zeros(K, "int32")
+    Y = _iman_conover_lhs(columns, P, n, group, world, rank, phases, scratch, False)
+    flags |= scratch
+    return Y
 
 
 def _iman_conover_lhs(columns, P, n, group, world, rank, phases, flags, defer):
