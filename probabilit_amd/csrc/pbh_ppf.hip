@@ -231,12 +231,6 @@ PBH_DI double gamma_ppf_lds(double q, const Params& prm, const PoissonTable& pt,
   return ppf_one<PBH_DIST_GAMMA>(q, prm.val[0], prm.val[1], prm.val[2], local);
 }
 
-// the same as a real call: a kernel's slow drain (igami's iteration inline sized the sweep kernel's
-// registers and spilled into its hot loop)
-__attribute__((noinline)) __device__ double gamma_ppf_lds_cold(double q, const Params& prm, const PoissonTable& pt,
-                                                                const sf::GammaGuide& T) {
-  return gamma_ppf_lds(q, prm, pt, T);
-}
 
 // igami_guided's interpolation branch and ppf_one's gamma wrapper, operation for operation:
 // true and *v = the value when the element needs no iteration; false sends it to the slow queue
@@ -328,7 +322,7 @@ __global__ __launch_bounds__(kGBlock) void k_ppf_gamma_lds(const double* __restr
     for (int t = threadIdx.x; t < nd; t += kGBlock) {
       const int64_t i = base + (ns <= kQCap ? slowq[t] : t);
       if (i >= n) continue;
-      const double x = gamma_ppf_lds_cold(q[i * q_stride], prm, pt, T);
+      const double x = gamma_ppf_lds(q[i * q_stride], prm, pt, T);
       out[i] = x;
       bad |= !isfinite(x);
     }

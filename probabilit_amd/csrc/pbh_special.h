@@ -140,11 +140,22 @@ PBH_HD inline double log_tab_pos_at(double x, const double* __restrict__ tab) {
   return s + lo;
 }
 
-// the general log_tab_at as a real call: a kernel's rare path (a subnormal argument), kept out of
-// the common path's code so that it is neither if-converted into it nor merged with it
-template <int S = 4>
-__attribute__((noinline)) PBH_HD inline double log_tab_cold(double x, const double* __restrict__ tab) {
-  return log_tab_at<S>(x, tab);
+// true when c holds on every active lane of the wave (device), c itself on the host.  A branch on
+// it is wave-uniform: a kernel's common path then runs without the selects of a rare case's code.
+PBH_HD inline bool wave_all(bool c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(!c) == 0ull;
+#else
+  return c;
+#endif
+}
+
+// ends the rare side of a wave_all branch: keeps the compiler from sinking the two sides' common
+// instructions into shared code (which needs every differing constant in a register on both)
+PBH_HD inline void rare_path_end() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __asm__ volatile("" ::: "memory");
+#endif
 }
 
 // e^y for y in [-700, 700] (the gamma guide's interpolated log x; its callers check the range):
@@ -174,8 +185,14 @@ PBH_HD inline double exp_tab(double y) { return exp_tab_at(y, &pbh_exp_tab[0][0]
 template <int S = 4>
 PBH_HD inline double log_odds_at(double p, const double* __restrict__ tab) {
   const double r = p / (1.0 - p);
-  if (r >= 0x1.0p-1022) return log_tab_pos_at<S>(r, tab);
-  return log_tab_cold<S>(r, tab);
+  double w;
+  if (wave_all(r >= 0x1.0p-1022)) {
+    w = log_tab_pos_at<S>(r, tab);
+  } else {
+    w = log_tab_at<S>(r, tab);
+    rare_path_end();
+  }
+  return w;
 }
 
 // ---------------------------------------------------------------- inverse normal CDF
@@ -208,10 +225,12 @@ PBH_HD inline double ndtri_centre(double y0) {
 }
 
 // Tail: ndtri_takes_tail(y0).  LT: log_tab's table and its stride (a kernel's LDS copy), or the
-// global table.  The second rational (z = sqrt(-2 log y) >= 8, i.e. y < exp(-32)) and the log of
-// a subnormal y are real calls: with them inline the compiler if-converted the branch on x < 8
-// into a per-lane select of every coefficient (~200 of the tail's ~420 instructions); now a wave
-// with no such lane runs one polynomial pair with scalar coefficients.  Same operations per lane.
+// global table.  A wave whose every y = min(y0, 1 - y0) is at least 1e-13 (always for the
+// van der Waerden scores, y >= 1 / (N + 1), and for LHS quantiles but for ~1e-13 / stratum width of
+// a stratum) takes a common path: log y and log x of positive normal arguments (no special-value
+// selects), and only the x < 8 rational (x = sqrt(-2 log y) <= 7.8), with scalar coefficients.
+// Inline, the branch on x < 8 had been if-converted into a per-lane select of all 34 coefficients
+// (~200 of ~420 instructions).  Any other wave runs the general code.  Same operations per lane.
 PBH_HD inline double ndtri_tail_near(double z) {  // x in [2, 8)
   const double P1[9] = {4.05544892305962419923e0, 3.15251094599893866154e1, 5.71628192246421288162e1,
                         4.40805073893200834700e1, 1.46849561928858024014e1, 2.18663306850790267539e0,
@@ -221,7 +240,7 @@ PBH_HD inline double ndtri_tail_near(double z) {  // x in [2, 8)
                         -3.80806407691578277194e-2, -9.33259480895457427372e-4};
   return z * polevl(z, P1, 8) / p1evl(z, Q1, 8);
 }
-__attribute__((noinline)) PBH_HD inline double ndtri_tail_far(double z) {  // x in [8, 64)
+PBH_HD inline double ndtri_tail_far(double z) {  // x in [8, 64)
   const double P2[9] = {3.23774891776946035970e0, 6.91522889068984211695e0, 3.93881025292474443415e0,
                         1.33303460815807542389e0, 2.01485389549179081538e-1, 1.23716634817820021358e-2,
                         3.01581553508235416007e-4, 2.65806974686737550832e-6, 6.23974539184983293730e-9};
@@ -239,22 +258,19 @@ PBH_HD inline double ndtri_tail_at(double y0, const double* __restrict__ lt) {
     y = 1.0 - y;
     negate = false;
   }
-  // y in (0, exp(-2)]: log y is finite and x = sqrt(-2 log y) lies in [2, 39), so log x needs no
-  // special-value handling, and log y only for a subnormal y
-  double ly;
-  if (y >= 0x1.0p-1022)
-    ly = log_tab_pos_at<S>(y, lt);
-  else
-    ly = log_tab_cold<S>(y, lt);
-  double x = sqrt(-2.0 * ly);
-  const double x0 = x - log_tab_pos_at<S>(x, lt) / x;
-  const double z = 1.0 / x;
-  double x1;
-  if (x < 8.0)
-    x1 = ndtri_tail_near(z);
-  else
-    x1 = ndtri_tail_far(z);
-  x = x0 - x1;
+  double x;
+  if (wave_all(y >= 1e-13)) {
+    x = sqrt(-2.0 * log_tab_pos_at<S>(y, lt));
+    const double x0 = x - log_tab_pos_at<S>(x, lt) / x;
+    x = x0 - ndtri_tail_near(1.0 / x);
+  } else {
+    x = sqrt(-2.0 * log_tab_at<S>(y, lt));
+    const double x0 = x - log_tab_at<S>(x, lt) / x;
+    const double z = 1.0 / x;
+    const double x1 = x < 8.0 ? ndtri_tail_near(z) : ndtri_tail_far(z);
+    x = x0 - x1;
+    rare_path_end();
+  }
   return negate ? -x : x;
 }
 PBH_HD inline double ndtri_tail(double y0) { return ndtri_tail_at(y0, &pbh_log_tab[0][0]); }
