@@ -628,7 +628,13 @@ __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int6
 // loads and stores two consecutive rows of a column with one 16-byte access (codes: 8 bytes), so
 // a tile takes half the memory instructions.  The even rows of the tile feed the first 16-row
 // MFMA block and the odd rows the second; the LDS transpose puts them back in row order.
-// Needs ld, ldc even and S / codes 16- / 8-byte aligned (checked on the host).
+// Needs ld, ldc even and S / codes 16- / 8-byte aligned (checked on the host).  The default step 3
+// (interleaved A/B, profiles/r04/README_ab.md: 13.5-13.6 against 15.0-15.1 ms per cfg3 step).
+// NT: non-temporal accesses as well (streaming: S, CS and the codes are not re-read by this kernel).
+typedef double v2d __attribute__((ext_vector_type(2)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+template <bool NT>
 __global__ __launch_bounds__(256) void k_apply_mfma_w2(double* __restrict__ S, int64_t n, int k, int64_t ld,
                                                        const double* __restrict__ M, uint32_t* __restrict__ codes,
                                                        int64_t ldc, CodeMap cm) {
@@ -663,7 +669,8 @@ __global__ __launch_bounds__(256) void k_apply_mfma_w2(double* __restrict__ S, i
       if (tw < tiles && c < k) {
         const double* src = &S[(int64_t)c * ld + r];
         if (r + 1 < n) {
-          v = *(const double2*)src;
+          const v2d t = NT ? __builtin_nontemporal_load((const v2d*)src) : *(const v2d*)src;
+          v = double2{t.x, t.y};
         } else if (r < n) {
           v.x = src[0];
         }
@@ -702,8 +709,18 @@ __global__ __launch_bounds__(256) void k_apply_mfma_w2(double* __restrict__ S, i
         const double v0 = tl[(2 * rp) * 33 + c], v1 = tl[(2 * rp + 1) * 33 + c];
         double* dst = &S[(int64_t)c * ld + r];
         if (r + 1 < n) {
-          *(double2*)dst = double2{v0, v1};
-          if (codes) *(uint2*)&codes[(int64_t)c * ldc + r] = uint2{code_of(v0, cm), code_of(v1, cm)};
+          const v2d t = {v0, v1};
+          if (NT)
+            __builtin_nontemporal_store(t, (v2d*)dst);
+          else
+            *(v2d*)dst = t;
+          if (codes) {
+            const v2u cc = {code_of(v0, cm), code_of(v1, cm)};
+            if (NT)
+              __builtin_nontemporal_store(cc, (v2u*)&codes[(int64_t)c * ldc + r]);
+            else
+              *(v2u*)&codes[(int64_t)c * ldc + r] = cc;
+          }
         } else {
           dst[0] = v0;
           if (codes) codes[(int64_t)c * ldc + r] = code_of(v0, cm);
@@ -854,15 +871,20 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
       const char* e = getenv("PBH_APPLY_NT");
       return e && atoi(e) == 1;
     }();
-    static const bool w2 = [] {
+    static const bool w2 = [] {  // PBH_APPLY_W2=0: the one-row kernel (variant tests)
       const char* e = getenv("PBH_APPLY_W2");
-      return e && atoi(e) == 1;
+      return !(e && atoi(e) == 0);
     }();
     const bool w2_ok = w2 && rows == 32 && ld % 2 == 0 && ((uintptr_t)S & 15) == 0 &&
                        (!codes || (ldc % 2 == 0 && ((uintptr_t)codes & 7) == 0));
-    if (w2_ok)
+    if (w2_ok && nt)
       PBH_TIMED(kKApply, s,
-                hipLaunchKernelGGL(k_apply_mfma_w2, dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc, c));
+                hipLaunchKernelGGL(k_apply_mfma_w2<true>, dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc,
+                                   c));
+    else if (w2_ok)
+      PBH_TIMED(kKApply, s,
+                hipLaunchKernelGGL(k_apply_mfma_w2<false>, dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc,
+                                   c));
     else if (rows == 32 && nt)
       PBH_TIMED(kKApply, s,
                 hipLaunchKernelGGL((k_apply_mfma<32, true>), dim3(gb > 0 ? gb : 1), b, 0, s, S, n, k, ld, M, codes, ldc,

@@ -1648,12 +1648,9 @@ int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs,
   PBH_CHECK_HIP(hipMemsetAsync(flags, 0, (size_t)kk * 4, s));
   // >= 64 K codes per block and at most 64 blocks per column: every block flushes its non-empty
   // counters with global atomics (~64 K each), which the PMC pass counted as ~2 GB of writes at
-  // 256 blocks per column (pmc_traffic_r72_ck1.json)
-  static const int64_t cap = [] {  // PBH_HIST_BLOCKS: blocks per column (fewer: fewer flush atomics)
-    const char* e = getenv("PBH_HIST_BLOCKS");
-    const int64_t v = e ? atoll(e) : 64;
-    return v >= 8 && v <= 256 ? v : 64;
-  }();
+  // 256 blocks per column (pmc_traffic_r72_ck1.json).  32 and 128 blocks measured no better
+  // (profiles/r04/README_ab.md).
+  constexpr int64_t cap = 64;
   int64_t blocks = (n + 65535) / 65536;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
