@@ -144,6 +144,21 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void k_
   }
 }
 
+// ndtri's branches alone over y = (hash(r) + 1) / (n + 1): MODE 1 every element through ndtri_centre
+// (y folded into the centre), MODE 2 every element through ndtri_tail (y folded into the tail)
+template <int MODE>
+__global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void k_branch(int64_t n,
+                                                                                        double* __restrict__ S) {
+  const double np1 = (double)(n + 1);
+  for (int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x; r < n; r += (int64_t)gridDim.x * kB) {
+    const double u = (double)((((uint64_t)(uint32_t)(r * 2654435761u)) * (uint64_t)n) >> 32) / np1;
+    double v;
+    if (MODE == 1) v = sf::ndtri_centre(0.1354 + 0.729 * u);
+    if (MODE == 2) v = sf::ndtri_tail(u < 0.5 ? u * 0.27 : 1.0 - (1.0 - u) * 0.27);
+    S[r] = v;
+  }
+}
+
 __global__ void k_write(int64_t n, double* __restrict__ S) {
   for (int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x; r < n; r += (int64_t)gridDim.x * kB) S[r] = (double)r;
 }
@@ -199,6 +214,9 @@ int main() {
   const float f24 = best([&] { hipLaunchKernelGGL(k_full<PermF24>, dim3(grid), dim3(kB), 0, 0, 7ull, n, S); });
   const float fh = best([&] { hipLaunchKernelGGL(k_full<PermHash>, dim3(grid), dim3(kB), 0, 0, 7ull, n, S); });
   const float w = best([&] { hipLaunchKernelGGL(k_write, dim3(8192), dim3(kB), 0, 0, n, S); });
+  const float brc = best([&] { hipLaunchKernelGGL(k_branch<1>, dim3(grid * 8), dim3(kB), 0, 0, n, S); });
+  const float brt = best([&] { hipLaunchKernelGGL(k_branch<2>, dim3(grid * 8), dim3(kB), 0, 0, n, S); });
+  printf("{\"centre_all\": %.4f, \"tail_all\": %.4f}\n", brc, brt);
   printf("{\"n\": %lld, \"perm_cur\": %.4f, \"perm_f24\": %.4f, \"full_cur\": %.4f, \"full_f24\": %.4f, "
          "\"full_hash\": %.4f, \"write\": %.4f, \"bad_strata_cur\": %lld, \"bad_strata_f24\": %lld}\n",
          (long long)n, pc, p24, fc, f24, fh, w, (long long)bc, (long long)b24);
