@@ -261,6 +261,8 @@ def main():
     e2e = end_to_end(root, ds, n, d, args.seed + args.warmup + args.steps, barrier, ms_per_step) \
         if (world == 1 and not args.no_e2e) else None
 
+    same_seed = reference_stream(root, args.seed, barrier) if (world == 1 and not args.no_e2e) else None
+
     sweep = ppf_sweep(lib, base, args.ppf_rows, args.seed) if (args.ppf_rows > 0 and rank == 0) else None
 
     cpu = None
@@ -281,7 +283,7 @@ def main():
                                            "out, positions back)") if world > 1 else "single",
                            "devices": torch.cuda.device_count() if world > 1 else 1},
                 "roofline": roofline, "pipeline_roofline": pipeline, "hbm_copy_peak": copy_peak,
-                "end_to_end": e2e, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels,
+                "end_to_end": e2e, "reference_stream": same_seed, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels,
                 "kernels_standalone": standalone}
         print(json.dumps(line))
     if dist is not None:
@@ -429,6 +431,25 @@ def end_to_end(root, ds, n, d, seed, barrier, device_ms):
             "d2h_GBps": round(nbytes / (d2h_ms / 1e3) / 1e9, 2), "bytes": nbytes,
             "what": f"Node.sample() with numpy samples_ on all columns (pinned-ring D2H, "
                     f"{device.__dict__['_STAGE_BYTES'] >> 20} MiB chunks)"}
+
+
+def reference_stream(root, seed, barrier, n=10_000_000, reps=2):
+    """The same-seed mode (stream="reference": scipy's LatinHypercube(d, rng=seed) stream bit for
+    bit, modeling.py:480,488 -> scipy _random_lhs) on the cfg3 graph at N = 1e7, device-resident
+    output: the device PCG64 uniforms, the d sequential Fisher-Yates shuffles on host threads
+    (pbh_lhs_reference) and their upload, then the same ppf + Iman-Conover.  A side figure."""
+    root.sample_device(n, random_state=seed, method="lhs", stream="reference")  # warm (workspaces)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(reps):
+        root.sample_device(n, random_state=seed + 1 + i, method="lhs", stream="reference")
+    barrier()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    d = root.num_distribution_nodes()
+    return {"value": round(n * d / (ms / 1e3) / 1e6, 2), "unit": "Msamples/s", "ms": round(ms, 1), "rows": n, "d": d,
+            "host_threads": os.environ.get("OMP_NUM_THREADS"),
+            "what": "Node.sample_device(1e7, method='lhs', stream='reference'): same results as the reference on "
+                    "the same seed; the shuffles are sequential per column (host threads)"}
 
 
 def cpu_baseline(n, d):
