@@ -10,3 +10,4 @@ timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS
 echo "pmc2 exit $?"
 cd $R
 bash tools/gpu/ab_env.sh ${TAG}_ab "-" "PBH_APPLY_NT=1"
+bash $R/tools/gpu/timeline.sh ${TAG}_tl > $R/gpurun_out/${TAG}_timeline.txt 2>&1; echo "timeline exit $?"; tail -25 $R/gpurun_out/${TAG}_timeline.txt

@@ -40,3 +40,21 @@ end = max(v[1] for v in tab.values())
 print(f"last step: {end / 1e6:.2f} ms, {len(step)} kernels")
 for (st, f), (a, b, busy, cnt) in sorted(tab.items(), key=lambda kv: kv[1][0]):
     print(f"stream {st:>3s} {f:10s} {a / 1e6:8.2f} .. {b / 1e6:8.2f} ms  busy {busy / 1e6:7.2f} ms  {cnt:5d} kernels")
+
+# device idle time inside the step: the gaps in the union of every kernel's [start, end), with the
+# kernels on either side of the largest ones (host synchronisations, launch latency)
+iv = sorted((int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0, r["Kernel_Name"]) for r in step)
+gaps, cur_end, prev = [], iv[0][1], iv[0][2]
+for a, b, nm in iv[1:]:
+    if a > cur_end:
+        gaps.append((a - cur_end, cur_end, prev[:40], nm[:40]))
+    if b > cur_end:
+        cur_end, prev = b, nm
+idle = sum(g[0] for g in gaps)
+print(f"device idle inside the step: {idle / 1e6:.2f} ms in {len(gaps)} gaps (busy union {(end - idle) / 1e6:.2f} ms)")
+for g, at, before, after in sorted(gaps, reverse=True)[:12]:
+    print(f"  gap {g / 1e3:8.1f} us at {at / 1e6:8.2f} ms  after {before}  before {after}")
+prev_steps = rows[:first]
+if prev_steps:
+    last_prev = max(int(r["End_Timestamp"]) for r in prev_steps)
+    print(f"gap from the previous step's last kernel: {(t0 - last_prev) / 1e3:.1f} us")
