@@ -62,7 +62,39 @@ typedef enum pbh_dist {
   PBH_DIST_LOMAX = 21,       /* c                                expm1(-log1p(-q) / c)          */
   PBH_DIST_GENEXTREME = 22,  /* c                                -expm1(-c x) / c, x = gumbel_r */
   PBH_DIST_GOMPERTZ = 23,    /* c                                log1p(-log1p(-q) / c)          */
-  PBH_DIST_CHI2 = 24         /* df                               2 gammaincinv(df / 2, q)       */
+  PBH_DIST_CHI2 = 24,        /* df                               2 gammaincinv(df / 2, q)       */
+  /* round 4: 30 more closed-form (or ndtri / gammaincinv based) scipy _ppf bodies; erlang is
+   * gamma (the same _ppf) and reuses PBH_DIST_GAMMA */
+  PBH_DIST_HALFCAUCHY = 25,   /*          tan(pi / 2 q) */
+  PBH_DIST_HALFLOGISTIC = 26, /*          2 atanh(q) */
+  PBH_DIST_HALFNORM = 27,     /*          ndtri((1 + q) / 2) */
+  PBH_DIST_ARCSINE = 28,      /*          sin(pi / 2 q)^2 */
+  PBH_DIST_HYPSECANT = 29,    /*          log(tan(pi q / 2)) */
+  PBH_DIST_POWERLAW = 30,     /* a        pow(q, 1/a) */
+  PBH_DIST_GENPARETO = 31,    /* c        -boxcox1p(-q, -c) */
+  PBH_DIST_FISK = 32,         /* c        burr with d = 1 */
+  PBH_DIST_BURR = 33,         /* c, d     (q^(-1/d) - 1)^(-1/c) */
+  PBH_DIST_BURR12 = 34,       /* c, d     expm1(-log1p(-q) / d)^(1/c) */
+  PBH_DIST_EXPONWEIB = 35,    /* a, c     (-log1p(-q^(1/a)))^(1/c) */
+  PBH_DIST_EXPONPOW = 36,     /* b        log1p(-log1p(-q))^(1/b) */
+  PBH_DIST_BRADFORD = 37,     /* c        expm1(q log1p(c)) / c */
+  PBH_DIST_ANGLIT = 38,       /*          asin(sqrt(q)) - pi/4 */
+  PBH_DIST_LEVY = 39,         /*          1 / ndtri(q/2)^2 */
+  PBH_DIST_LEVY_L = 40,       /*          -1 / ndtri((q+1)/2)^2 */
+  PBH_DIST_GIBRAT = 41,       /*          exp(ndtri(q)) */
+  PBH_DIST_INVWEIBULL = 42,   /* c        (-log q)^(-1/c) */
+  PBH_DIST_LOGLAPLACE = 43,   /* c        (2q)^(1/c) | (2(1-q))^(-1/c) */
+  PBH_DIST_TRUNCEXPON = 44,   /* b        -log1p(q expm1(-b)) */
+  PBH_DIST_CHI = 45,          /* df       sqrt(2 gammaincinv(df/2, q)) */
+  PBH_DIST_MAXWELL = 46,      /*          sqrt(2 gammaincinv(1.5, q)) */
+  PBH_DIST_NAKAGAMI = 47,     /* nu       sqrt(gammaincinv(nu, q) / nu) */
+  PBH_DIST_DWEIBULL = 48,     /* c        +-(-log(2 min(q, 1-q)))^(1/c) */
+  PBH_DIST_KAPPA3 = 49,       /* a        (a / (q^-a - 1))^(1/a) */
+  PBH_DIST_GENHALFLOGISTIC = 50,/* c        (1 - ((1-q)/(1+q))^c) / c */
+  PBH_DIST_ALPHA = 51,        /* a        1 / (a - ndtri(q ndtr(a))) */
+  PBH_DIST_FATIGUELIFE = 52,  /* c        (c z + sqrt((c z)^2 + 4))^2 / 4 */
+  PBH_DIST_GENLOGISTIC = 53,  /* c        -log(powm1(q, -1/c)) */
+  PBH_DIST_TRAPEZOID = 54     /* c, d     three pieces at cdf(c), cdf(d) */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

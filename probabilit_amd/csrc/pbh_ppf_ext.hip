@@ -35,14 +35,44 @@ struct Params4 {
   __device__ __forceinline__ double at(int j, int64_t i) const { return ptr[j] ? ptr[j][i] : val[j]; }
 };
 
-constexpr bool is_closed(int d) { return d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_CHI2; }
+constexpr bool is_closed(int d) { return d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID; }
 
 constexpr int closed_shapes(int d) {
-  return d == PBH_DIST_LOGUNIFORM ? 2
+  return (d == PBH_DIST_LOGUNIFORM || d == PBH_DIST_BURR || d == PBH_DIST_BURR12 || d == PBH_DIST_EXPONWEIB ||
+          d == PBH_DIST_TRAPEZOID)
+             ? 2
          : (d == PBH_DIST_WEIBULL_MIN || d == PBH_DIST_WEIBULL_MAX || d == PBH_DIST_PARETO || d == PBH_DIST_LOMAX ||
-            d == PBH_DIST_GENEXTREME || d == PBH_DIST_GOMPERTZ || d == PBH_DIST_CHI2)
+            d == PBH_DIST_GENEXTREME || d == PBH_DIST_GOMPERTZ || d == PBH_DIST_CHI2 || d == PBH_DIST_POWERLAW ||
+            d == PBH_DIST_GENPARETO || d == PBH_DIST_FISK || d == PBH_DIST_EXPONPOW || d == PBH_DIST_BRADFORD ||
+            d == PBH_DIST_INVWEIBULL || d == PBH_DIST_LOGLAPLACE || d == PBH_DIST_TRUNCEXPON || d == PBH_DIST_CHI ||
+            d == PBH_DIST_NAKAGAMI || d == PBH_DIST_DWEIBULL || d == PBH_DIST_KAPPA3 ||
+            d == PBH_DIST_GENHALFLOGISTIC || d == PBH_DIST_ALPHA || d == PBH_DIST_FATIGUELIFE ||
+            d == PBH_DIST_GENLOGISTIC)
              ? 1
              : 0;
+}
+
+// scipy.special.boxcox1p (scipy _boxcox.pxd): log1p(x) for a vanishing lambda, else
+// expm1(lambda log1p(x)) / lambda
+__device__ __forceinline__ double boxcox1p(double x, double lmbda) {
+  const double lgx = log1p(x);
+  if (fabs(lmbda) < 1e-19 || (fabs(lgx) < 1e-289 && fabs(lmbda) < 1e273)) return lgx;
+  return expm1(lmbda * lgx) / lmbda;
+}
+
+// scipy.special.powm1 (Boost powm1) for x > 0: expm1(y log x) when that is the accurate form,
+// else pow(x, y) - 1
+__device__ __forceinline__ double powm1(double x, double y) {
+  if (x > 0.0 && (fabs(y * (x - 1.0)) < 0.5 || fabs(y) < 0.2)) {
+    const double l = y * log(x);
+    if (l < 0.5) return expm1(l);
+  }
+  return pow(x, y) - 1.0;
+}
+
+// trapezoid._cdf(x, c, d) at x = c and x = d (the middle piece), the breaks of its _ppf
+__device__ __forceinline__ double trapezoid_mid_cdf(double x, double c, double d) {
+  return (c + 2.0 * (x - c)) / (d - c + 1.0);
 }
 
 // _argcheck and the support [_a, _b] of scipy's class (rv_continuous default: every shape > 0)
@@ -67,7 +97,32 @@ __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo,
     if (s0 < 0.0) lo = 1.0 / fmin(s0, -tiny);
     return isfinite(s0);
   }
+  if constexpr (D == PBH_DIST_HALFCAUCHY || D == PBH_DIST_HALFLOGISTIC || D == PBH_DIST_HALFNORM ||
+                D == PBH_DIST_POWERLAW || D == PBH_DIST_GENPARETO || D == PBH_DIST_FISK || D == PBH_DIST_BURR ||
+                D == PBH_DIST_BURR12 || D == PBH_DIST_EXPONWEIB || D == PBH_DIST_EXPONPOW ||
+                D == PBH_DIST_BRADFORD || D == PBH_DIST_LEVY || D == PBH_DIST_GIBRAT || D == PBH_DIST_INVWEIBULL ||
+                D == PBH_DIST_LOGLAPLACE || D == PBH_DIST_TRUNCEXPON || D == PBH_DIST_CHI ||
+                D == PBH_DIST_MAXWELL || D == PBH_DIST_NAKAGAMI || D == PBH_DIST_KAPPA3 ||
+                D == PBH_DIST_GENHALFLOGISTIC || D == PBH_DIST_ALPHA || D == PBH_DIST_FATIGUELIFE ||
+                D == PBH_DIST_ARCSINE || D == PBH_DIST_TRAPEZOID)
+    lo = 0.0;
+  if constexpr (D == PBH_DIST_ARCSINE || D == PBH_DIST_POWERLAW || D == PBH_DIST_BRADFORD ||
+                D == PBH_DIST_TRAPEZOID)
+    hi = 1.0;
+  if constexpr (D == PBH_DIST_LEVY_L) hi = 0.0;
+  if constexpr (D == PBH_DIST_ANGLIT) {
+    lo = -sf::kPi / 4;
+    hi = sf::kPi / 4;
+  }
+  if constexpr (D == PBH_DIST_GENPARETO) {  // _argcheck isfinite(c); support [0, -1 / c) for c < 0
+    if (s0 < 0.0) hi = -1.0 / s0;
+    return isfinite(s0);
+  }
+  if constexpr (D == PBH_DIST_TRUNCEXPON) hi = s0;  // support [0, b]
+  if constexpr (D == PBH_DIST_GENHALFLOGISTIC) hi = 1.0 / s0;  // support [0, 1 / c]
+  if constexpr (D == PBH_DIST_TRAPEZOID) return s0 >= 0.0 && s0 <= 1.0 && s1 >= 0.0 && s1 <= 1.0 && s1 >= s0;
   if constexpr (closed_shapes(D) == 1) return s0 > 0.0;
+  if constexpr (closed_shapes(D) == 2) return s0 > 0.0 && s1 > 0.0;
   return true;
 }
 
@@ -100,6 +155,60 @@ __device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
   }
   if constexpr (D == PBH_DIST_GOMPERTZ) return log1p(-1.0 / s0 * log1p(-q));
   if constexpr (D == PBH_DIST_CHI2) return 2.0 * sf::igami(s0 / 2.0, q);
+  // round 4 (scipy 1.15 _continuous_distns.py _ppf bodies, operation for operation)
+  if constexpr (D == PBH_DIST_HALFCAUCHY) return tan(sf::kPi / 2 * q);
+  if constexpr (D == PBH_DIST_HALFLOGISTIC) return 2 * atanh(q);
+  if constexpr (D == PBH_DIST_HALFNORM) return sf::ndtri((1 + q) / 2.0);
+  if constexpr (D == PBH_DIST_ARCSINE) {
+    const double v = sin(sf::kPi / 2.0 * q);
+    return v * v;  // ** 2.0: numpy's square
+  }
+  if constexpr (D == PBH_DIST_HYPSECANT) return log(tan(sf::kPi * q / 2.0));
+  if constexpr (D == PBH_DIST_POWERLAW) return pow(q, 1.0 / s0);
+  if constexpr (D == PBH_DIST_GENPARETO) return -boxcox1p(-q, -s0);
+  if constexpr (D == PBH_DIST_FISK) return pow(1.0 / q - 1, -1.0 / s0);  // q ** -1.0: numpy's reciprocal
+  if constexpr (D == PBH_DIST_BURR) return pow(pow(q, -1.0 / s1) - 1, -1.0 / s0);
+  if constexpr (D == PBH_DIST_BURR12) return pow(expm1(-1 / s1 * log1p(-q)), 1 / s0);
+  if constexpr (D == PBH_DIST_EXPONWEIB) return pow(-log1p(-pow(q, 1.0 / s0)), 1.0 / s1);
+  if constexpr (D == PBH_DIST_EXPONPOW) return pow(log1p(-log1p(-q)), 1.0 / s0);
+  if constexpr (D == PBH_DIST_BRADFORD) return expm1(q * log1p(s0)) / s0;
+  if constexpr (D == PBH_DIST_ANGLIT) return asin(sqrt(q)) - sf::kPi / 4;
+  if constexpr (D == PBH_DIST_LEVY) {
+    const double v = -sf::ndtri(q / 2);  // _norm_isf(q / 2)
+    return 1.0 / (v * v);
+  }
+  if constexpr (D == PBH_DIST_LEVY_L) {
+    const double v = sf::ndtri((q + 1.0) / 2);
+    return -1.0 / (v * v);
+  }
+  if constexpr (D == PBH_DIST_GIBRAT) return exp(sf::ndtri(q));
+  if constexpr (D == PBH_DIST_INVWEIBULL) return pow(-log(q), -1.0 / s0);
+  if constexpr (D == PBH_DIST_LOGLAPLACE) return q < 0.5 ? pow(2.0 * q, 1.0 / s0) : pow(2 * (1.0 - q), -1.0 / s0);
+  if constexpr (D == PBH_DIST_TRUNCEXPON) return -log1p(q * expm1(-s0));
+  if constexpr (D == PBH_DIST_CHI) return sqrt(2 * sf::igami(.5 * s0, q));
+  if constexpr (D == PBH_DIST_MAXWELL) return sqrt(2 * sf::igami(1.5, q));
+  if constexpr (D == PBH_DIST_NAKAGAMI) return sqrt(1.0 / s0 * sf::igami(s0, q));
+  if constexpr (D == PBH_DIST_DWEIBULL) {
+    double fac = 2. * (q <= 0.5 ? q : 1. - q);
+    fac = pow(-log(fac), 1.0 / s0);
+    return q > 0.5 ? fac : -fac;
+  }
+  if constexpr (D == PBH_DIST_KAPPA3) return pow(s0 / (pow(q, -s0) - 1.0), 1.0 / s0);
+  if constexpr (D == PBH_DIST_GENHALFLOGISTIC) return 1.0 / s0 * (1 - pow((1.0 - q) / (1.0 + q), s0));
+  if constexpr (D == PBH_DIST_ALPHA) return 1.0 / (s0 - sf::ndtri(q * sf::ndtr(s0)));
+  if constexpr (D == PBH_DIST_FATIGUELIFE) {
+    const double t = s0 * sf::ndtri(q);
+    const double u = t + sqrt(t * t + 4);
+    return 0.25 * (u * u);
+  }
+  if constexpr (D == PBH_DIST_GENLOGISTIC) return -log(powm1(q, -1.0 / s0));
+  if constexpr (D == PBH_DIST_TRAPEZOID) {
+    const double c = s0, d = s1;
+    const double qc = trapezoid_mid_cdf(c, c, d), qd = trapezoid_mid_cdf(d, c, d);
+    if (q < qc) return sqrt(q * c * (1 + d - c));
+    if (q <= qd) return 0.5 * q * (1 + d - c) + 0.5 * c;
+    return 1 - sqrt((1 - q) * (d - c + 1) * (1 - d));
+  }
   return sf::kNaN;
 }
 
@@ -203,6 +312,36 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_GENEXTREME)
     PBH_EXT(PBH_DIST_GOMPERTZ)
     PBH_EXT(PBH_DIST_CHI2)
+    PBH_EXT(PBH_DIST_HALFCAUCHY)
+    PBH_EXT(PBH_DIST_HALFLOGISTIC)
+    PBH_EXT(PBH_DIST_HALFNORM)
+    PBH_EXT(PBH_DIST_ARCSINE)
+    PBH_EXT(PBH_DIST_HYPSECANT)
+    PBH_EXT(PBH_DIST_POWERLAW)
+    PBH_EXT(PBH_DIST_GENPARETO)
+    PBH_EXT(PBH_DIST_FISK)
+    PBH_EXT(PBH_DIST_BURR)
+    PBH_EXT(PBH_DIST_BURR12)
+    PBH_EXT(PBH_DIST_EXPONWEIB)
+    PBH_EXT(PBH_DIST_EXPONPOW)
+    PBH_EXT(PBH_DIST_BRADFORD)
+    PBH_EXT(PBH_DIST_ANGLIT)
+    PBH_EXT(PBH_DIST_LEVY)
+    PBH_EXT(PBH_DIST_LEVY_L)
+    PBH_EXT(PBH_DIST_GIBRAT)
+    PBH_EXT(PBH_DIST_INVWEIBULL)
+    PBH_EXT(PBH_DIST_LOGLAPLACE)
+    PBH_EXT(PBH_DIST_TRUNCEXPON)
+    PBH_EXT(PBH_DIST_CHI)
+    PBH_EXT(PBH_DIST_MAXWELL)
+    PBH_EXT(PBH_DIST_NAKAGAMI)
+    PBH_EXT(PBH_DIST_DWEIBULL)
+    PBH_EXT(PBH_DIST_KAPPA3)
+    PBH_EXT(PBH_DIST_GENHALFLOGISTIC)
+    PBH_EXT(PBH_DIST_ALPHA)
+    PBH_EXT(PBH_DIST_FATIGUELIFE)
+    PBH_EXT(PBH_DIST_GENLOGISTIC)
+    PBH_EXT(PBH_DIST_TRAPEZOID)
 #undef PBH_EXT
     default:
       return false;

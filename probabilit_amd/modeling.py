@@ -26,6 +26,7 @@ import ctypes
 import functools
 import itertools
 import numbers
+import warnings
 
 import networkx as nx
 import numpy as np
@@ -592,7 +593,8 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "binom": ("n", "p"), "bernoulli": ("p",), "weibull_min": ("c",), "weibull_max": ("c",),
                 "logistic": (), "cauchy": (), "laplace": (), "gumbel_r": (), "gumbel_l": (), "pareto": ("b",),
                 "loguniform": ("a", "b"), "reciprocal": ("a", "b"), "rayleigh": (), "lomax": ("c",),
-                "genextreme": ("c",), "gompertz": ("c",), "chi2": ("df",)}
+                "genextreme": ("c",), "gompertz": ("c",), "chi2": ("df",), "erlang": ("a",),
+                "halfcauchy": (), "halflogistic": (), "halfnorm": (), "arcsine": (), "hypsecant": (), "powerlaw": ('a',), "genpareto": ('c',), "fisk": ('c',), "burr": ('c', 'd',), "burr12": ('c', 'd',), "exponweib": ('a', 'c',), "exponpow": ('b',), "bradford": ('c',), "anglit": (), "levy": (), "levy_l": (), "gibrat": (), "invweibull": ('c',), "loglaplace": ('c',), "truncexpon": ('b',), "chi": ('df',), "maxwell": (), "nakagami": ('nu',), "dweibull": ('c',), "kappa3": ('a',), "genhalflogistic": ('c',), "alpha": ('a',), "fatiguelife": ('c',), "genlogistic": ('c',), "trapezoid": ('c', 'd',)}
 _DISCRETE = {"poisson", "binom", "bernoulli"}
 # distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so
 # that Iman-Conover takes them as generated columns (pbh_ppf.hip k_lhs_sorted_ppf / k_place_gen;
@@ -656,7 +658,12 @@ class Distribution(AbstractDistribution):
                 raise NotImplementedError(f"array-valued parameter of shape {a.shape} for size {n}")
             return device.to_device(a)
 
-        return [resolve(v) for v in _parse_scipy_args(name, self.args, self.kwargs)]
+        vals = _parse_scipy_args(name, self.args, self.kwargs)
+        if name == "erlang" and not isinstance(vals[0], Node) and not np.all(np.floor(vals[0]) == vals[0]):
+            # scipy's erlang_gen._argcheck warns (and samples anyway)
+            warnings.warn("The shape parameter of the erlang distribution has been given a non-integer value "
+                          f"{np.asarray(vals[0])!r}.", RuntimeWarning, stacklevel=4)
+        return [resolve(v) for v in vals]
 
     def _sample_device(self, ev, column, out=None):
         n = ev.size

@@ -118,9 +118,28 @@ _CLOSED = [("weibull_min", dict(c=1.7)), ("weibull_min", dict(c=0.4, loc=-2.0, s
            ("chi2", dict(df=1.0)), ("chi2", dict(df=5.5, loc=1.0, scale=2.0)), ("chi2", dict(df=55.0)),
            ("weibull_min", dict(c=-1.0)), ("pareto", dict(b=0.0)), ("loguniform", dict(a=2.0, b=1.0)),
            ("genextreme", dict(c=np.inf)), ("logistic", dict(scale=-1.0)), ("chi2", dict(df=-2.0))]
+# round 4: 30 more closed forms (pbh_ppf_ext.hip closed_ppf01, PBH_DIST_HALFCAUCHY..TRAPEZOID)
+_CLOSED2 = [("halfcauchy", dict()), ("halfcauchy", dict(loc=1.0, scale=2.0)), ("halflogistic", dict()),
+            ("halfnorm", dict()), ("halfnorm", dict(loc=-1.0, scale=0.5)), ("arcsine", dict()),
+            ("hypsecant", dict()), ("powerlaw", dict(a=1.66)), ("powerlaw", dict(a=0.3, scale=4.0)),
+            ("genpareto", dict(c=0.1)), ("genpareto", dict(c=-0.5)), ("genpareto", dict(c=0.0)),
+            ("fisk", dict(c=3.09)), ("burr", dict(c=10.5, d=4.3)), ("burr", dict(c=0.8, d=0.6, loc=1.0)),
+            ("burr12", dict(c=10.0, d=4.0)), ("burr12", dict(c=0.7, d=2.5)), ("exponweib", dict(a=2.89, c=1.95)),
+            ("exponpow", dict(b=2.7)), ("bradford", dict(c=0.3)), ("bradford", dict(c=40.0)), ("anglit", dict()),
+            ("levy", dict()), ("levy", dict(loc=2.0, scale=0.1)), ("levy_l", dict()), ("gibrat", dict()),
+            ("invweibull", dict(c=10.6)), ("invweibull", dict(c=0.7)), ("loglaplace", dict(c=3.25)),
+            ("truncexpon", dict(b=4.69)), ("truncexpon", dict(b=0.01)), ("chi", dict(df=0.78)),
+            ("chi", dict(df=7.0, scale=2.0)), ("maxwell", dict()), ("nakagami", dict(nu=4.97)),
+            ("nakagami", dict(nu=0.6)), ("dweibull", dict(c=2.07)), ("kappa3", dict(a=1.0)),
+            ("kappa3", dict(a=0.3)), ("genhalflogistic", dict(c=0.77)), ("alpha", dict(a=3.57)),
+            ("fatiguelife", dict(c=29.0)), ("fatiguelife", dict(c=0.3)), ("genlogistic", dict(c=0.41)),
+            ("genlogistic", dict(c=5.0)), ("trapezoid", dict(c=0.2, d=0.8)), ("trapezoid", dict(c=0.0, d=1.0)),
+            ("trapezoid", dict(c=0.5, d=0.5)), ("trapezoid", dict(c=0.7, d=0.3)), ("genpareto", dict(c=np.nan)),
+            ("burr", dict(c=-1.0, d=1.0)), ("powerlaw", dict(a=0.0)), ("erlang", dict(a=3)),
+            ("erlang", dict(a=1, loc=1.0, scale=2.0))]
 
 
-@pytest.mark.parametrize("name,kw", _CLOSED)
+@pytest.mark.parametrize("name,kw", _CLOSED + _CLOSED2)
 def test_closed_form_ppf(gpu, name, kw):
     import scipy.stats
 
@@ -193,7 +212,7 @@ def test_closed_form_correlated_iman_conover(gpu):
 _LHS_EXT = [("beta", dict(a=3.4, b=2.6, loc=0, scale=10)), ("beta", dict(a=0.5, b=0.5)),
             ("beta", dict(a=7.0, b=5.0, loc=-1.0, scale=3.0)), ("truncnorm", dict(a=-1.0, b=1.0, loc=2.0, scale=0.5)),
             ("truncnorm", dict(a=3.0, b=3.3)), ("binom", dict(n=20, p=0.3)), ("binom", dict(n=1000, p=0.7, loc=2)),
-            ("bernoulli", dict(p=0.25))] + [c for c in _CLOSED[:30]]
+            ("bernoulli", dict(p=0.25))] + [c for c in _CLOSED[:30]] + [c for c in _CLOSED2[:48]]
 
 
 @pytest.mark.parametrize("name,kw", _LHS_EXT)
