@@ -4,7 +4,7 @@ set -o pipefail
 TAG=${1:-r4e}
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out/$TAG
 timeout -k 10 900 python -u -m pytest tests/test_gpu_dists.py tests/test_gpu_step4_gen.py tests/test_gpu_ic.py tests/test_gpu_scale.py tests/test_gpu_distributed.py tests/test_gpu_step4_buckets.py -m gpu -q -rf --timeout 600 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
-rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/${TAG}_tests.log; [ $rc -eq 0 ] || exit $rc
+rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/${TAG}_tests.log; grep -E "^FAILED" gpurun_out/${TAG}_tests.log | head -40; [ $rc -le 1 ] || exit $rc
 bash tools/gpu/ab_env.sh ${TAG}_ab "-" "PBH_FINISH_CLASSES=0" "PBH_APPLY_NT=1" || exit $?
 bash tools/gpu/pmc.sh $TAG || exit $?
 python3 -c "
