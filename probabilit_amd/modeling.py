@@ -377,7 +377,8 @@ class Node(abc.ABC):
         return self._evaluate(source, correlator, gc_strategy, to_host=False, group=group)
 
     def _evaluate(self, source, correlator, gc_strategy, to_host, group=None):
-        assert nx.is_directed_acyclic_graph(self.to_graph())
+        G = self.to_graph()
+        assert nx.is_directed_acyclic_graph(G)
         n_dim = source.d
         assert n_dim == self.num_distribution_nodes()
         world, rank = 1, 0
@@ -395,19 +396,20 @@ class Node(abc.ABC):
         if isinstance(correlator, str):
             correlator = {"imanconover": ImanConover, "cholesky": Cholesky}[correlator.lower()]
 
-        for node in set(self.nodes()):
+        all_nodes = set(G.nodes) if G.number_of_nodes() else {self}
+        for node in all_nodes:
             if "_smp" in node.__dict__:
                 del node.samples_
 
         gc = GarbageCollector(strategy=gc_strategy).set_sink(self)
-        isns = sorted({n for n in self.nodes() if n._is_initial_sampling_node()}, key=lambda n: n._id)
-        G = self.to_graph()
+        isns = sorted({n for n in all_nodes if n._is_initial_sampling_node()}, key=lambda n: n._id)
+        isn_set = set(isns)
         ev = _Evaluation(size, list(G.nodes))
 
         # correlations are a property of the graph: gather and validate them first so that
         # the correlated ISNs can be written straight into one (K, N) block (:542-568)
         correlations = []
-        for node in set(self.nodes()):
+        for node in all_nodes:
             correlations.extend(getattr(node, "_correlations", []))
         variable_sets = [set(v) for (v, _) in correlations]
         all_variables = sorted(functools.reduce(set.union, variable_sets, set()), key=lambda n: n._id)
@@ -415,16 +417,17 @@ class Node(abc.ABC):
         # Fast path: correlated ISNs drawn from the native LHS with plain-number parameters
         # are handed to Iman-Conover as generator descriptors; their uncorrelated samples are
         # overwritten by the correlator anyway (:582-583), so they are never materialised.
+        all_set = set(all_variables)
         generated = (bool(correlations) and isinstance(source, qmc.LHSSource)
                      and isinstance(correlator, type) and issubclass(correlator, ImanConover)
-                     and set(all_variables) <= set(isns)
+                     and all_set <= isn_set
                      and all(type(v) is Distribution and v.distr in _FUSED_LHS and v.is_leaf
                              for v in all_variables))
         if world > 1 and correlations and not generated:
             raise NotImplementedError("row-sharded evaluation correlates natively generated LHS columns of leaf "
                                       "Distributions with Iman-Conover; evaluate this graph on one GPU")
         deferred = {}
-        if correlations and set(all_variables) <= set(isns) and not generated:
+        if correlations and all_set <= isn_set and not generated:
             block = device.empty((len(all_variables), size))
             block_row = {v: j for j, v in enumerate(all_variables)}
 
@@ -432,11 +435,12 @@ class Node(abc.ABC):
         fused = not correlations and dag.try_evaluate(list(nx.topological_sort(G)), isns, source, ev, gc)
         if not fused:
             for node in isns:  # (:529-538)
-                for anc in nx.topological_sort(G.subgraph(nx.ancestors(G, node))):
-                    assert isinstance(anc, (Constant, Transform))
-                    anc._set_device(anc._sample_device(ev))
+                if not node.is_leaf:  # (a leaf has no ancestors to sample)
+                    for anc in nx.topological_sort(G.subgraph(nx.ancestors(G, node))):
+                        assert isinstance(anc, (Constant, Transform))
+                        anc._set_device(anc._sample_device(ev))
                 assert isinstance(node, AbstractDistribution)
-                if generated and node in all_variables:
+                if generated and node in all_set:
                     deferred[node] = source.next_column()
                     continue
                 out = block[block_row[node]] if node in block_row else None
@@ -444,7 +448,7 @@ class Node(abc.ABC):
 
             for variables, _ in correlations:  # (:548-551)
                 for variable in variables:
-                    if variable not in isns:
+                    if variable not in isn_set:
                         raise ValueError(f"Cannot correlate variable: {variable}")
             for vars1, vars2 in itertools.combinations(variable_sets, 2):  # (:554-558)
                 common = vars1.intersection(vars2)
