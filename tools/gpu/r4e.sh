@@ -19,3 +19,4 @@ timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INST
 echo "pmc1 exit $?"
 cd $R
 bash tools/gpu/timeline.sh ${TAG}_tl > gpurun_out/${TAG}_timeline.txt 2>&1; echo "timeline exit $?"; tail -22 gpurun_out/${TAG}_timeline.txt
+timeout -k 10 300 python tools/ext_sweep.py 10000000 > gpurun_out/${TAG}_ext_sweep.json 2>&1; echo "ext_sweep exit $?"; cat gpurun_out/${TAG}_ext_sweep.json | tail -3
