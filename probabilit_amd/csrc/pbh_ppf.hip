@@ -1517,6 +1517,7 @@ int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* par
     }
     g->ext = true;
     for (int j = 0; j < nparams; ++j) g->xval[j] = params[j].value;
+    g->table = ext_gen_table(dist, g->xval, nparams, s);
     *out = g;
     return PBH_OK;
   }
@@ -1614,7 +1615,8 @@ int gen_sorted(const GenColumn* g, int64_t t0, int64_t nt, double* out, int32_t*
   }
   if (nt == 0) return PBH_OK;
   if (g->ext)
-    return ext_gen_sorted(g->seed, n, g->col, g->dist, g->xval, t0, nt, out, flag, counts, heads, hcur, hcap, s);
+    return ext_gen_sorted(g->seed, n, g->col, g->dist, g->xval, g->table, t0, nt, out, flag, counts, heads, hcur, hcap,
+                          s);
   static const bool fast_heads = [] {  // PBH_DISCRETE_SCAN=1: evaluate every stratum
     const char* e = getenv("PBH_DISCRETE_SCAN");
     return !(e && e[0] == '1');
@@ -1665,12 +1667,13 @@ static double cert_gap(int dist, const double* v);
 double gen_cert_gap(const GenColumn* g) {
   // cached per (family, parameters): the supremum scan costs ~4 ms of host time
   static std::mutex mu;
-  static std::map<std::array<double, 4>, double> cache;
-  const std::array<double, 4> key = {(double)g->dist, g->prm.val[0], g->prm.val[1], g->prm.val[2]};
+  static std::map<std::array<double, 5>, double> cache;
+  const double* v = g->ext ? g->xval : g->prm.val;
+  const std::array<double, 5> key = {(double)g->dist, v[0], v[1], v[2], g->ext ? v[3] : 0.0};
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  const double T = cert_gap(g->dist, g->prm.val);
+  const double T = cert_gap(g->dist, v);
   cache[key] = T;
   return T;
 }
@@ -1725,6 +1728,29 @@ static double cert_gap(int dist, const double* v) {
       lo = 1e-300, hi = 1e300, logy = true;
       break;
     }
+    case PBH_DIST_BETA: {  // the guided inverse (sfx::beta_ppf_guided) is within ~1e-12 of the exact one
+      const double a = v[0], b = v[1];
+      loc = v[2], scale = v[3], eps = 1e-9;
+      if (!(a >= 1.0 && b >= 1.0 && isfinite(a) && isfinite(b))) return 0.0;  // f0 bounded on [0, 1]
+      const double lb = lgamma(a) + lgamma(b) - lgamma(a + b);
+      f0 = [a, b, lb](double y) {
+        if (!(y > 0.0 && y < 1.0)) return (a == 1.0 && y == 0.0) || (b == 1.0 && y == 1.0) ? exp(-lb) : 0.0;
+        return exp((a - 1.0) * log(y) + (b - 1.0) * log1p(-y) - lb);
+      };
+      break;
+    }
+    case PBH_DIST_TRUNCNORM: {  // phi(y) / (Phi(b) - Phi(a)) on [a, b]; a log-space inverse, few-ulp accurate
+      const double a = v[0], b = v[1];
+      loc = v[2], scale = v[3], eps = 1e-9;
+      if (!(a < b) || !isfinite(a) || !isfinite(b)) return 0.0;
+      const double mass = 0.5 * (erfc(-b / sqrt(2.0)) - erfc(-a / sqrt(2.0)));
+      if (!(mass > 1e-300)) return 0.0;
+      f0 = [a, b, mass](double y) {
+        return y >= a && y <= b ? 0.3989422804014327 * exp(-0.5 * y * y) / mass : 0.0;
+      };
+      lo = a, hi = b;
+      break;
+    }
     default:
       return 0.0;
   }
@@ -1760,6 +1786,9 @@ int gen_certify(const GenColumn* g, int64_t t0, int64_t nt, double T, uint32_t* 
   hipLaunchKernelGGL(k_cert_scan, dim3(ppf_grid(nt)), dim3(kBlock), 0, s, g->seed, g->n, t0, nt, g->col, T, list, cap,
                      count);
   PBH_CHECK_LAUNCH();
+  if (g->ext)
+    return ext_gen_cert_eval(g->seed, g->n, g->col, g->dist, g->xval, g->table, t0, nt, list, cap, count, flag, counts,
+                             s);
   switch (g->dist) {
 #define PBH_CASE(D)                                                                                               \
   case D:                                                                                                         \
@@ -1787,8 +1816,8 @@ static int place_launch(const GenColumn* g, const uint64_t* pairs, const uint32_
                         int64_t y_rs, int32_t* idx, const int32_t* state, hipStream_t s) {
   const int64_t n = g->n;
   if (g->ext)
-    return ext_gen_place(g->seed, n, g->col, g->dist, g->xval, pairs, BYROW ? pidx : nullptr, rows, y, y_rs, idx, state,
-                         s);
+    return ext_gen_place(g->seed, n, g->col, g->dist, g->xval, g->table, pairs, BYROW ? pidx : nullptr, rows, y, y_rs,
+                         idx, state, s);
   const int64_t blocks = (rows + kGenRows - 1) / kGenRows;
   if (blocks <= 0) return PBH_OK;
   int j0 = 0, jn = 0;

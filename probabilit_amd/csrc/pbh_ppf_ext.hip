@@ -32,8 +32,41 @@ namespace {
 struct Params4 {
   const double* ptr[4];
   double val[4];
+  sfx::BetaGuide bg;  // beta with scalar (a, b): the guide table (bg.z == NULL: none)
   __device__ __forceinline__ double at(int j, int64_t i) const { return ptr[j] ? ptr[j][i] : val[j]; }
 };
+
+// the beta guide for scalar (a, b) (sfx::BetaGuide): nodes, then the midpoint check
+__global__ void k_beta_guide(double a, double b, double lb, double* z, double* d1, double* d2) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < sfx::kBetaGuideM) sfx::beta_guide_entry(a, b, lb, sfx::kBetaGuideW0 + j * sfx::kBetaGuideH, &z[j], &d1[j], &d2[j]);
+}
+
+__global__ void k_beta_guide_check(double a, double b, sfx::BetaGuide T, double* ok) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < sfx::kBetaGuideM) ok[j] = j < sfx::kBetaGuideM - 1 ? sfx::beta_guide_check(a, b, T, j) : 0.0;
+}
+
+// the setup table of `dist` with these parameters (stream-ordered allocation, NULL when the
+// distribution has none): beta with scalar, valid (a, b) -> its guide
+double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t s) {
+  if (dist != PBH_DIST_BETA || nparams < 2 || params[0].ptr || params[1].ptr) return nullptr;
+  const double a = params[0].value, b = params[1].value;
+  if (!(a > 0.0 && b > 0.0 && isfinite(a) && isfinite(b))) return nullptr;
+  constexpr int m = sfx::kBetaGuideM;
+  double* t = nullptr;
+  if (hipMallocAsync((void**)&t, (size_t)4 * m * sizeof(double), s) != hipSuccess) return nullptr;
+  const unsigned g = (unsigned)((m + 63) / 64);
+  hipLaunchKernelGGL(k_beta_guide, dim3(g), dim3(64), 0, s, a, b, sfx::lbeta(a, b), t, t + m, t + 2 * m);
+  const sfx::BetaGuide T{t, t + m, t + 2 * m, t + 3 * m};
+  hipLaunchKernelGGL(k_beta_guide_check, dim3(g), dim3(64), 0, s, a, b, T, t + 3 * m);
+  return t;
+}
+
+sfx::BetaGuide guide_of(const double* t) {
+  constexpr int m = sfx::kBetaGuideM;
+  return t ? sfx::BetaGuide{t, t + m, t + 2 * m, t + 3 * m} : sfx::BetaGuide{};
+}
 
 constexpr bool is_closed(int d) { return d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID; }
 
@@ -252,7 +285,7 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
     if (q == 1.0) return upper * scale + loc;
     double x;
     if constexpr (D == PBH_DIST_BETA)
-      x = sfx::beta_ppf01(q, a, b);
+      x = p.bg.z ? sfx::beta_ppf_guided(q, a, b, p.bg) : sfx::beta_ppf01(q, a, b);
     else
       x = sfx::truncnorm_ppf01(q, a, b);
     (void)inf;
@@ -361,6 +394,8 @@ int launch_ext(int dist, const double* q, int64_t q_stride, const LhsCol* lc, in
     prm.val[j] = params[j].value;
   }
   if (n == 0) return PBH_OK;
+  double* table = build_table(dist, params, nparams, s);
+  prm.bg = guide_of(table);
   dim3 g(grid_for(n, 256, 16384)), b(256);
   const LhsCol l = lc ? *lc : LhsCol{0, 1, 0, 0};
   const bool known = dispatch_ext(dist, [&](auto tag) {
@@ -370,6 +405,7 @@ int launch_ext(int dist, const double* q, int64_t q_stride, const LhsCol* lc, in
     else
       PBH_TIMED(kKPpf, s, hipLaunchKernelGGL((k_ppf_ext<D, false>), g, b, 0, s, q, q_stride, l, n, prm, out, flag));
   });
+  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));  // stream-ordered: after the kernel
   if (!known) {
     set_error("ppf: unknown distribution id %d", dist);
     return PBH_ERR_UNSUPPORTED;
@@ -545,9 +581,46 @@ __global__ __launch_bounds__(256) void k_ext_place(const uint64_t* __restrict__ 
   }
 }
 
-Params4 scalar_params(const double* val, int np) {
+// the certificate's exact evaluation (k_cert_eval's role for the base set): the listed pairs
+// (t, t + 1) and both ends of the segment, counted for ties / inversions
+template <int D>
+__global__ __launch_bounds__(256) void k_ext_cert_eval(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
+                                                       Params4 prm, const uint32_t* __restrict__ list, uint32_t cap,
+                                                       const uint32_t* __restrict__ count, int32_t* flag,
+                                                       unsigned long long* counts) {
+  Philox ph(seed);
+  const uint32_t m = *count;
+  unsigned long long ties = 0, inv = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 2) {
+    const double x = gen_value<D>(ph, threadIdx.x == 0 ? t0 : t0 + nt - 1, col, n, prm);
+    if (!isfinite(x)) {
+      if (flag) atomicOr(flag, 1);
+      ties += 1;
+    }
+    if (threadIdx.x == 0 && m > cap) ties += 1;
+  }
+  const uint32_t mm = m < cap ? m : cap;
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < mm; k += gridDim.x * 256) {
+    const int64_t t = t0 + list[k];
+    const double a = gen_value<D>(ph, t, col, n, prm), b = gen_value<D>(ph, t + 1, col, n, prm);
+    ties += a == b;
+    inv += !(a <= b);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ties += __shfl_xor(ties, o, 64);
+    inv += __shfl_xor(inv, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && (ties | inv)) {
+    atomicAdd(&counts[0], ties);
+    atomicAdd(&counts[1], inv);
+  }
+}
+
+Params4 scalar_params(const double* val, int np, const double* table) {
   Params4 p{};
   for (int j = 0; j < 4; ++j) p.val[j] = j < np ? val[j] : 0.0;
+  p.bg = guide_of(table);
   return p;
 }
 
@@ -563,13 +636,13 @@ int ext_nparams(int dist) {
 
 bool ext_is_discrete(int dist) { return dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI; }
 
-int ext_gen_sorted(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, int64_t t0, int64_t nt,
-                   double* out, int32_t* flag, unsigned long long* counts, uint32_t* heads, uint32_t* hcur,
-                   uint32_t hcap, hipStream_t s) {
+int ext_gen_sorted(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, const double* table,
+                   int64_t t0, int64_t nt, double* out, int32_t* flag, unsigned long long* counts, uint32_t* heads,
+                   uint32_t* hcur, uint32_t hcap, hipStream_t s) {
   const int np = ext_nparams(dist);
   PBH_REQUIRE(np >= 0, "ext_gen_sorted: distribution %d is not an extended one", dist);
   if (nt == 0) return PBH_OK;
-  const Params4 prm = scalar_params(val, np);
+  const Params4 prm = scalar_params(val, np, table);
   // binom / bernoulli, counts and heads only: the binary-search heads when the values span few
   // integers (n + 1 at most); the kernel reports anything else as an inversion
   if (ext_is_discrete(dist) && counts && heads && !out && nt >= 2) {
@@ -598,14 +671,14 @@ int ext_gen_sorted(uint64_t seed, int64_t n, uint32_t col, int dist, const doubl
   return PBH_OK;
 }
 
-int ext_gen_place(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, const uint64_t* pairs,
-                  const uint32_t* pidx, int64_t rows, double* y, int64_t y_rs, int32_t* idx, const int32_t* state,
-                  hipStream_t s) {
+int ext_gen_place(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, const double* table,
+                  const uint64_t* pairs, const uint32_t* pidx, int64_t rows, double* y, int64_t y_rs, int32_t* idx,
+                  const int32_t* state, hipStream_t s) {
   const int np = ext_nparams(dist);
   PBH_REQUIRE(np >= 0, "ext_gen_place: distribution %d is not an extended one", dist);
   const int64_t blocks = (rows + kExtGenRows - 1) / kExtGenRows;
   if (blocks <= 0) return PBH_OK;
-  const Params4 prm = scalar_params(val, np);
+  const Params4 prm = scalar_params(val, np, table);
   const dim3 g((unsigned)(blocks < 256 * 8 ? blocks : 256 * 8)), b(256);
   dispatch_ext(dist, [&](auto tag) {
     constexpr int D = decltype(tag)::value;
@@ -619,6 +692,28 @@ int ext_gen_place(uint64_t seed, int64_t n, uint32_t col, int dist, const double
   });
   PBH_CHECK_LAUNCH();
   return PBH_OK;
+}
+
+int ext_gen_cert_eval(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, const double* table,
+                      int64_t t0, int64_t nt, const uint32_t* list, uint32_t cap, const uint32_t* count, int32_t* flag,
+                      unsigned long long* counts, hipStream_t s) {
+  const int np = ext_nparams(dist);
+  PBH_REQUIRE(np >= 0, "ext_gen_cert_eval: distribution %d is not an extended one", dist);
+  const Params4 prm = scalar_params(val, np, table);
+  dispatch_ext(dist, [&](auto tag) {
+    constexpr int D = decltype(tag)::value;
+    PBH_TIMED(kKLhsSorted, s,
+              hipLaunchKernelGGL(k_ext_cert_eval<D>, dim3(512), dim3(256), 0, s, seed, n, t0, nt, col, prm, list, cap,
+                                 count, flag, counts));
+  });
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+double* ext_gen_table(int dist, const double* val, int np, hipStream_t s) {
+  pbh_param prm[4];
+  for (int j = 0; j < 4; ++j) prm[j] = pbh_param{nullptr, j < np ? val[j] : 0.0};
+  return build_table(dist, prm, np, s);
 }
 
 int ppf_ext(int dist, const double* q, int64_t q_stride, int64_t n, const pbh_param* params, int nparams, double* out,

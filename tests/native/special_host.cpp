@@ -114,6 +114,23 @@ void sfh_incbet(double a, double b, const double* x, long n, double* out) {
 void sfh_beta_ppf(double a, double b, const double* q, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = sfx::beta_ppf01(q[i], a, b);
 }
+// beta_ppf_guided with the guide built on the host as k_beta_guide / k_beta_guide_check build it;
+// out[n] (one past the draws) receives the fraction of guide intervals that passed the check
+void sfh_beta_guided(double a, double b, const double* q, long n, double* out) {
+  const int m = sfx::kBetaGuideM;
+  std::vector<double> t(4 * (size_t)m);
+  const double lb = sfx::lbeta(a, b);
+  for (int j = 0; j < m; ++j)
+    sfx::beta_guide_entry(a, b, lb, sfx::kBetaGuideW0 + j * sfx::kBetaGuideH, &t[j], &t[m + j], &t[2 * m + j]);
+  const sfx::BetaGuide T{t.data(), t.data() + m, t.data() + 2 * m, t.data() + 3 * m};
+  double okc = 0.0;
+  for (int j = 0; j < m; ++j) {
+    t[3 * m + j] = j < m - 1 ? sfx::beta_guide_check(a, b, T, j) : 0.0;
+    okc += t[3 * m + j];
+  }
+  for (long i = 0; i < n; ++i) out[i] = sfx::beta_ppf_guided(q[i], a, b, T);
+  out[n] = okc / (m - 1);
+}
 void sfh_binom_ppf(double nn, double p, const double* q, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = sfx::binom_ppf01(q[i], nn, p);
 }

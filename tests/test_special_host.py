@@ -148,6 +148,25 @@ def test_incbet_and_beta_ppf(sfh, a, b):
     np.testing.assert_allclose(got, sp.betaincinv(a, b, q), rtol=1e-10, atol=1e-300)
 
 
+@pytest.mark.parametrize("a,b", [(3.4, 2.6), (7.0, 5.0), (2.0, 3.0), (1.0, 1.0), (0.5, 0.5), (0.1, 10.0),
+                                 (50.0, 80.0), (200.0, 0.7), (1.3, 4.7)])
+def test_beta_guide(sfh, a, b):
+    """The beta guide table (sfx::beta_ppf_guided: quintic Hermite of logit x in logit q, checked
+    at every interval's midpoint) against scipy's betaincinv, and its coverage of the grid."""
+    rng = np.random.default_rng(int(a * 10 + b))
+    q = np.concatenate([rng.random(200_000), np.linspace(1e-9, 1 - 1e-9, 2001),
+                        [1e-30, 2.0**-53 / 1e8, 0.5, 1 - 2**-52]])
+    x = np.ascontiguousarray(q)
+    out = np.empty(q.size + 1)
+    f = sfh.sfh_beta_guided
+    f.restype = None
+    f(ctypes.c_double(a), ctypes.c_double(b), x.ctypes.data_as(ctypes.c_void_p), ctypes.c_long(q.size),
+      out.ctypes.data_as(ctypes.c_void_p))
+    got, coverage = out[:-1], out[-1]
+    np.testing.assert_allclose(got, sp.betaincinv(a, b, q), rtol=1e-10, atol=1e-300)
+    assert coverage > 0.5, coverage  # most of the grid interpolates (the rest is exact)
+
+
 @pytest.mark.parametrize("n,p", [(1, 0.3), (10, 0.5), (37, 0.01), (1000, 0.7), (20, 0.0), (20, 1.0)])
 def test_binom_ppf(sfh, n, p):
     import scipy.stats as st
