@@ -27,7 +27,6 @@ struct Step4Shared {
   uint32_t* cls;     // per column: top-byte counts of each msd1 tile class (8 x 256)
   uint32_t* cstart;  // per column: each class's start in every top-byte group (8 x 256)
   uint32_t* tpre;
-  uint32_t* fcls;     // per column: items of each finish class in every placement group (256 x 8)
   uint32_t* seghist;  // per column: kAdaptSegments counts of CS (adaptive code map)
   uint32_t* amap;     // per column: adaptive code map, kAdaptMapWords words (bases, then slopes)
   int32_t* state;

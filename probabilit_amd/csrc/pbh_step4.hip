@@ -475,30 +475,19 @@ __global__ __launch_bounds__(256) void k_make_codes_adapt(const double* __restri
 // group through its own cursor (cstart, cur + x * 256): 1/8 of the tiles contend on a cursor,
 // and the runs of one sub-range are all written from one XCD (its L2 merges the lines); k_hist16
 // counts the classes with the same tile size.
-//
-// fcls (fused finish): the counts of every (placement group, finish class) pair, fcls[g * 8 + x]:
-// group g = row >> s_top (the finish's top row-placement level), class x = (code >> 17) mod 8 (the
-// finish block of a top-16 bucket b is b / 2, and blocks b, b + 8 share an XCD).  The finish gives
-// each class its own sub-range of every group (k_finish_q).  A tile's 4096-row halves lie in one
-// group each (groups are 2^s_top >= 4096 rows, aligned); counted by ballots, one LDS add per
-// wave, class and half, one global add per (tile half, class).
 template <int NT, int IPT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8))) void k_msd1x(
     const uint32_t* __restrict__ codes, int64_t n, const uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ rout, const uint32_t* __restrict__ cstart, int cpad,
-    const int32_t* __restrict__ state, uint32_t* __restrict__ fcls, int s_top) {
+    const int32_t* __restrict__ state) {
   constexpr int kTile = NT * IPT;
-  constexpr int kHalves = kTile / 4096;  // 4096-row parts of a tile (a slot's part: j * NT / 4096)
-  static_assert(kTile % 4096 == 0 && 4096 % NT == 0, "tile parts");
   if (*state) return;  // uniform: this column takes the general path
   __shared__ uint32_t cnt[256], lst[256 + NT / 64], gb[256];
   __shared__ uint32_t sk[kTile];
-  __shared__ uint32_t fc[kHalves * 8];
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kTile;
   const int m = (int)((n - base) < kTile ? (n - base) : kTile);
   if (t < 256) cnt[t] = 0;
-  if (t < kHalves * 8) fc[t] = 0;
   __syncthreads();
   uint32_t key[IPT], slot[IPT];
 #pragma unroll
@@ -508,28 +497,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8))) void k_
   }
 #pragma unroll
   for (int j = 0; j < IPT; ++j) slot[j] = (j * NT + t < m) ? atomicAdd(&cnt[key[j] >> 24], 1u) : 0u;
-  if (fcls) {  // uniform
-    uint32_t fcw[kHalves][8] = {};
-#pragma unroll
-    for (int j = 0; j < IPT; ++j) {
-      const bool v = j * NT + t < m;
-      const uint64_t b0 = __ballot(v && ((key[j] >> 17) & 1u)), b1 = __ballot(v && ((key[j] >> 18) & 1u)),
-                     b2 = __ballot(v && ((key[j] >> 19) & 1u)), bv = __ballot(v);
-#pragma unroll
-      for (int x = 0; x < 8; ++x)
-        fcw[j * NT / 4096][x] += (uint32_t)__popcll(bv & ((x & 1) ? b0 : ~b0) & ((x & 2) ? b1 : ~b1) &
-                                                    ((x & 4) ? b2 : ~b2));
-    }
-    if ((t & 63) == 0) {
-#pragma unroll
-      for (int h = 0; h < kHalves; ++h)
-#pragma unroll
-        for (int x = 0; x < 8; ++x)
-          if (fcw[h][x]) atomicAdd(&fc[h * 8 + x], fcw[h][x]);
-    }
-  }
   __syncthreads();
-  if (fcls && t < kHalves * 8 && fc[t]) atomicAdd(&fcls[(((base + (t >> 3) * 4096) >> s_top) << 3) + (t & 7)], fc[t]);
   const uint32_t my = t < 256 ? cnt[t] : 0u;
   const uint32_t ex = block_excl_scan256(my, lst);  // waves past the fourth add nothing
   // the cursor add's round trip overlaps the first LDS scatter: its result is stored to gb only
@@ -1056,9 +1024,8 @@ union FinishQLds {
 template <int BINS, int NT, bool Q = true>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 8 : 4))) void k_finish_q(
     const uint16_t* __restrict__ keys, const uint32_t* __restrict__ rows, const double* __restrict__ x,
-    const uint32_t* __restrict__ start, int s_top, uint32_t* __restrict__ gcur, int cpad,
-    const uint32_t* __restrict__ fcls, uint64_t* __restrict__ out, int32_t* __restrict__ flags,
-    const int32_t* __restrict__ state) {
+    const uint32_t* __restrict__ start, int s_top, uint32_t* __restrict__ gcur, int cpad, uint64_t* __restrict__ out,
+    int32_t* __restrict__ flags, const int32_t* __restrict__ state) {
   if (*state) return;
   constexpr int FB = 2;  // buckets per block (one per block measured 24 -> 42 ms per step)
   constexpr int kShift = 16 - __builtin_ctz(BINS);
@@ -1096,20 +1063,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
   const uint32_t my = t < 256 ? gcnt[t] : 0u;
   const uint32_t gex = block_excl_scan256(my, goff);  // waves past 4 add nothing
   if (t < 256) goff[t] = gex;
-  // group t's region [t << s_top, ...): with fcls, class x = blockIdx.x mod 8 (the blocks of one XCD)
-  // appends to its own sub-range of it (the counts of the classes below x first), so the partial
-  // 128-byte lines at the ends of one block's runs are completed by the next block of the same XCD
-  // in that XCD's L2 instead of being written back partially from two
-  uint32_t mybase = 0u;
-  if (my) {
-    uint32_t off = 0u, ci = (uint32_t)t;
-    if (fcls) {
-      const uint32_t xc = blockIdx.x & 7u;
-      for (uint32_t x = 0; x < xc; ++x) off += fcls[t * 8 + x];
-      ci = (uint32_t)t * 8u + xc;
-    }
-    mybase = (uint32_t)(((uint64_t)t << s_top) + off + atomicAdd(&gcur[ci * cpad], my));
-  }
+  const uint32_t mybase = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * cpad], my)) : 0u;
   uint64_t pr[FB * kIt];
   int total = 0;
 #pragma unroll
@@ -1500,8 +1454,8 @@ size_t step4_gen_shared_bytes(int k) {
   // per column: hist 65536 + start 65537 + cur1 8 x 256 * pad + cur2 65536 + curF 256 * pad +
   // cls 2048 + cstart 2048 + tpre 257 + seghist + amap (u32), state / flags / retry
   const size_t pad = (size_t)cur_pad();
-  return (size_t)k * ((65536 + 65537 + 8 * 256 * pad + 65536 + 8 * 256 * pad + 2048 + 2048 + 257 + 2048 +
-                       kAdaptSegments + kAdaptMapWords) * 4 + 64) + 512;
+  return (size_t)k * ((65536 + 65537 + 8 * 256 * pad + 65536 + 8 * 256 * pad + 2048 + 2048 + 257 + kAdaptSegments +
+                       kAdaptMapWords) * 4 + 64) + 512;
 }
 
 size_t step4_gen_column_bytes(int64_t n) {
@@ -1531,8 +1485,6 @@ void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh) {
   p += (size_t)k * 2048 * 4;
   sh.tpre = (uint32_t*)p;
   p += (size_t)k * 257 * 4;
-  sh.fcls = (uint32_t*)p;
-  p += (size_t)k * 2048 * 4;
   sh.seghist = (uint32_t*)p;
   p += (size_t)k * kAdaptSegments * 4;
   p = (char*)(((uintptr_t)p + 63) & ~(uintptr_t)63);
@@ -1619,15 +1571,6 @@ static int msd_tile_log() {
   return v;
 }
 
-// PBH_FINISH_CLASSES=0: one cursor per placement group for every finish block (round 3's layout)
-static bool finish_classes() {
-  static const bool on = [] {
-    const char* e = getenv("PBH_FINISH_CLASSES");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 bool step4_fused() {
   static const bool v = [] {
     const char* e = getenv("PBH_STEP4_FUSED");  // "0": position-order finish + every placement level
@@ -1701,7 +1644,6 @@ int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs,
   PBH_CHECK_HIP(hipMemsetAsync(sh.cur2 + (int64_t)c0 * 65536, 0, (size_t)kk * 65536 * 4, s));
   PBH_CHECK_HIP(hipMemsetAsync(sh.curF + c0 * cw, 0, kk * cw * 4, s));
   PBH_CHECK_HIP(hipMemsetAsync(cls, 0, (size_t)kk * 2048 * 4, s));
-  PBH_CHECK_HIP(hipMemsetAsync(sh.fcls + (int64_t)c0 * 2048, 0, (size_t)kk * 2048 * 4, s));
   PBH_CHECK_HIP(hipMemsetAsync(state, 0, (size_t)kk * 4, s));
   PBH_CHECK_HIP(hipMemsetAsync(flags, 0, (size_t)kk * 4, s));
   // >= 64 K codes per block and at most 64 blocks per column: every block flushes its non-empty
@@ -1806,14 +1748,10 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
   uint32_t* cur1 = sh.cur1 + (int64_t)c * 8 * 256 * cur_pad();
   uint32_t* cur2 = sh.cur2 + (int64_t)c * 65536;
   const uint32_t* tp = sh.tpre + (int64_t)c * 257;
-  int shifts[4];
-  const int nl = place_levels(n, shifts);
-  const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;  // the finish's placement groups: row >> s_top
-  uint32_t* fcls = step4_fused() && finish_classes() ? sh.fcls + (int64_t)c * 2048 : nullptr;
   if (tlog == 13) {
     PBH_TIMED(kKMsd1, s,
               hipLaunchKernelGGL((k_msd1x<1024, 8>), dim3((unsigned)t1), dim3(1024), 0, s, codes, n, start, cur1,
-                                 cb.keys32, cb.rows1, cst, cur_pad(), state, fcls, s_top));
+                                 cb.keys32, cb.rows1, cst, cur_pad(), state));
     PBH_CHECK_LAUNCH();
     PBH_TIMED(kKMsd2, s,
               hipLaunchKernelGGL((k_msd2x<1024, 8>), dim3((unsigned)(t1 + 256)), dim3(1024), 0, s, cb.keys32, cb.rows1,
@@ -1821,7 +1759,7 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
   } else {
     PBH_TIMED(kKMsd1, s,
               hipLaunchKernelGGL((k_msd1x<256, 16>), dim3((unsigned)t1), dim3(256), 0, s, codes, n, start, cur1,
-                                 cb.keys32, cb.rows1, cst, cur_pad(), state, fcls, s_top));
+                                 cb.keys32, cb.rows1, cst, cur_pad(), state));
     PBH_CHECK_LAUNCH();
     PBH_TIMED(kKMsd2, s,
               hipLaunchKernelGGL((k_msd2x<512, 8>), dim3((unsigned)(t1 + 256)), dim3(512), 0, s, cb.keys32, cb.rows1,
@@ -1829,6 +1767,9 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
   }
   PBH_CHECK_LAUNCH();
   if (step4_fused()) {
+    int shifts[4];
+    const int nl = place_levels(n, shifts);
+    const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
     // PBH_FINISH_CFG (A/B measurements, profiles/r03/README_ab.md): 29 (default) = k_finish_q over
     // 512 threads, 1024 bins, the run members' CS values read in pass 2; 28 = the same with those
     // reads queued through LDS; 30 = queued, 2048 bins; 26 = 256 threads (round 2's k_finish_ah).
@@ -1845,7 +1786,7 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
 #define PBH_FINQ(BINS, NT, Q)                                                                                    \
   PBH_TIMED(kKFinish, s,                                                                                         \
             hipLaunchKernelGGL((k_finish_q<BINS, NT, Q>), dim3(65536 / 2), dim3(NT), 0, s, cb.keys16, cb.rows2, cs, \
-                               start, s_top, gc, cpad, fcls, cb.pairs[0], sh.flags + c, state))
+                               start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state))
     if (segcap) {
       PBH_TIMED(kKFinish, s,
                 hipLaunchKernelGGL((k_finish_fused<2, 4096>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
