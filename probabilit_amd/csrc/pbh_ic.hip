@@ -867,9 +867,9 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
     }();
     const int64_t tiles = (n + rows - 1) / rows;
     const unsigned gb = (unsigned)((tiles + 3) / 4 < 8192 ? (tiles + 3) / 4 : 8192);
-    static const bool nt = [] {
+    static const bool nt = [] {  // PBH_APPLY_NT=0: cached accesses (r4e A/B: 12.8 against 13.2 ms per step)
       const char* e = getenv("PBH_APPLY_NT");
-      return e && atoi(e) == 1;
+      return !(e && atoi(e) == 0);
     }();
     static const bool w2 = [] {  // PBH_APPLY_W2=0: the one-row kernel (variant tests)
       const char* e = getenv("PBH_APPLY_W2");

@@ -1160,6 +1160,94 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
   }
 }
 
+// The same scores with the tail compacted per WAVE instead of per block (the default; PBH_SCORES_WAVE=0
+// selects k_perm_scores): each wave takes 512 consecutive rows per step (8 a lane), writes its centre
+// scores straight to S (coalesced), and pushes the tail arguments onto its own LDS stack; whenever 64
+// are queued the wave evaluates them as one full-width batch and scatters them into S (rows of its
+// recent steps: merged in L2).  No block barrier after the heads' staging, no LDS staging of the
+// results, no ragged drain: the block-wide queue spent ~50 VALU instructions per score on its
+// bookkeeping and idled at four barriers per tile (tools/microbench_feistel.hip, r4e PMC pass).
+// Each wave's sum (its partial for the step-2 means) is formed in a fixed order: the queue order
+// is the lanes' order (ballots, no atomics), so the result is deterministic.  Same values.
+constexpr int kWaveQ = 576;  // a wave's tail stack: at most 63 left over + 8 x 64 pushed in a step
+
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores_w(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
+                                                          int64_t nrows, const uint32_t* __restrict__ heads,
+                                                          int64_t nheads, double* __restrict__ S,
+                                                          double* __restrict__ partial) {
+  __shared__ double qarg[kBlock / 64][kWaveQ];
+  __shared__ uint32_t qrow[kBlock / 64][kWaveQ];
+  extern __shared__ uint32_t lheads[];
+  Philox ph(seed);
+  FeistelPerm fp(ph, (uint64_t)n, col);
+  const double np1 = (double)(n + 1);
+  if (heads && nheads <= kLdsHeads) {
+    for (int64_t i = threadIdx.x; i < nheads; i += kBlock) lheads[i] = heads[i];
+    __syncthreads();
+    heads = lheads;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  double* qa = qarg[w];
+  uint32_t* qr = qrow[w];
+  double sum = 0.0;
+  int qc = 0;  // wave-uniform: queued tail arguments
+  const int64_t gw = (int64_t)blockIdx.x * (kBlock / 64) + w, W = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t base = gw * 512; base < nrows; base += W * 512) {
+    uint64_t tt[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t i = base + j * 64 + lane;
+      tt[j] = n > 1 && i < nrows ? fp.round_trip((uint64_t)(row0 + i)) : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      while (tt[j] >= (uint64_t)n) tt[j] = fp.round_trip(tt[j]);
+#pragma unroll 2
+    for (int j = 0; j < 8; ++j) {
+      const int64_t i = base + j * 64 + lane;
+      const bool valid = i < nrows;
+      double y = 0.5;
+      if (valid) {
+        const uint64_t t = tt[j];
+        const double rank = heads ? run_average_rank(heads, nheads, n, (int64_t)t) : (double)(t + 1);
+        y = rank / np1;
+      }
+      const bool tail = valid && sf::ndtri_takes_tail(y);
+      if (valid && !tail) {
+        const double v = sf::ndtri_centre(y);
+        S[i] = v;
+        sum += v;
+      }
+      const uint64_t m = __ballot(tail);
+      if (tail) {
+        const int slot = qc + (int)__popcll(m & lt);
+        qa[slot] = y;
+        qr[slot] = (uint32_t)i;
+      }
+      qc += (int)__popcll(m);
+    }
+    while (qc >= 64) {  // full-width batches off the top of the stack (the step's strata are dead here)
+      qc -= 64;
+      const double a = qa[qc + lane];
+      const uint32_t r = qr[qc + lane];
+      const double v = sf::ndtri_tail(a);
+      S[r] = v;
+      sum += v;
+    }
+  }
+  if (lane < qc) {  // the leftover (< 64): once per wave
+    const double v = sf::ndtri_tail(qa[lane]);
+    S[qr[lane]] = v;
+    sum += v;
+  }
+  if (partial) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) partial[gw] = sum;
+  }
+}
+
 // Run heads of a sorted segment x[0..m): position p is a head when p == 0 (unless x[0] is
 // the value before the segment, first_is_prev) or x[p] != x[p - 1]; heads are reported as
 // t0 + p (t0 - 1 + p with first_is_prev).  Two passes: per-tile counts, then ordered writes.
@@ -1915,16 +2003,31 @@ int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStre
   return PBH_OK;
 }
 
-unsigned perm_scores_blocks(int64_t nrows) { return compact_grid(nrows); }
+static bool scores_wave() {  // PBH_SCORES_WAVE=0: the block-compacted k_perm_scores (A/B, variant tests)
+  static const bool on = [] {
+    const char* e = getenv("PBH_SCORES_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// blocks of the scores kernel; its partial sums: one per block (k_perm_scores) or per wave
+static unsigned scores_grid(int64_t nrows) { return compact_grid(nrows); }
+unsigned perm_scores_blocks(int64_t nrows) { return scores_grid(nrows) * (scores_wave() ? kBlock / 64 : 1); }
 
 int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, const uint32_t* heads,
                 int64_t nheads, double* S, hipStream_t s, double* partial) {
   PBH_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "perm_scores: rows outside [0, n)");
   if (nrows == 0) return PBH_OK;
-  PBH_TIMED(kKPermScores, s,
-            hipLaunchKernelGGL(k_perm_scores, dim3(compact_grid(nrows)), dim3(kBlock),
-                               heads && nheads <= kLdsHeads ? (size_t)nheads * 4 : 0, s, seed, n, (uint32_t)col,
-                               row0, nrows, heads, nheads, S, partial));
+  const size_t lds = heads && nheads <= kLdsHeads ? (size_t)nheads * 4 : 0;
+  if (scores_wave())
+    PBH_TIMED(kKPermScores, s,
+              hipLaunchKernelGGL(k_perm_scores_w, dim3(scores_grid(nrows)), dim3(kBlock), lds, s, seed, n,
+                                 (uint32_t)col, row0, nrows, heads, nheads, S, partial));
+  else
+    PBH_TIMED(kKPermScores, s,
+              hipLaunchKernelGGL(k_perm_scores, dim3(scores_grid(nrows)), dim3(kBlock), lds, s, seed, n,
+                                 (uint32_t)col, row0, nrows, heads, nheads, S, partial));
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
