@@ -113,95 +113,15 @@ PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm_in, const P
   flag_nonfinite(flag, bad);
 }
 
-// The same with ndtri's tail compacted per WAVE (the default; PBH_PPF_WAVE=0: per block, above): a
-// wave takes 512 consecutive draws per step, stores its centre values straight to out and stacks
-// its tail arguments in its own LDS queue, evaluated 64 at a time (full width) at the end of the
-// step and scattered into out -- no block barrier in the loop, no LDS staging of the results, no
-// ragged drain (the scores kernel's A/B, profiles/r04/README_ab.md).  Same values.
-constexpr int kWaveQ2 = 576;  // at most 63 left over + 8 x 64 pushed in a step
-struct WaveQueue {
-  double arg[kBlock / 64][kWaveQ2];
-  int64_t idx[kBlock / 64][kWaveQ2];
-};
-
-template <int D, bool SC, class Q>
-PBH_DI void ppf_compacted_w(int64_t n, const Q& qof, const Params& prm_in, const PoissonTable& pt,
-                            double* __restrict__ out, int32_t* flag, WaveQueue& wq, const double* lt = nullptr) {
-  Params prm = prm_in;
-  if constexpr (SC) prm.ptr[0] = prm.ptr[1] = prm.ptr[2] = nullptr;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t ltm = lane ? (~0ull >> (64 - lane)) : 0ull;
-  double* qa = wq.arg[w];
-  int64_t* qi = wq.idx[w];
-  bool bad = false;
-  int qc = 0;  // wave-uniform
-  const int64_t gw = (int64_t)blockIdx.x * (kBlock / 64) + w, W = (int64_t)gridDim.x * (kBlock / 64);
-  for (int64_t base = gw * 512; base < n; base += W * 512) {
-    double qv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t i = base + j * 64 + lane;
-      qv[j] = i < n ? qof(i) : 0.5;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t i = base + j * 64 + lane;
-      const bool valid = i < n;
-      const bool tail = valid && sf::ndtri_takes_tail(qv[j]);
-      if (valid && !tail) {
-        const double x = ppf_one<D, 1>(qv[j], prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
-        out[i] = x;
-        bad |= !isfinite(x);
-      }
-      const uint64_t m = __ballot(tail);
-      if (tail) {
-        const int slot = qc + (int)__popcll(m & ltm);
-        qa[slot] = qv[j];
-        qi[slot] = i;
-      }
-      qc += (int)__popcll(m);
-    }
-    while (qc >= 64) {
-      qc -= 64;
-      const double a = qa[qc + lane];
-      const int64_t i = qi[qc + lane];
-      const double x = ppf_one<D, 2>(a, prm.at(0, i), prm.at(1, i), prm.at(2, i), pt, lt);
-      out[i] = x;
-      bad |= !isfinite(x);
-    }
-  }
-  if (lane < qc) {
-    const int64_t i = qi[lane];
-    const double x = ppf_one<D, 2>(qa[lane], prm.at(0, i), prm.at(1, i), prm.at(2, i), pt, lt);
-    out[i] = x;
-    bad |= !isfinite(x);
-  }
-  flag_nonfinite(flag, bad);
-}
-
-bool ppf_wave() {  // PBH_PPF_WAVE=0: the block-queue compaction (A/B, variant tests)
-  static const bool on = [] {
-    const char* e = getenv("PBH_PPF_WAVE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-unsigned wave_grid(int64_t n) { return grid_for(n, 4 * 512, 256 * 8); }  // blocks of 4 waves x 512 draws
-
-template <int D, bool SC, bool WQ = false>
+template <int D, bool SC>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_c(const double* __restrict__ q, int64_t q_stride, int64_t n,
                                                   Params prm, PoissonTable pt, double* __restrict__ out,
                                                   int32_t* flag) {
-  __shared__ std::conditional_t<WQ, WaveQueue, TailQueue> tq;
-  __shared__ double res[WQ ? 1 : kCTile];
+  __shared__ TailQueue tq;
+  __shared__ double res[kCTile];
   __shared__ double lt[kLog3N];
-  stage_log3(lt);
-  if constexpr (WQ) {
-    __syncthreads();
-    ppf_compacted_w<D, SC>(n, [&](int64_t i) { return q[i * q_stride]; }, prm, pt, out, flag, tq, lt);
-  } else {  // (ppf_compacted's first barrier follows)
-    ppf_compacted<D, SC>(n, [&](int64_t i) { return q[i * q_stride]; }, prm, pt, out, flag, tq, res, lt);
-  }
+  stage_log3(lt);  // (ppf_compacted's first barrier follows)
+  ppf_compacted<D, SC>(n, [&](int64_t i) { return q[i * q_stride]; }, prm, pt, out, flag, tq, res, lt);
 }
 
 template <int D>
@@ -275,20 +195,16 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf(uint64_t seed, int64
   }
 }
 
-template <int D, bool SC, bool WQ = false>
+template <int D, bool SC>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_c(uint64_t seed, int64_t n, int64_t row0, int64_t nrows,
                                                       uint32_t col, Params prm, PoissonTable pt,
                                                       double* __restrict__ out, int32_t* flag) {
-  __shared__ std::conditional_t<WQ, WaveQueue, TailQueue> tq;
-  __shared__ double res[WQ ? 1 : kCTile];
+  __shared__ TailQueue tq;
+  __shared__ double res[kCTile];
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
-  if constexpr (WQ)
-    ppf_compacted_w<D, SC>(nrows, [&](int64_t i) { return lhs_quantile(ph, fp, (uint64_t)(row0 + i), col); }, prm, pt,
-                           out, flag, tq);
-  else
-    ppf_compacted<D, SC>(nrows, [&](int64_t i) { return lhs_quantile(ph, fp, (uint64_t)(row0 + i), col); }, prm, pt,
-                         out, flag, tq, res);
+  ppf_compacted<D, SC>(nrows, [&](int64_t i) { return lhs_quantile(ph, fp, (uint64_t)(row0 + i), col); }, prm, pt, out,
+                   flag, tq, res);
 }
 
 // ---------------------------------------------------------------- gamma: guide table in LDS
@@ -1462,23 +1378,17 @@ struct SobolCol {
   double scale;
 };
 
-template <int D, bool SC, bool WQ = false>
+template <int D, bool SC>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_sobol_ppf_c(SobolCol sc, int64_t row0, int64_t nrows, Params prm,
                                                                PoissonTable pt, double* __restrict__ out,
                                                                int32_t* flag) {
-  __shared__ std::conditional_t<WQ, WaveQueue, TailQueue> tq;
-  __shared__ double res[WQ ? 1 : kCTile];
+  __shared__ TailQueue tq;
+  __shared__ double res[kCTile];
   __shared__ uint32_t T[1024];
   build_sobol_tables(sc.sv, T);
   __syncthreads();
-  if constexpr (WQ)
-    ppf_compacted_w<D, SC>(
-        nrows, [&](int64_t i) { return (double)sobol_point(T, sc.shift, (uint64_t)(row0 + i)) * sc.scale; }, prm, pt,
-        out, flag, tq);
-  else
-    ppf_compacted<D, SC>(
-        nrows, [&](int64_t i) { return (double)sobol_point(T, sc.shift, (uint64_t)(row0 + i)) * sc.scale; }, prm, pt,
-        out, flag, tq, res);
+  ppf_compacted<D, SC>(nrows, [&](int64_t i) { return (double)sobol_point(T, sc.shift, (uint64_t)(row0 + i)) * sc.scale; },
+                   prm, pt, out, flag, tq, res);
 }
 
 template <int D>
@@ -1523,11 +1433,9 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
 #define PBH_CASE(D) \
   case D:           \
     if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
-      PBH_TIMED(kKPpf, s,                                                                                       \
-                hipLaunchKernelGGL((ppf_wave() ? (scalar_params(prm) ? k_ppf_c<D, true, true> : k_ppf_c<D, false, true>) \
-                                               : (scalar_params(prm) ? k_ppf_c<D, true> : k_ppf_c<D, false>)),   \
-                                   dim3(ppf_wave() ? wave_grid(n) : grid_for(n, kCTile, 8192)), b, 0, s, q, qs, n,  \
-                                   prm, pt, out, flag));                                                        \
+      PBH_TIMED(kKPpf, s, hipLaunchKernelGGL((scalar_params(prm) ? k_ppf_c<D, true> : k_ppf_c<D, false>),            \
+                                             dim3(grid_for(n, kCTile, 8192)), b, 0, s, q, qs, n, prm, pt, out,  \
+                                             flag));                                                            \
     else if (streamable)                                                                                        \
       PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_v<D>, gv, b, 0, s, q, n, prm, pt, out, flag));               \
     else                                                                                                        \
@@ -1569,11 +1477,9 @@ int launch_lhs_ppf(int dist, uint64_t seed, int64_t n, int64_t row0, int64_t nro
   case D:           \
     if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
       PBH_TIMED(kKLhsPpf, s,                                                                                    \
-                hipLaunchKernelGGL((ppf_wave() ? (scalar_params(prm) ? k_lhs_ppf_c<D, true, true>                \
-                                                                     : k_lhs_ppf_c<D, false, true>)              \
-                                               : (scalar_params(prm) ? k_lhs_ppf_c<D, true> : k_lhs_ppf_c<D, false>)), \
-                                   dim3(ppf_wave() ? wave_grid(nrows) : compact_grid(nrows)), b, 0, s, seed, n, row0, \
-                                   nrows, col, prm, pt, out, flag));                                            \
+                hipLaunchKernelGGL((scalar_params(prm) ? k_lhs_ppf_c<D, true> : k_lhs_ppf_c<D, false>),            \
+                                   dim3(compact_grid(nrows)), b, 0, s, seed, n, row0, nrows, col, prm, pt, out, \
+                                   flag));                                                                      \
     else                                                                                                        \
       PBH_TIMED(kKLhsPpf, s,                                                                                    \
                 hipLaunchKernelGGL(k_lhs_ppf<D>, g, b, 0, s, seed, n, row0, nrows, col, prm, pt, out, flag));   \
@@ -2272,12 +2178,9 @@ extern "C" int pbh_sobol_ppf(const uint32_t* sv_host, const uint32_t* shift_host
   case D:                                                                                                         \
     if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                                    \
       PBH_TIMED(kKPpf, s,                                                                                         \
-                hipLaunchKernelGGL((ppf_wave() ? (scalar_params(prm) ? k_sobol_ppf_c<D, true, true>                \
-                                                                     : k_sobol_ppf_c<D, false, true>)              \
-                                               : (scalar_params(prm) ? k_sobol_ppf_c<D, true>                      \
-                                                                     : k_sobol_ppf_c<D, false>)),                  \
-                                   dim3(ppf_wave() ? wave_grid(nrows) : compact_grid(nrows)), b, 0, s, sc, row0,   \
-                                   nrows, prm, pt, out, nonfinite_flag));                                         \
+                hipLaunchKernelGGL((scalar_params(prm) ? k_sobol_ppf_c<D, true> : k_sobol_ppf_c<D, false>),         \
+                                   dim3(compact_grid(nrows)), b, 0, s, sc, row0, nrows, prm, pt, out,             \
+                                   nonfinite_flag));                                                              \
     else                                                                                                          \
       PBH_TIMED(kKPpf, s,                                                                                         \
                 hipLaunchKernelGGL(k_sobol_ppf<D>, g, b, 0, s, sc, row0, nrows, prm, pt, out, nonfinite_flag));  \

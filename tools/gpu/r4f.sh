@@ -6,8 +6,6 @@ R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 600 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/${TAG}_tests.log; grep -E "^FAILED" gpurun_out/${TAG}_tests.log | head -20; [ $rc -le 1 ] || exit $rc
 bash tools/gpu/ab_env.sh ${TAG}_ab "-" "PBH_SCORES_WAVE=0" || exit $?
-for V in 1 0; do PBH_PPF_WAVE=$V timeout -k 10 300 python tools/ppf_sweep.py > gpurun_out/${TAG}_sweep_wave$V.json 2>&1; echo "sweep wave=$V exit $?"; python3 -c "
-import json,sys; d=json.load(open('gpurun_out/${TAG}_sweep_wave$V.json')); print('frac', d['frac'], {k: v['ms'] for k, v in d['per_dist'].items() if 'norm' in k})"; done
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 rc=$?; echo "bench exit $rc"; [ $rc -eq 0 ] || exit $rc
 python3 tools/show_bench.py gpurun_out/${TAG}_bench.json | head -24
