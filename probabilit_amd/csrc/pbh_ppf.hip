@@ -1083,95 +1083,20 @@ constexpr int64_t kLdsHeads = 4096;  // run heads staged in LDS by k_perm_scores
 // Van der Waerden scores of an LHS column, rows [row0, row0 + nrows), in row order: the rank
 // of row r is pi(r) + 1 (untied), or the run average of stratum pi(r) (heads != NULL), so
 // S[r] = ndtri(rank / (n + 1)) (correlation.py:394-395) without sorting anything.  Ranks of
-// consecutive rows are random, so ndtri's tail is compacted (see TailQueue).  With
-// partial != NULL each block also writes the sum of its scores to partial[blockIdx.x] (the
-// column mean of step 2 without re-reading S; summed in a fixed order by k_means).
-__global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
-                                                        int64_t nrows, const uint32_t* __restrict__ heads,
-                                                        int64_t nheads, double* __restrict__ S,
-                                                        double* __restrict__ partial) {
-  __shared__ TailQueue tq;
-  __shared__ double res[kCTile];
-  __shared__ double sh[kBlock / 64];
-  extern __shared__ uint32_t lheads[];  // a tied column's run heads (dynamic LDS; 0 bytes otherwise)
-  Philox ph(seed);
-  FeistelPerm fp(ph, (uint64_t)n, col);
-  const double np1 = (double)(n + 1);
-  double sum = 0.0;
-  if (heads && nheads <= kLdsHeads) {  // the binary search reads LDS instead of L1/L2
-    for (int64_t i = threadIdx.x; i < nheads; i += kBlock) lheads[i] = heads[i];
-    __syncthreads();
-    heads = lheads;
-  }
-  for (int64_t base = (int64_t)blockIdx.x * kCTile; base < nrows; base += (int64_t)gridDim.x * kCTile) {
-    if (threadIdx.x == 0) tq.count = 0;
-    __syncthreads();
-    // the strata of all kCIpt items first: independent Feistel chains the compiler interleaves
-    // (one straight-line block; the rare cycle walks are finished afterwards)
-    uint64_t tt[kCIpt];
-#pragma unroll
-    for (int j = 0; j < kCIpt; ++j) {
-      const int64_t i = base + j * kBlock + threadIdx.x;
-      tt[j] = n > 1 && i < nrows ? fp.round_trip((uint64_t)(row0 + i)) : 0;
-    }
-#pragma unroll
-    for (int j = 0; j < kCIpt; ++j)
-      while (tt[j] >= (uint64_t)n) tt[j] = fp.round_trip(tt[j]);
-#pragma unroll 2
-    for (int j = 0; j < kCIpt; ++j) {
-      const int p = j * kBlock + threadIdx.x;
-      const int64_t i = base + p;
-      const bool valid = i < nrows;
-      double y = 0.5;
-      if (valid) {
-        const uint64_t t = tt[j];
-        const double rank = heads ? run_average_rank(heads, nheads, n, (int64_t)t) : (double)(t + 1);
-        y = rank / np1;
-      }
-      const bool tail = valid && sf::ndtri_takes_tail(y);
-      if (valid && !tail) res[p] = sf::ndtri_centre(y);
-      tail_push(tq, tail, y, p);
-    }
-    __syncthreads();
-    const int T = tq.count;
-    for (int t = threadIdx.x; t < T; t += kBlock) res[tq.pos[t]] = sf::ndtri_tail(tq.arg[t]);  // (an LDS copy of the log table measured 1 ms per step slower here)
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kCIpt; ++j) {
-      const int p = j * kBlock + threadIdx.x;
-      const int64_t i = base + p;
-      if (i < nrows) {
-        const double v = res[p];
-        S[i] = v;
-        sum += v;
-      }
-    }
-  }
-  if (partial) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = sum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double b = 0.0;
-      for (int w = 0; w < kBlock / 64; ++w) b += sh[w];
-      partial[blockIdx.x] = b;
-    }
-  }
-}
-
-// The same scores with the tail compacted per WAVE instead of per block (the default; PBH_SCORES_WAVE=0
-// selects k_perm_scores): each wave takes 512 consecutive rows per step (8 a lane), writes its centre
-// scores straight to S (coalesced), and pushes the tail arguments onto its own LDS stack; whenever 64
-// are queued the wave evaluates them as one full-width batch and scatters them into S (rows of its
-// recent steps: merged in L2).  No block barrier after the heads' staging, no LDS staging of the
-// results, no ragged drain: the block-wide queue spent ~50 VALU instructions per score on its
-// bookkeeping and idled at four barriers per tile (tools/microbench_feistel.hip, r4e PMC pass).
-// Each wave's sum (its partial for the step-2 means) is formed in a fixed order: the queue order
-// is the lanes' order (ballots, no atomics), so the result is deterministic.  Same values.
+// consecutive rows are random, so ndtri's tail (27% of the ranks, ~3.4x the centre's cost) is
+// compacted per WAVE: each wave takes 512 consecutive rows per step (8 a lane), writes its centre
+// scores straight to S (coalesced), and pushes the tail arguments onto its own LDS stack; at the
+// end of the step it evaluates them 64 at a time (full width) and scatters them into S (rows of
+// its recent steps: merged in L2).  No block barrier after the heads' staging, no LDS staging of
+// the results, no ragged drain: round 3's block-wide queue spent ~50 VALU instructions per score
+// on its bookkeeping and idled at four barriers per 2048-row tile (r4e PMC pass of
+// tools/microbench_feistel.hip; interleaved A/B r4f: 22.4-22.7 against 24.3-25.1 ms per step).
+// With partial != NULL each wave writes the sum of its scores to partial[wave] (the column mean of
+// step 2 without re-reading S; summed in a fixed order by k_means): formed in a fixed order, since
+// the queue order is the lanes' order (ballots, no atomics), so the result is deterministic.
 constexpr int kWaveQ = 576;  // a wave's tail stack: at most 63 left over + 8 x 64 pushed in a step
 
-__global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores_w(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
                                                           int64_t nrows, const uint32_t* __restrict__ heads,
                                                           int64_t nheads, double* __restrict__ S,
                                                           double* __restrict__ partial) {
@@ -2003,31 +1928,18 @@ int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStre
   return PBH_OK;
 }
 
-static bool scores_wave() {  // PBH_SCORES_WAVE=0: the block-compacted k_perm_scores (A/B, variant tests)
-  static const bool on = [] {
-    const char* e = getenv("PBH_SCORES_WAVE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// blocks of the scores kernel; its partial sums: one per block (k_perm_scores) or per wave
+// blocks of the scores kernel; its partial sums: one per wave
 static unsigned scores_grid(int64_t nrows) { return compact_grid(nrows); }
-unsigned perm_scores_blocks(int64_t nrows) { return scores_grid(nrows) * (scores_wave() ? kBlock / 64 : 1); }
+unsigned perm_scores_blocks(int64_t nrows) { return scores_grid(nrows) * (kBlock / 64); }
 
 int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, const uint32_t* heads,
                 int64_t nheads, double* S, hipStream_t s, double* partial) {
   PBH_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "perm_scores: rows outside [0, n)");
   if (nrows == 0) return PBH_OK;
   const size_t lds = heads && nheads <= kLdsHeads ? (size_t)nheads * 4 : 0;
-  if (scores_wave())
-    PBH_TIMED(kKPermScores, s,
-              hipLaunchKernelGGL(k_perm_scores_w, dim3(scores_grid(nrows)), dim3(kBlock), lds, s, seed, n,
-                                 (uint32_t)col, row0, nrows, heads, nheads, S, partial));
-  else
-    PBH_TIMED(kKPermScores, s,
-              hipLaunchKernelGGL(k_perm_scores, dim3(scores_grid(nrows)), dim3(kBlock), lds, s, seed, n,
-                                 (uint32_t)col, row0, nrows, heads, nheads, S, partial));
+  PBH_TIMED(kKPermScores, s,
+            hipLaunchKernelGGL(k_perm_scores, dim3(scores_grid(nrows)), dim3(kBlock), lds, s, seed, n, (uint32_t)col,
+                               row0, nrows, heads, nheads, S, partial));
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }

@@ -197,8 +197,7 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     (PBH_APPLY_ROWS=64), the poisson run heads from every stratum instead of the boundary search
     (PBH_DISCRETE_SCAN=1), the code histogram with the tile-class counts per code (PBH_HIST_CLASS=0),
     step 3 with one-row accesses (PBH_APPLY_W2=0; the default pairs rows in 16-byte accesses, the odd
-    N taking its one-row tail) or with cached paired accesses (PBH_APPLY_NT=0; the default is non-temporal),
-    the scores with the block-wide tail queue (PBH_SCORES_WAVE=0; the default queues per wave)
+    N taking its one-row tail) or with cached paired accesses (PBH_APPLY_NT=0; the default is non-temporal)
     -- step-4 indices equal to the oracle's and the outputs within 1e-10.  600 001 rows: 8 histogram
     blocks per column, so the default takes the class-major k_hist16c."""
     import os
@@ -213,7 +212,7 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     ref = _oracle(n, dists, seed, C)
     for env in ({"PBH_HIST_CLASS": "0"}, {"PBH_MSD_TILE": "4096", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"},
                 {"PBH_FINISH_CFG": "30"}, {"PBH_GAMMA_WIN": "0"}, {"PBH_PLACE_TOP": "0"}, {"PBH_APPLY_ROWS": "64"},
-                {"PBH_DISCRETE_SCAN": "1"}, {"PBH_APPLY_W2": "0"}, {"PBH_APPLY_NT": "0"}, {"PBH_SCORES_WAVE": "0"}):
+                {"PBH_DISCRETE_SCAN": "1"}, {"PBH_APPLY_W2": "0"}, {"PBH_APPLY_NT": "0"}):
         dd = tmp_path / "_".join(f"{k}{v}" for k, v in env.items())
         dd.mkdir()
         script = _VARIANT_SCRIPT.format(root=root, tests=os.path.join(root, "tests"), d=str(dd), n=n, dists=dists,
