@@ -598,7 +598,13 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "logistic": (), "cauchy": (), "laplace": (), "gumbel_r": (), "gumbel_l": (), "pareto": ("b",),
                 "loguniform": ("a", "b"), "reciprocal": ("a", "b"), "rayleigh": (), "lomax": ("c",),
                 "genextreme": ("c",), "gompertz": ("c",), "chi2": ("df",), "erlang": ("a",),
-                "halfcauchy": (), "halflogistic": (), "halfnorm": (), "arcsine": (), "hypsecant": (), "powerlaw": ('a',), "genpareto": ('c',), "fisk": ('c',), "burr": ('c', 'd',), "burr12": ('c', 'd',), "exponweib": ('a', 'c',), "exponpow": ('b',), "bradford": ('c',), "anglit": (), "levy": (), "levy_l": (), "gibrat": (), "invweibull": ('c',), "loglaplace": ('c',), "truncexpon": ('b',), "chi": ('df',), "maxwell": (), "nakagami": ('nu',), "dweibull": ('c',), "kappa3": ('a',), "genhalflogistic": ('c',), "alpha": ('a',), "fatiguelife": ('c',), "genlogistic": ('c',), "trapezoid": ('c', 'd',)}
+                "halfcauchy": (), "halflogistic": (), "halfnorm": (), "arcsine": (), "hypsecant": (),
+                "powerlaw": ("a",), "genpareto": ("c",), "fisk": ("c",), "burr": ("c", "d"),
+                "burr12": ("c", "d"), "exponweib": ("a", "c"), "exponpow": ("b",), "bradford": ("c",),
+                "anglit": (), "levy": (), "levy_l": (), "gibrat": (), "invweibull": ("c",),
+                "loglaplace": ("c",), "truncexpon": ("b",), "chi": ("df",), "maxwell": (), "nakagami": ("nu",),
+                "dweibull": ("c",), "kappa3": ("a",), "genhalflogistic": ("c",), "alpha": ("a",),
+                "fatiguelife": ("c",), "genlogistic": ("c",), "trapezoid": ("c", "d")}
 _DISCRETE = {"poisson", "binom", "bernoulli"}
 # distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so
 # that Iman-Conover takes them as generated columns (pbh_ppf.hip k_lhs_sorted_ppf / k_place_gen;
