@@ -34,7 +34,6 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 
 LAUNCH_BYTES = {
     "k_lhs_sorted_ppf": 0,       # stratum-ordered generation for the tie / inversion counts only: nothing stored
     "k_perm_scores": 8,          # write S 8 (ranks from the LHS permutation: no sort of X)
-    "k_scores_gram": 8,          # write S 8, the Gram from the tiles in LDS   (all columns)
     "k_gram": 8,                 # read S 8                                   (all columns)
     "k_apply": 20,               # read S 8, write CS 8 + code 4              (all columns)
     "k_hist16": 4,               # read code 4                                (all columns)
@@ -47,7 +46,7 @@ LAUNCH_BYTES = {
     "k_digit_hist<u32>": 4, "k_scatter<u32>": 16, "k_code_runs": 17, "k_scatter<place>": 24, "k_place": 20,
     "k_lhs_ppf": 8, "k_ppf": 16, "k_elementwise": 24,
 }
-ALL_COLUMNS = {"k_gram", "k_apply", "k_hist16", "k_scores_gram"}
+ALL_COLUMNS = {"k_gram", "k_apply", "k_hist16"}
 
 
 def kernel_bytes(name, n, k):
@@ -62,7 +61,7 @@ PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k
                                   "k_scatter<unsigned int, double>"],
              "k_code_runs": ["k_code_buckets", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
              "k_apply": ["k_apply_mfma_w2<true>", "k_apply_mfma_w2<false>", "k_apply_mfma", "k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"],
-             "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"], "k_scores_gram": ["k_scores_gram"],
+             "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"],
              "k_finish": ["k_finish_q<1024, 512, false>", "k_finish_q<1024, 512, true>", "k_finish_q<2048, 512, true>",
                           "k_finish_q<1024, 256, true>", "k_finish_ah<2048>", "k_finish_ah<1024>", "k_finish_ah<4096>", "k_finish_fused<2, 4096>", "k_finish_fused<2, 4096, false>",
                           "k_finish_fused<2, 4096, true>", "k_finish_fused<1, 4096>", "k_finish_fused<2, 2048>",

@@ -72,7 +72,7 @@ size_t ic_bytes(int64_t n, int k, bool carve, void* base, IcLayout* L) {
   void* S = c.take((size_t)n * k * 8);
   void* sx = c.take((size_t)n * k * 8);
   void* rws = c.take(reorder_ws_bytes(n));
-  void* part = c.take(std::max(gram_partials_bytes(k), k <= 32 ? scores_gram_ws_bytes() : (size_t)0));
+  void* part = c.take(gram_partials_bytes(k));
   void* means = c.take((size_t)k * 8);
   void* gram = c.take((size_t)k * k * 8);
   void* Lm = c.take((size_t)k * k * 8);
@@ -311,17 +311,6 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
   // ---- step 1: van der Waerden scores of every column (+ the sorted column for step 4)
   PBH_CHECK_HIP(hipMemsetAsync(L.flag, 0, sizeof(int32_t), s));
   bool all_generated = true;  // every column's scores came from perm_scores (with partial sums)
-  // scores + step 2 in one pass (k_scores_gram) when every column is generated, k <= 32 and the
-  // tied columns' run heads fit its LDS list; PBH_SCORES_GRAM=0: per-column scores, then the Gram
-  static const bool sg_on = [] {
-    const char* e = getenv("PBH_SCORES_GRAM");
-    return !(e && e[0] == '0');
-  }();
-  std::vector<int> sg_pending;  // generated columns whose scores wait for k_scores_gram
-  std::vector<const uint32_t*> sg_heads((size_t)k, nullptr);
-  std::vector<int64_t> sg_nheads((size_t)k, 0);
-  int64_t sg_heads_total = 0;
-  const bool sg_try = sg_on && a->columns && k <= 32;
   std::vector<char> regenerable(k, 0);  // step 4 may regenerate sort(X[:, c])[p] from p (gen_place)
   // Generated columns: every sorted column first, with its tie / inversion counts and run heads
   // but without storing it (step 4 regenerates sort(X)[p]; the fallbacks materialise it on
@@ -407,18 +396,10 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
           }
           if (st) return st;
         }
-        regenerable[c] = 1;
-        const bool listed = heads == nullptr || heads == L.heads_all + (int64_t)c * kHeadsCap;  // not L.tmp
-        if (sg_try && listed && sg_heads_total + (heads ? nheads : 0) <= kScoresGramHeads) {
-          sg_pending.push_back(c);
-          sg_heads[c] = heads;
-          sg_nheads[c] = nheads;
-          sg_heads_total += heads ? nheads : 0;
-          continue;
-        }
         st = perm_scores(g.seed, n, g.lhs_col, 0, n, heads, nheads, S_c, s,
                          L.colpart + (int64_t)c * perm_scores_blocks(n));
         if (st) return st;
+        regenerable[c] = 1;
         continue;
       }
       // not monotone on this grid: materialise the column in row order and sort it
@@ -439,24 +420,6 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
     if (st) return st;
     have_sx[c] = 1;
-  }
-  const bool sg_fused = all_generated && (int)sg_pending.size() == k;
-  if (sg_fused) {
-    std::vector<uint64_t> seeds((size_t)k);
-    std::vector<int> cols((size_t)k);
-    for (int c = 0; c < k; ++c) {
-      seeds[c] = a->columns[c].seed;
-      cols[c] = a->columns[c].lhs_col;
-    }
-    st = scores_gram(n, k, seeds.data(), cols.data(), sg_heads.data(), sg_nheads.data(), L.S, n, L.partials, L.means,
-                     L.gram, s);
-    if (st) return st;
-  } else {
-    for (int c : sg_pending) {
-      st = perm_scores(a->columns[c].seed, n, a->columns[c].lhs_col, 0, n, sg_heads[c], sg_nheads[c],
-                       L.S + (int64_t)c * n, s, L.colpart + (int64_t)c * perm_scores_blocks(n));
-      if (st) return st;
-    }
   }
   struct Ev {
     hipEvent_t e = nullptr;
@@ -527,15 +490,13 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     PBH_CHECK_HIP(hipMemcpyAsync(a->scores_out, L.S, (size_t)n * k * 8, hipMemcpyDeviceToDevice, s));
 
   // ---- step 2: E = corrcoef(S) on the host from the device Gram matrix
-  if (!sg_fused) {  // (k_scores_gram left the means and the Gram behind)
-    if (all_generated)  // the scores kernels left per-block sums behind
-      st = means_from_partials(L.colpart, (int)perm_scores_blocks(n), k, (double)n, L.means, s);
-    else
-      st = column_means(L.S, n, k, n, L.partials, L.means, s);
-    if (st) return st;
-    st = centered_gram(L.S, n, k, n, L.means, L.partials, L.gram, s);
-    if (st) return st;
-  }
+  if (all_generated)  // the scores kernels left per-block sums behind
+    st = means_from_partials(L.colpart, (int)perm_scores_blocks(n), k, (double)n, L.means, s);
+  else
+    st = column_means(L.S, n, k, n, L.partials, L.means, s);
+  if (st) return st;
+  st = centered_gram(L.S, n, k, n, L.means, L.partials, L.gram, s);
+  if (st) return st;
   PBH_CHECK_HIP(hipMemcpyAsync(G.data(), L.gram, (size_t)k * k * 8, hipMemcpyDeviceToHost, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));
   if (flag_host) {

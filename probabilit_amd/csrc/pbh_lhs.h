@@ -21,16 +21,6 @@ int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, 
                 int64_t nheads, double* S, hipStream_t s, double* partial = nullptr);
 // number of partial sums perm_scores writes for nrows rows
 unsigned perm_scores_blocks(int64_t nrows);
-
-// Scores of k <= 32 LHS columns (n rows each, column c at S + c * ld) together with step 2's
-// column means and centered Gram, in one pass (k_scores_gram): seeds[c], cols[c] as for
-// perm_scores; heads[c] / nheads[c] the sorted run heads of a tied column (nullptr / 0 untied),
-// at most kScoresGramHeads in all.  ws: scores_gram_ws_bytes().  means (k), gram (k x k) as
-// column_means + centered_gram leave them.
-constexpr int kScoresGramHeads = 2048;
-size_t scores_gram_ws_bytes();
-int scores_gram(int64_t n, int k, const uint64_t* seeds, const int* cols, const uint32_t* const* heads,
-                const int64_t* nheads, double* S, int64_t ld, void* ws, double* means, double* gram, hipStream_t s);
 // Run heads of a sorted segment x[0..m) (see k_heads_write); *count = number written (syncs).
 size_t run_heads_ws_bytes(int64_t m);
 int run_heads(const double* x, int64_t m, int64_t t0, bool first_is_prev, uint32_t* heads, int64_t* count,

@@ -15,7 +15,6 @@
 
 #include "pbh_error.h"
 #include "pbh_ppf_core.h"
-#include "pbh_lhs.h"
 #include "pbh_ppf_ext.h"
 #include "pbh_rng.h"
 #include "pbh_special.h"
@@ -1174,219 +1173,6 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
   }
 }
 
-// Scores and step 2 in one pass, for k <= 32 generated columns (pbh_api.hip, single GPU): the
-// scores kernel is VALU-bound (Feistel + ndtri) and the separate Gram pass re-read all of S from
-// HBM (25.6 GB, 4.9 ms per step at cfg3), so here each wave keeps the tile it has just scored --
-// 32 rows x 32 columns, in LDS -- and feeds it to v_mfma_f64_16x16x4_f64 before moving on.  Lane
-// l scores row (l & 31) of column 2j + (l >> 5) for j = 0..15: 32 consecutive rows of one column
-// per half-wave, so the centre scores go straight to S in 256-byte runs; the Feistel keys of the
-// 32 columns come from LDS.  ndtri's tail is compacted per wave as in k_perm_scores (a stack of
-// at most 127 entries, drained 64 at a time); the tile's last < 64 entries are drained before its
-// MFMAs.  The wave then adds the tile's uncentered products (three 16 x 16 tiles of the 32 x 32
-// upper block triangle, as k_gram_mfma) and its column sums; the four waves' sums meet in LDS at
-// the end, one partial per block, reduced in a fixed order by k_sg_reduce, and centered by
-// k_sg_final (sum S_i S_j - sum_i sum_j / n: the means of scores are ~0, nothing cancels).  Every
-// order is fixed, so the result is deterministic.  The tile is stored [column][row ^ swizzle]:
-// the half-waves' column runs and the MFMA's 16-column x 4-row reads are both conflict-free.
-typedef double sg_f64x4 __attribute__((ext_vector_type(4)));
-constexpr int kSGRows = 32;                   // rows of a wave tile
-constexpr int kSGQ = 128;                     // a wave's tail stack
-constexpr int kSGParts = 32 * 32 + 32;        // a block's partial: products (i <= j), column sums
-constexpr int kSGBlocksMax = 1024;
-constexpr int kSGChains = 4;               // Feistel evaluations in flight per lane
-
-struct ScoresGramCols {
-  uint32_t rk[32][4];          // Feistel keys of each column
-  const uint32_t* heads[32];   // a tied column's sorted run heads (device), nullptr untied
-  uint32_t hoff[33];           // column c's run heads at [hoff[c], hoff[c + 1]) of the LDS list
-};
-
-__device__ __forceinline__ int sg_at(int c, int row) { return c * kSGRows + (row ^ ((c & 7) << 2)); }
-
-// orders a wave's LDS accesses across lanes (no block barrier)
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__global__ __launch_bounds__(kBlock) PBH_OCC void k_scores_gram(FeistelPerm fp, int k, int64_t nrows,
-                                                          ScoresGramCols cols, double* __restrict__ S, int64_t ld,
-                                                          double* __restrict__ partial) {
-  __shared__ double tile[kBlock / 64][32 * kSGRows];
-  __shared__ double qarg[kBlock / 64][kSGQ];
-  __shared__ uint16_t qidx[kBlock / 64][kSGQ];
-  __shared__ uint32_t srk[32][4];
-  __shared__ uint32_t shoff[33];
-  extern __shared__ uint32_t lheads[];
-  for (int c = 0; c < k; ++c) {
-    const int h0 = (int)cols.hoff[c], nh = (int)cols.hoff[c + 1] - h0;
-    for (int i = threadIdx.x; i < nh; i += kBlock) lheads[h0 + i] = cols.heads[c][i];
-  }
-  if (threadIdx.x < 128) srk[threadIdx.x >> 2][threadIdx.x & 3] = cols.rk[threadIdx.x >> 2][threadIdx.x & 3];
-  if (threadIdx.x < 33) shoff[threadIdx.x] = cols.hoff[threadIdx.x];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double* T = tile[w];
-  for (int e = lane; e < 32 * kSGRows; e += 64) T[e] = 0.0;  // columns >= k stay zero
-  __syncthreads();
-  const uint64_t n = fp.n;
-  const double np1 = (double)(n + 1);
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  double* qa = qarg[w];
-  uint16_t* qi = qidx[w];
-  const int row = lane & 31, half = lane >> 5;
-  const int npairs = (k + 1) >> 1;
-  sg_f64x4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c11 = c00;
-  double csum = 0.0;  // lanes < 32: column `lane`
-  const int64_t ntiles = (nrows + kSGRows - 1) / kSGRows;
-  const int64_t gw = (int64_t)blockIdx.x * (kBlock / 64) + w, W = (int64_t)gridDim.x * (kBlock / 64);
-  for (int64_t tb = gw; tb < ntiles; tb += W) {
-    const int64_t r = tb * kSGRows + row;
-    const bool inrow = r < nrows;
-    int qc = 0;  // wave-uniform
-    for (int j0 = 0; j0 < npairs; j0 += kSGChains) {
-      uint64_t tt[kSGChains];
-#pragma unroll
-      for (int jj = 0; jj < kSGChains; ++jj) {
-        const int c = 2 * (j0 + jj) + half;
-        tt[jj] = inrow && c < k && n > 1 ? fp.round_trip_keys((uint64_t)r, srk[c]) : 0;
-      }
-#pragma unroll
-      for (int jj = 0; jj < kSGChains; ++jj) {
-        const int c = 2 * (j0 + jj) + half;
-        while (tt[jj] >= n) tt[jj] = fp.round_trip_keys(tt[jj], srk[c]);
-      }
-#pragma unroll 1
-      for (int jj = 0; jj < kSGChains; ++jj) {
-        const int c = 2 * (j0 + jj) + half;
-        const bool valid = inrow && c < k;
-        double y = 0.5;
-        if (valid) {
-          const int h0 = (int)shoff[c], nh = (int)shoff[c + 1] - h0;
-          const uint64_t t = tt[jj];
-          const double rank = nh ? run_average_rank(lheads + h0, nh, (int64_t)n, (int64_t)t) : (double)(t + 1);
-          y = rank / np1;
-        }
-        const bool tail = valid && sf::ndtri_takes_tail(y);
-        if (c < k && !tail) {
-          double v = 0.0;
-          if (valid) {
-            v = sf::ndtri_centre(y);
-            S[(int64_t)c * ld + r] = v;
-          }
-          T[sg_at(c, row)] = v;
-        }
-        const uint64_t m = __ballot(tail);
-        if (tail) {
-          const int slot = qc + (int)__popcll(m & lt);
-          qa[slot] = y;
-          qi[slot] = (uint16_t)sg_at(c, row);
-        }
-        qc += (int)__popcll(m);
-        if (qc >= 64) {  // a full-width batch off the top of the stack
-          qc -= 64;
-          wave_lds_sync();
-          const double a = qa[qc + lane];
-          const int e = qi[qc + lane];
-          const double v = sf::ndtri_tail(a);
-          T[e] = v;
-          const int ec = e / kSGRows, er = (e % kSGRows) ^ ((ec & 7) << 2);
-          S[(int64_t)ec * ld + tb * kSGRows + er] = v;
-          wave_lds_sync();
-        }
-      }
-    }
-    if (qc > 0) {  // the tile's last (< 64) tail entries
-      wave_lds_sync();
-      if (lane < qc) {
-        const double a = qa[lane];
-        const int e = qi[lane];
-        const double v = sf::ndtri_tail(a);
-        T[e] = v;
-        const int ec = e / kSGRows, er = (e % kSGRows) ^ ((ec & 7) << 2);
-        S[(int64_t)ec * ld + tb * kSGRows + er] = v;
-      }
-    }
-    wave_lds_sync();
-#pragma unroll 1
-    for (int q = 0; q < kSGRows / 4; ++q) {
-      const int rr = 4 * q + (lane >> 4), cc = lane & 15;
-      const double a0 = T[sg_at(cc, rr)];
-      const double a1 = T[sg_at(16 + cc, rr)];
-      c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a0, c00, 0, 0, 0);
-      c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a1, c01, 0, 0, 0);
-      c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, a1, c11, 0, 0, 0);
-    }
-    if (lane < 32) {
-      double s = 0.0;
-#pragma unroll 8
-      for (int rr = 0; rr < kSGRows; ++rr) s += T[sg_at(lane, rr)];
-      csum += s;
-    }
-    wave_lds_sync();  // the next tile's writes after this tile's reads
-  }
-  // the four waves' sums, in a fixed order: red[w][tile][reg][lane], then the column sums
-  __syncthreads();
-  double* red = &tile[0][0];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    red[((w * 3 + 0) * 4 + g) * 64 + lane] = c00[g];
-    red[((w * 3 + 1) * 4 + g) * 64 + lane] = c01[g];
-    red[((w * 3 + 2) * 4 + g) * 64 + lane] = c11[g];
-  }
-  if (lane < 32) red[3072 + w * 32 + lane] = csum;
-  __syncthreads();
-  double* out = partial + (int64_t)blockIdx.x * kSGParts;
-  for (int e = threadIdx.x; e < 3 * 4 * 64; e += kBlock) {  // e = (tile * 4 + reg) * 64 + lane
-    const int tl = e / 256, g = (e >> 6) & 3, l = e & 63;
-    const double v = ((red[((0 * 3 + tl) * 4 + g) * 64 + l] + red[((1 * 3 + tl) * 4 + g) * 64 + l]) +
-                      red[((2 * 3 + tl) * 4 + g) * 64 + l]) +
-                     red[((3 * 3 + tl) * 4 + g) * 64 + l];
-    const int i = (l >> 4) + 4 * g + (tl == 2 ? 16 : 0);
-    const int j = (l & 15) + (tl >= 1 ? 16 : 0);
-    if (i <= j) out[i * 32 + j] = v;
-  }
-  if (threadIdx.x < 32) {
-    const int c = threadIdx.x;
-    out[1024 + c] = ((red[3072 + c] + red[3072 + 32 + c]) + red[3072 + 64 + c]) + red[3072 + 96 + c];
-  }
-}
-
-// raw[e] = sum over the nb block partials of entry e (one block per entry in use; strided sums,
-// then a fixed tree)
-__global__ __launch_bounds__(256) void k_sg_reduce(const double* __restrict__ partial, int nb, int k,
-                                                   double* __restrict__ raw) {
-  __shared__ double sh[256];
-  const int e = blockIdx.x, t = threadIdx.x;
-  const bool used = e < 1024 ? ((e >> 5) < k && (e & 31) < k && (e >> 5) <= (e & 31)) : (e - 1024) < k;
-  if (!used) return;
-  double s = 0.0;
-  for (int b = t; b < nb; b += 256) s += partial[(int64_t)b * kSGParts + e];
-  sh[t] = s;
-  __syncthreads();
-#pragma unroll
-  for (int o = 128; o > 0; o >>= 1) {
-    if (t < o) sh[t] += sh[t + o];
-    __syncthreads();
-  }
-  if (t == 0) raw[e] = sh[0];
-}
-
-// means[c] = sum_c / n; gram[i][j] = sum S_i S_j - sum_i sum_j / n (the centered Gram)
-__global__ void k_sg_final(const double* __restrict__ raw, int k, double n, double* __restrict__ means,
-                           double* __restrict__ gram) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < k) means[e] = raw[1024 + e] / n;
-  if (e >= k * k) return;
-  int i = e / k, j = e % k;
-  if (i > j) {
-    const int t = i;
-    i = j;
-    j = t;
-  }
-  gram[e] = raw[i * 32 + j] - raw[1024 + i] * raw[1024 + j] / n;
-}
-
 // Run heads of a sorted segment x[0..m): position p is a head when p == 0 (unless x[0] is
 // the value before the segment, first_is_prev) or x[p] != x[p - 1]; heads are reported as
 // t0 + p (t0 - 1 + p with first_is_prev).  Two passes: per-tile counts, then ordered writes.
@@ -2154,37 +1940,6 @@ int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, 
   PBH_TIMED(kKPermScores, s,
             hipLaunchKernelGGL(k_perm_scores, dim3(scores_grid(nrows)), dim3(kBlock), lds, s, seed, n, (uint32_t)col,
                                row0, nrows, heads, nheads, S, partial));
-  PBH_CHECK_LAUNCH();
-  return PBH_OK;
-}
-
-size_t scores_gram_ws_bytes() { return (size_t)(kSGBlocksMax + 1) * kSGParts * 8; }
-
-int scores_gram(int64_t n, int k, const uint64_t* seeds, const int* cols, const uint32_t* const* heads,
-                const int64_t* nheads, double* S, int64_t ld, void* ws, double* means, double* gram, hipStream_t s) {
-  PBH_REQUIRE(k >= 1 && k <= 32 && n >= 1 && ld >= n, "scores_gram: k in [1, 32], ld >= n");
-  ScoresGramCols sc = {};
-  int64_t nh_all = 0;
-  for (int c = 0; c < k; ++c) {
-    const FeistelPerm f(Philox(seeds[c]), (uint64_t)n, (uint32_t)cols[c]);
-    for (int i = 0; i < 4; ++i) sc.rk[c][i] = f.rk[i];
-    sc.hoff[c] = (uint32_t)nh_all;
-    sc.heads[c] = heads[c];
-    nh_all += heads[c] ? nheads[c] : 0;
-  }
-  for (int c = k; c <= 32; ++c) sc.hoff[c] = (uint32_t)nh_all;
-  PBH_REQUIRE(nh_all <= kScoresGramHeads, "scores_gram: too many run heads for LDS");
-  const FeistelPerm fp(Philox(seeds[0]), (uint64_t)n, (uint32_t)cols[0]);
-  const int64_t ntiles = (n + kSGRows - 1) / kSGRows;
-  int64_t nb = (ntiles + kBlock / 64 - 1) / (kBlock / 64);
-  if (nb > kSGBlocksMax) nb = kSGBlocksMax;
-  double* partial = (double*)ws;
-  double* raw = partial + (int64_t)kSGBlocksMax * kSGParts;
-  PBH_TIMED(kKScoresGram, s,
-            hipLaunchKernelGGL(k_scores_gram, dim3((unsigned)nb), dim3(kBlock), (size_t)nh_all * 4, s, fp, k, n, sc, S,
-                               ld, partial));
-  hipLaunchKernelGGL(k_sg_reduce, dim3(kSGParts), dim3(256), 0, s, partial, (int)nb, k, raw);
-  hipLaunchKernelGGL(k_sg_final, dim3((k * k + 255) / 256), dim3(256), 0, s, raw, k, (double)n, means, gram);
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }

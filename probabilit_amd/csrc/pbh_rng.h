@@ -146,19 +146,16 @@ struct FeistelPerm {
     return small ? (uint64_t)(mul24(L, B) + R) : (uint64_t)L * B + R;
   }
 
-  PBH_HD inline uint64_t round_trip(uint64_t x) const { return round_trip_keys(x, rk); }
-
-  // the same rounds under another column's keys (k_scores_gram: one lane, many columns)
-  PBH_HD inline uint64_t round_trip_keys(uint64_t x, const uint32_t* keys) const {
+  PBH_HD inline uint64_t round_trip(uint64_t x) const {
     uint32_t L, R;
     split(x, L, R);
 #pragma unroll
     for (int i = 0; i < kRounds; ++i) {
       if (i & 1) {
-        const uint32_t h = reduce(F(L, keys[i]), B);
+        const uint32_t h = reduce(F(L, rk[i]), B);
         R = R + h >= B ? R + h - B : R + h;
       } else {
-        const uint32_t h = reduce(F(R, keys[i]), A);
+        const uint32_t h = reduce(F(R, rk[i]), A);
         L = L + h >= A ? L + h - A : L + h;
       }
     }

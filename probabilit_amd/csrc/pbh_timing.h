@@ -42,7 +42,6 @@ enum KernelId {
   kKPlaceMsd,
   kKPlaceGen,
   kKDag,
-  kKScoresGram,
   kKCount
 };
 

@@ -197,8 +197,7 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     (PBH_APPLY_ROWS=64), the poisson run heads from every stratum instead of the boundary search
     (PBH_DISCRETE_SCAN=1), the code histogram with the tile-class counts per code (PBH_HIST_CLASS=0),
     step 3 with one-row accesses (PBH_APPLY_W2=0; the default pairs rows in 16-byte accesses, the odd
-    N taking its one-row tail) or with cached paired accesses (PBH_APPLY_NT=0; the default is non-temporal),
-    the scores kernel and the Gram pass apart (PBH_SCORES_GRAM=0; the default fuses them)
+    N taking its one-row tail) or with cached paired accesses (PBH_APPLY_NT=0; the default is non-temporal)
     -- step-4 indices equal to the oracle's and the outputs within 1e-10.  600 001 rows: 8 histogram
     blocks per column, so the default takes the class-major k_hist16c."""
     import os
@@ -213,7 +212,7 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     ref = _oracle(n, dists, seed, C)
     for env in ({"PBH_HIST_CLASS": "0"}, {"PBH_MSD_TILE": "4096", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"},
                 {"PBH_FINISH_CFG": "30"}, {"PBH_GAMMA_WIN": "0"}, {"PBH_PLACE_TOP": "0"}, {"PBH_APPLY_ROWS": "64"},
-                {"PBH_DISCRETE_SCAN": "1"}, {"PBH_APPLY_W2": "0"}, {"PBH_APPLY_NT": "0"}, {"PBH_SCORES_GRAM": "0"}):
+                {"PBH_DISCRETE_SCAN": "1"}, {"PBH_APPLY_W2": "0"}, {"PBH_APPLY_NT": "0"}):
         dd = tmp_path / "_".join(f"{k}{v}" for k, v in env.items())
         dd.mkdir()
         script = _VARIANT_SCRIPT.format(root=root, tests=os.path.join(root, "tests"), d=str(dd), n=n, dists=dists,
@@ -223,43 +222,6 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
         assert r.returncode == 0, (env, r.stderr[-3000:])
         np.testing.assert_array_equal(np.load(dd / "idx.npy"), ref["idx"], err_msg=str(env))
         assert_close(np.load(dd / "Y.npy"), ref["Y"], rtol=1e-10, what=str(env))
-
-
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("n,d,seed,dists", [(33, 3, 41, None), (4097, 2, 43, None), (100_003, 32, 42, None),
-                                            (300_001, 5, 44, [("poisson", {"mu": 4.0}), ("norm", {}),
-                                                              ("poisson", {"mu": 30.0}), ("gamma", {"a": 2.0}),
-                                                              ("binom", {"n": 20, "p": 0.3})])])
-def test_scores_gram_fused_equals_separate(gpu, tmp_path, n, d, seed, dists):
-    """k_scores_gram (the scores, column means and centered Gram of k <= 32 generated columns in
-    one pass, the default) against the scores kernel and the Gram pass apart (PBH_SCORES_GRAM=0,
-    in its own process): the same scores bit for bit, E within 1e-12 (the Gram's sums run in
-    another order), and both with the oracle's step-4 indices.  Cases: a partial last tile and an
-    odd column count (33 x 3), two columns, the 32 of cfg3, and tied columns whose run heads share
-    the kernel's LDS list (poisson, binom)."""
-    import os
-    import subprocess
-    import sys
-
-    from oracle.pipeline import cfg3_corr, cfg_dists
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    dists = dists or cfg_dists(d)
-    C = cfg3_corr(d)
-    fused = _debug_run(n, dists, seed, C)
-    dd = tmp_path / "separate"
-    dd.mkdir()
-    script = _VARIANT_SCRIPT.format(root=root, tests=os.path.join(root, "tests"), d=str(dd), n=n, dists=dists,
-                                  seed=seed, C=C.tolist())
-    r = subprocess.run([sys.executable, "-c", script], env={**os.environ, "PBH_SCORES_GRAM": "0"},
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    np.testing.assert_array_equal(fused["S"], np.load(dd / "S.npy"))
-    assert_close(fused["E"], np.load(dd / "E.npy"), rtol=1e-12, atol=1e-14, what="E fused vs separate")
-    ref = _oracle(n, dists, seed, C)
-    np.testing.assert_array_equal(fused["idx"], ref["idx"])
-    np.testing.assert_array_equal(np.load(dd / "idx.npy"), ref["idx"])
-    assert_close(fused["Y"], ref["Y"], rtol=1e-10, what="fused scores + Gram")
 
 
 @pytest.mark.parametrize("shape", [0.1, 0.25])
