@@ -389,6 +389,7 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
           if (gen_discrete(a->columns[c].dist) && nheads <= cap) {  // appended heads, put in order
             heads = L.heads_all + (int64_t)c * kHeadsCap;
             st = sort_heads(heads, nheads, s);
+            if (!st) st = gen_set_runs(gens.g[c], heads, nheads, s);  // step 4 reads each run's value
           } else {  // too many distinct values for the list: from the materialised column
             heads = (uint32_t*)L.tmp;
             st = materialise(c);

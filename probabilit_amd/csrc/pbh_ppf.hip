@@ -1015,6 +1015,90 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_poisson(const uint
   }
 }
 
+// A discrete column's placement from its runs (gen_set_runs): the sorted column is constant on
+// each run [heads[i], heads[i + 1]) of strata, so the value of stratum p is vals[run of p] --
+// bit-identical to evaluating it, by the definition of the heads (every stratum whose value
+// differs from its predecessor's) -- found through a guide over p >> shift (most cells lie in
+// one run: one compare) instead of the jitter hash and the CDF-table search of every row.  The
+// runs, their values and the guide sit in (dynamic) LDS next to the 4096-row block.
+constexpr int kRunsGuideMax = 2048;
+constexpr int64_t kRunsLdsMax = 1024;  // runs staged in LDS (12 B each)
+
+__device__ __forceinline__ int runs_guide_shift(int64_t n) {
+  int sh = 0;
+  while (((n - 1) >> sh) + 1 > kRunsGuideMax) ++sh;
+  return sh;
+}
+
+template <bool BYROW = false>
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_runs(const uint64_t* __restrict__ pairs,
+                                                           const uint32_t* __restrict__ pidx, int64_t rows, int64_t n,
+                                                           const uint32_t* __restrict__ heads,
+                                                           const double* __restrict__ vals, int nruns,
+                                                           double* __restrict__ y, int64_t y_rs,
+                                                           int32_t* __restrict__ idx,
+                                                           const int32_t* __restrict__ state) {
+  if (state && *state) return;
+  extern __shared__ double rlds[];
+  __shared__ double buf[kGenRows];
+  double* lv = rlds;                                   // nruns values
+  uint32_t* lh = (uint32_t*)(rlds + nruns);            // nruns heads
+  uint32_t* lg = lh + nruns;                           // guide
+  const int sh = runs_guide_shift(n);
+  const int ng = (int)(((n - 1) >> sh) + 1);
+  for (int i = threadIdx.x; i < nruns; i += kBlock) {
+    lv[i] = vals[i];
+    lh[i] = heads[i];
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < ng; g += kBlock) {  // guide[g] = the run holding stratum g << sh
+    const uint32_t t = (uint32_t)((int64_t)g << sh);
+    int lo = 0, hi = nruns;  // first head > t
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (lh[mid] <= t)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    lg[g] = (uint32_t)(lo - 1);
+  }
+  __syncthreads();
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
+    for (int h = 0; h < kGenRows; h += 4 * kBlock) {  // 4 independent chains per thread
+      uint64_t pr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = h + j * kBlock + threadIdx.x;
+        if constexpr (BYROW)
+          pr[j] = p < cnt ? ((uint64_t)(r0 + p) << 32) | pidx[r0 + p] : ~0ull;
+        else
+          pr[j] = p < cnt ? pairs[r0 + p] : ~0ull;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (pr[j] != ~0ull) {
+          const uint32_t t = (uint32_t)pr[j];
+          uint32_t r = lg[t >> sh];
+          while (r + 1 < (uint32_t)nruns && lh[r + 1] <= t) ++r;
+          const int64_t row = (int64_t)(pr[j] >> 32);
+          if (!BYROW && idx) idx[row] = (int32_t)t;
+          buf[row - r0] = lv[r];
+        }
+      }
+    }
+    __syncthreads();
+    if (y_rs == 1) {
+      for (int p = threadIdx.x; p < cnt; p += kBlock) y[r0 + p] = buf[p];
+    } else {
+      for (int p = threadIdx.x; p < cnt; p += kBlock) y[(r0 + p) * y_rs] = buf[p];
+    }
+    __syncthreads();
+  }
+}
+
 // counts[0] += #(x[t] == x[t+1]), counts[1] += #(x[t] > x[t+1] or unordered)
 __global__ __launch_bounds__(kBlock) void k_check_sorted(const double* __restrict__ x, int64_t n,
                                                          unsigned long long* counts) {
@@ -1511,6 +1595,9 @@ struct GenColumn {
   double* table;
   bool ext;        // an extended distribution (pbh_ppf_ext.hip): its kernels take xval
   double xval[4];
+  const uint32_t* rheads = nullptr;  // a discrete column's sorted run heads (gen_set_runs)
+  double* rvals = nullptr;           // the value of each run
+  int64_t nruns = 0;
 };
 
 int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* params, int nparams, GenColumn** out,
@@ -1546,6 +1633,7 @@ int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* par
 void gen_destroy(GenColumn* g, hipStream_t s) {
   if (!g) return;
   if (g->table) (void)hipFreeAsync(g->table, s);
+  if (g->rvals) (void)hipFreeAsync(g->rvals, s);
   delete g;
 }
 
@@ -1828,6 +1916,19 @@ template <bool BYROW>
 static int place_launch(const GenColumn* g, const uint64_t* pairs, const uint32_t* pidx, int64_t rows, double* y,
                         int64_t y_rs, int32_t* idx, const int32_t* state, hipStream_t s) {
   const int64_t n = g->n;
+  if (g->rvals) {  // a discrete column with its runs: values from the run table
+    const int64_t blocks = (rows + kGenRows - 1) / kGenRows;
+    if (blocks <= 0) return PBH_OK;
+    int sh = 0;
+    while (((n - 1) >> sh) + 1 > kRunsGuideMax) ++sh;
+    const size_t lds = (size_t)g->nruns * 12 + (size_t)(((n - 1) >> sh) + 1) * 4;
+    PBH_TIMED(kKPlaceGen, s,
+              hipLaunchKernelGGL(k_place_gen_runs<BYROW>, dim3((unsigned)(blocks < 256 * 8 ? blocks : 256 * 8)),
+                                 dim3(kBlock), lds, s, pairs, pidx, rows, n, g->rheads, g->rvals, (int)g->nruns, y,
+                                 y_rs, idx, state));
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
   if (g->ext)
     return ext_gen_place(g->seed, n, g->col, g->dist, g->xval, g->table, pairs, BYROW ? pidx : nullptr, rows, y, y_rs,
                          idx, state, s);
@@ -1897,6 +1998,26 @@ int gen_place(const GenColumn* g, const uint64_t* pairs, int64_t n, double* y, i
 
 int gen_values_at(const GenColumn* g, const uint32_t* p, int64_t m, double* y, int64_t y_rs, hipStream_t s) {
   return place_launch<true>(g, nullptr, p, m, y, y_rs, nullptr, nullptr, s);
+}
+
+int gen_set_runs(GenColumn* g, const uint32_t* heads, int64_t nh, hipStream_t s) {
+  static const bool on = [] {  // PBH_PLACE_RUNS=0 (A/B): every row through the inverse CDF
+    const char* e = getenv("PBH_PLACE_RUNS");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || !gen_discrete(g->dist) || nh < 1 || nh > kRunsLdsMax || g->n < 1) return PBH_OK;
+  double* v = nullptr;
+  PBH_CHECK_HIP(hipMallocAsync((void**)&v, (size_t)nh * 8, s));
+  const int st = gen_values_at(g, heads, nh, v, 1, s);  // the value of each run: its head's
+  if (st != PBH_OK) {
+    (void)hipFreeAsync(v, s);
+    return st;
+  }
+  if (g->rvals) (void)hipFreeAsync(g->rvals, s);
+  g->rvals = v;
+  g->rheads = heads;
+  g->nruns = nh;
+  return PBH_OK;
 }
 
 int lhs_sorted_ppf(uint64_t seed, int64_t n, int64_t t0, int64_t nt, int col, int dist, const pbh_param* params,

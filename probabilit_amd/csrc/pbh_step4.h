@@ -120,6 +120,11 @@ int gen_place(const GenColumn* g, const uint64_t* pairs, int64_t n, double* y, i
 // y[i * y_rs] = value of stratum p[i] for i < m (the row owner of a row-sharded run: the sorted
 // positions of its rows, sent back by the column's owner; the same kernels as gen_place)
 int gen_values_at(const GenColumn* g, const uint32_t* p, int64_t m, double* y, int64_t y_rs, hipStream_t s);
+// A discrete column's sorted run heads (heads[0] == 0, increasing, no inversion in the column):
+// its placement then reads each run's value from a table (k_place_gen_runs) instead of evaluating
+// the inverse CDF per row.  heads must stay valid while g is placed.  No-op unless the column is
+// discrete with 1 <= nh <= 1024 runs (or with PBH_PLACE_RUNS=0).
+int gen_set_runs(GenColumn* g, const uint32_t* heads, int64_t nh, hipStream_t s);
 // p_out[row] = p for every pair (row << 32 | p) of `pairs` grouped by 4096-row block, the block
 // assembled in LDS and written contiguously (the owner's step-4 output of a row-sharded run);
 // state (optional device word): skip when non-zero

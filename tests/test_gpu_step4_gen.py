@@ -197,8 +197,9 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     (PBH_APPLY_ROWS=64), the poisson run heads from every stratum instead of the boundary search
     (PBH_DISCRETE_SCAN=1), the code histogram with the tile-class counts per code (PBH_HIST_CLASS=0),
     step 3 with one-row accesses (PBH_APPLY_W2=0; the default pairs rows in 16-byte accesses, the odd
-    N taking its one-row tail) or with cached paired accesses (PBH_APPLY_NT=0; the default is non-temporal)
-    -- step-4 indices equal to the oracle's and the outputs within 1e-10.  600 001 rows: 8 histogram
+    N taking its one-row tail) or with cached paired accesses (PBH_APPLY_NT=0; the default is non-temporal),
+    the discrete columns' values through the inverse CDF per row (PBH_PLACE_RUNS=0; the default reads
+    them from the run table) -- step-4 indices equal to the oracle's and the outputs within 1e-10.  600 001 rows: 8 histogram
     blocks per column, so the default takes the class-major k_hist16c."""
     import os
     import subprocess
@@ -212,7 +213,7 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     ref = _oracle(n, dists, seed, C)
     for env in ({"PBH_HIST_CLASS": "0"}, {"PBH_MSD_TILE": "4096", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"},
                 {"PBH_FINISH_CFG": "30"}, {"PBH_GAMMA_WIN": "0"}, {"PBH_PLACE_TOP": "0"}, {"PBH_APPLY_ROWS": "64"},
-                {"PBH_DISCRETE_SCAN": "1"}, {"PBH_APPLY_W2": "0"}, {"PBH_APPLY_NT": "0"}):
+                {"PBH_DISCRETE_SCAN": "1"}, {"PBH_APPLY_W2": "0"}, {"PBH_APPLY_NT": "0"}, {"PBH_PLACE_RUNS": "0"}):
         dd = tmp_path / "_".join(f"{k}{v}" for k, v in env.items())
         dd.mkdir()
         script = _VARIANT_SCRIPT.format(root=root, tests=os.path.join(root, "tests"), d=str(dd), n=n, dists=dists,
@@ -222,6 +223,22 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
         assert r.returncode == 0, (env, r.stderr[-3000:])
         np.testing.assert_array_equal(np.load(dd / "idx.npy"), ref["idx"], err_msg=str(env))
         assert_close(np.load(dd / "Y.npy"), ref["Y"], rtol=1e-10, what=str(env))
+
+
+@pytest.mark.parametrize("dists", [[("norm", {}), ("poisson", {"mu": 2000.0}), ("binom", {"n": 50, "p": 0.4})],
+                                   [("gamma", {"a": 2.0}), ("bernoulli", {"p": 0.3}), ("poisson", {"mu": 0.5})]])
+def test_discrete_placement_from_runs(gpu, dists):
+    """A discrete column's step-4 values come from its run table (k_place_gen_runs: the value of
+    each run of equal strata values, found through a guide over the stratum) instead of the
+    inverse CDF of every row: poisson(2000) has ~400 runs, many of them shorter than a guide cell
+    in the tails; bernoulli two; binom and poisson(0.5) a handful.  Indices and values are the
+    oracle's."""
+    C = np.array([[1.0, 0.5, 0.2], [0.5, 1.0, 0.3], [0.2, 0.3, 1.0]])
+    n = 300_001
+    Y, idx = _run(n, dists, 17, C)
+    ref = _oracle(n, dists, 17, C)
+    np.testing.assert_array_equal(idx, ref["idx"])
+    assert_close(Y, ref["Y"], rtol=1e-10, what=f"runs placement {dists}")
 
 
 @pytest.mark.parametrize("shape", [0.1, 0.25])
