@@ -636,8 +636,9 @@ __global__ __launch_bounds__(kBlock) void k_cert_eval(uint64_t seed, int64_t n, 
 // is this column's value in stratum p, regenerated here (lhs_sorted_quantile + ppf_one: the
 // same function k_lhs_sorted_ppf evaluates, so bit-identical to the stored sorted column)
 // instead of being carried through the placement passes.  The block is assembled in LDS and
-// written out contiguously.  norm / lognorm compact ndtri's tail (TailQueue, positions = row
-// offsets in the block); gamma / poisson stage their tables in LDS (random p: table gathers).
+// written out contiguously.  norm / lognorm compact ndtri's tail per wave (k_place_gen_w);
+// gamma / poisson stage their tables in LDS (random p: table gathers); a discrete column with its
+// runs reads each run's value (k_place_gen_runs).
 constexpr int kGenRows = 1 << kGenPlaceShift;
 
 // BYROW (the row owner of a row-sharded run, pbh_lhs_values_at): the item at position p of a block
@@ -649,27 +650,16 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
                                                       uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
                                                       double* __restrict__ y, int64_t y_rs, int32_t* __restrict__ idx,
                                                       const int32_t* __restrict__ state) {
+  static_assert(D != PBH_DIST_NORM && D != PBH_DIST_LOGNORM, "ndtri-based distributions: k_place_gen_w");
   if (state && *state) return;
-  constexpr bool kCompact = D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM;
   __shared__ double buf[kGenRows];
-  // the tail queue only where ndtri is evaluated (20 KiB of LDS the others would hold for nothing)
-  struct NoQueue {
-    double arg[1];
-    uint16_t pos[1];
-    int count;
-  };
-  __shared__ std::conditional_t<kCompact, TailQueue, NoQueue> tq[1];
   Philox ph(seed);
   const double p0 = prm.val[0], p1 = prm.val[1], p2 = prm.val[2];
   for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
     const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
     for (int h = 0; h < kGenRows; h += kCTile) {
-      if (kCompact) {
-        if (threadIdx.x == 0) tq[0].count = 0;
-        __syncthreads();
-      }
-      // every pair of the tile first (loads issued together; see ppf_compacted)
+      // every pair of the tile first (loads issued together)
       uint64_t pa[kCIpt];
 #pragma unroll
       for (int j = 0; j < kCIpt; ++j) {
@@ -679,37 +669,109 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
 #pragma unroll
       for (int j = 0; j < kCIpt; ++j) {
         const int p = h + j * kBlock + threadIdx.x;
-        const bool valid = p < cnt;
-        double q = 0.5;
-        int off = 0;
-        if (valid) {
-          uint32_t t;
-          if constexpr (BYROW) {
-            t = (uint32_t)pa[j];
-            off = p;
-          } else {
-            const uint64_t pr = pa[j];
-            t = (uint32_t)pr;
-            const int64_t row = (int64_t)(pr >> 32);
-            if (idx) idx[row] = (int32_t)t;
-            off = (int)(row - r0);
-          }
-          q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
-        }
-        if constexpr (kCompact) {
-          const bool tail = valid && sf::ndtri_takes_tail(q);
-          if (valid && !tail) buf[off] = ppf_one<D, 1>(q, p0, p1, p2, pt);
-          tail_push(tq[0], tail, q, off);
+        if (p >= cnt) continue;
+        uint32_t t;
+        int off;
+        if constexpr (BYROW) {
+          t = (uint32_t)pa[j];
+          off = p;
         } else {
-          if (valid) buf[off] = ppf_one<D>(q, p0, p1, p2, pt);
+          const uint64_t pr = pa[j];
+          t = (uint32_t)pr;
+          const int64_t row = (int64_t)(pr >> 32);
+          if (idx) idx[row] = (int32_t)t;
+          off = (int)(row - r0);
         }
-      }
-      if (kCompact) {
-        __syncthreads();
-        const int T = tq[0].count;
-        for (int i = threadIdx.x; i < T; i += kBlock) buf[tq[0].pos[i]] = ppf_one<D, 2>(tq[0].arg[i], p0, p1, p2, pt);
+        buf[off] = ppf_one<D>(lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n), p0, p1, p2, pt);
       }
     }
+    __syncthreads();
+    if (y_rs == 1) {
+      for (int p = threadIdx.x; p < cnt; p += kBlock) y[r0 + p] = buf[p];
+    } else {
+      for (int p = threadIdx.x; p < cnt; p += kBlock) y[(r0 + p) * y_rs] = buf[p];
+    }
+    __syncthreads();
+  }
+}
+
+// norm / lognorm placement with ndtri's tail compacted per WAVE (as k_perm_scores): wave w takes
+// items [1024 w, 1024 w + 1024) of the 4096-row block, 8 per lane per step, puts the centre values
+// into the block's LDS image and pushes the tail arguments onto its own stack, which it drains 64
+// at a time (full width) after each half-step; the last < 64 go before the block's one barrier.
+// k_place_gen's block-wide queue spent two barriers and a ragged drain on every 2048 items.
+constexpr int kPGQ = 192;  // a wave's tail stack: at most 63 left over + 2 x 64 pushed in a quarter-step
+constexpr int kPGStep = 2;  // items per lane between two drains (the stacks keep 4 blocks per CU)
+
+template <int D, bool BYROW = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_place_gen_w(const uint64_t* __restrict__ pairs,
+                                                        const uint32_t* __restrict__ pidx, int64_t rows, int64_t n,
+                                                        uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
+                                                        double* __restrict__ y, int64_t y_rs,
+                                                        int32_t* __restrict__ idx, const int32_t* __restrict__ state) {
+  static_assert(D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM, "ndtri-based distributions only");
+  if (state && *state) return;
+  __shared__ double buf[kGenRows];
+  __shared__ double qarg[kBlock / 64][kPGQ];
+  __shared__ uint16_t qpos[kBlock / 64][kPGQ];
+  Philox ph(seed);
+  const double p0 = prm.val[0], p1 = prm.val[1], p2 = prm.val[2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  double* qa = qarg[w];
+  uint16_t* qp = qpos[w];
+  constexpr int kPerWave = kGenRows / (kBlock / 64);
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((rows - r0) < kGenRows ? (rows - r0) : kGenRows);
+    int qc = 0;  // wave-uniform
+    for (int h = w * kPerWave; h < (w + 1) * kPerWave; h += 512) {
+      uint64_t pa[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = h + j * 64 + lane;
+        pa[j] = p >= cnt ? 0ull : BYROW ? (uint64_t)pidx[r0 + p] : pairs[r0 + p];
+      }
+#pragma unroll
+      for (int part = 0; part < 8 / kPGStep; ++part) {
+#pragma unroll
+        for (int jj = 0; jj < kPGStep; ++jj) {
+          const int j = part * kPGStep + jj;
+          const int p = h + j * 64 + lane;
+          const bool valid = p < cnt;
+          double q = 0.5;
+          int off = 0;
+          if (valid) {
+            uint32_t t;
+            if constexpr (BYROW) {
+              t = (uint32_t)pa[j];
+              off = p;
+            } else {
+              const uint64_t pr = pa[j];
+              t = (uint32_t)pr;
+              const int64_t row = (int64_t)(pr >> 32);
+              if (idx) idx[row] = (int32_t)t;
+              off = (int)(row - r0);
+            }
+            q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
+          }
+          const bool tail = valid && sf::ndtri_takes_tail(q);
+          if (valid && !tail) buf[off] = ppf_one<D, 1>(q, p0, p1, p2, pt);
+          const uint64_t m = __ballot(tail);
+          if (tail) {
+            const int slot = qc + (int)__popcll(m & lt);
+            qa[slot] = q;
+            qp[slot] = (uint16_t)off;
+          }
+          qc += (int)__popcll(m);
+        }
+        while (qc >= 64) {  // full-width batches off the top of the stack
+          qc -= 64;
+          buf[qp[qc + lane]] = ppf_one<D, 2>(qa[qc + lane], p0, p1, p2, pt);
+        }
+      }
+    }
+    if (lane < qc) buf[qp[lane]] = ppf_one<D, 2>(qa[lane], p0, p1, p2, pt);
     __syncthreads();
     if (y_rs == 1) {
       for (int p = threadIdx.x; p < cnt; p += kBlock) y[r0 + p] = buf[p];
@@ -1960,6 +2022,19 @@ static int place_launch(const GenColumn* g, const uint64_t* pairs, const uint32_
     return PBH_OK;
   }
   const unsigned gr = (unsigned)(blocks < 256 * 8 ? blocks : 256 * 8);
+  if (g->dist == PBH_DIST_NORM || g->dist == PBH_DIST_LOGNORM) {
+#define PBH_WCASE(D)                                                                                   \
+  PBH_TIMED(kKPlaceGen, s,                                                                             \
+            hipLaunchKernelGGL((k_place_gen_w<D, BYROW>), dim3(gr), dim3(kBlock), 0, s, pairs, pidx, rows, n, \
+                               g->seed, g->col, g->prm, g->pt, y, y_rs, idx, state))
+    if (g->dist == PBH_DIST_NORM)
+      PBH_WCASE(PBH_DIST_NORM);
+    else
+      PBH_WCASE(PBH_DIST_LOGNORM);
+#undef PBH_WCASE
+    PBH_CHECK_LAUNCH();
+    return PBH_OK;
+  }
   if (const size_t pl = poisson_lds_bytes(g->dist, g->prm, g->pt)) {
     PBH_TIMED(kKPlaceGen, s,
               hipLaunchKernelGGL(k_place_gen_poisson<BYROW>, dim3(gr), dim3(kBlock), pl, s, pairs, pidx, rows, n,
@@ -1974,10 +2049,8 @@ static int place_launch(const GenColumn* g, const uint64_t* pairs, const uint32_
               hipLaunchKernelGGL((k_place_gen<D, BYROW>), dim3(gr), dim3(kBlock), 0, s, pairs, pidx, rows, n,  \
                                  g->seed, g->col, g->prm, g->pt, y, y_rs, idx, state));                      \
     break;
-    PBH_CASE(PBH_DIST_NORM)
     PBH_CASE(PBH_DIST_UNIFORM)
     PBH_CASE(PBH_DIST_EXPON)
-    PBH_CASE(PBH_DIST_LOGNORM)
     PBH_CASE(PBH_DIST_TRIANG)
     PBH_CASE(PBH_DIST_GAMMA)
     PBH_CASE(PBH_DIST_POISSON)
