@@ -214,7 +214,7 @@ __global__ __launch_bounds__(T) void k_rank_finish(const uint64_t* __restrict__ 
     double avg = (double)(start + 1) + (double)(end - start) / 2.0;
     uint32_t row = sr[pad(p)];
     if constexpr (MODE == kModeScores) {
-      out.scores[row] = sf::ndtri(avg / np1);
+      out.scores[row] = sf::ppnd16(avg / np1);  // the scores of k_perm_scores (sf::ppnd16)
     } else if constexpr (MODE == kModeGather) {
       int64_t idx = (int64_t)avg - 1;
       out.y[(int64_t)row * out.y_rs] = out.sorted_src[idx];

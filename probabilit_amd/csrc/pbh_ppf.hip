@@ -650,7 +650,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen(const uint64_t* __
                                                       uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
                                                       double* __restrict__ y, int64_t y_rs, int32_t* __restrict__ idx,
                                                       const int32_t* __restrict__ state) {
-  static_assert(D != PBH_DIST_NORM && D != PBH_DIST_LOGNORM, "ndtri-based distributions: k_place_gen_w");
+  static_assert(D != PBH_DIST_NORM && D != PBH_DIST_LOGNORM, "norm / lognorm: k_place_gen_w");
   if (state && *state) return;
   __shared__ double buf[kGenRows];
   Philox ph(seed);
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                                                         uint64_t seed, uint32_t col, Params prm, PoissonTable pt,
                                                         double* __restrict__ y, int64_t y_rs,
                                                         int32_t* __restrict__ idx, const int32_t* __restrict__ state) {
-  static_assert(D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM, "ndtri-based distributions only");
+  static_assert(D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM, "norm / lognorm only");
   if (state && *state) return;
   __shared__ double buf[kGenRows];
   __shared__ double qarg[kBlock / 64][kPGQ];
@@ -1228,8 +1228,8 @@ constexpr int64_t kLdsHeads = 4096;  // run heads staged in LDS by k_perm_scores
 
 // Van der Waerden scores of an LHS column, rows [row0, row0 + nrows), in row order: the rank
 // of row r is pi(r) + 1 (untied), or the run average of stratum pi(r) (heads != NULL), so
-// S[r] = ndtri(rank / (n + 1)) (correlation.py:394-395) without sorting anything.  Ranks of
-// consecutive rows are random, so ndtri's tail (27% of the ranks, ~3.4x the centre's cost) is
+// S[r] = Phi^-1(rank / (n + 1)) (correlation.py:394-395; sf::ppnd16) without sorting anything.
+// Ranks of consecutive rows are random, so the tail (15% of the ranks, ~3x the centre's cost) is
 // compacted per WAVE: each wave takes 512 consecutive rows per step (8 a lane), writes its centre
 // scores straight to S (coalesced), and pushes the tail arguments onto its own LDS stack; at the
 // end of the step it evaluates them 64 at a time (full width) and scatters them into S (rows of
@@ -1284,9 +1284,9 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
         const double rank = heads ? run_average_rank(heads, nheads, n, (int64_t)t) : (double)(t + 1);
         y = rank / np1;
       }
-      const bool tail = valid && sf::ndtri_takes_tail(y);
+      const bool tail = valid && sf::ppnd16_takes_tail(y);
       if (valid && !tail) {
-        const double v = sf::ndtri_centre(y);
+        const double v = sf::ppnd16_centre(y);
         S[i] = v;
         sum += v;
       }
@@ -1302,13 +1302,13 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
       qc -= 64;
       const double a = qa[qc + lane];
       const uint32_t r = qr[qc + lane];
-      const double v = sf::ndtri_tail(a);
+      const double v = sf::ppnd16_tail(a);
       S[r] = v;
       sum += v;
     }
   }
   if (lane < qc) {  // the leftover (< 64): once per wave
-    const double v = sf::ndtri_tail(qa[lane]);
+    const double v = sf::ppnd16_tail(qa[lane]);
     S[qr[lane]] = v;
     sum += v;
   }

@@ -53,6 +53,27 @@ PBH_HD inline double p1evl(double x, const double* c, int n) {
   return a;
 }
 
+// polevl / p1evl over a function-local array of literal coefficients (ndtri's rationals): the
+// same operations, with each coefficient re-made in scalar registers where it is used (the empty
+// asm) -- hoisted out of a kernel's loop, they otherwise sit in vector registers (~30 of them for
+// ndtri's centre and tail), which caps the norm kernels at 128 VGPRs / 4 waves per SIMD
+PBH_HD inline double lit(double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __asm__("" : "+s"(c));
+#endif
+  return c;
+}
+PBH_HD inline double polevl_lit(double x, const double* c, int n) {
+  double a = lit(c[0]);
+  for (int i = 1; i <= n; ++i) a = a * x + lit(c[i]);
+  return a;
+}
+PBH_HD inline double p1evl_lit(double x, const double* c, int n) {
+  double a = x + lit(c[0]);
+  for (int i = 1; i < n; ++i) a = a * x + lit(c[i]);
+  return a;
+}
+
 // ---------------------------------------------------------------- table-driven log
 #include "pbh_log_table.inc"
 
@@ -220,7 +241,7 @@ PBH_HD inline double ndtri_centre(double y0) {
                         1.59056225126211695515e1, -1.18331621121330003142e0};
   const double y = y0 - 0.5;
   const double y2 = y * y;
-  const double x = y + y * (y2 * polevl(y2, P0, 4) / p1evl(y2, Q0, 8));
+  const double x = y + y * (y2 * polevl_lit(y2, P0, 4) / p1evl_lit(y2, Q0, 8));
   return x * kSqrt2Pi;
 }
 
@@ -238,7 +259,7 @@ PBH_HD inline double ndtri_tail_near(double z) {  // x in [2, 8)
   const double Q1[8] = {1.57799883256466749731e1, 4.53907635128879210584e1, 4.13172038254672030440e1,
                         1.50425385692907503408e1, 2.50464946208309415979e0, -1.42182922854787788574e-1,
                         -3.80806407691578277194e-2, -9.33259480895457427372e-4};
-  return z * polevl(z, P1, 8) / p1evl(z, Q1, 8);
+  return z * polevl_lit(z, P1, 8) / p1evl_lit(z, Q1, 8);
 }
 PBH_HD inline double ndtri_tail_far(double z) {  // x in [8, 64)
   const double P2[9] = {3.23774891776946035970e0, 6.91522889068984211695e0, 3.93881025292474443415e0,
@@ -247,7 +268,7 @@ PBH_HD inline double ndtri_tail_far(double z) {  // x in [8, 64)
   const double Q2[8] = {6.02427039364742014255e0, 3.67983563856160859403e0, 1.37702099489081330271e0,
                         2.16236993594496635890e-1, 1.34204006088543189037e-2, 3.28014464682127739104e-4,
                         2.89247864745380683936e-6, 6.79019408009981274425e-9};
-  return z * polevl(z, P2, 8) / p1evl(z, Q2, 8);
+  return z * polevl_lit(z, P2, 8) / p1evl_lit(z, Q2, 8);
 }
 
 template <int S = 4>
@@ -282,6 +303,83 @@ PBH_HD inline double ndtri(double y0) {
   if (y0 < 0.0 || y0 > 1.0) return kNaN;
   if (ndtri_takes_tail(y0)) return ndtri_tail(y0);
   return ndtri_centre(y0);
+}
+
+// ---------------------------------------------------------------- inverse normal CDF, PPND16
+// Wichura's AS 241 (PPND16, Applied Statistics 37(3), 1988): Phi^-1(p) to ~1e-16 relative with
+// one rational of degree 7/7 for |p - 1/2| <= 0.425 (85% of uniform p) and, beyond it, one in
+// r = sqrt(-log min(p, 1 - p)) (1.6 <= r <= 5 below p = e^-25, a second one past it).  It gives the
+// van der Waerden scores (k_perm_scores, and the general path's rank_finish, so both agree): half
+// the FP64 work of Cephes's ndtri (ndtri above: a wider tail region, two logs, three divisions) --
+// centre ~27 and tail ~75 VALU instructions against ~40 and ~140.  It is not Cephes's rounding:
+// within 1.1e-15 relative of scipy's ndtri (mean 1 ulp; tests/test_special_host.py), inside the
+// scores' 1e-14 gate (tests/test_gpu_ic.py).  The norm / lognorm ppf keeps ndtri: there an ulp of
+// z is not enough -- loc + scale z cancels near zero (norm(5, 2) at q = Phi(-2.5)), and the ppf
+// gate is 1e-10 relative to scipy's value.
+// Horner with fused multiply-adds over c[0..7] (c a function-local coefficient array; lit: scalar
+// registers at the point of use -- hoisted, the 32 of them sat in vector registers and spilled)
+PBH_HD inline double ppnd16_horner7(const double* c, double r) {
+  double v = lit(c[7]);
+#pragma unroll
+  for (int k = 6; k >= 0; --k) v = fma(v, r, lit(c[k]));
+  return v;
+}
+
+// true when ppnd16(p) takes the tail rational: p in (0, 1) with |p - 1/2| > 0.425
+PBH_HD inline bool ppnd16_takes_tail(double p) { return p > 0.0 && p < 1.0 && fabs(p - 0.5) > 0.425; }
+
+// centre: |p - 1/2| <= 0.425
+PBH_HD inline double ppnd16_centre(double p) {
+  const double A[8] = {3.3871328727963666080e0, 1.3314166789178437745e+2, 1.9715909503065514427e+3,
+                       1.3731693765509461125e+4, 4.5921953931549871457e+4, 6.7265770927008700853e+4,
+                       3.3430575583588128105e+4, 2.5090809287301226727e+3};
+  const double B[8] = {1.0, 4.2313330701600911252e+1, 6.8718700749205790830e+2, 5.3941960214247511077e+3,
+                       2.1213794301586595867e+4, 3.9307895800092710610e+4, 2.8729085735721942674e+4,
+                       5.2264952788528545610e+3};
+  const double q = p - 0.5;
+  const double r = fma(-q, q, 0.180625);
+  return q * ppnd16_horner7(A, r) / ppnd16_horner7(B, r);
+}
+
+// tail: ppnd16_takes_tail(p).  A wave whose every min(p, 1 - p) is at least 1e-10 (the scores,
+// and LHS quantiles but for ~1e-10 / stratum width of a stratum) has r <= 4.8: log of a positive
+// normal argument and the first tail rational only; any other wave runs the general code.
+template <int S = 4>
+PBH_HD inline double ppnd16_tail_at(double p, const double* __restrict__ lt) {
+  const double C[8] = {1.42343711074968357734e0, 4.63033784615654529590e0, 5.76949722146069140550e0,
+                       3.64784832476320460504e0, 1.27045825245236838258e0, 2.41780725177450611770e-1,
+                       2.27238449892691845833e-2, 7.74545014278341407640e-4};
+  const double D[8] = {1.0, 2.05319162663775882187e0, 1.67638483018380384940e0, 6.89767334985100004550e-1,
+                       1.48103976427480074590e-1, 1.51986665636164571966e-2, 5.47593808499534494600e-4,
+                       1.05075007164441684324e-9};
+  const double E[8] = {6.65790464350110377720e0, 5.46378491116411436990e0, 1.78482653991729133580e0,
+                       2.96560571828504891230e-1, 2.65321895265761230930e-2, 1.24266094738807843860e-3,
+                       2.71155556874348757815e-5, 2.01033439929228813265e-7};
+  const double F[8] = {1.0, 5.99832206555887937690e-1, 1.36929880922735805310e-1, 1.48753612908506148525e-2,
+                       7.86869131145613259100e-4, 1.84631831751005468180e-5, 1.42151175831644588870e-7,
+                       2.04426310338993978564e-15};
+  const bool lower = p < 0.5;
+  const double y = lower ? p : 1.0 - p;  // exact for p > 1/2
+  double v;
+  if (wave_all(y >= 1e-10)) {
+    const double r = sqrt(-log_tab_pos_at<S>(y, lt)) - 1.6;
+    v = ppnd16_horner7(C, r) / ppnd16_horner7(D, r);
+  } else {
+    const double r = sqrt(-log_tab_at<S>(y, lt));
+    v = r <= 5.0 ? ppnd16_horner7(C, r - 1.6) / ppnd16_horner7(D, r - 1.6)
+                 : ppnd16_horner7(E, r - 5.0) / ppnd16_horner7(F, r - 5.0);
+    rare_path_end();
+  }
+  return lower ? -v : v;
+}
+PBH_HD inline double ppnd16_tail(double p) { return ppnd16_tail_at(p, &pbh_log_tab[0][0]); }
+
+// Phi^-1(p): -inf / +inf at 0 / 1, NaN outside [0, 1]
+PBH_HD inline double ppnd16(double p) {
+  if (p == 0.0) return -kInf;
+  if (p == 1.0) return kInf;
+  if (!(p >= 0.0 && p <= 1.0)) return kNaN;
+  return ppnd16_takes_tail(p) ? ppnd16_tail(p) : ppnd16_centre(p);
 }
 
 // ---------------------------------------------------------------- erf / erfc (for Temme)

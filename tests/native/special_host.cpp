@@ -62,6 +62,10 @@ void sfh_ndtri(const double* q, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = sf::ndtri(q[i]);
 }
 
+void sfh_ppnd16(const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sf::ppnd16(q[i]);
+}
+
 void sfh_igami(double a, const double* p, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = sf::igami(a, p[i]);
 }

@@ -66,6 +66,23 @@ def test_ndtri_matches_scipy(sfh):
     assert r.max() <= 1e-13
 
 
+def test_ppnd16_matches_scipy(sfh):
+    """sf::ppnd16 (AS 241, the device norm / lognorm ppf and van der Waerden scores) against scipy's
+    ndtri: within 2e-15 relative everywhere (quantiles from 1e-300 to 1 - 1e-16, the van der
+    Waerden grid), about one ulp on average; infinities at 0 and 1, NaN outside."""
+    rng = np.random.default_rng(5)
+    q = np.concatenate([_quantiles(), rng.random(1_000_000), 10.0 ** (-rng.random(200_000) * 300),
+                        1.0 - 10.0 ** (-rng.random(200_000) * 16), np.arange(1, 200_002) / 200_002.0,
+                        [0.0, 1.0, -0.5, 1.5, np.nan, 0.075, 0.925, 0.5, np.nextafter(0.075, 1)]])
+    got = _call(sfh, "sfh_ppnd16", q)
+    ref = sp.ndtri(q)
+    assert (np.isnan(got) == np.isnan(ref)).all()
+    r = _rel(got, ref)
+    assert r.max() <= 2e-15, r.max()
+    fin = np.isfinite(ref) & (ref != 0.0)
+    assert np.mean(np.abs(got[fin] - ref[fin]) / np.spacing(np.abs(ref[fin]))) < 1.5
+
+
 @pytest.mark.parametrize("a", [0.05, 0.1, 0.3, 0.7, 1.0, 2.0, 5.0, 20.0, 45.0, 100.0, 250.0, 1e3, 1e4, 1e5])
 def test_gammaincinv_and_guided_table(sfh, a):
     q = _quantiles()
