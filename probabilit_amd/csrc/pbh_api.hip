@@ -345,20 +345,51 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
   if (a->columns && defer)
     for (int c = 0; c < k; ++c) any_deferred |= (deferred[c] = !gen_discrete(a->columns[c].dist)) != 0;
   if (a->columns) {
-    for (int c = 0; c < k; ++c) {
-      const pbh_ic_column& g = a->columns[c];
-      pbh_param prm[4];
-      for (int j = 0; j < 4; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
-      st = gen_create(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, &gens.g[c], s);
-      if (st) return st;
-      if (deferred[c]) continue;  // counted next to steps 1-3 (below)
-      // run heads only for a discrete column (few runs); a continuous one ties rarely, if ever,
-      // and would append every stratum
-      const bool discrete = gen_discrete(g.dist);
-      st = gen_sorted(gens.g[c], 0, n, nullptr, g.nonfinite_flag, L.counts + 2 * c, s,
-                      discrete ? L.heads_all + (int64_t)c * kHeadsCap : nullptr, discrete ? L.hcur + c : nullptr,
-                      discrete ? kHeadsCap : 0);
-      if (st) return st;
+    // the columns' inverse-CDF tables (gamma / beta guides, poisson CDFs) and the discrete columns'
+    // counts and run heads (small latency-bound kernels, ~1.8 ms one after another at cfg3) run
+    // side by side on the step-4 lanes' streams, idle this early in the call; the caller's stream
+    // then waits for all of them
+    {
+      const int nts = step4_streams();  // 1 in measurement mode (pbh_set_serial)
+      hipStream_t ts[kStep4MaxStreams];
+      std::vector<hipEvent_t> tev;
+      struct Cleanup {
+        std::vector<hipEvent_t>& v;
+        ~Cleanup() {
+          for (hipEvent_t e : v) (void)hipEventDestroy(e);
+        }
+      } cleanup{tev};
+      auto order = [&](hipStream_t from, hipStream_t to) -> int {
+        if (from == to) return PBH_OK;
+        hipEvent_t e = nullptr;
+        PBH_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        tev.push_back(e);
+        PBH_CHECK_HIP(hipEventRecord(e, from));
+        PBH_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
+        return PBH_OK;
+      };
+      for (int i = 0; i < nts; ++i) {
+        ts[i] = nts > 1 ? step4_side_stream(i) : s;
+        if (!ts[i]) ts[i] = s;
+        if ((st = order(s, ts[i]))) return st;
+      }
+      for (int c = 0; c < k; ++c) {
+        const pbh_ic_column& g = a->columns[c];
+        pbh_param prm[4];
+        for (int j = 0; j < 4; ++j) prm[j] = pbh_param{nullptr, g.params[j]};
+        st = gen_create(g.seed, n, g.lhs_col, g.dist, prm, g.nparams, &gens.g[c], ts[c % nts]);
+        if (st) return st;
+        if (deferred[c]) continue;  // counted next to steps 1-3 (below)
+        // run heads only for a discrete column (few runs); a continuous one ties rarely, if ever,
+        // and would append every stratum (on the stream that built the column's table)
+        const bool discrete = gen_discrete(g.dist);
+        st = gen_sorted(gens.g[c], 0, n, nullptr, g.nonfinite_flag, L.counts + 2 * c, ts[c % nts],
+                        discrete ? L.heads_all + (int64_t)c * kHeadsCap : nullptr, discrete ? L.hcur + c : nullptr,
+                        discrete ? kHeadsCap : 0);
+        if (st) return st;
+      }
+      for (int i = 0; i < nts; ++i)
+        if ((st = order(ts[i], s))) return st;
     }
     PBH_CHECK_HIP(hipMemcpyAsync(cnt_host.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
     PBH_CHECK_HIP(hipStreamSynchronize(s));

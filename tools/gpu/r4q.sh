@@ -1,0 +1,10 @@
+set -o pipefail
+# Round 4: column tables built side by side on the lane streams, the msd2 tile map in LDS (A/B
+# PBH_MSD2_MAP=0), and the host-side profile of a bench call.
+TAG=${1:-r4q}
+R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_step4_gen.py tests/test_gpu_ic.py tests/test_gpu_certificate.py tests/test_gpu_dists.py -m gpu -q -rf --timeout 600 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
+rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/${TAG}_tests.log; grep -E "^FAILED" gpurun_out/${TAG}_tests.log | head -20; [ $rc -le 1 ] || exit $rc
+bash tools/gpu/ab_env.sh ${TAG}_ab "-" "PBH_MSD2_MAP=0" || exit $?
+timeout -k 10 300 python tools/profile_host.py 100000000 3 > gpurun_out/${TAG}_host.txt 2>&1
+echo "host exit $?"; head -45 gpurun_out/${TAG}_host.txt
