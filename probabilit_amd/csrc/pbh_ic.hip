@@ -384,6 +384,7 @@ __global__ void k_gram_reduce(const double* __restrict__ partials, int nb, int k
 // The four waves' tiles are summed through LDS in a fixed order at the end (deterministic).
 // partials[(block * 32 + i) * 32 + j] for i <= j, as k_gram_rows_reduce<32> expects.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef double v2d __attribute__((ext_vector_type(2)));
 constexpr int GM_ROWS = 128;
 
 __global__ __launch_bounds__(256) void k_gram_mfma(const double* __restrict__ S, int64_t n, int k, int64_t ld,
@@ -397,24 +398,38 @@ __global__ __launch_bounds__(256) void k_gram_mfma(const double* __restrict__ S,
 #pragma unroll
   for (int j = 0; j < 8; ++j) mu[j] = (w * 8 + j) < k ? means[w * 8 + j] : 0.0;
   f64x4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c11 = c00;
-  // the next chunk's loads are issued before this chunk's MFMAs (register prefetch)
-  double pre[GM_ROWS / 64][8];
+  // the next chunk's loads are issued before this chunk's MFMAs (register prefetch); with
+  // `pair` (ld even, S 16-byte aligned: the host checks) a lane reads rows 2 l and 2 l + 1 of a
+  // column in one 16-byte access, half the load instructions of one row per lane
+  static_assert(GM_ROWS == 128, "one 16-byte pair per lane and column");
+  double pre[2][8];
+  const bool pair = (ld % 2 == 0) && ((uintptr_t)S % 16 == 0);
   auto load = [&](int64_t rb) {
+    const int64_t r = rb + 2 * lane;
 #pragma unroll
-    for (int h = 0; h < GM_ROWS / 64; ++h) {
-      const int64_t r = rb + h * 64 + lane;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = w * 8 + j;
-        pre[h][j] = (c < k && r < r1) ? S[(int64_t)c * ld + r] : 0.0;
+    for (int j = 0; j < 8; ++j) {
+      const int c = w * 8 + j;
+      double a = 0.0, b = 0.0;
+      if (c < k) {
+        const double* src = &S[(int64_t)c * ld + r];
+        if (pair && r + 1 < r1) {
+          const v2d t = __builtin_nontemporal_load((const v2d*)src);
+          a = t.x;
+          b = t.y;
+        } else {
+          a = r < r1 ? src[0] : 0.0;
+          b = r + 1 < r1 ? src[1] : 0.0;
+        }
       }
+      pre[0][j] = a;
+      pre[1][j] = b;
     }
   };
   if (r0 < r1) load(r0);
   for (int64_t rb = r0; rb < r1; rb += GM_ROWS) {
 #pragma unroll
-    for (int h = 0; h < GM_ROWS / 64; ++h) {
-      const int row = h * 64 + lane;
+    for (int h = 0; h < 2; ++h) {
+      const int row = 2 * lane + h;
       const int64_t r = rb + row;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -642,7 +657,6 @@ __global__ __launch_bounds__(256) void k_apply_mfma(double* __restrict__ S, int6
 // Needs ld, ldc even and S / codes 16- / 8-byte aligned (checked on the host).  The default step 3
 // (interleaved A/B, profiles/r04/README_ab.md: 13.5-13.6 against 15.0-15.1 ms per cfg3 step).
 // NT: non-temporal accesses as well (streaming: S, CS and the codes are not re-read by this kernel).
-typedef double v2d __attribute__((ext_vector_type(2)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
 template <bool NT>
