@@ -39,3 +39,4 @@ for i in range(calls):
     print(f"call {i}: {1e3 * (time.perf_counter() - t):.2f} ms", flush=True)
 st = pstats.Stats(pr)
 st.sort_stats("tottime").print_stats(25)
+st.sort_stats("cumulative").print_stats(45)
