@@ -1770,15 +1770,17 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     int shifts[4];
     const int nl = place_levels(n, shifts);
     const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
-    // PBH_FINISH_CFG (A/B measurements, profiles/r03/README_ab.md): 29 (default) = k_finish_q over
-    // 512 threads, 1024 bins, the run members' CS values read in pass 2; 28 = the same with those
-    // reads queued through LDS; 30 = queued, 2048 bins; 26 = 256 threads (round 2's k_finish_ah).
+    // PBH_FINISH_CFG (A/B measurements, profiles/r03/ and r04/README_ab.md): 31 (default) =
+    // k_finish_q over 512 threads, 2048 bins, the run members' CS values read in pass 2 (r4s-r4u:
+    // 23.2-23.6 against 23.9-24.5 ms per step with 1024 bins, 29; 512 bins measured 25.7-26.2);
+    // 28 = 1024 bins with those reads queued through LDS; 30 = queued, 2048 bins; 26 = 256 threads
+    // (round 2's k_finish_ah).
     // (Both buckets' phases merged into one pass, ~10 barriers instead of ~21: 23.7-24.1 against
     // 24.1-24.3 ms per step, within run-to-run noise; not kept.)
     // The segmented XCD-class output (PBH_FINISH_XCD=1) always takes k_finish_fused.
     static const int cfg = [] {
       const char* e = getenv("PBH_FINISH_CFG");
-      return e ? atoi(e) : 29;
+      return e ? atoi(e) : 31;
     }();
     uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
     const int cpad = cur_pad();
@@ -1795,8 +1797,9 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
       switch (cfg) {
         case 26: PBH_FINQ(1024, 256, false); break;
         case 28: PBH_FINQ(1024, 512, true); break;
+        case 29: PBH_FINQ(1024, 512, false); break;
         case 30: PBH_FINQ(2048, 512, true); break;
-        default: PBH_FINQ(1024, 512, false); break;
+        default: PBH_FINQ(2048, 512, false); break;
       }
     }
 #undef PBH_FINQ

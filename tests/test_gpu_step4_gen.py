@@ -192,7 +192,7 @@ def _debug_run(n, dists, seed, C):
 def test_step4_variants_match_the_oracle(gpu, tmp_path):
     """Every A/B switch of the generated-column path, each in its own process (they are read
     once): 4096-row code-pass tiles (PBH_MSD_TILE=4096), the 256-thread finish (PBH_FINISH_CFG=26),
-    the queued finish (28, 30), the whole gamma table in LDS
+    the queued finish (28, 30), the 1024-bin finish (29; the default counts on 2048 bins), the whole gamma table in LDS
     (PBH_GAMMA_WIN=0), the placement levels' other split (PBH_PLACE_TOP=0), 64-row step-3 tiles
     (PBH_APPLY_ROWS=64), the poisson run heads from every stratum instead of the boundary search
     (PBH_DISCRETE_SCAN=1), the code histogram with the tile-class counts per code (PBH_HIST_CLASS=0),
@@ -211,7 +211,7 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     n, d, seed = 600_001, 8, 31
     dists, C = cfg_dists(d), cfg3_corr(d)
     ref = _oracle(n, dists, seed, C)
-    for env in ({"PBH_HIST_CLASS": "0"}, {"PBH_MSD_TILE": "4096", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"},
+    for env in ({"PBH_HIST_CLASS": "0"}, {"PBH_MSD_TILE": "4096", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"}, {"PBH_FINISH_CFG": "29"},
                 {"PBH_FINISH_CFG": "30"}, {"PBH_GAMMA_WIN": "0"}, {"PBH_PLACE_TOP": "0"}, {"PBH_APPLY_ROWS": "64"},
                 {"PBH_DISCRETE_SCAN": "1"}, {"PBH_APPLY_W2": "0"}, {"PBH_APPLY_NT": "0"}, {"PBH_PLACE_RUNS": "0"}):
         dd = tmp_path / "_".join(f"{k}{v}" for k, v in env.items())
