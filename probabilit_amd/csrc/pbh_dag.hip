@@ -123,7 +123,7 @@ PBH_DI bool gen_compacted(const double (&q)[kDIpt], const bool (&valid)[kDIpt], 
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < kDIpt; ++j) {
-    const bool tail = sf::ndtri_takes_tail(q[j]);  // never for rows past n (q = 0.5)
+    const bool tail = normal_takes_tail(q[j], normal_loc<D>(p[0], p[1]));  // never for rows past n (q = 0.5)
     if (!tail) {
       const double x = ppf_one<D, 1>(q[j], p[0], p[1], p[2], pt);
       out[item(j)] = x;

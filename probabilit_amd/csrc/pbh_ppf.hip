@@ -89,7 +89,7 @@ PBH_DI void ppf_compacted(int64_t n, const Q& qof, const Params& prm_in, const P
       const int64_t i = base + p;
       const bool valid = i < n;
       const double qv = qa[j];
-      const bool tail = valid && sf::ndtri_takes_tail(qv);
+      const bool tail = valid && normal_takes_tail(qv, normal_loc<D>(prm.at(0, i), prm.at(1, i)));
       if (valid && !tail) res[p] = ppf_one<D, 1>(qv, prm.at(0, i), prm.at(1, i), prm.at(2, i), pt);
       tail_push(tq, tail, qv, p);
     }
@@ -755,7 +755,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             }
             q = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
           }
-          const bool tail = valid && sf::ndtri_takes_tail(q);
+          const bool tail = valid && normal_takes_tail(q, normal_loc<D>(p0, p1));
           if (valid && !tail) buf[off] = ppf_one<D, 1>(q, p0, p1, p2, pt);
           const uint64_t m = __ballot(tail);
           if (tail) {

@@ -67,16 +67,30 @@ constexpr int kLog3N = 128 * 3;
 PBH_DI void stage_log3(double* lt) {
   for (int k = threadIdx.x; k < kLog3N; k += blockDim.x) lt[k] = (&sf::pbh_log_tab[0][0])[4 * (k / 3) + k % 3];
 }
-PBH_DI double tail_of(double q, const double* lt) {
+// The normal quantile of norm / lognorm: with loc = 0, Wichura's PPND16 (sf::ppnd16, half the
+// FP64 work; within 1.1e-15 of scipy's ndtri, and scale z or exp(s z) scale keeps that relative
+// error), with any other loc Cephes' ndtri, bit for bit (loc + scale z cancels near zero, where an
+// ulp of z would break the 1e-10 gate).  Each element's loc decides, in every kernel, so the
+// sorted generator, the placement, the certificate and the plain ppf agree.
+template <int D>
+PBH_DI double normal_loc(double p0, double p1) {
+  return D == PBH_DIST_NORM ? p0 : p1;
+}
+PBH_DI bool normal_takes_tail(double q, double loc) {
+  return loc == 0.0 ? sf::ppnd16_takes_tail(q) : sf::ndtri_takes_tail(q);
+}
+PBH_DI double tail_of(double q, const double* lt, bool fast) {
 #ifdef PBH_NO_LDS_LOGEXP  // A/B build: the global table
-  return sf::ndtri_tail(q);
+  return fast ? sf::ppnd16_tail(q) : sf::ndtri_tail(q);
 #else
+  if (fast) return lt ? sf::ppnd16_tail_at<3>(q, lt) : sf::ppnd16_tail(q);
   return lt ? sf::ndtri_tail_at<3>(q, lt) : sf::ndtri_tail(q);
 #endif
 }
 
 // ppf of one element for distribution D; p = (shape..., loc, scale) already resolved.
-// PART selects ndtri's branch for norm / lognorm (0: ndtri, 1: ndtri_centre, 2: ndtri_tail),
+// PART selects the normal quantile's branch for norm / lognorm (0: whole, 1: centre, 2: tail, of
+// PPND16 or ndtri as the element's loc decides: normal_takes_tail),
 // for the compacted kernels that know which one an element takes.
 // COLD_GAMMA: igami_guided's fallbacks as a call (see igami_guided)
 // lt: for PART 2, log_tab's table in LDS with entry stride 3 (stage_log3), else the global table
@@ -115,13 +129,19 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
     if (!(q > 0.0 && q < 1.0)) return kNaN;
     double x;
     if constexpr (D == PBH_DIST_NORM) {
-      x = PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? tail_of(q, lt) : sf::ndtri(q);
+      const bool fast = loc == 0.0;  // (normal_takes_tail)
+      x = PART == 1   ? (fast ? sf::ppnd16_centre(q) : sf::ndtri_centre(q))
+          : PART == 2 ? tail_of(q, lt, fast)
+                      : (fast ? sf::ppnd16(q) : sf::ndtri(q));
     } else if constexpr (D == PBH_DIST_UNIFORM) {
       x = q;
     } else if constexpr (D == PBH_DIST_EXPON) {
       x = -sf::log1p_(-q);  // scipy expon._ppf: -sc.log1p(-q), the Cephes log1p
     } else if constexpr (D == PBH_DIST_LOGNORM) {
-      x = exp(shape * (PART == 1 ? sf::ndtri_centre(q) : PART == 2 ? tail_of(q, lt) : sf::ndtri(q)));
+      const bool fast = loc == 0.0;
+      x = exp(shape * (PART == 1   ? (fast ? sf::ppnd16_centre(q) : sf::ndtri_centre(q))
+                       : PART == 2 ? tail_of(q, lt, fast)
+                                   : (fast ? sf::ppnd16(q) : sf::ndtri(q))));
     } else if constexpr (D == PBH_DIST_TRIANG) {
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
