@@ -67,30 +67,35 @@ constexpr int kLog3N = 128 * 3;
 PBH_DI void stage_log3(double* lt) {
   for (int k = threadIdx.x; k < kLog3N; k += blockDim.x) lt[k] = (&sf::pbh_log_tab[0][0])[4 * (k / 3) + k % 3];
 }
-// The normal quantile of norm / lognorm: with loc = 0, Wichura's PPND16 (sf::ppnd16, half the
-// FP64 work; within 1.1e-15 of scipy's ndtri, and scale z or exp(s z) scale keeps that relative
-// error), with any other loc Cephes' ndtri, bit for bit (loc + scale z cancels near zero, where an
-// ulp of z would break the 1e-10 gate).  Each element's loc decides, in every kernel, so the
-// sorted generator, the placement, the certificate and the plain ppf agree.
+// The normal quantile of norm / lognorm is Wichura's PPND16 (sf::ppnd16: half the FP64 work of
+// Cephes' ndtri, within 1.1e-15 of scipy's ndtri).  scale z and exp(s z) scale keep that relative
+// error; loc + (those) does not where it cancels -- norm(5, 2) near x = 0 -- so an element whose
+// result lies within 2^-12 of its cancelling parts takes Cephes' ndtri instead, bit for bit with
+// scipy (normal_guard): the result stays within ~5e-12 of scipy's everywhere, inside the 1e-10
+// gate.  The same function in every kernel: the sorted generator, the placement, the certificate
+// and the plain ppf agree.
 template <int D>
 PBH_DI double normal_loc(double p0, double p1) {
   return D == PBH_DIST_NORM ? p0 : p1;
 }
-PBH_DI bool normal_takes_tail(double q, double loc) {
-  return loc == 0.0 ? sf::ppnd16_takes_tail(q) : sf::ndtri_takes_tail(q);
-}
-PBH_DI double tail_of(double q, const double* lt, bool fast) {
+PBH_DI bool normal_takes_tail(double q, double /*loc*/) { return sf::ppnd16_takes_tail(q); }
+PBH_DI double tail_of(double q, const double* lt) {
 #ifdef PBH_NO_LDS_LOGEXP  // A/B build: the global table
-  return fast ? sf::ppnd16_tail(q) : sf::ndtri_tail(q);
+  return sf::ppnd16_tail(q);
 #else
-  if (fast) return lt ? sf::ppnd16_tail_at<3>(q, lt) : sf::ppnd16_tail(q);
-  return lt ? sf::ndtri_tail_at<3>(q, lt) : sf::ndtri_tail(q);
+  return lt ? sf::ppnd16_tail_at<3>(q, lt) : sf::ppnd16_tail(q);
 #endif
+}
+// z = PPND16's quantile, v = its scaled value (scale z, or exp(s z) scale), m = the magnitude its
+// error is relative to (|v|, or s |z| |v| for lognorm): true when loc + v keeps that error within
+// 2^-12 of itself, i.e. PPND16's result is inside the gate; false sends the element to ndtri
+PBH_DI bool normal_guard(double v, double m, double loc) {
+  return loc == 0.0 || fabs(v + loc) >= 0x1p-12 * m;
 }
 
 // ppf of one element for distribution D; p = (shape..., loc, scale) already resolved.
-// PART selects the normal quantile's branch for norm / lognorm (0: whole, 1: centre, 2: tail, of
-// PPND16 or ndtri as the element's loc decides: normal_takes_tail),
+// PART selects the normal quantile's branch for norm / lognorm (0: whole, 1: centre, 2: tail of
+// PPND16; normal_takes_tail; normal_guard's rare elements take ndtri whole),
 // for the compacted kernels that know which one an element takes.
 // COLD_GAMMA: igami_guided's fallbacks as a call (see igami_guided)
 // lt: for PART 2, log_tab's table in LDS with entry stride 3 (stage_log3), else the global table
@@ -129,19 +134,25 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
     if (!(q > 0.0 && q < 1.0)) return kNaN;
     double x;
     if constexpr (D == PBH_DIST_NORM) {
-      const bool fast = loc == 0.0;  // (normal_takes_tail)
-      x = PART == 1   ? (fast ? sf::ppnd16_centre(q) : sf::ndtri_centre(q))
-          : PART == 2 ? tail_of(q, lt, fast)
-                      : (fast ? sf::ppnd16(q) : sf::ndtri(q));
+      x = PART == 1 ? sf::ppnd16_centre(q) : PART == 2 ? tail_of(q, lt) : sf::ppnd16(q);
+      const bool ok = normal_guard(x * scale, fabs(x * scale), loc);
+      if (!sf::wave_all(ok)) {  // cancellation near x = 0: Cephes' ndtri, bit for bit
+        if (!ok) x = sf::ndtri(q);
+        sf::rare_path_end();
+      }
     } else if constexpr (D == PBH_DIST_UNIFORM) {
       x = q;
     } else if constexpr (D == PBH_DIST_EXPON) {
       x = -sf::log1p_(-q);  // scipy expon._ppf: -sc.log1p(-q), the Cephes log1p
     } else if constexpr (D == PBH_DIST_LOGNORM) {
-      const bool fast = loc == 0.0;
-      x = exp(shape * (PART == 1   ? (fast ? sf::ppnd16_centre(q) : sf::ndtri_centre(q))
-                       : PART == 2 ? tail_of(q, lt, fast)
-                                   : (fast ? sf::ppnd16(q) : sf::ndtri(q))));
+      const double z = PART == 1 ? sf::ppnd16_centre(q) : PART == 2 ? tail_of(q, lt) : sf::ppnd16(q);
+      x = exp(shape * z);
+      const double v = x * scale;
+      const bool ok = normal_guard(v, fabs(v) * (1.0 + shape * fabs(z)), loc);
+      if (!sf::wave_all(ok)) {
+        if (!ok) x = exp(shape * sf::ndtri(q));
+        sf::rare_path_end();
+      }
     } else if constexpr (D == PBH_DIST_TRIANG) {
       // np.where(q < c, sqrt(c q), 1 - sqrt((1 - c)(1 - q)))
       x = (q < shape) ? sqrt(shape * q) : 1.0 - sqrt((1.0 - shape) * (1.0 - q));
