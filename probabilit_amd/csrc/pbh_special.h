@@ -309,13 +309,13 @@ PBH_HD inline double ndtri(double y0) {
 // Wichura's AS 241 (PPND16, Applied Statistics 37(3), 1988): Phi^-1(p) to ~1e-16 relative with
 // one rational of degree 7/7 for |p - 1/2| <= 0.425 (85% of uniform p) and, beyond it, one in
 // r = sqrt(-log min(p, 1 - p)) (1.6 <= r <= 5 below p = e^-25, a second one past it).  It gives the
-// van der Waerden scores (k_perm_scores, and the general path's rank_finish, so both agree): half
-// the FP64 work of Cephes's ndtri (ndtri above: a wider tail region, two logs, three divisions) --
-// centre ~27 and tail ~75 VALU instructions against ~40 and ~140.  It is not Cephes's rounding:
-// within 1.1e-15 relative of scipy's ndtri (mean 1 ulp; tests/test_special_host.py), inside the
-// scores' 1e-14 gate (tests/test_gpu_ic.py).  The norm / lognorm ppf keeps ndtri: there an ulp of
-// z is not enough -- loc + scale z cancels near zero (norm(5, 2) at q = Phi(-2.5)), and the ppf
-// gate is 1e-10 relative to scipy's value.
+// van der Waerden scores (k_perm_scores, and the general path's rank_finish, so both agree) and the
+// norm / lognorm ppf (ppf_one, pbh_ppf_core.h): half the FP64 work of Cephes's ndtri (ndtri above:
+// a wider tail region, two logs, three divisions) -- centre ~27 and tail ~75 VALU instructions
+// against ~40 and ~140.  It is not Cephes's rounding: within 1.1e-15 relative of scipy's ndtri
+// (mean 1 ulp; tests/test_special_host.py), inside the scores' 1e-14 gate (tests/test_gpu_ic.py).
+// Where loc + scale z cancels (norm(5, 2) at q = Phi(-2.5)) an ulp of z is not enough for the ppf's
+// 1e-10 gate: ppf_one's normal_guard sends those elements to ndtri.
 // Horner with fused multiply-adds over c[0..7] (c a function-local coefficient array; lit: scalar
 // registers at the point of use -- hoisted, the 32 of them sat in vector registers and spilled)
 PBH_HD inline double ppnd16_horner7(const double* c, double r) {
