@@ -351,6 +351,9 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     // then waits for all of them
     {
       const int nts = step4_streams();  // 1 in measurement mode (pbh_set_serial)
+      // an early return below (a column's table or counts failing) leaves work queued on the side
+      // streams that reads the tables ~Gens frees: join them on every exit path
+      if (nts > 1) sync_on_exit.side = true;
       hipStream_t ts[kStep4MaxStreams];
       std::vector<hipEvent_t> tev;
       struct Cleanup {

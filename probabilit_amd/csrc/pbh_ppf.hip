@@ -358,19 +358,23 @@ unsigned gamma_lds_grid(int64_t n) { return grid_for(n, kGBlock, 256); }  // one
 
 // ---------------------------------------------------------------- poisson: CDF table in LDS
 // The same gather pattern: poisson_from_table reads guide[floor(q 2^11)] and then cdf[lo..]
-// at random positions, two dependent gathers per draw.  The CDF table (32 sd + 53 entries) and
-// the 2048-entry guide are staged in LDS (dynamic, <= 56 KiB) when the table is short enough;
-// same table, same search, same result.
-constexpr int64_t kPoissonLdsMaxLen = 6144;
+// at random positions, two dependent gathers per draw.  The CDF table (32 sd + 53 entries), its
+// scipy windows (one double per entry) and the 2048-entry guide are staged in LDS (dynamic,
+// <= 56 KiB) when the table is short enough; same table, same search, same result.
+constexpr int64_t kPoissonLdsMaxLen = 3072;
 
 PBH_DI PoissonTable stage_poisson(const PoissonTable& pt, double* lds) {
   const int nb = 1 << kPoissonGuideBits;
-  int32_t* g = reinterpret_cast<int32_t*>(lds + pt.len);
-  for (int k = threadIdx.x; k < (int)pt.len; k += blockDim.x) lds[k] = pt.cdf[k];
+  int32_t* g = reinterpret_cast<int32_t*>(lds + 2 * pt.len);
+  for (int k = threadIdx.x; k < (int)pt.len; k += blockDim.x) {
+    lds[k] = pt.cdf[k];
+    lds[pt.len + k] = pt.win[k];
+  }
   for (int k = threadIdx.x; k < nb; k += blockDim.x) g[k] = pt.cdf_guide[k];
   __syncthreads();
   PoissonTable local = pt;
   local.cdf = lds;
+  local.win = lds + pt.len;
   local.cdf_guide = g;
   return local;
 }
@@ -429,7 +433,7 @@ size_t poisson_lds_bytes(int dist, const Params& prm, const PoissonTable& pt) {
   if (!on || dist != PBH_DIST_POISSON || !pt.cdf || !pt.cdf_guide || pt.len <= 0 || pt.len > kPoissonLdsMaxLen ||
       prm.ptr[0] || prm.ptr[1])
     return 0;
-  return (size_t)pt.len * sizeof(double) + ((size_t)1 << kPoissonGuideBits) * sizeof(int32_t);
+  return (size_t)2 * pt.len * sizeof(double) + ((size_t)1 << kPoissonGuideBits) * sizeof(int32_t);
 }
 
 // The same LHS column in stratum order: out[t] = ppf(q) for the row pi^-1(t) that holds
@@ -536,7 +540,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_sorted_ppf(uint64_t seed
 // monotone and finite at both ends means finite throughout).  Any count, a list overflow or a
 // non-finite end is reported as a tie, and the caller redoes the call with the exact counts
 // (k_lhs_sorted_ppf): the certificate can only confirm "no tie, no inversion".
-__global__ __launch_bounds__(kBlock) void k_cert_scan(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_cert_scan(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
                                                       double T, uint32_t* __restrict__ list, uint32_t cap,
                                                       uint32_t* __restrict__ count) {
   // candidates gather in LDS and leave with one global atomic per block flush: one atomic per
@@ -593,7 +597,7 @@ __global__ __launch_bounds__(kBlock) void k_cert_scan(uint64_t seed, int64_t n, 
 }
 
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_cert_eval(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
+__global__ __launch_bounds__(kBlock) PBH_OCC void k_cert_eval(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
                                                       Params prm, PoissonTable pt, const uint32_t* __restrict__ list,
                                                       uint32_t cap, const uint32_t* __restrict__ count, int32_t* flag,
                                                       unsigned long long* counts) {
@@ -765,10 +769,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
           }
           qc += (int)__popcll(m);
         }
+        // the stack is written by some lanes and read by others of the same wave: keep the
+        // compiler from moving LDS accesses across the push / drain boundary (no instruction)
+        __builtin_amdgcn_wave_barrier();
         while (qc >= 64) {  // full-width batches off the top of the stack
           qc -= 64;
           buf[qp[qc + lane]] = ppf_one<D, 2>(qa[qc + lane], p0, p1, p2, pt);
         }
+        __builtin_amdgcn_wave_barrier();
       }
     }
     if (lane < qc) buf[qp[lane]] = ppf_one<D, 2>(qa[lane], p0, p1, p2, pt);
@@ -1298,6 +1306,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
       }
       qc += (int)__popcll(m);
     }
+    __builtin_amdgcn_wave_barrier();  // pushes by some lanes, reads by others: no reordering across
     while (qc >= 64) {  // full-width batches off the top of the stack (the step's strata are dead here)
       qc -= 64;
       const double a = qa[qc + lane];
@@ -1306,6 +1315,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
       S[r] = v;
       sum += v;
     }
+    __builtin_amdgcn_wave_barrier();
   }
   if (lane < qc) {  // the leftover (< 64): once per wave
     const double v = sf::ppnd16_tail(qa[lane]);
@@ -1379,9 +1389,13 @@ __global__ void k_gamma_guide_check(double a, sf::GammaGuide T, double* ok) {
   if (j < T.m) ok[j] = (j < T.m - 1) ? sf::gamma_guide_check(a, T, j) : 0.0;
 }
 
-__global__ void k_poisson_table(double mu, int64_t k_lo, int64_t len, double* cdf) {
+// cdf[j] = pdtr(k_lo + j, mu); win[j] = the end of scipy's window above cdf[j - 1] (pbh_cdflib.h)
+__global__ void k_poisson_table(double mu, int64_t k_lo, int64_t len, double* cdf, double* win) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < len) cdf[j] = sf::pdtr((double)(k_lo + j), mu);
+  if (j < len) {
+    cdf[j] = sf::pdtr((double)(k_lo + j), mu);
+    win[j] = cdf::poisson_window_hi((double)(k_lo + j), mu);
+  }
 }
 
 // guide[b] = first j with cdf[j] >= b / 2^kPoissonGuideBits (len when none)
@@ -1629,14 +1643,15 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
       int64_t k_hi = (int64_t)ceil(mu + 20.0 * sd + 40.0);
       int64_t len = k_hi - k_lo + 1;
       const int nb = 1 << kPoissonGuideBits;
-      PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)len * sizeof(double) + (size_t)nb * 4, s));
+      PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)2 * len * sizeof(double) + (size_t)nb * 4, s));
       hipLaunchKernelGGL(k_poisson_table, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, mu, k_lo, len,
-                         *table);
+                         *table, *table + len);
       PBH_CHECK_LAUNCH();
-      int32_t* guide = (int32_t*)(*table + len);
+      int32_t* guide = (int32_t*)(*table + 2 * len);
       hipLaunchKernelGGL(k_poisson_guide, dim3((unsigned)(nb / 256)), dim3(256), 0, s, *table, len, guide);
       PBH_CHECK_LAUNCH();
       pt.cdf = *table;
+      pt.win = *table + len;
       pt.cdf_guide = guide;
       pt.k_lo = k_lo;
       pt.len = len;
@@ -1709,7 +1724,7 @@ void gen_destroy(GenColumn* g, hipStream_t s) {
 // takes this path only when the last value is finite and the values span at most kDiscreteSpan.
 constexpr int kDiscreteSpan = 4096;
 
-__global__ __launch_bounds__(256) void k_discrete_heads(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
+__global__ __launch_bounds__(256) PBH_OCC void k_discrete_heads(uint64_t seed, int64_t n, int64_t t0, int64_t nt, uint32_t col,
                                                         Params prm, PoissonTable pt, int32_t* flag,
                                                         unsigned long long* counts, uint32_t* __restrict__ heads,
                                                         uint32_t* __restrict__ hcur, uint32_t hcap) {
@@ -1748,6 +1763,36 @@ __global__ __launch_bounds__(256) void k_discrete_heads(uint64_t seed, int64_t n
         lo = mid;
     }
     b[i] = (uint32_t)hi;
+    // scipy's window above pdtr(k - 1, mu) (PoissonTable::win): its strata take k - 1 or k, so
+    // the search (which needs non-decreasing values) is exact unless the window holds two strata
+    // whose values decrease.  q_t lies in (t / n, (t + 1) / n], so the window's strata are within
+    // [c n - 1, w n] (padded by 1); when two or more of their quantiles fall in it, their values
+    // are checked here and a decrease is counted as an inversion (the caller then counts the
+    // column exactly).  At cfg3 (N = 1e8, mu <= 30) a window is narrower than a stratum.
+    const int64_t j = (int64_t)k - pt.k_lo;
+    if (j >= 1 && j < pt.len && pt.win[j] > pt.cdf[j - 1]) {
+      const double c = pt.cdf[j - 1], w = pt.win[j];
+      const int64_t ta = max(t0, (int64_t)floor(c * (double)n) - 2);
+      const int64_t tb = min(t0 + nt - 1, (int64_t)floor(w * (double)n) + 1);
+      int inside = 0;
+      for (int64_t t = ta; t <= tb && inside < 2 && tb - ta <= 256; ++t) {
+        const double qt = lhs_sorted_quantile(ph, (uint64_t)t, col, (uint64_t)n);
+        inside += qt >= c && qt < w;
+      }
+      if (tb - ta > 256) {
+        atomicAdd(&counts[1], 1ull);
+      } else if (inside >= 2) {
+        double prev = value(ta);
+        for (int64_t t = ta + 1; t <= tb; ++t) {
+          const double v = value(t);
+          if (v < prev) {
+            atomicAdd(&counts[1], 1ull);
+            break;
+          }
+          prev = v;
+        }
+      }
+    }
   }
   __syncthreads();
   uint32_t mine = 0;

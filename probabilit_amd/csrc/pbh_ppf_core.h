@@ -3,6 +3,7 @@
 #pragma once
 #include <math.h>
 
+#include "pbh_cdflib.h"
 #include "pbh_error.h"
 #include "pbh_special.h"
 
@@ -24,6 +25,7 @@ constexpr int kPoissonGuideBits = 11;  // 2048 guide buckets
 
 struct PoissonTable {
   const double* cdf;  // poisson: cdf[j] = pdtr(k_lo + j, mu) for scalar mu, else NULL
+  const double* win;  // win[j] = cdf::poisson_window_hi(k_lo + j, mu): scipy's window above cdf[j - 1]
   const int32_t* cdf_guide;  // cdf_guide[b] = first j with cdf[j] >= b / 2^kPoissonGuideBits
   int64_t k_lo;
   int64_t len;
@@ -33,7 +35,7 @@ struct PoissonTable {
 };
 
 // smallest k >= 0 with pdtr(k, mu) >= q, by stepping from a Cornish-Fisher guess.
-__attribute__((noinline)) __device__ double poisson_search(double q, double mu) {  // rare: a real call
+PBH_DI double poisson_definition_search(double q, double mu) {
   if (mu == 0.0) return 0.0;
   double z = sf::ndtri(q);  // a starting guess only (the search decides k)
   double g = floor(mu + sqrt(mu) * z + (z * z - 1.0) / 6.0);
@@ -50,15 +52,29 @@ __attribute__((noinline)) __device__ double poisson_search(double q, double mu) 
   return k;
 }
 
-// First j with cdf[j] >= q, by the guide table (Chen & Asau 1974): q lies in bucket
-// b = floor(q 2^bits) (exact: a power-of-two scale), whose guide entry is the answer for
-// q = b / 2^bits <= q, so a short forward scan from it ends at the answer -- the same j as a
-// binary search over the table, in ~1 probe instead of log2(len) dependent ones.
+// The rare poisson lanes, one call site per kernel (a real call: its code does not size the
+// callers' registers).  k < 0: q lies outside the CDF table (or there is none), so the
+// definition is searched first.  Then, when q lies in the window just above pdtr(k - 1, mu) where
+// scipy's pdtrik-based ppf can answer k - 1 (pbh_cdflib.h), scipy's computation itself decides.
+__attribute__((noinline)) __device__ double poisson_rare(double q, double mu, double k) {
+  if (k < 0.0) k = poisson_definition_search(q, mu);
+  if (k >= 1.0 && q < cdf::poisson_window_hi(k, mu)) return cdf::poisson_ppf_scipy(q, mu);
+  return k;
+}
+
+// scipy's poisson ppf (before loc) from the CDF table: the first j with cdf[j] >= q by the guide
+// table (Chen & Asau 1974: q lies in bucket b = floor(q 2^bits), exact for a power-of-two scale,
+// whose guide entry is the answer for q = b / 2^bits <= q, so a short forward scan from it ends at
+// the answer -- the same j as a binary search over the table, in ~1 probe instead of log2(len)
+// dependent ones), i.e. the smallest k with pdtr(k, mu) >= q; lanes outside the table or inside
+// scipy's window above cdf[j - 1] (win[j], a few 1e-10 of the quantile) take poisson_rare.
 PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
   int64_t lo = t.cdf_guide[(int)(q * (double)(1 << kPoissonGuideBits))];
   while (lo < t.len && t.cdf[lo] < q) ++lo;
-  if (lo == t.len || (lo == 0 && t.k_lo > 0)) return poisson_search(q, mu);  // outside coverage
-  return (double)(t.k_lo + lo);
+  const bool outside = lo == t.len || (lo == 0 && t.k_lo > 0);
+  double k = (double)(t.k_lo + lo);
+  if (outside || q < t.win[lo]) k = poisson_rare(q, mu, outside ? -1.0 : k);
+  return k;
 }
 
 // log_tab's table staged in LDS without its padding column (3 KiB): ndtri's tail reads two random
@@ -107,7 +123,7 @@ PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTa
     if (q == 0.0) return -1.0 + loc;
     if (cond0 && q == 1.0) return kInf + loc;
     if (cond0 && q > 0.0 && q < 1.0) {
-      double k = pt.cdf ? poisson_from_table(q, mu, pt) : poisson_search(q, mu);
+      double k = pt.cdf ? poisson_from_table(q, mu, pt) : poisson_rare(q, mu, -1.0);
       return k + loc;
     }
     return kNaN;

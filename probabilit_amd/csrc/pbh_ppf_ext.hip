@@ -643,11 +643,13 @@ int ext_gen_sorted(uint64_t seed, int64_t n, uint32_t col, int dist, const doubl
   PBH_REQUIRE(np >= 0, "ext_gen_sorted: distribution %d is not an extended one", dist);
   if (nt == 0) return PBH_OK;
   const Params4 prm = scalar_params(val, np, table);
-  // binom / bernoulli, counts and heads only: the binary-search heads when the values span few
-  // integers (n + 1 at most); the kernel reports anything else as an inversion
+  // binom / bernoulli, counts and heads only: the binary-search heads when the values are integers
+  // (an integer loc) spanning few of them (n + 1 at most); any other column (a non-integer loc
+  // moves every value off the integers) takes k_ext_sorted, which counts exactly
   if (ext_is_discrete(dist) && counts && heads && !out && nt >= 2) {
     const double nn = dist == PBH_DIST_BINOM ? val[0] : 1.0;
-    if (nn >= 0.0 && nn + 1.0 < (double)kExtDiscreteSpan) {
+    const double loc = dist == PBH_DIST_BINOM ? val[2] : val[1];
+    if (nn >= 0.0 && nn + 1.0 < (double)kExtDiscreteSpan && isfinite(loc) && loc == floor(loc)) {
       const bool known = dispatch_ext(dist, [&](auto tag) {
         constexpr int D = decltype(tag)::value;
         if constexpr (D == PBH_DIST_BINOM || D == PBH_DIST_BERNOULLI)

@@ -15,6 +15,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu on the GPU box")
 
 
+def record(name, obj):
+    """Print an at-scale measurement and keep it as JSON under gpurun_out/records/ (merged back
+    from the GPU box; the committed copies live under profiles/)."""
+    import json
+
+    text = json.dumps(obj, indent=1, default=float)
+    print(f"[record {name}] {text}")
+    d = os.environ.get("PBH_RECORD_DIR", os.path.join(ROOT, "gpurun_out", "records"))
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, f"{name}.json"), "w") as f:
+        f.write(text + "\n")
+
+
 def golden(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 

@@ -139,3 +139,57 @@ void sfh_binom_ppf(double nn, double p, const double* q, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = sfx::binom_ppf01(q[i], nn, p);
 }
 }
+
+// ---- cdflib's pdtrik (pbh_cdflib.h): the poisson ppf's window lanes
+#include "pbh_cdflib.h"
+
+extern "C" {
+void sfh_pdtrik(double mu, const double* p, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = cdf::pdtrik(p[i], mu);
+}
+void sfh_poisson_ppf_scipy(double mu, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = cdf::poisson_ppf_scipy(q[i], mu);
+}
+void sfh_poisson_window_hi(double mu, const double* k, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = cdf::poisson_window_hi(k[i], mu);
+}
+// gratio's P(a, x) (out) for x[i]
+void sfh_gratio_p(double a, const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) {
+    double p, q;
+    cdf::gratio(a, x[i], &p, &q);
+    out[i] = p;
+  }
+}
+void sfh_gratio_q(double a, const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) {
+    double p, q;
+    cdf::gratio(a, x[i], &p, &q);
+    out[i] = q;
+  }
+}
+void sfh_cdflib_gamma(const double* a, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = cdf::gamma_a(a[i]);
+}
+void sfh_erfc1(double ind, const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = cdf::erfc1((int)ind, x[i]);
+}
+void sfh_rlog(const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = cdf::rlog(x[i]);
+}
+}
+
+extern "C" {
+// The device's poisson ppf restated on the host (pbh_ppf_core.h poisson_from_table / poisson_rare):
+// the definition (smallest k with pdtr(k, mu) >= q) by a search of the CDF table, then scipy's
+// pdtrik computation for q in the window win[k] above pdtr(k - 1, mu).  out[i] = NaN-free k.
+void sfh_poisson_ppf_device(double mu, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) {
+    double k = 0.0;
+    if (mu > 0.0) {
+      while (sf::pdtr(k, mu) < q[i] && k < 1e7) k += 1.0;
+    }
+    out[i] = (k >= 1.0 && q[i] < cdf::poisson_window_hi(k, mu)) ? cdf::poisson_ppf_scipy(q[i], mu) : k;
+  }
+}
+}

@@ -146,7 +146,8 @@ def _dag(kind):
         from probabilit_amd import distributions as dists
 
         ds = [dists.PERT(0, 6, 10), Distribution("binom", n=20, p=0.3), Distribution("bernoulli", p=0.25),
-              Distribution("weibull_min", c=1.7), dists.PERT(1, 2, 9, gamma=10)]
+              Distribution("weibull_min", c=1.7), dists.PERT(1, 2, 9, gamma=10),
+              Distribution("binom", n=12, p=0.6, loc=0.5)]  # non-integer loc: the exact count path
         return NoOp(*ds).correlate(*ds, corr_mat=_target(len(ds))), "lhs"
     r = 0
     for _ in range(20):  # README mutual-fund loop (BASELINE config 5)

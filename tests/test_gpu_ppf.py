@@ -17,11 +17,11 @@ pytestmark = pytest.mark.gpu
 
 RTOL = 1e-10
 
-# scipy's poisson ppf is ceil(pdtrik(q, mu)) with a one-step pdtr correction; cdflib's root
-# finder loses the answer when q underflows (< ~1e-160 for mu >= 1000) or q = 1 - 2^-53 for
-# mu >= 2500, where it returns a k with pdtr(k, mu) < q.  The device kernel
-# computes the defining quantity, the smallest k with pdtr(k, mu) >= q; outside this domain
-# the test checks that definition instead of scipy's value.
+# scipy's poisson ppf is ceil(pdtrik(q, mu)) with a one-step pdtr correction; the device
+# reproduces it (the definition from its CDF table, cdflib's search restated in pbh_cdflib.h
+# inside the window above each CDF value).  Where cdflib's own incomplete gamma loses accuracy --
+# q underflowing (< ~1e-160 for mu >= 1000) or q = 1 - 2^-53 for mu >= 2500 -- scipy can return a
+# k with pdtr(k, mu) < q; outside this domain the test accepts scipy's value or the definition.
 POISSON_DOMAIN = (1e-150, 1.0 - 2.0**-52)
 
 
@@ -36,6 +36,8 @@ def _check_poisson(q, out, exp, mu, loc=0.0):
     mu = np.broadcast_to(mu, q.shape)
     for i in np.flatnonzero(~inside & np.isfinite(exp) & (q > 0) & (q < 1)):
         k = out[i]
+        if k == exp[i]:  # the device follows scipy's pdtrik search inside its windows (pbh_cdflib.h)
+            continue
         assert sc.pdtr(k, mu[i]) >= q[i] and (k == 0 or sc.pdtr(k - 1, mu[i]) < q[i]), (q[i], k)
 
 
@@ -262,38 +264,46 @@ def test_gamma_guide_every_interval(gpu, a):
     assert_close(out, exp, rtol=RTOL, what=f"gamma(a={a}) guide intervals")
 
 
-@pytest.mark.parametrize("mu", [0.3, 4.0, 30.0, 250.0, 2500.0])
-def test_poisson_table_every_boundary(gpu, mu):
-    """The CDF table + Chen-Asau guide at every table boundary, for every k with pdtr(k, mu)
-    in (1e-140, 1 - 2^-48): q = pdtr(k, mu) exactly and one ulp either side, and q one part in
-    1e6 either side.  The device computes the definition, the smallest k with pdtr(k, mu) >= q.
-    scipy's poisson.ppf is ceil(pdtrik(q, mu)) with a one-step pdtr correction BELOW only;
-    cdflib's root finder stops at a relative tolerance, so just above a CDF value scipy
-    returns the k whose pdtr is below q -- measured windows (relative, above pdtr(k, mu)):
-    < 1e-12 at mu = 0.3, < 1e-10 at mu = 4, < 1e-9 at mu = 30, < 1e-6 at mu = 250 and 2500.
-    There the two may differ by one (documented deviation); one part in 1e6
-    away from every boundary they must agree exactly."""
+@pytest.mark.parametrize("mu,near", [(0.3, 1e-13), (4.0, 1e-13), (30.0, 1e-13), (250.0, 1e-8), (2500.0, 1e-8),
+                                     (20000.0, 1e-8)])
+def test_poisson_table_every_boundary(gpu, mu, near):
+    """scipy's poisson ppf at every table boundary: for every k with pdtr(k, mu) in (1e-140, 1 - 1e-5),
+    q = pdtr(k, mu) exactly, one ulp either side, 40 offsets of 1e-16 .. 1e-6 relative above it
+    (where scipy's pdtrik-based answer falls to k - 1 hundreds of times) and 1e-6 either side.
+    The device answers the definition from its CDF table and runs scipy's cdflib search
+    (pbh_cdflib.h) inside the window above each CDF value, so it must equal scipy.stats.poisson.ppf
+    except (a) within `near` relative of a CDF value, where the compiled gratio's last bits decide
+    (tests/test_special_host.py pins the restatement), and (b) scipy's deep tail (mu >= 2500,
+    q < ~1e-50), where cdflib's own incomplete gamma loses accuracy and scipy is off the definition
+    while the device is on it.  The scalar-mu LDS table (mu <= 8900), the global table (mu = 2e4)
+    and the per-row (composite) search must agree bit for bit.  The counts go to records/."""
     import scipy.special as sc
 
+    from conftest import record
     from oracle.ppf import ppf as ref_ppf
     from probabilit_amd import native
 
+    rng = np.random.default_rng(int(mu))
     k = np.arange(0, int(mu + 40 * np.sqrt(mu) + 40), dtype=np.float64)
     c = sc.pdtr(k, mu)
     c = c[(c > 1e-140) & (c < 1.0 - 1e-5)]
-    near = np.concatenate([c, np.nextafter(c, 0.0), np.nextafter(c, 1.0)])
-    out_near, exp_near = native.ppf("poisson", near, mu=mu), ref_ppf("poisson", near, mu=mu)
-    assert np.all(np.abs(out_near - exp_near) <= 1.0)
-    assert int(np.count_nonzero(out_near != exp_near)) <= len(c)
-    far = np.concatenate([c * (1.0 - 1e-6), c * (1.0 + 1e-6)])
-    out, exp = native.ppf("poisson", far, mu=mu), ref_ppf("poisson", far, mu=mu)
+    q = np.concatenate([c, np.nextafter(c, 0.0), np.nextafter(c, 1.0), c * (1.0 - 1e-6), c * (1.0 + 1e-6)] +
+                       [c * (1.0 + 10.0 ** rng.uniform(-16, -6, c.size)) for _ in range(40)])
+    q = q[(q > 0) & (q < 1)]
+    out, exp = native.ppf("poisson", q, mu=mu), ref_ppf("poisson", q, mu=mu)
+    per_row = native.ppf("poisson", q, mu=np.full(q.shape, mu))
+    np.testing.assert_array_equal(per_row, out)
 
     def defining(k, q):  # smallest k with pdtr(k, mu) >= q (scipy's own pdtr)
         return (sc.pdtr(k, mu) >= q) & ((k == 0) | (sc.pdtr(k - 1, mu) < q))
 
+    table = sc.pdtr(np.arange(0, int(mu + 60 * np.sqrt(mu) + 80), dtype=np.float64), mu)
+    definition = np.searchsorted(table, q, side="left").astype(np.float64)
     diff = out != exp
-    # every disagreement is scipy off the definition (its deep tail: q ~ 1e-52 at mu = 2500,
-    # cdflib's relative tolerance) with the device on it
-    assert not np.any(diff & defining(exp, far)), far[diff & defining(exp, far)]
-    assert np.all(defining(out[diff], far[diff]))
-    assert int(diff.sum()) <= 8
+    off = np.min(np.abs(q[diff][:, None] / c[None, :] - 1.0), axis=1) if diff.any() else np.zeros(0)
+    tail = ~defining(exp[diff], q[diff]) & defining(out[diff], q[diff])
+    assert np.all((off < near) | tail), (q[diff][~((off < near) | tail)][:6], out[diff][:6], exp[diff][:6])
+    record(f"poisson_boundaries_mu{mu:g}", {
+        "mu": mu, "quantiles": int(q.size), "scipy_below_definition": int(np.count_nonzero(exp < definition)),
+        "device_differs_from_scipy": int(diff.sum()), "of_which_within_near": int(np.count_nonzero(off < near)),
+        "of_which_scipy_deep_tail": int(np.count_nonzero(tail & ~(off < near))), "near": near})

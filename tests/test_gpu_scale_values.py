@@ -4,9 +4,11 @@
   regenerates as sort(X)[p] -- on 10^6 random strata against scipy.stats.<dist>.ppf of the same
   native quantiles (1e-10 relative; poisson exact).
 * cfg3, N = 1e8, poisson columns: every one of the 1e8 strata near a CDF boundary (relative
-  window 1e-6 around each pdtr(k, mu), 10^3 times the widest documented deviation) against scipy;
-  between boundaries both are constant in q, so this counts every +-1 output of the column.  The
-  count is printed; each must be +-1 inside the documented window.
+  window 1e-6 around each pdtr(k, mu), 10^4 times scipy's widest deviation from the definition at
+  these mu) against scipy; between boundaries both are constant in q, so this compares every
+  output of the column.  They must be equal (the device runs scipy's pdtrik search inside the
+  windows, pbh_cdflib.h); the counts, including how often scipy differs from the definition
+  there, go to records/.
 * cfg2, N = 1e7, d = 8, uncorrelated, through Node.sample_device: against oracle.pipeline's scipy
   ppf of the same native quantile matrix.
 * cfg5, N = 1e8 (Sobol', seed 3: a seed whose points avoid q = 0): the fused graph kernel's sink
@@ -19,7 +21,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from conftest import assert_close
+from conftest import assert_close, record
 
 pytestmark = pytest.mark.gpu
 
@@ -101,15 +103,14 @@ def test_cfg3_poisson_boundaries_1e8_every_stratum(gpu):
         xs, qs = x[idx].cpu().numpy(), q[idx].cpu().numpy()
         del x, q
         exp = ref_ppf("poisson", qs, mu=mu)
+        table = sc.pdtr(np.arange(0, int(mu + 60 * np.sqrt(mu) + 80), dtype=np.float64), mu)
+        definition = np.searchsorted(table, qs, side="left").astype(np.float64)
         diff = xs != exp
-        # each difference: +-1, q within the documented window above a CDF value (< 1e-9 at mu = 30)
-        if diff.any():
-            assert np.all(np.abs(xs[diff] - exp[diff]) == 1.0)
-            rel = np.min(np.abs(qs[diff][:, None] / b[None, :] - 1.0), axis=1)
-            assert np.all(rel < 1e-9), rel
         report.append({"column": j, "mu": mu, "strata_near_boundaries": int(idx.numel()),
-                       "plus_minus_one": int(diff.sum())})
-    print("poisson +-1 outputs over every stratum at N=1e8:", report)
+                       "device_differs_from_scipy": int(diff.sum()),
+                       "scipy_differs_from_definition": int(np.count_nonzero(exp != definition))})
+    record("cfg3_poisson_boundaries_1e8", report)
+    assert all(r["device_differs_from_scipy"] == 0 for r in report), report
 
 
 @pytest.mark.timeout(600)
@@ -124,13 +125,15 @@ def test_cfg2_1e7_uncorrelated_vs_oracle(gpu):
     Q = native.fill_lhs(qmc.seed_from(seed), n, d)  # the native quantile matrix of this seed (row order)
     X = ppf_columns(Q, cfg_dists(d), threads=THREADS)
     del Q
+    counts = {}
     for j, x in enumerate(ds):
         got = device.to_host(x.samples_device)
         if cfg_dists(d)[j][0] == "poisson":
-            bad = got != X[:, j]
-            assert int(bad.sum()) <= 2 and np.all(np.abs(got[bad] - X[bad, j]) == 1.0), int(bad.sum())
+            counts[j] = int(np.count_nonzero(got != X[:, j]))
         else:
             assert_close(got, X[:, j], rtol=RTOL, what=f"cfg2 column {j}")
+    record("cfg2_1e7_poisson_vs_scipy", {"device_differs_from_scipy_per_poisson_column": counts})
+    assert not any(counts.values()), counts
 
 
 @pytest.mark.timeout(600)

@@ -254,3 +254,32 @@ def test_gamma_placement_slow_list(gpu, shape):
     ref = _oracle(200_003, dists, 41, C)
     np.testing.assert_array_equal(idx, ref["idx"])
     assert_close(Y, ref["Y"], rtol=1e-10, what=f"gamma(a={shape}) placement")
+
+
+def test_bad_last_column_returns_an_error_and_leaves_the_device_usable(gpu):
+    """A column list whose LAST entry has a bad parameter count: pbh_iman_conover has by then
+    queued the earlier columns' tables and counts on the step-4 side streams, so its error return
+    must join those streams before their tables are freed.  The call raises, and the
+    same columns with the count fixed then give the oracle's result."""
+    import ctypes
+
+    from probabilit_amd import _lib, device, qmc
+    from probabilit_amd.correlation import ImanConover
+    from probabilit_amd.modeling import Distribution
+
+    dists = [("poisson", {"mu": 4.0}), ("gamma", {"a": 2.0}), ("norm", {}), ("poisson", {"mu": 30.0})]
+    C = np.array([[1.0, 0.4, 0.2, 0.1], [0.4, 1.0, 0.3, 0.2], [0.2, 0.3, 1.0, 0.3], [0.1, 0.2, 0.3, 1.0]])
+    n = 200_001
+    flags = device.zeros(len(dists), "int32")
+    cols = []
+    for j, (nm, kw) in enumerate(dists):
+        params = [float(p) for p in Distribution(nm, **kw)._params(n)]
+        cols.append(_lib.ICColumn(qmc.seed_from(5), j, _lib.DIST_IDS[nm], (ctypes.c_double * 4)(*params),
+                                  len(params) + (1 if j == len(dists) - 1 else 0), flags.data_ptr() + 4 * j))
+    with pytest.raises(Exception):
+        ImanConover().set_target(C)._transform_generated(cols, n)
+    device.synchronize()
+    Y, idx = _run(n, dists, 5, C)
+    ref = _oracle(n, dists, 5, C)
+    np.testing.assert_array_equal(idx, ref["idx"])
+    assert_close(Y, ref["Y"], rtol=1e-10, what="after the failed call")
