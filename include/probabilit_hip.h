@@ -94,7 +94,13 @@ typedef enum pbh_dist {
   PBH_DIST_ALPHA = 51,        /* a        1 / (a - ndtri(q ndtr(a))) */
   PBH_DIST_FATIGUELIFE = 52,  /* c        (c z + sqrt((c z)^2 + 4))^2 / 4 */
   PBH_DIST_GENLOGISTIC = 53,  /* c        -log(powm1(q, -1/c)) */
-  PBH_DIST_TRAPEZOID = 54     /* c, d     three pieces at cdf(c), cdf(d) */
+  PBH_DIST_TRAPEZOID = 54,    /* c, d     three pieces at cdf(c), cdf(d) */
+  /* round 5: modeling.py:805-807 samples any scipy.stats name */
+  PBH_DIST_GEOM = 55,         /* p, loc (discrete)   ceil(log1p(-q) / log1p(-p)), one step down */
+  PBH_DIST_RANDINT = 56,      /* low, high, loc (discrete)  ceil(q (high - low) + low) - 1, one step down */
+  PBH_DIST_NBINOM = 57,       /* n, p, loc (discrete)  smallest k: I_p(n, k + 1) >= q (Boost) */
+  PBH_DIST_INVGAMMA = 58,     /* a        1 / gammainccinv(a, q) */
+  PBH_DIST_T = 59             /* df       stdtrit(df, q), through the incomplete beta */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

@@ -68,7 +68,11 @@ sfx::BetaGuide guide_of(const double* t) {
   return t ? sfx::BetaGuide{t, t + m, t + 2 * m, t + 3 * m} : sfx::BetaGuide{};
 }
 
-constexpr bool is_closed(int d) { return d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID; }
+constexpr bool is_closed(int d) {
+  return (d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID) || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T;
+}
+// discrete distributions beyond binom / bernoulli (round 5): p, loc / low, high, loc / n, p, loc
+constexpr bool is_discrete2(int d) { return d == PBH_DIST_GEOM || d == PBH_DIST_RANDINT || d == PBH_DIST_NBINOM; }
 
 constexpr int closed_shapes(int d) {
   return (d == PBH_DIST_LOGUNIFORM || d == PBH_DIST_BURR || d == PBH_DIST_BURR12 || d == PBH_DIST_EXPONWEIB ||
@@ -80,7 +84,7 @@ constexpr int closed_shapes(int d) {
             d == PBH_DIST_INVWEIBULL || d == PBH_DIST_LOGLAPLACE || d == PBH_DIST_TRUNCEXPON || d == PBH_DIST_CHI ||
             d == PBH_DIST_NAKAGAMI || d == PBH_DIST_DWEIBULL || d == PBH_DIST_KAPPA3 ||
             d == PBH_DIST_GENHALFLOGISTIC || d == PBH_DIST_ALPHA || d == PBH_DIST_FATIGUELIFE ||
-            d == PBH_DIST_GENLOGISTIC)
+            d == PBH_DIST_GENLOGISTIC || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T)
              ? 1
              : 0;
 }
@@ -137,7 +141,7 @@ __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo,
                 D == PBH_DIST_LOGLAPLACE || D == PBH_DIST_TRUNCEXPON || D == PBH_DIST_CHI ||
                 D == PBH_DIST_MAXWELL || D == PBH_DIST_NAKAGAMI || D == PBH_DIST_KAPPA3 ||
                 D == PBH_DIST_GENHALFLOGISTIC || D == PBH_DIST_ALPHA || D == PBH_DIST_FATIGUELIFE ||
-                D == PBH_DIST_ARCSINE || D == PBH_DIST_TRAPEZOID)
+                D == PBH_DIST_ARCSINE || D == PBH_DIST_TRAPEZOID || D == PBH_DIST_INVGAMMA)
     lo = 0.0;
   if constexpr (D == PBH_DIST_ARCSINE || D == PBH_DIST_POWERLAW || D == PBH_DIST_BRADFORD ||
                 D == PBH_DIST_TRAPEZOID)
@@ -235,6 +239,9 @@ __device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
     return 0.25 * (u * u);
   }
   if constexpr (D == PBH_DIST_GENLOGISTIC) return -log(powm1(q, -1.0 / s0));
+  // round 5
+  if constexpr (D == PBH_DIST_INVGAMMA) return 1.0 / sf::igamci(s0, q);  // invgamma._ppf
+  if constexpr (D == PBH_DIST_T) return sfx::t_ppf01(q, s0);  // t._ppf = stdtrit (cdflib, ~2.5e-11)
   if constexpr (D == PBH_DIST_TRAPEZOID) {
     const double c = s0, d = s1;
     const double qc = trapezoid_mid_cdf(c, c, d), qd = trapezoid_mid_cdf(d, c, d);
@@ -257,6 +264,30 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
     if (!ok || !(q >= 0.0 && q <= 1.0)) return nan;
     if (q == 1.0) return n + loc;
     return sfx::binom_ppf01(q, n, pp) + loc;
+  } else if constexpr (is_discrete2(D)) {
+    // rv_discrete.ppf: q == 0 -> _a - 1 + loc whatever the arguments, q == 1 -> _b + loc for valid
+    // ones, NaN otherwise; _a = 1 (geom), low (randint), 0 (nbinom)
+    if constexpr (D == PBH_DIST_GEOM) {
+      const double pp = p.at(0, i), loc = p.at(1, i);
+      if (q == 0.0) return 0.0 + loc;
+      if (!(pp > 0.0 && pp <= 1.0 && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
+      if (q == 1.0) return inf + loc;
+      return sfx::geom_ppf01(q, pp) + loc;
+    } else if constexpr (D == PBH_DIST_RANDINT) {
+      const double low = p.at(0, i), high = p.at(1, i), loc = p.at(2, i);
+      if (q == 0.0) return low - 1.0 + loc;
+      // _argcheck: high > low, both integral (x == np.round(x))
+      if (!(high > low && low == rint(low) && high == rint(high) && loc == loc) || !(q >= 0.0 && q <= 1.0))
+        return nan;
+      if (q == 1.0) return high - 1.0 + loc;
+      return sfx::randint_ppf01(q, low, high) + loc;
+    } else {  // nbinom
+      const double n = p.at(0, i), pp = p.at(1, i), loc = p.at(2, i);
+      if (q == 0.0) return -1.0 + loc;
+      if (!(n > 0.0 && pp > 0.0 && pp <= 1.0 && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
+      if (q == 1.0) return inf + loc;
+      return sfx::nbinom_ppf01(q, n, pp) + loc;
+    }
   } else if constexpr (is_closed(D)) {
     constexpr int S = closed_shapes(D);
     const double s0 = S > 0 ? p.at(0, i) : 0.0, s1 = S > 1 ? p.at(1, i) : 0.0;
@@ -375,6 +406,11 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_FATIGUELIFE)
     PBH_EXT(PBH_DIST_GENLOGISTIC)
     PBH_EXT(PBH_DIST_TRAPEZOID)
+    PBH_EXT(PBH_DIST_GEOM)
+    PBH_EXT(PBH_DIST_RANDINT)
+    PBH_EXT(PBH_DIST_NBINOM)
+    PBH_EXT(PBH_DIST_INVGAMMA)
+    PBH_EXT(PBH_DIST_T)
 #undef PBH_EXT
     default:
       return false;
@@ -383,10 +419,8 @@ bool dispatch_ext(int dist, F&& f) {
 
 int launch_ext(int dist, const double* q, int64_t q_stride, const LhsCol* lc, int64_t n, const pbh_param* params,
                int nparams, double* out, int32_t* flag, hipStream_t s) {
-  const int want = dist == PBH_DIST_BERNOULLI ? 2
-                   : dist == PBH_DIST_BINOM   ? 3
-                   : is_closed(dist)          ? closed_shapes(dist) + 2
-                                              : 4;
+  const int want = ext_nparams(dist);
+  PBH_REQUIRE(want >= 0, "ppf: unknown distribution id %d", dist);
   PBH_REQUIRE(nparams == want && params, "ppf: distribution %d takes %d parameters, got %d", dist, want, nparams);
   Params4 prm{};
   for (int j = 0; j < nparams; ++j) {
@@ -627,14 +661,51 @@ Params4 scalar_params(const double* val, int np, const double* table) {
 }  // namespace
 
 int ext_nparams(int dist) {
-  if (dist == PBH_DIST_BERNOULLI) return 2;
-  if (dist == PBH_DIST_BINOM) return 3;
+  if (dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_GEOM) return 2;
+  if (dist == PBH_DIST_BINOM || dist == PBH_DIST_RANDINT || dist == PBH_DIST_NBINOM) return 3;
   if (dist == PBH_DIST_BETA || dist == PBH_DIST_TRUNCNORM) return 4;
   if (is_closed(dist)) return closed_shapes(dist) + 2;
   return -1;
 }
 
-bool ext_is_discrete(int dist) { return dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI; }
+bool ext_is_discrete(int dist) {
+  return dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI || is_discrete2(dist);
+}
+
+namespace {
+// An upper bound on the number of distinct values a discrete column takes for quantiles in (0, 1)
+// (inf when unknown), and its loc: the binary-search heads need integer values spanning few of them
+void discrete_span(int dist, const double* val, double* span, double* loc) {
+  const double top = 1.0 - 0x1p-53;  // the largest quantile below 1
+  *span = sf::kInf;
+  *loc = sf::kNaN;
+  switch (dist) {
+    case PBH_DIST_BINOM:
+      if (val[0] >= 0.0) *span = val[0] + 1.0;
+      *loc = val[2];
+      break;
+    case PBH_DIST_BERNOULLI:
+      *span = 2.0;
+      *loc = val[1];
+      break;
+    case PBH_DIST_GEOM:
+      if (val[0] > 0.0 && val[0] <= 1.0) *span = sfx::geom_ppf01(top, val[0]) + 1.0;
+      *loc = val[1];
+      break;
+    case PBH_DIST_RANDINT:
+      if (val[1] > val[0]) *span = val[1] - val[0] + 1.0;
+      *loc = val[2];
+      break;
+    case PBH_DIST_NBINOM:
+      if (val[0] > 0.0 && val[1] > 0.0 && val[1] <= 1.0 && val[0] < 1e6 && val[1] > 1e-6)
+        *span = sfx::nbinom_ppf01(top, val[0], val[1]) + 1.0;
+      *loc = val[2];
+      break;
+    default:
+      break;
+  }
+}
+}  // namespace
 
 int ext_gen_sorted(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, const double* table,
                    int64_t t0, int64_t nt, double* out, int32_t* flag, unsigned long long* counts, uint32_t* heads,
@@ -647,12 +718,12 @@ int ext_gen_sorted(uint64_t seed, int64_t n, uint32_t col, int dist, const doubl
   // (an integer loc) spanning few of them (n + 1 at most); any other column (a non-integer loc
   // moves every value off the integers) takes k_ext_sorted, which counts exactly
   if (ext_is_discrete(dist) && counts && heads && !out && nt >= 2) {
-    const double nn = dist == PBH_DIST_BINOM ? val[0] : 1.0;
-    const double loc = dist == PBH_DIST_BINOM ? val[2] : val[1];
-    if (nn >= 0.0 && nn + 1.0 < (double)kExtDiscreteSpan && isfinite(loc) && loc == floor(loc)) {
+    double span, loc;
+    discrete_span(dist, val, &span, &loc);
+    if (span < (double)kExtDiscreteSpan && isfinite(loc) && loc == floor(loc)) {
       const bool known = dispatch_ext(dist, [&](auto tag) {
         constexpr int D = decltype(tag)::value;
-        if constexpr (D == PBH_DIST_BINOM || D == PBH_DIST_BERNOULLI)
+        if constexpr (D == PBH_DIST_BINOM || D == PBH_DIST_BERNOULLI || is_discrete2(D))
           PBH_TIMED(kKLhsSorted, s,
                     hipLaunchKernelGGL(k_ext_discrete_heads<D>, dim3(1), dim3(256), 0, s, seed, n, t0, nt, col, prm,
                                        flag, counts, heads, hcur, hcap));

@@ -410,5 +410,98 @@ PBH_HD inline double binom_ppf01(double q, double n, double p) {
   return k;
 }
 
+
+// ---- round 5: geom, randint, nbinom, t (scipy 1.15 _ppf bodies)
+
+// geom._ppf(q, p) (scipy/stats/_discrete_distns.py), numpy's log1p / expm1 (the C library's):
+//   vals = ceil(log1p(-q) / log1p(-p)); temp = _cdf(vals - 1, p) = -expm1(log1p(-p) floor(vals - 1))
+//   where((temp >= q) & (vals > 0), vals - 1, vals)
+PBH_HD inline double geom_ppf01(double q, double p) {
+  const double lp = log1p(-p);
+  const double vals = ceil(log1p(-q) / lp);
+  const double temp = -expm1(lp * floor(vals - 1.0));
+  return (temp >= q && vals > 0.0) ? vals - 1.0 : vals;
+}
+
+// randint._ppf(q, low, high): vals = ceil(q (high - low) + low) - 1; vals1 = clip(vals - 1, low, high);
+// temp = _cdf(vals1) = (floor(vals1) - low + 1) / (high - low); where(temp >= q, vals1, vals)
+PBH_HD inline double randint_ppf01(double q, double low, double high) {
+  const double vals = ceil(q * (high - low) + low) - 1.0;
+  const double vals1 = fmin(fmax(vals - 1.0, low), high);
+  const double temp = (floor(vals1) - low + 1.0) / (high - low);
+  return temp >= q ? vals1 : vals;
+}
+
+// negative binomial CDF P(X <= k) = I_p(n, k + 1) and its complement I_{1-p}(k + 1, n) (Boost's
+// nbinom cdf, the incomplete beta ratio; Cephes incbet restated above)
+PBH_HD inline double nbdtr(double k, double n, double p) {
+  if (p >= 1.0) return 1.0;
+  return incbet(n, k + 1.0, p);
+}
+PBH_HD inline double nbdtrc(double k, double n, double p) {
+  if (p >= 1.0) return 0.0;
+  return incbet(k + 1.0, n, 1.0 - p);
+}
+
+// scipy nbinom._ppf = Boost's discrete quantile (integer_round_up): the smallest k >= 0 with
+// nbdtr(k, n, p) >= q; above the median on the complement, nbdtrc(k) <= 1 - q, as binom_ppf01
+PBH_HD inline double nbinom_ppf01(double q, double n, double p) {
+  if (p >= 1.0) return 0.0;
+  const double m = n * (1.0 - p) / p, sd = sqrt(n * (1.0 - p)) / p;
+  double k = floor(m + sd * ndtri(q));
+  if (!(k >= 0.0)) k = 0.0;
+  if (k > 9.0e15) k = 9.0e15;
+  if (q <= 0.5) {
+    if (nbdtr(k, n, p) >= q) {
+      while (k > 0.0 && nbdtr(k - 1.0, n, p) >= q) k -= 1.0;
+    } else {
+      do {
+        k += 1.0;
+      } while (nbdtr(k, n, p) < q && k < 1.0e18);
+    }
+    return k;
+  }
+  const double r = 1.0 - q;
+  if (nbdtrc(k, n, p) <= r) {
+    while (k > 0.0 && nbdtrc(k - 1.0, n, p) <= r) k -= 1.0;
+  } else {
+    do {
+      k += 1.0;
+    } while (nbdtrc(k, n, p) > r && k < 1.0e18);
+  }
+  return k;
+}
+
+// Student's t quantile (scipy t._ppf = stdtrit, cdflib's root search, accurate to ~2.5e-11): the
+// exact quantile through the incomplete beta.  With pp = 2 min(q, 1 - q) = P(|T| >= |t|):
+// below pp = 1/2, x = df / (df + t^2) solves I_x(df / 2, 1 / 2) = pp (x is then at most the
+// median, so 1 - x >= ~0.45 / df keeps its relative error below 1e-11 up to df = 1e5); from
+// pp = 1/2 on, y = 1 - x solves I_y(1 / 2, df / 2) = 1 - pp, exact there.  Beyond df = 1e5 the
+// Cornish-Fisher series in 1 / df (Abramowitz & Stegun 26.7.5, four terms: the next is below
+// 1e-15 relative for |z| <= 8.3) from the normal quantile.
+PBH_HD inline double t_ppf01(double q, double df) {
+  if (isinf(df)) return ndtri(q);
+  if (q == 0.5) return 0.0;
+  if (df >= 1e5) {
+    const double z = ndtri(q), z2 = z * z, u = 1.0 / df;
+    const double g1 = (z2 + 1.0) * z / 4.0;
+    const double g2 = ((5.0 * z2 + 16.0) * z2 + 3.0) * z / 96.0;
+    const double g3 = (((3.0 * z2 + 19.0) * z2 + 17.0) * z2 - 15.0) * z / 384.0;
+    const double g4 = ((((79.0 * z2 + 776.0) * z2 + 1482.0) * z2 - 1920.0) * z2 - 945.0) * z / 92160.0;
+    return z + (g1 + (g2 + (g3 + g4 * u) * u) * u) * u;
+  }
+  const double pp = q < 0.5 ? 2.0 * q : 2.0 * (1.0 - q);
+  double t2;
+  if (pp < 0.5) {
+    const double x = beta_ppf01(pp, 0.5 * df, 0.5);
+    t2 = df * ((1.0 - x) / x);
+  } else {
+    const double y = beta_ppf01(1.0 - pp, 0.5, 0.5 * df);
+    t2 = df * (y / (1.0 - y));
+  }
+  const double t = sqrt(t2);
+  return q < 0.5 ? -t : t;
+}
+
 }  // namespace sfx
 }  // namespace pbh

@@ -85,10 +85,11 @@ int step4_gen_place_passes(int c, int64_t n, const Step4Shared& sh, const Step4C
 // A generated LHS column's inverse-CDF setup (scalar parameters; gamma guide / poisson CDF
 // tables built once), shared by the stratum-ordered generator and the final placement.
 struct GenColumn;
-// a distribution whose generated sorted column has runs of equal values (poisson, binom, bernoulli):
-// step 1 takes its tie count and run heads up front (never deferred)
+// a distribution whose generated sorted column has runs of equal values (poisson, binom, bernoulli,
+// geom, randint, nbinom): step 1 takes its tie count and run heads up front (never deferred)
 inline bool gen_discrete(int dist) {
-  return dist == PBH_DIST_POISSON || dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI;
+  return dist == PBH_DIST_POISSON || dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI ||
+         dist == PBH_DIST_GEOM || dist == PBH_DIST_RANDINT || dist == PBH_DIST_NBINOM;
 }
 int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* params, int nparams, GenColumn** out,
                hipStream_t s);

@@ -604,8 +604,9 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "anglit": (), "levy": (), "levy_l": (), "gibrat": (), "invweibull": ("c",),
                 "loglaplace": ("c",), "truncexpon": ("b",), "chi": ("df",), "maxwell": (), "nakagami": ("nu",),
                 "dweibull": ("c",), "kappa3": ("a",), "genhalflogistic": ("c",), "alpha": ("a",),
-                "fatiguelife": ("c",), "genlogistic": ("c",), "trapezoid": ("c", "d")}
-_DISCRETE = {"poisson", "binom", "bernoulli"}
+                "fatiguelife": ("c",), "genlogistic": ("c",), "trapezoid": ("c", "d"),
+                "geom": ("p",), "randint": ("low", "high"), "nbinom": ("n", "p"), "invgamma": ("a",), "t": ("df",)}
+_DISCRETE = {"poisson", "binom", "bernoulli", "geom", "randint", "nbinom"}
 # distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so
 # that Iman-Conover takes them as generated columns (pbh_ppf.hip k_lhs_sorted_ppf / k_place_gen;
 # the extended set pbh_ppf_ext.hip k_ext_sorted / k_ext_place): every distribution with a kernel

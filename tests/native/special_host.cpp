@@ -193,3 +193,22 @@ void sfh_poisson_ppf_device(double mu, const double* q, long n, double* out) {
   }
 }
 }
+
+extern "C" {
+// ---- round 5 distributions (pbh_special_ext.h): scipy's _ppf for 0 < q < 1
+void sfh_geom_ppf(double p, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::geom_ppf01(q[i], p);
+}
+void sfh_randint_ppf(double low, double high, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::randint_ppf01(q[i], low, high);
+}
+void sfh_nbinom_ppf(double nn, double p, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::nbinom_ppf01(q[i], nn, p);
+}
+void sfh_t_ppf(double df, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = sfx::t_ppf01(q[i], df);
+}
+void sfh_invgamma_ppf(double a, const double* q, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = 1.0 / sf::igamci(a, q[i]);
+}
+}

@@ -2,9 +2,11 @@
 tests/test_gpu_scale.py and tools/parity_1e8.py.  The device side runs the production
 Iman-Conover path of Node.sample(method="lhs") on natively generated cfg3 columns; the
 reference side recomputes the correlated scores the reference's way (correlation.py:398-414:
-np.corrcoef, np.linalg.cholesky, scipy.linalg.solve_triangular, then @ P.T) from the device's
-own scores, ranks them (rankdata(...).astype(int) - 1, correlation.py:422) and counts the
-step-4 index mismatches."""
+np.corrcoef, np.linalg.cholesky, scipy.linalg.solve_triangular, then @ P.T), ranks them
+(rankdata(...).astype(int) - 1, correlation.py:422) and counts the step-4 index mismatches.
+Two legs: scores="device" starts from the device's step-1 scores S; scores="reference" runs the
+reference's step 1 as well (correlation.py:394-395): X = scipy.stats ppf of the same native
+quantiles (modeling.py:807), rankdata(X, 'average') / (N + 1), scipy.special.ndtri."""
 
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -179,7 +181,65 @@ def gate(cs_ref_cols, y_cols, sx_cols, cs_dev_cols=None, threads=4, log=None):
         return list(ex.map(one, range(k)))
 
 
-def gate_all(n, d, seed, C, threads=8, log=print):
+def _chunked(fn, x, threads, chunk=1 << 22):
+    """fn over row chunks of a 1-D array on a thread pool (numpy / scipy ufuncs release the GIL)."""
+    out = np.empty(x.shape[0])
+
+    def run(r0):
+        out[r0:r0 + chunk] = fn(x[r0:r0 + chunk])
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(run, range(0, x.shape[0], chunk)))
+    return out
+
+
+def reference_scores(col, name, kw, n, threads=16):
+    """The reference's step 1 for one generated column (correlation.py:394-395) from the reference's
+    own values: X = scipy.stats.<name>(**kw).ppf(q) of the column's native quantiles q
+    (modeling.py:807), ranks = rankdata(X, 'average'), S = ndtri(ranks / (N + 1)).
+
+    The ranks are taken in stratum order: the device sorts the quantiles (torch.sort, which also
+    gives the row of every stratum), scipy's ppf runs on them in that order, and where its values
+    never decrease, rankdata(X) is the stratum position, averaged over each run of equal values --
+    the same numbers rankdata's argsort gives, without a 10^8-element sort per column.  A decrease
+    (a non-monotone scipy ppf) falls back to scipy.stats.rankdata on the row-order X.
+    Returns (S in row order, host (N,), info dict)."""
+    import scipy.special
+    import scipy.stats
+    import torch
+
+    from oracle.ppf import ppf
+    from probabilit_amd import _lib, device
+
+    q = device.empty(n)
+    _lib.check(_lib.load().pbh_fill_lhs(col.seed, n, 0, n, col.lhs_col, 1, q.data_ptr(), n, device.stream()))
+    qs, order = torch.sort(q)
+    del q
+    qs_h, order_h = device.to_host(qs), order.cpu().numpy()
+    del qs, order
+    xs = _chunked(lambda v: ppf(name, v, **kw), qs_h, threads)
+    del qs_h
+    dx = np.diff(xs)
+    info = {"column": int(col.lhs_col), "dist": name, "params": kw, "ties": int(np.count_nonzero(dx == 0)),
+            "decreases": int(np.count_nonzero(dx < 0))}
+    if info["decreases"]:
+        xrow = np.empty(n)
+        xrow[order_h] = xs
+        rank_row = scipy.stats.rankdata(xrow)
+    else:
+        if info["ties"]:
+            starts = np.concatenate([[0], np.flatnonzero(dx != 0) + 1])
+            ends = np.concatenate([starts[1:], [n]])
+            rank_t = np.repeat((starts + 1 + ends) / 2.0, ends - starts)  # 'average' over each run
+        else:
+            rank_t = np.arange(1, n + 1, dtype=np.float64)
+        rank_row = np.empty(n)
+        rank_row[order_h] = rank_t
+    del xs, dx, order_h
+    return _chunked(lambda v: scipy.special.ndtri(v / (n + 1)), rank_row, threads), info
+
+
+def gate_all(n, d, seed, C, threads=8, log=print, scores="device"):
     """The §8(d) gate over every column (tools/parity_1e8.py, tests/test_gpu_scale.py): the
     production path on the device keeping S, then on the host E = np.corrcoef(S)
     (correlation.py:398), L = cholesky(E), D = solve_triangular(L, S.T).T, CS = D @ P.T
@@ -189,12 +249,37 @@ def gate_all(n, d, seed, C, threads=8, log=print):
 
     t0 = time.time()
     Y, S, CS, E_dev, P, gen = run_device(n, d, seed, C)
-    S_host = device.to_host(S)
-    del S
-    E_ref = np.corrcoef(S_host.T, rowvar=False)  # the reference's S is (N, K): S_host.T
-    log(f"[{time.time() - t0:6.1f}s] max |E_dev - E_ref| = {float(np.max(np.abs(E_dev - E_ref))):.3e}")
-    cs_ref = reference_cs(S_host, E_ref, P)
-    del S_host
+    extra = {}
+    if scores == "reference":
+        from oracle.pipeline import cfg_dists
+
+        S_dev = S
+        S_ref = np.empty((n, d))  # the reference's S: (N, K), C order (correlation.py:395)
+        infos, worst_s = [], 0.0
+        for j, (name, kw) in enumerate(cfg_dists(d)):
+            sj, info = reference_scores(gen[j], name, kw, n, threads=threads)
+            info["max_abs_s_dev_minus_ref"] = float(np.max(np.abs(device.to_host(S_dev[j]) - sj)))
+            worst_s = max(worst_s, info["max_abs_s_dev_minus_ref"])
+            S_ref[:, j] = sj
+            del sj
+            infos.append(info)
+            log(f"[{time.time() - t0:6.1f}s] reference step 1, column {j}: {info}")
+        del S_dev, S
+        E_ref = np.corrcoef(S_ref, rowvar=False)  # correlation.py:398, on the reference's own scores
+        log(f"[{time.time() - t0:6.1f}s] max |E_dev - E_ref| = {float(np.max(np.abs(E_dev - E_ref))):.3e}")
+        import scipy.linalg
+
+        L = np.linalg.cholesky(E_ref)  # correlation.py:405-414, literally
+        cs_ref = scipy.linalg.solve_triangular(L, S_ref.T, lower=True).T @ np.asarray(P).T
+        del S_ref
+        extra = {"step1": infos, "max_abs_s_dev_minus_ref": worst_s}
+    else:
+        S_host = device.to_host(S)
+        del S
+        E_ref = np.corrcoef(S_host.T, rowvar=False)  # the reference's S is (N, K): S_host.T
+        log(f"[{time.time() - t0:6.1f}s] max |E_dev - E_ref| = {float(np.max(np.abs(E_dev - E_ref))):.3e}")
+        cs_ref = reference_cs(S_host, E_ref, P)
+        del S_host
     log(f"[{time.time() - t0:6.1f}s] reference CS done")
 
     def one(j):
@@ -224,8 +309,11 @@ def gate_all(n, d, seed, C, threads=8, log=print):
                 done.append(r["column"])
     finally:
         stop.set()
-    return {"what": "SURVEY.md §8(d) step-4 parity gate: device (production path) vs the reference's "
-                    "corrcoef/cholesky/solve_triangular/@P.T/rankdata on the device scores S",
+    what = ("SURVEY.md §8(d) step-4 parity gate: device (production path) vs the reference's "
+            + ("own steps 1-4: scipy ppf of the native quantiles, rankdata/(N+1), ndtri, corrcoef, cholesky, "
+               "solve_triangular, @P.T, rankdata" if scores == "reference" else
+               "corrcoef/cholesky/solve_triangular/@P.T/rankdata on the device scores S"))
+    return {"what": what, "scores": scores, **extra,
             "workload": f"cfg3 (cfg2 set x4), N={n}, d={d}, native LHS seed {seed}, "
                         "target C = 0.9 corrcoef(A) + 0.1 I",
             "rows": n, "d": d, "seed": seed,

@@ -304,3 +304,103 @@ def test_ext_generated_iman_conover(gpu, kind, n):
     NoOp(*ds).sample_from_quantiles(q)
     X = np.column_stack([x.samples_ for x in ds])
     np.testing.assert_array_equal(fast, iman_conover(X, C)["Y"])
+
+
+# round 5: geom, randint, nbinom (exact) and invgamma, t (1e-10 relative):
+# sampled, fused with the native LHS, and on the generated-column Iman-Conover path
+_R5_DISCRETE = [("geom", dict(p=0.3)), ("geom", dict(p=0.02, loc=3)), ("geom", dict(p=1.0)),
+                ("geom", dict(p=1e-6)), ("randint", dict(low=2, high=7)), ("randint", dict(low=-5, high=100, loc=1)),
+                ("randint", dict(low=0, high=1)), ("randint", dict(low=2.5, high=7)),
+                ("nbinom", dict(n=3.5, p=0.4)), ("nbinom", dict(n=20, p=0.9)),
+                ("nbinom", dict(n=0.5, p=0.05, loc=2)), ("nbinom", dict(n=5, p=1.0)), ("nbinom", dict(n=100, p=0.3))]
+_R5_CONT = [("invgamma", dict(a=2.5)), ("invgamma", dict(a=0.3, loc=1.0, scale=2.0)), ("invgamma", dict(a=60.0)),
+            ("t", dict(df=1.0)), ("t", dict(df=2.5, loc=1.0, scale=3.0)), ("t", dict(df=0.4)), ("t", dict(df=30.0)),
+            ("t", dict(df=1e4)), ("t", dict(df=3e7)), ("t", dict(df=np.inf)), ("t", dict(df=-1.0))]
+
+
+@pytest.mark.parametrize("name,kw", _R5_DISCRETE + _R5_CONT)
+def test_round5_distributions_ppf(gpu, name, kw):
+    """The round-5 names against scipy's ppf on random and edge quantiles; discrete exactly
+    (geom: numpy's log1p / expm1 ratio with scipy's one-step correction; randint: its closed
+    form; nbinom: Boost's smallest k with I_p(n, k + 1) >= q), continuous to 1e-10 (t: scipy's
+    stdtrit is cdflib's root search, itself within ~2.5e-11 of the quantile computed here)."""
+    import scipy.stats
+
+    from probabilit_amd import native
+
+    q = np.concatenate([_q(20_000, 9), [-0.5, 1.5, np.nan]])
+    with np.errstate(all="ignore"):
+        ref = getattr(scipy.stats, name)(**kw).ppf(q)
+    got = native.ppf(name, q, **kw)
+    if name in ("geom", "randint", "nbinom"):
+        np.testing.assert_array_equal(got, ref)
+    else:
+        assert_close(got, ref, rtol=1e-10, atol=1e-13, what=f"{name} {kw}")
+
+
+@pytest.mark.parametrize("name,kw", [c for c in _R5_DISCRETE + _R5_CONT if "2.5" not in str(c[1].get("low", ""))
+                                     and c[1].get("df", 1.0) > 0])
+def test_round5_fused_lhs(gpu, name, kw):
+    import scipy.stats
+
+    from probabilit_amd import native
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.qmc import seed_from
+
+    n, s = 30_000, 23
+    q = native.fill_lhs(seed_from(s), n, 1)[:, 0]
+    with np.errstate(all="ignore"):
+        ref = getattr(scipy.stats, name)(**kw).ppf(q)
+    got = D(name, **kw).sample(n, method="lhs", random_state=s)
+    if name in ("geom", "randint", "nbinom"):
+        np.testing.assert_array_equal(got, ref)
+    else:
+        assert_close(got, ref, rtol=1e-10, atol=1e-13, what=f"LHS {name} {kw}")
+
+
+def test_round5_composite_parameters(gpu):
+    """Per-row parameters (composite nodes, modeling.py:796-802) for every round-5 name."""
+    import scipy.stats
+
+    from probabilit_amd import native
+
+    n = 8_000
+    rng = np.random.default_rng(12)
+    q = rng.random(n)
+    p, a, df = 0.05 + 0.9 * rng.random(n), 0.5 + 5 * rng.random(n), 0.5 + 20 * rng.random(n)
+    low = np.floor(rng.uniform(-10, 10, n))
+    np.testing.assert_array_equal(native.ppf("geom", q, p=p), scipy.stats.geom(p).ppf(q))
+    np.testing.assert_array_equal(native.ppf("randint", q, low=low, high=low + 7), scipy.stats.randint(low, low + 7).ppf(q))
+    np.testing.assert_array_equal(native.ppf("nbinom", q, n=a, p=p), scipy.stats.nbinom(a, p).ppf(q))
+    assert_close(native.ppf("invgamma", q, a=a), scipy.stats.invgamma(a).ppf(q), what="composite invgamma")
+    assert_close(native.ppf("t", q, df=df), scipy.stats.t(df).ppf(q), what="composite t")
+
+
+def test_round5_generated_iman_conover(gpu):
+    """geom / randint / nbinom / invgamma / t correlated with method="lhs" take the generated-column
+    path (discrete ones with their run heads): bit-identical to the general path on the same
+    native quantiles, and equal to the oracle's Iman-Conover of the uncorrelated samples."""
+    from oracle.ic import iman_conover
+    from probabilit_amd import native
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.modeling import NoOp
+    from probabilit_amd.qmc import seed_from
+
+    def graph():
+        return [D("geom", p=0.3), D("randint", low=-3, high=40), D("nbinom", n=3.5, p=0.4), D("invgamma", a=2.5),
+                D("t", df=4.0, loc=1.0), D("norm")]
+
+    n, d = 40_000, 6
+    C = np.corrcoef(np.random.default_rng(d).normal(size=(d, d + 2)))
+    ds = graph()
+    root = NoOp(*ds).correlate(*ds, corr_mat=C)
+    root.sample(n, random_state=13, method="lhs")
+    fast = np.column_stack([x.samples_ for x in ds])
+    q = native.fill_lhs(seed_from(13), n, d)
+    root.sample_from_quantiles(q)
+    general = np.column_stack([x.samples_ for x in ds])
+    np.testing.assert_array_equal(fast, general)
+    ds = graph()
+    NoOp(*ds).sample_from_quantiles(q)
+    X = np.column_stack([x.samples_ for x in ds])
+    np.testing.assert_array_equal(fast, iman_conover(X, C)["Y"])

@@ -65,3 +65,28 @@ def test_cfg3_step4_mismatch_gate_1e8_all_columns(gpu):
     assert doc["violations_total"] == 0, [c for c in doc["columns"] if c["violations"]]
     # the gate's premise: the two CS agree to rounding
     assert doc["max_abs_cs_dev_minus_ref"] < 1e-12, doc["max_abs_cs_dev_minus_ref"]
+
+
+@pytest.mark.timeout(1200)
+def test_cfg3_step4_gate_1e8_reference_steps_1_2(gpu):
+    """The same gate with the reference's own steps 1-2: X = scipy ppf of the
+    native quantiles (modeling.py:807), S_ref = ndtri(rankdata(X) / (N + 1)) (correlation.py:394-
+    395), E_ref = np.corrcoef(S_ref), then cholesky / solve_triangular / @ P.T / rankdata on the
+    reference's arrays (:398-422), against the device's production indices on all 32 columns at
+    N = 1e8.  Every mismatch must be an adjacent-rank swap or exact tie with reference
+    |dCS| < 1e-13; the document (mismatches, their |dCS_ref|, the score and E differences) goes
+    to records/ (committed as profiles/r05/parity_1e8_ref_*.json)."""
+    import json
+
+    import scale_parity as sp
+
+    from conftest import record
+    from oracle.pipeline import cfg3_corr
+
+    doc = sp.gate_all(100_000_000, 32, 0, cfg3_corr(32), threads=16, scores="reference",
+                      log=lambda m: print(m if isinstance(m, str) else json.dumps(m), flush=True))
+    record("parity_1e8_reference_steps", doc)
+    assert all(c["decreases"] == 0 for c in doc["step1"]), doc["step1"]
+    assert doc["violations_total"] == 0, [c for c in doc["columns"] if c["violations"]]
+    assert doc["max_abs_s_dev_minus_ref"] < 1e-14, doc["max_abs_s_dev_minus_ref"]
+    assert doc["max_abs_cs_dev_minus_ref"] < 1e-12, doc["max_abs_cs_dev_minus_ref"]

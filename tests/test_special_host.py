@@ -367,3 +367,50 @@ def test_poisson_window_covers_scipy_deviations(sfh):
         assert np.all(ref[dev] == k[dev] - 1), mu
         hi = _call(sfh, "sfh_poisson_window_hi", mu, k[dev])
         assert np.all(q[dev] < hi), (mu, q[dev][q[dev] >= hi][:4])
+
+
+# ---- round 5 distributions on the host (pbh_special_ext.h), against scipy
+@pytest.mark.parametrize("p", [0.3, 0.01, 0.999, 1.0, 1e-6])
+def test_geom_ppf(sfh, p):
+    import scipy.stats as st
+
+    q = _quantiles()
+    q = q[(q > 0) & (q < 1)]
+    with np.errstate(divide="ignore"):
+        ref = st.geom(p).ppf(q)
+    np.testing.assert_array_equal(_call(sfh, "sfh_geom_ppf", p, q), ref)
+
+
+@pytest.mark.parametrize("low,high", [(2, 7), (-5, 100), (0, 1), (-1e6, 3e6)])
+def test_randint_ppf(sfh, low, high):
+    import scipy.stats as st
+
+    q = _quantiles()
+    q = q[(q > 0) & (q < 1)]
+    np.testing.assert_array_equal(_call(sfh, "sfh_randint_ppf", low, high, q), st.randint(low, high).ppf(q))
+
+
+@pytest.mark.parametrize("n,p", [(3.5, 0.4), (1, 0.5), (20, 0.9), (0.5, 0.05), (100, 0.3)])
+def test_nbinom_ppf(sfh, n, p):
+    import scipy.stats as st
+
+    q = np.random.default_rng(int(n * 10)).random(20000)
+    np.testing.assert_array_equal(_call(sfh, "sfh_nbinom_ppf", n, p, q), st.nbinom(n, p).ppf(q))
+
+
+@pytest.mark.parametrize("df", [0.5, 1.0, 2.5, 5.0, 30.0, 300.0, 1e4, 9e4, 1e5, 3e7, np.inf])
+def test_t_ppf(sfh, df):
+    import scipy.stats as st
+
+    rng = np.random.default_rng(3)
+    q = np.concatenate([rng.random(20000), 10.0 ** rng.uniform(-15, -1, 2000), 1 - 10.0 ** rng.uniform(-15, -1, 2000)])
+    np.testing.assert_allclose(_call(sfh, "sfh_t_ppf", df, q), st.t(df).ppf(q), rtol=1e-10)
+
+
+@pytest.mark.parametrize("a", [0.1, 1.0, 2.5, 30.0, 500.0])
+def test_invgamma_ppf(sfh, a):
+    import scipy.stats as st
+
+    q = _quantiles()
+    q = q[(q > 0) & (q < 1)]
+    np.testing.assert_allclose(_call(sfh, "sfh_invgamma_ppf", a, q), st.invgamma(a).ppf(q), rtol=1e-12)
