@@ -327,7 +327,7 @@ def pmc_valu(kernel):
 
 
 # the sweep kernel each cfg2 distribution takes (pbh_ppf.hip launch_ppf), for its VALU-busy figure
-SWEEP_KERNELS = {"norm": "k_ppf_c<0, true>", "lognorm": "k_ppf_c<3, true>", "gamma": "k_ppf_gamma_lds",
+SWEEP_KERNELS = {"norm": "k_ppf_c<0, true>", "lognorm": "k_ppf_c<3, true>", "gamma": "k_ppf_gamma_w<false>",
                  "poisson": "k_ppf_poisson_lds", "triang": "k_ppf_v<4>", "uniform": "k_ppf_v<1>",
                  "expon": "k_ppf_v<2>"}
 

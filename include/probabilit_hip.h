@@ -350,6 +350,13 @@ int pbh_ic_owned_column(pbh_ic_owned* h, int32_t i, const double* cs, double* y,
                         void* ready_event, void* done_event, void* stream);
 int pbh_ic_owned_finish(pbh_ic_owned* h, int32_t* redone_host, void* stream);
 int pbh_ic_owned_destroy(pbh_ic_owned* h, void* stream);
+/* Every uncorrelated native-LHS leaf of a graph in one call (the per-node loop of
+ * Node.sample_from_quantiles, modeling.py:529-538, for leaf Distributions with scalar parameters):
+ * column c of out (ld apart) = pbh_lhs_ppf of cols[c] over rows [row0, row0 + nrows); the columns'
+ * setups and kernels run side by side on internal streams, joined to `stream`.  nonfinite_flag and
+ * the params follow pbh_ic_column. */
+int pbh_lhs_ppf_columns(const pbh_ic_column* cols, int32_t k, int64_t n, int64_t row0, int64_t nrows, double* out,
+                        int64_t ld, void* stream);
 /* y[i * y_rs] = sort(X[:, column])[p[i]] for i < m: a generated column's value at sorted
  * positions p (the row owner's half of a row-sharded step 4: Y[r] = sort(X)[rank - 1],
  * correlation.py:423, p from the column's owner). */

@@ -53,7 +53,7 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_permcorr_climb", "pbh_sobol_ppf", "pbh_lhs_reference_workspace_size",
            "pbh_lhs_reference", "pbh_lhs_reference_perms", "pbh_hbm_copy", "pbh_dag_eval",
            "pbh_lhs_sorted_counts", "pbh_sort_heads", "pbh_ic_owned_workspace_size", "pbh_ic_owned_create",
-           "pbh_ic_owned_column", "pbh_ic_owned_finish", "pbh_lhs_values_at", "pbh_ic_owned_destroy", "pbh_event_create",
+           "pbh_ic_owned_column", "pbh_ic_owned_finish", "pbh_lhs_values_at", "pbh_lhs_ppf_columns", "pbh_ic_owned_destroy", "pbh_event_create",
            "pbh_event_destroy", "pbh_event_record", "pbh_stream_wait_event", "pbh_event_synchronize",
            "pbh_set_serial"]
 
@@ -187,6 +187,7 @@ def load():
         "pbh_ic_owned_create": ([ctypes.POINTER(ICColumn), ctypes.c_int32, i64, vp, sz, ctypes.POINTER(vp), vp], i32),
         "pbh_ic_owned_column": ([vp, ctypes.c_int32, vp, vp, i64, vp, vp, vp, vp], i32),
         "pbh_lhs_values_at": ([ctypes.POINTER(ICColumn), i64, vp, i64, vp, i64, vp], i32),
+        "pbh_lhs_ppf_columns": ([ctypes.POINTER(ICColumn), i32, i64, i64, i64, vp, i64, vp], i32),
         "pbh_ic_owned_finish": ([vp, vp, vp], i32),
         "pbh_ic_owned_destroy": ([vp, vp], i32),
         "pbh_event_create": ([ctypes.POINTER(vp)], i32),

@@ -12,6 +12,7 @@
 #include <stdlib.h>
 
 #include <type_traits>
+#include <vector>
 
 #include "pbh_error.h"
 #include "pbh_ppf_core.h"
@@ -1035,6 +1036,195 @@ __global__ __launch_bounds__(256) void k_place_gen_gamma_slow(const uint64_t* __
   }
 }
 
+// ---------------------------------------------------------------- gamma sweep on a guide window
+// (round 5) k_ppf_gamma_lds stages the whole 120 KiB guide, so one 1024-thread workgroup runs per
+// CU, with two block barriers per 4096-item tile around its LDS slow queue and igami's iteration
+// inline (128 VGPRs with spills): latency-bound (wave_active 0.28).  These kernels stage the window
+// of the guide that quantiles in [2.3e-9, 1 - 2.3e-9] reach (|w| <= 19.9: 1275 nodes, 40 KiB, as
+// the step-4 placement does), take no barrier after the staging, and append every item the window
+// cannot interpolate (a quantile beyond the window, an interval without the midpoint check, q at 0
+// or 1, invalid parameters) to a global list, one atomic per wave; k_ppf_gamma_slow then evaluates
+// the list with ppf_one and the global table -- the same function and values as gamma_ppf_lds, so
+// every value is bit-identical -- or every row when the list overflowed.
+constexpr double kGSweepW = 19.9;
+#ifndef PBH_GSWEEP_PER
+#define PBH_GSWEEP_PER 4
+#endif
+#ifndef PBH_GSWEEP_BLOCK
+#define PBH_GSWEEP_BLOCK 512
+#endif
+#ifndef PBH_GSWEEP_WAVES
+#define PBH_GSWEEP_WAVES 6
+#endif
+constexpr int kGSweepPer = PBH_GSWEEP_PER;  // items per thread per tile, their quantiles loaded a tile ahead
+constexpr int kGSBlock = PBH_GSWEEP_BLOCK;  // 512: three workgroups per CU (46 KiB of LDS each), 80 VGPRs
+
+struct GammaLhs {  // the fused native-LHS column (LHS = true): quantile of row row0 + i
+  uint64_t seed;
+  int64_t n, row0;
+  uint32_t col;
+};
+
+template <bool LHS>
+__global__ __launch_bounds__(kGSBlock) __attribute__((amdgpu_waves_per_eu(PBH_GSWEEP_WAVES))) void k_ppf_gamma_w(
+    const double* __restrict__ q, int64_t q_stride, int64_t n, GammaLhs lc, Params prm, PoissonTable pt,
+    double* __restrict__ out, int32_t* flag, int j0, int jn, unsigned long long* __restrict__ slow, uint32_t cap) {
+  __shared__ double win[4 * kGWin];  // y, d1, d2, ok of nodes j0 .. j0 + jn - 1
+  __shared__ double ltab_s[kLogTabN], etab_s[kExpTabN];
+  double *ltab = ltab_s, *etab = etab_s;
+  stage_logexp(ltab, etab);
+  const sf::GammaGuide& G = pt.guide;
+  for (int k = threadIdx.x; k < 4 * jn; k += kGSBlock) {
+    const int a = k / jn, i = k - a * jn;
+    win[a * kGWin + i] = G.y[(int64_t)a * G.m + j0 + i];  // the four global arrays are contiguous
+  }
+  __syncthreads();
+  Philox ph(lc.seed);
+  FeistelPerm fp(ph, (uint64_t)(LHS ? lc.n : 1), lc.col);
+  const double shape = prm.val[0], loc = prm.val[1], scale = prm.val[2];
+  const bool cond0 = (shape > 0.0) && (scale > 0.0) && (loc == loc) && pt.has_gamma;
+  constexpr int kTile = kGSweepPer * kGSBlock;
+  const int64_t step = (int64_t)gridDim.x * kTile;
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  auto quantile = [&](int64_t i) -> double {
+    if constexpr (LHS)
+      return lhs_quantile(ph, fp, (uint64_t)(lc.row0 + i), lc.col);
+    else
+      return q[i * q_stride];
+  };
+  double qn[kGSweepPer];
+  if constexpr (!LHS) {
+#pragma unroll
+    for (int j = 0; j < kGSweepPer; ++j) {
+      const int64_t i = (int64_t)blockIdx.x * kTile + j * kGSBlock + threadIdx.x;
+      qn[j] = i < n ? q[i * q_stride] : 0.5;
+    }
+  }
+  bool bad = false;
+  for (int64_t base = (int64_t)blockIdx.x * kTile; base < n; base += step) {
+    double qv[kGSweepPer];
+#pragma unroll
+    for (int j = 0; j < kGSweepPer; ++j) {
+      if constexpr (LHS) {
+        const int64_t i = base + j * kGSBlock + threadIdx.x;
+        qv[j] = i < n ? quantile(i) : 0.5;
+      } else {
+        qv[j] = qn[j];
+        const int64_t i = base + step + j * kGSBlock + threadIdx.x;
+        qn[j] = i < n ? q[i * q_stride] : 0.5;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kGSweepPer; ++j) {
+      const int64_t i = base + j * kGSBlock + threadIdx.x;
+      const bool valid = i < n;
+      const double qq = qv[j];
+      // igami_guided's interpolation branch and ppf_one's gamma wrapper, operation for operation
+      bool fast = valid && cond0 && qq > 0.0 && qq < 1.0;
+      double v = 0.0;
+      if (fast) {
+        const double w = sf::log_odds_at(qq, ltab);
+        const double u = (w - G.z0) * G.inv_h;
+        fast = u >= 0.0 && u < (double)(G.m - 1);
+        if (fast) {
+          const int jj = (int)u;
+          const int jl = jj - j0;
+          fast = jl >= 0 && jl < jn - 1;
+          if (fast) {
+            const double yy = sf::guide_interp_arr(win, win + kGWin, win + 2 * kGWin, G.h, jl, u - (double)jj);
+            fast = yy >= -680.0 && yy <= 700.0 && win[3 * kGWin + jl] != 0.0;
+            if (fast) v = sf::exp_tab_at(yy, etab) * scale + loc;
+          }
+        }
+      }
+      if (fast) {
+        out[i] = v;
+        bad |= !isfinite(v);
+      }
+      const bool sl = valid && !fast;
+      const uint64_t m = __ballot(sl);
+      if (m) {  // wave-uniform
+        const int leader = __builtin_ctzll(m);
+        unsigned long long b0 = 0;
+        if (lane == leader) b0 = atomicAdd(&slow[0], (unsigned long long)__popcll(m));
+        b0 = __shfl(b0, leader, 64);
+        const unsigned long long k = b0 + (unsigned long long)__popcll(m & below);
+        if (sl && k < cap) slow[1 + k] = (unsigned long long)i;
+      }
+    }
+  }
+  flag_nonfinite(flag, bad);
+}
+
+template <bool LHS>
+__global__ __launch_bounds__(256) void k_ppf_gamma_slow(const double* __restrict__ q, int64_t q_stride, int64_t n,
+                                                        GammaLhs lc, Params prm, PoissonTable pt,
+                                                        double* __restrict__ out, int32_t* flag,
+                                                        const unsigned long long* __restrict__ slow, uint32_t cap) {
+  const unsigned long long count = slow[0];
+  if (count == 0) return;
+  const bool all = count > cap;
+  const int64_t m = all ? n : (int64_t)count;
+  Philox ph(lc.seed);
+  FeistelPerm fp(ph, (uint64_t)(LHS ? lc.n : 1), lc.col);
+  bool bad = false;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < m; k += (int64_t)gridDim.x * 256) {
+    const int64_t i = all ? k : (int64_t)slow[1 + k];
+    double qi;
+    if constexpr (LHS)
+      qi = lhs_quantile(ph, fp, (uint64_t)(lc.row0 + i), lc.col);
+    else
+      qi = q[i * q_stride];
+    const double x = ppf_one<PBH_DIST_GAMMA>(qi, prm.val[0], prm.val[1], prm.val[2], pt);
+    out[i] = x;
+    bad |= !isfinite(x);
+  }
+  flag_nonfinite(flag, bad);
+}
+
+// The windowed gamma sweep (pbh_ppf / pbh_lhs_ppf with scalar a, loc, scale): false when it does not
+// apply (PBH_GAMMA_WIN=0, no guide, a window wider than kGWin)
+bool launch_gamma_w(const double* q, int64_t qs, int64_t n, const GammaLhs* lc, const Params& prm,
+                    const PoissonTable& pt, double* out, int32_t* flag, hipStream_t s, int* status) {
+  int j0 = 0, jn = 0;
+  *status = PBH_OK;
+  if (!gamma_win_on() || !gamma_window_w(kGSweepW, pt.guide, kGWin, &j0, &jn)) return false;
+  if (n <= 0) return true;
+  const uint32_t cap = (uint32_t)((n >> 8) + 4096 < (1u << 30) ? (n >> 8) + 4096 : (1u << 30));
+  unsigned long long* slow = nullptr;
+  if (hipMallocAsync((void**)&slow, ((size_t)cap + 1) * 8, s) != hipSuccess) {
+    *status = PBH_ERR_HIP;
+    set_error("pbh_ppf: hipMallocAsync of the gamma slow list failed");
+    return true;
+  }
+  if (hipMemsetAsync(slow, 0, 8, s) != hipSuccess) {
+    (void)hipFreeAsync(slow, s);
+    *status = PBH_ERR_HIP;
+    set_error("pbh_ppf: hipMemsetAsync failed");
+    return true;
+  }
+  const GammaLhs l = lc ? *lc : GammaLhs{0, 1, 0, 0};
+  const unsigned gw = grid_for(n, kGSweepPer * kGSBlock, 256 * 3 * 512 / kGSBlock), gs = 256 * 4;
+  if (lc) {
+    PBH_TIMED(kKLhsPpf, s, {
+      hipLaunchKernelGGL(k_ppf_gamma_w<true>, dim3(gw), dim3(kGSBlock), 0, s, q, qs, n, l, prm, pt, out, flag, j0, jn,
+                         slow, cap);
+      hipLaunchKernelGGL(k_ppf_gamma_slow<true>, dim3(gs), dim3(256), 0, s, q, qs, n, l, prm, pt, out, flag, slow, cap);
+    });
+  } else {
+    PBH_TIMED(kKPpf, s, {
+      hipLaunchKernelGGL(k_ppf_gamma_w<false>, dim3(gw), dim3(kGSBlock), 0, s, q, qs, n, l, prm, pt, out, flag, j0,
+                         jn, slow, cap);
+      hipLaunchKernelGGL(k_ppf_gamma_slow<false>, dim3(gs), dim3(256), 0, s, q, qs, n, l, prm, pt, out, flag, slow,
+                         cap);
+    });
+  }
+  if (hipGetLastError() != hipSuccess) *status = PBH_ERR_HIP;
+  (void)hipFreeAsync(slow, s);  // stream-ordered: after the slow kernel
+  return true;
+}
+
 // poisson with the CDF table + guide in (dynamic) LDS
 template <bool BYROW = false>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_poisson(const uint64_t* __restrict__ pairs,
@@ -1503,6 +1693,8 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
                           ((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0 && stream_enabled();
   dim3 gv(grid_for(n, kVTile, 256 * 8));
   if (gamma_lds_ok(dist, prm, pt)) {
+    int st = PBH_OK;
+    if (launch_gamma_w(q, qs, n, nullptr, prm, pt, out, flag, s, &st)) return st;
     PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_gamma_lds, dim3(gamma_lds_grid(n)), dim3(kGBlock), 0, s, q, qs, n,
                                            prm, pt, out, flag));
     PBH_CHECK_LAUNCH();
@@ -1546,6 +1738,9 @@ int launch_lhs_ppf(int dist, uint64_t seed, int64_t n, int64_t row0, int64_t nro
                    const Params& prm, const PoissonTable& pt, double* out, int32_t* flag, hipStream_t s) {
   dim3 g(ppf_grid(nrows)), b(kBlock);
   if (gamma_lds_ok(dist, prm, pt)) {
+    int st = PBH_OK;
+    const GammaLhs lc{seed, n, row0, col};
+    if (launch_gamma_w(nullptr, 0, nrows, &lc, prm, pt, out, flag, s, &st)) return st;
     PBH_TIMED(kKLhsPpf, s, hipLaunchKernelGGL(k_lhs_ppf_gamma_lds, dim3(gamma_lds_grid(nrows)), dim3(kGBlock), 0, s,
                                               seed, n, row0, nrows, col, prm, pt, out, flag));
     PBH_CHECK_LAUNCH();
@@ -1661,6 +1856,21 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
 }
 
 }  // namespace
+
+// The gamma guide of shape a in a fresh stream-ordered allocation (4 x kGammaGuideM doubles: y, d1,
+// d2, ok; the layout with_params builds for gamma), for the extended distributions whose ppf is
+// gammaincinv (chi, maxwell, nakagami, chi2: pbh_ppf_ext.hip).  NULL for an invalid a.
+double* gamma_guide_table(double a, hipStream_t s) {
+  if (!(a > 0.0 && isfinite(a))) return nullptr;
+  const int m = sf::kGammaGuideM;
+  double* tb = nullptr;
+  if (hipMallocAsync((void**)&tb, (size_t)4 * m * sizeof(double), s) != hipSuccess) return nullptr;
+  sf::GammaGuide T{tb, tb + m, tb + 2 * m, tb + 3 * m, m, sf::kGammaGuideZ0, sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
+  const unsigned g = (unsigned)((m + 63) / 64);
+  hipLaunchKernelGGL(k_gamma_guide, dim3(g), dim3(64), 0, s, a, T, tb, tb + m, tb + 2 * m);
+  hipLaunchKernelGGL(k_gamma_guide_check, dim3(g), dim3(64), 0, s, a, T, tb + 3 * m);
+  return tb;
+}
 
 struct GenColumn {
   uint64_t seed;
@@ -2250,6 +2460,56 @@ extern "C" int pbh_lhs_ppf(uint64_t seed, int64_t n, int64_t row0, int64_t nrows
   st = launch_lhs_ppf(dist, seed, n, row0, nrows, (uint32_t)col, prm, pt, out, nonfinite_flag, s);
   if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));
   return st;
+}
+
+// Every column of a graph's uncorrelated native-LHS leaves in one call (round 5, cfg2): each
+// column's inverse-CDF setup (gamma guide, poisson / binom CDF tables, beta guide: latency-bound
+// kernels of 10-100 us) and its fused LHS + ppf kernel run on one of the step-4 lanes' streams,
+// so the columns' setups overlap one another instead of queueing on the caller's stream; the
+// caller's stream then waits for every lane.  Values are the per-column pbh_lhs_ppf's, bit for bit.
+extern "C" int pbh_lhs_ppf_columns(const pbh_ic_column* cols, int32_t k, int64_t n, int64_t row0, int64_t nrows,
+                                   double* out, int64_t ld, void* stream) {
+  PBH_REQUIRE(cols && k >= 1 && n >= 1 && row0 >= 0 && nrows >= 0 && row0 + nrows <= n && out && ld >= nrows,
+              "pbh_lhs_ppf_columns: bad arguments");
+  if (nrows == 0) return PBH_OK;
+  hipStream_t s = as_stream(stream);
+  const int nts = step4_streams();  // 1 in the serial measurement mode
+  hipStream_t ts[kStep4MaxStreams];
+  std::vector<hipEvent_t> ev;
+  struct Cleanup {
+    std::vector<hipEvent_t>& v;
+    bool joined = false;
+    ~Cleanup() {
+      if (!joined) step4_sync_side_streams();  // an error return: no lane may still read a table
+      for (hipEvent_t e : v) (void)hipEventDestroy(e);
+    }
+  } cleanup{ev};
+  auto order = [&](hipStream_t from, hipStream_t to) -> int {
+    if (from == to) return PBH_OK;
+    hipEvent_t e = nullptr;
+    PBH_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev.push_back(e);
+    PBH_CHECK_HIP(hipEventRecord(e, from));
+    PBH_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
+    return PBH_OK;
+  };
+  const int nl = nts < k ? nts : k;
+  for (int i = 0; i < nl; ++i) {
+    ts[i] = nl > 1 ? step4_side_stream(i) : s;
+    if (!ts[i]) ts[i] = s;
+    if (int st = order(s, ts[i])) return st;
+  }
+  for (int c = 0; c < k; ++c) {
+    pbh_param prm[4];
+    for (int j = 0; j < 4; ++j) prm[j] = pbh_param{nullptr, cols[c].params[j]};
+    if (int st = pbh_lhs_ppf(cols[c].seed, n, row0, nrows, cols[c].lhs_col, cols[c].dist, prm, cols[c].nparams,
+                             out + (int64_t)c * ld, cols[c].nonfinite_flag, ts[c % nl]))
+      return st;
+  }
+  for (int i = 0; i < nl; ++i)
+    if (int st = order(ts[i], s)) return st;
+  cleanup.joined = true;
+  return PBH_OK;
 }
 
 extern "C" int pbh_fill_lhs(uint64_t seed, int64_t n, int64_t row0, int64_t nrows, int col0, int ncols,

@@ -28,6 +28,8 @@ int ext_gen_place(uint64_t seed, int64_t n, uint32_t col, int dist, const double
 // a column's setup table (stream-ordered allocation, freed with hipFreeAsync; NULL when none):
 // beta with scalar (a, b) -> its guide (sfx::BetaGuide)
 double* ext_gen_table(int dist, const double* val, int np, hipStream_t s);
+// pbh_ppf.hip: the gamma guide of shape a (4 x sf::kGammaGuideM doubles), stream-ordered allocation
+double* gamma_guide_table(double a, hipStream_t s);
 // the certificate's exact evaluation of the listed pairs (see k_cert_scan / k_cert_eval, pbh_ppf.hip)
 int ext_gen_cert_eval(uint64_t seed, int64_t n, uint32_t col, int dist, const double* val, const double* table,
                       int64_t t0, int64_t nt, const uint32_t* list, uint32_t cap, const uint32_t* count, int32_t* flag,

@@ -33,8 +33,55 @@ struct Params4 {
   const double* ptr[4];
   double val[4];
   sfx::BetaGuide bg;  // beta with scalar (a, b): the guide table (bg.z == NULL: none)
+  sf::GammaGuide gg;  // chi, maxwell, nakagami, chi2 with a scalar shape: gammaincinv's guide (gg.y == NULL: none)
+  sf::GammaAux ga;
+  const double* dt;   // binom, bernoulli, nbinom with scalar parameters: CDF (dt) and its complement
+  int dlen;           // (dt + dlen) of k = 0 .. dlen - 1 (dt == NULL: none)
   __device__ __forceinline__ double at(int j, int64_t i) const { return ptr[j] ? ptr[j][i] : val[j]; }
 };
+
+// the CDF tables of a scalar-parameter discrete distribution: cdf[k] and its complement for
+// k = 0 .. len - 1, by the same functions the per-draw search evaluates (so every lookup answers
+// what that search would)
+template <int D>
+__global__ void k_discrete_table(double s0, double s1, int len, double* __restrict__ cdf, double* __restrict__ ccdf) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= len) return;
+  if constexpr (D == PBH_DIST_NBINOM) {
+    cdf[k] = sfx::nbdtr((double)k, s0, s1);
+    ccdf[k] = sfx::nbdtrc((double)k, s0, s1);
+  } else {  // binom (n, p); bernoulli is binom with n = 1
+    const double n = D == PBH_DIST_BINOM ? s0 : 1.0, pp = D == PBH_DIST_BINOM ? s1 : s0;
+    cdf[k] = sfx::bdtr((double)k, n, pp);
+    ccdf[k] = sfx::bdtrc((double)k, n, pp);
+  }
+}
+
+// binom_ppf01 / nbinom_ppf01 from the tables: below the median the first k with cdf[k] >= q, above
+// it the first k with ccdf[k] <= 1 - q (binary searches); -1 when the answer lies past the table
+__device__ __forceinline__ double discrete_from_table(double q, const double* cdf, int len) {
+  const double* ccdf = cdf + len;
+  int lo = 0, hi = len;  // first index in [lo, hi) satisfying the predicate
+  if (q <= 0.5) {
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cdf[mid] >= q)
+        hi = mid;
+      else
+        lo = mid + 1;
+    }
+  } else {
+    const double r = 1.0 - q;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (ccdf[mid] <= r)
+        hi = mid;
+      else
+        lo = mid + 1;
+    }
+  }
+  return lo < len ? (double)lo : -1.0;
+}
 
 // the beta guide for scalar (a, b) (sfx::BetaGuide): nodes, then the midpoint check
 __global__ void k_beta_guide(double a, double b, double lb, double* z, double* d1, double* d2) {
@@ -47,9 +94,68 @@ __global__ void k_beta_guide_check(double a, double b, sfx::BetaGuide T, double*
   if (j < sfx::kBetaGuideM) ok[j] = j < sfx::kBetaGuideM - 1 ? sfx::beta_guide_check(a, b, T, j) : 0.0;
 }
 
+constexpr int kDiscreteTableMax = 1 << 16;  // CDF entries of a discrete distribution's table
+
+// the shape a of gammaincinv(a, q) behind chi (df / 2), maxwell (1.5), nakagami (nu), chi2 (df / 2)
+inline double gamma_family_a(int dist, double s0) {
+  return dist == PBH_DIST_MAXWELL ? 1.5 : dist == PBH_DIST_NAKAGAMI ? s0 : 0.5 * s0;
+}
+constexpr bool is_gamma_family(int d) {
+  return d == PBH_DIST_CHI || d == PBH_DIST_MAXWELL || d == PBH_DIST_NAKAGAMI || d == PBH_DIST_CHI2;
+}
+
+// the discrete table's length for scalar parameters (0: none): every k up to the answer at the
+// largest quantile below 1 for binom / bernoulli (n + 1 values), and for nbinom up to its answer at
+// q = 1 - 2^-40 (the rare q beyond take the per-draw search)
+int discrete_table_len(int dist, const double* v) {
+  if (dist == PBH_DIST_BINOM) {
+    if (!(v[0] >= 0.0 && v[0] == floor(v[0]) && v[1] >= 0.0 && v[1] <= 1.0 && v[0] + 1.0 <= kDiscreteTableMax)) return 0;
+    return (int)v[0] + 1;
+  }
+  if (dist == PBH_DIST_BERNOULLI) return (v[0] >= 0.0 && v[0] <= 1.0) ? 2 : 0;
+  if (dist == PBH_DIST_NBINOM) {
+    if (!(v[0] > 0.0 && v[1] > 0.0 && v[1] < 1.0 && v[0] < 1e6 && v[1] > 1e-4)) return 0;
+    const double top = sfx::nbinom_ppf01(1.0 - 0x1p-40, v[0], v[1]);
+    return top + 1.0 <= kDiscreteTableMax ? (int)top + 1 : 0;
+  }
+  return 0;
+}
+
 // the setup table of `dist` with these parameters (stream-ordered allocation, NULL when the
-// distribution has none): beta with scalar, valid (a, b) -> its guide
+// distribution has none): beta with scalar, valid (a, b) -> its guide; chi / maxwell / nakagami /
+// chi2 with a scalar shape -> gammaincinv's guide (pbh_ppf.hip gamma_guide_table); binom /
+// bernoulli / nbinom with scalar parameters -> [len, CDF (len), complement (len)]
 double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t s) {
+  if (is_gamma_family(dist)) {
+    if (dist != PBH_DIST_MAXWELL && (nparams < 1 || params[0].ptr)) return nullptr;
+    return gamma_guide_table(gamma_family_a(dist, nparams ? params[0].value : 0.0), s);
+  }
+  if (dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_NBINOM) {
+    const int ns = dist == PBH_DIST_BERNOULLI ? 1 : 2;
+    if (nparams < ns) return nullptr;
+    double v[2] = {0.0, 0.0};
+    for (int j = 0; j < ns; ++j) {
+      if (params[j].ptr) return nullptr;
+      v[j] = params[j].value;
+    }
+    const int len = discrete_table_len(dist, v);
+    if (len <= 0) return nullptr;
+    double* t = nullptr;
+    if (hipMallocAsync((void**)&t, (size_t)(2 * len + 1) * sizeof(double), s) != hipSuccess) return nullptr;
+    const double hdr = (double)len;
+    if (hipMemcpyAsync(t, &hdr, sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess) {
+      (void)hipFreeAsync(t, s);
+      return nullptr;
+    }
+    const dim3 g((unsigned)((len + 255) / 256)), b(256);
+    if (dist == PBH_DIST_BINOM)
+      hipLaunchKernelGGL(k_discrete_table<PBH_DIST_BINOM>, g, b, 0, s, v[0], v[1], len, t + 1, t + 1 + len);
+    else if (dist == PBH_DIST_BERNOULLI)
+      hipLaunchKernelGGL(k_discrete_table<PBH_DIST_BERNOULLI>, g, b, 0, s, v[0], v[1], len, t + 1, t + 1 + len);
+    else
+      hipLaunchKernelGGL(k_discrete_table<PBH_DIST_NBINOM>, g, b, 0, s, v[0], v[1], len, t + 1, t + 1 + len);
+    return t;
+  }
   if (dist != PBH_DIST_BETA || nparams < 2 || params[0].ptr || params[1].ptr) return nullptr;
   const double a = params[0].value, b = params[1].value;
   if (!(a > 0.0 && b > 0.0 && isfinite(a) && isfinite(b))) return nullptr;
@@ -66,6 +172,24 @@ double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t 
 sfx::BetaGuide guide_of(const double* t) {
   constexpr int m = sfx::kBetaGuideM;
   return t ? sfx::BetaGuide{t, t + m, t + 2 * m, t + 3 * m} : sfx::BetaGuide{};
+}
+
+// Params4's view of build_table's table for `dist` (scalar parameters p.val)
+void attach_table(int dist, const double* t, Params4& p) {
+  if (!t) return;
+  if (dist == PBH_DIST_BETA) {
+    p.bg = guide_of(t);
+  } else if (is_gamma_family(dist)) {
+    const int m = sf::kGammaGuideM;
+    const double a = gamma_family_a(dist, p.val[0]);
+    p.gg = sf::GammaGuide{t, t + m, t + 2 * m, t + 3 * m, m, sf::kGammaGuideZ0, sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
+    p.ga = sf::gamma_aux(a);
+  } else if (dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_NBINOM) {
+    const int ns = dist == PBH_DIST_BERNOULLI ? 1 : 2;
+    p.dlen = discrete_table_len(dist, p.val);  // the same length the table was built with
+    p.dt = p.dlen > 0 ? t + 1 : nullptr;
+    (void)ns;
+  }
 }
 
 constexpr bool is_closed(int d) {
@@ -263,6 +387,10 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
     if (q == 0.0) return -1.0 + loc;  // rv_discrete.ppf places _a - 1 + loc at q == 0 whatever the args
     if (!ok || !(q >= 0.0 && q <= 1.0)) return nan;
     if (q == 1.0) return n + loc;
+    if (p.dt) {  // scalar (n, p): the CDF tables
+      const double k = discrete_from_table(q, p.dt, p.dlen);
+      if (k >= 0.0) return k + loc;
+    }
     return sfx::binom_ppf01(q, n, pp) + loc;
   } else if constexpr (is_discrete2(D)) {
     // rv_discrete.ppf: q == 0 -> _a - 1 + loc whatever the arguments, q == 1 -> _b + loc for valid
@@ -286,6 +414,10 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
       if (q == 0.0) return -1.0 + loc;
       if (!(n > 0.0 && pp > 0.0 && pp <= 1.0 && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
       if (q == 1.0) return inf + loc;
+      if (p.dt) {
+        const double k = discrete_from_table(q, p.dt, p.dlen);
+        if (k >= 0.0) return k + loc;
+      }
       return sfx::nbinom_ppf01(q, n, pp) + loc;
     }
   } else if constexpr (is_closed(D)) {
@@ -297,6 +429,20 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
     if (!ok || !(q >= 0.0 && q <= 1.0)) return nan;
     if (q == 0.0) return lo * scale + loc;
     if (q == 1.0) return hi * scale + loc;
+    if constexpr (is_gamma_family(D)) {
+      if (p.gg.y) {  // gammaincinv through the guide (igami_guided: within ~1e-12 of igami)
+        const double g = sf::igami_guided(D == PBH_DIST_MAXWELL ? 1.5 : D == PBH_DIST_NAKAGAMI ? s0 : .5 * s0, q,
+                                          &p.ga, p.gg);
+        double x;
+        if constexpr (D == PBH_DIST_CHI2)
+          x = 2.0 * g;
+        else if constexpr (D == PBH_DIST_NAKAGAMI)
+          x = sqrt(1.0 / s0 * g);
+        else
+          x = sqrt(2 * g);
+        return x * scale + loc;
+      }
+    }
     return closed_ppf01<D>(q, s0, s1) * scale + loc;
   } else {
     const double a = p.at(0, i), b = p.at(1, i), loc = p.at(2, i), scale = p.at(3, i);
@@ -429,7 +575,7 @@ int launch_ext(int dist, const double* q, int64_t q_stride, const LhsCol* lc, in
   }
   if (n == 0) return PBH_OK;
   double* table = build_table(dist, params, nparams, s);
-  prm.bg = guide_of(table);
+  attach_table(dist, table, prm);
   dim3 g(grid_for(n, 256, 16384)), b(256);
   const LhsCol l = lc ? *lc : LhsCol{0, 1, 0, 0};
   const bool known = dispatch_ext(dist, [&](auto tag) {
@@ -651,10 +797,10 @@ __global__ __launch_bounds__(256) void k_ext_cert_eval(uint64_t seed, int64_t n,
   }
 }
 
-Params4 scalar_params(const double* val, int np, const double* table) {
+Params4 scalar_params(int dist, const double* val, int np, const double* table) {
   Params4 p{};
   for (int j = 0; j < 4; ++j) p.val[j] = j < np ? val[j] : 0.0;
-  p.bg = guide_of(table);
+  attach_table(dist, table, p);
   return p;
 }
 
@@ -713,7 +859,7 @@ int ext_gen_sorted(uint64_t seed, int64_t n, uint32_t col, int dist, const doubl
   const int np = ext_nparams(dist);
   PBH_REQUIRE(np >= 0, "ext_gen_sorted: distribution %d is not an extended one", dist);
   if (nt == 0) return PBH_OK;
-  const Params4 prm = scalar_params(val, np, table);
+  const Params4 prm = scalar_params(dist, val, np, table);
   // binom / bernoulli, counts and heads only: the binary-search heads when the values are integers
   // (an integer loc) spanning few of them (n + 1 at most); any other column (a non-integer loc
   // moves every value off the integers) takes k_ext_sorted, which counts exactly
@@ -751,7 +897,7 @@ int ext_gen_place(uint64_t seed, int64_t n, uint32_t col, int dist, const double
   PBH_REQUIRE(np >= 0, "ext_gen_place: distribution %d is not an extended one", dist);
   const int64_t blocks = (rows + kExtGenRows - 1) / kExtGenRows;
   if (blocks <= 0) return PBH_OK;
-  const Params4 prm = scalar_params(val, np, table);
+  const Params4 prm = scalar_params(dist, val, np, table);
   const dim3 g((unsigned)(blocks < 256 * 8 ? blocks : 256 * 8)), b(256);
   dispatch_ext(dist, [&](auto tag) {
     constexpr int D = decltype(tag)::value;
@@ -772,7 +918,7 @@ int ext_gen_cert_eval(uint64_t seed, int64_t n, uint32_t col, int dist, const do
                       unsigned long long* counts, hipStream_t s) {
   const int np = ext_nparams(dist);
   PBH_REQUIRE(np >= 0, "ext_gen_cert_eval: distribution %d is not an extended one", dist);
-  const Params4 prm = scalar_params(val, np, table);
+  const Params4 prm = scalar_params(dist, val, np, table);
   dispatch_ext(dist, [&](auto tag) {
     constexpr int D = decltype(tag)::value;
     PBH_TIMED(kKLhsSorted, s,

@@ -434,17 +434,46 @@ class Node(abc.ABC):
         # a graph of leaf draws, constants and float64 transforms runs as one kernel
         fused = not correlations and dag.try_evaluate(list(nx.topological_sort(G)), isns, source, ev, gc)
         if not fused:
+            # the ISNs' quantile columns in the reference's order (:529-538); native-LHS leaves with
+            # plain-number parameters are then drawn together by one call (pbh_lhs_ppf_columns: their
+            # inverse-CDF setups overlap), the rest one by one
+            columns = {node: source.next_column() for node in isns}
+            group = []
+            if isinstance(source, qmc.LHSSource):
+                group = [node for node in isns
+                         if type(node) is Distribution and node.is_leaf and node.distr in _FUSED_LHS
+                         and not (generated and node in all_set) and node not in block_row
+                         and all(not isinstance(v, Node) and np.ndim(v) == 0
+                                 for v in _parse_scipy_args(node.distr, node.args, node.kwargs))]
+            if len(group) >= 2:
+                group = [(node, node._params(size)) for node in group]
+                cols = []
+                for node, params in group:
+                    _, seed, n_total, col, row0 = columns[node]
+                    cols.append(_lib.ICColumn(seed, col, _lib.DIST_IDS[node.distr],
+                                              (ctypes.c_double * 4)(*(params + [0.0] * (4 - len(params)))),
+                                              len(params), ev.flag_ptr(node)))
+                gblock = device.empty((len(group), size))
+                arr = (_lib.ICColumn * len(cols))(*cols)
+                _lib.check(_lib.load().pbh_lhs_ppf_columns(arr, len(cols), source.n, source.row0, size,
+                                                           gblock.data_ptr(), size, device.stream()),
+                           "pbh_lhs_ppf_columns")
+                for j, (node, _) in enumerate(group):
+                    node._set_device(gblock[j])
+            grouped = {node for node, _ in group} if len(group) >= 2 else ()
             for node in isns:  # (:529-538)
+                if node in grouped:
+                    continue
                 if not node.is_leaf:  # (a leaf has no ancestors to sample)
                     for anc in nx.topological_sort(G.subgraph(nx.ancestors(G, node))):
                         assert isinstance(anc, (Constant, Transform))
                         anc._set_device(anc._sample_device(ev))
                 assert isinstance(node, AbstractDistribution)
                 if generated and node in all_set:
-                    deferred[node] = source.next_column()
+                    deferred[node] = columns[node]
                     continue
                 out = block[block_row[node]] if node in block_row else None
-                node._set_device(node._sample_device(ev, source.next_column(), out=out))
+                node._set_device(node._sample_device(ev, columns[node], out=out))
 
             for variables, _ in correlations:  # (:548-551)
                 for variable in variables:

@@ -415,3 +415,26 @@ def test_round5_generated_iman_conover(gpu):
     NoOp(*ds).sample_from_quantiles(q)
     X = np.column_stack([x.samples_ for x in ds])
     np.testing.assert_array_equal(fast, iman_conover(X, C)["Y"])
+
+
+def test_grouped_lhs_columns(gpu):
+    """Uncorrelated native-LHS leaves outside the fused DAG kernel (an extended name in the
+    graph) are drawn by one pbh_lhs_ppf_columns call, their table/guide setups spread over the
+    step-4 lanes' streams: every column bit-identical to its own pbh_lhs_ppf (column index = the
+    node's place in _id order, modeling.py:529-538), and a one-leaf graph is unchanged."""
+    from probabilit_amd import native
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.modeling import NoOp
+    from probabilit_amd.qmc import seed_from
+
+    spec = [("gamma", dict(a=2.5, scale=3.0)), ("poisson", dict(mu=30.0)), ("beta", dict(a=2.0, b=3.0)),
+            ("binom", dict(n=20, p=0.3)), ("t", dict(df=4.0, loc=1.0)), ("norm", dict(loc=1.0, scale=2.0)),
+            ("gamma", dict(a=0.7)), ("nbinom", dict(n=3.5, p=0.4)), ("lognorm", dict(s=0.5))]
+    n, s = 50_001, 31
+    ds = [D(name, **kw) for name, kw in spec]
+    NoOp(*ds).sample(n, random_state=s, method="lhs")
+    for col, ((name, kw), d) in enumerate(zip(spec, ds)):
+        np.testing.assert_array_equal(d.samples_, native.lhs_ppf(name, seed_from(s), n, col, **kw), err_msg=name)
+    one = D("beta", a=2.0, b=3.0)
+    NoOp(one).sample(n, random_state=s, method="lhs")
+    np.testing.assert_array_equal(one.samples_, native.lhs_ppf("beta", seed_from(s), n, 0, a=2.0, b=3.0))

@@ -20,7 +20,10 @@ def main():
     out = {"rows": n, "sweep_ms": {}}
     cases = [("norm", {}), ("beta", dict(a=3.4, b=2.6, scale=10.0)), ("beta", dict(a=0.5, b=0.5)),
              ("truncnorm", dict(a=-1.0, b=2.0)), ("binom", dict(n=20, p=0.3)), ("weibull_min", dict(c=1.7)),
-             ("chi", dict(df=3.0)), ("burr12", dict(c=2.0, d=3.0)), ("trapezoid", dict(c=0.2, d=0.8))]
+             ("chi", dict(df=3.0)), ("burr12", dict(c=2.0, d=3.0)), ("trapezoid", dict(c=0.2, d=0.8)),
+             ("bernoulli", dict(p=0.3)), ("maxwell", {}), ("nakagami", dict(nu=4.97)), ("chi2", dict(df=5.5)),
+             ("nbinom", dict(n=3.5, p=0.4)), ("geom", dict(p=0.3)), ("randint", dict(low=2, high=40)),
+             ("invgamma", dict(a=2.5)), ("t", dict(df=4.0))]
     for name, kw in cases:
         native.ppf(name, q, return_device=True, **kw)
         ms = []

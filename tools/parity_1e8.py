@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--out", default="")
+    ap.add_argument("--scores", choices=("device", "reference"), default="device",
+                    help="reference: the reference's own step 1 (scipy ppf, rankdata, ndtri) and step 2 too")
     a = ap.parse_args()
 
     import scale_parity as sp
@@ -40,7 +42,7 @@ def main():
     def log(msg):
         print(f"[{time.time() - t0:7.1f}s] {msg if isinstance(msg, str) else json.dumps(msg)}", flush=True)
 
-    doc = sp.gate_all(a.rows, a.d, a.seed, cfg3_corr(a.d), threads=a.threads, log=log)
+    doc = sp.gate_all(a.rows, a.d, a.seed, cfg3_corr(a.d), threads=a.threads, log=log, scores=a.scores)
     s = json.dumps(doc, indent=1)
     print(s)
     if a.out:
