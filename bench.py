@@ -436,8 +436,14 @@ def end_to_end(root, ds, n, d, seed, barrier, device_ms):
 def reference_stream(root, seed, barrier, n=10_000_000, reps=2):
     """The same-seed mode (stream="reference": scipy's LatinHypercube(d, rng=seed) stream bit for
     bit, modeling.py:480,488 -> scipy _random_lhs) on the cfg3 graph at N = 1e7, device-resident
-    output: the device PCG64 uniforms, the d sequential Fisher-Yates shuffles on host threads
-    (pbh_lhs_reference) and their upload, then the same ppf + Iman-Conover.  A side figure."""
+    output: the device PCG64 uniforms, the d Fisher-Yates shuffles decoded on the device
+    (pbh_lhs_reference -> pbh_lhs_dev.hip: banded classification, a host walk of the ambiguous
+    draws, an exact check of every decision, permutations from the swap targets), then the same
+    ppf + Iman-Conover through the general (materialised) path.  A side figure."""
+    import ctypes
+
+    from probabilit_amd import _lib
+
     root.sample_device(n, random_state=seed, method="lhs", stream="reference")  # warm (workspaces)
     barrier()
     t0 = time.perf_counter()
@@ -446,10 +452,12 @@ def reference_stream(root, seed, barrier, n=10_000_000, reps=2):
     barrier()
     ms = (time.perf_counter() - t0) / reps * 1e3
     d = root.num_distribution_nodes()
+    dev, att, amb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+    _lib.check(_lib.load().pbh_lhs_reference_stats(ctypes.byref(dev), ctypes.byref(att), ctypes.byref(amb)))
     return {"value": round(n * d / (ms / 1e3) / 1e6, 2), "unit": "Msamples/s", "ms": round(ms, 1), "rows": n, "d": d,
-            "host_threads": os.environ.get("OMP_NUM_THREADS"),
+            "shuffles_on_device": bool(dev.value), "decode_attempts": att.value, "ambiguous_draws": amb.value,
             "what": "Node.sample_device(1e7, method='lhs', stream='reference'): same results as the reference on "
-                    "the same seed; the shuffles are sequential per column (host threads)"}
+                    "the same seed (the shuffle stream decoded on the device), then ppf + Iman-Conover"}
 
 
 def cpu_baseline(n, d):

@@ -158,9 +158,13 @@ int pbh_pcg64_random(const uint64_t* state_host, const uint64_t* inc_host, int64
  * has32 / buf32: the engine Generator's PCG64 state before the call ({low, high} words and numpy's
  * buffered 32-bit half).  u = rng.uniform(size=(n, d)) is drawn on the device, the d Fisher-Yates
  * shuffles of arange(1, n + 1) (numpy Generator.shuffle: random_interval with masked rejection
- * on buffered 32-bit draws) run on the host -- one sequential stream, replayed per column in
- * parallel threads after a counting pass -- and q = (perm - u) / n is combined on the device into
- * q (column-major, column c at q + c * ldq).  n < 2^31.  Workspace: pbh_lhs_reference_workspace_size.
+ * on buffered 32-bit draws; one sequential stream) are decoded on the device: every draw is
+ * classified against the band of states its column can be in, the few ambiguous ones are walked
+ * in order on the host, and every decision is then re-checked against the rule at the state its
+ * prefix implies; the permutation follows from the swap targets without replaying the swaps.  A
+ * failed check retries with a wider band, then falls back to the host shuffles (parallel threads
+ * after a counting pass).  q = (perm - u) / n is combined on the device into q (column-major,
+ * column c at q + c * ldq).  n < 2^31.  Workspace: pbh_lhs_reference_workspace_size.
  * pbh_lhs_reference_perms is the host half alone: the d permutations (d x n int32, row c = the
  * shuffled column c) from the stream state at the first shuffle draw; state_out_host (optional,
  * 4 words) receives the state after the last one (state low, high, has32, buf32). */
@@ -169,6 +173,11 @@ int pbh_lhs_reference(const uint64_t* state_host, const uint64_t* inc_host, int3
                       int32_t d, double* q, int64_t ldq, void* ws, size_t ws_bytes, void* stream);
 int pbh_lhs_reference_perms(const uint64_t* state_host, const uint64_t* inc_host, int32_t has32, uint32_t buf32,
                             int64_t n, int32_t d, int32_t* perms_host, uint64_t* state_out_host);
+/* The device decode's band half-width in standard deviations of the steps done (default 6; each
+ * retry doubles it); sigmas = 0 only reads it.  pbh_lhs_reference_stats: the last call's record
+ * (device = 1: decoded on the device; attempts; ambiguous draws walked on the host). */
+int pbh_lhs_reference_band(double sigmas, double* previous);
+int pbh_lhs_reference_stats(int32_t* device, int32_t* attempts, int64_t* ambiguous);
 
 /* Scrambled Halton points, bit-exact with scipy.stats.qmc.Halton(d, rng=...) (modeling.py:481,488):
  * column c is the van der Corput sequence in base bases_host[c] with counts_host[c] digit

@@ -6,13 +6,16 @@
 //                                                    row-major: on the device (pbh_pcg64_random)
 //   perms = d shuffles of arange(1, n + 1)           numpy Generator.shuffle: for i = n-1 .. 1,
 //                                                    j = random_interval(i) (masked rejection on
-//                                                    buffered 32-bit halves), swap: on the host
+//                                                    buffered 32-bit halves), swap: on the device
+//                                                    (pbh_lhs_dev.hip), host threads as fallback
 //   q     = (perms.T - u) / n                        on the device (k_lhs_combine)
 //
 // The shuffles are one sequential stream (a column's rejections decide where the next column's
-// draws start), so they run on the host CPU: a counting pass walks the stream once to find each
-// column's starting state, then the columns are shuffled in parallel threads, each replaying its
-// own stretch of the stream with the swap targets prefetched ahead of the swaps.
+// draws start).  pbh_lhs_reference decodes them on the device (pbh_lhs_dev.hip: banded parallel
+// classification, a host walk of the ambiguous draws, an exact check of every decision); the
+// host shuffles here are its fallback and pbh_lhs_reference_perms: a counting pass walks the
+// stream once to find each column's starting state, then the columns are shuffled in parallel
+// threads, each replaying its own stretch of the stream with the swap targets prefetched.
 #include <stdlib.h>
 #include <string.h>
 
@@ -21,6 +24,7 @@
 #include <vector>
 
 #include "pbh_error.h"
+#include "pbh_lhs_dev.h"
 #include "pbh_mt.h"
 #include "pbh_timing.h"
 
@@ -171,10 +175,14 @@ extern "C" int pbh_lhs_reference(const uint64_t* state_host, const uint64_t* inc
   hipStream_t s = as_stream(stream);
   int32_t* perms_dev = (int32_t*)ws;
   void* pcg_ws = (char*)ws + (((size_t)n * d * 4 + 255) & ~(size_t)255);
-  // u: draws 0 .. n d - 1, row-major, into q's column-major layout (overlaps the host shuffles)
-  int st = pbh_pcg64_random(state_host, inc_host, 0, n, d, q, ldq, pcg_ws, 128 * sizeof(u128), stream);
+  // u and the shuffles on the device (pbh_lhs_dev.hip), or, when its check fails, u again and
+  // the shuffles on the host: draws 0 .. n d - 1 row-major into q's column-major layout; the
+  // shuffles continue the stream after the n d doubles (uniform() leaves the 32-bit buffer)
+  bool done = false;
+  int st = lhs_reference_device(state_host, inc_host, has32 != 0, buf32, n, d, q, ldq, perms_dev, s, &done);
+  if (st || done) return st;
+  st = pbh_pcg64_random(state_host, inc_host, 0, n, d, q, ldq, pcg_ws, 128 * sizeof(u128), stream);
   if (st) return st;
-  // the shuffles continue the stream after the n d doubles (uniform() leaves the 32-bit buffer)
   u128 s0 = ((u128)state_host[1] << 64) | state_host[0];
   const u128 inc = ((u128)inc_host[1] << 64) | inc_host[0];
   std::vector<u128> table(128);

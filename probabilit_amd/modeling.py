@@ -438,29 +438,29 @@ class Node(abc.ABC):
             # plain-number parameters are then drawn together by one call (pbh_lhs_ppf_columns: their
             # inverse-CDF setups overlap), the rest one by one
             columns = {node: source.next_column() for node in isns}
-            group = []
+            leaves = []
             if isinstance(source, qmc.LHSSource):
-                group = [node for node in isns
+                leaves = [node for node in isns
                          if type(node) is Distribution and node.is_leaf and node.distr in _FUSED_LHS
                          and not (generated and node in all_set) and node not in block_row
                          and all(not isinstance(v, Node) and np.ndim(v) == 0
                                  for v in _parse_scipy_args(node.distr, node.args, node.kwargs))]
-            if len(group) >= 2:
-                group = [(node, node._params(size)) for node in group]
+            if len(leaves) >= 2:
+                leaves = [(node, node._params(size)) for node in leaves]
                 cols = []
-                for node, params in group:
+                for node, params in leaves:
                     _, seed, n_total, col, row0 = columns[node]
                     cols.append(_lib.ICColumn(seed, col, _lib.DIST_IDS[node.distr],
                                               (ctypes.c_double * 4)(*(params + [0.0] * (4 - len(params)))),
                                               len(params), ev.flag_ptr(node)))
-                gblock = device.empty((len(group), size))
+                gblock = device.empty((len(leaves), size))
                 arr = (_lib.ICColumn * len(cols))(*cols)
                 _lib.check(_lib.load().pbh_lhs_ppf_columns(arr, len(cols), source.n, source.row0, size,
                                                            gblock.data_ptr(), size, device.stream()),
                            "pbh_lhs_ppf_columns")
-                for j, (node, _) in enumerate(group):
+                for j, (node, _) in enumerate(leaves):
                     node._set_device(gblock[j])
-            grouped = {node for node, _ in group} if len(group) >= 2 else ()
+            grouped = {node for node, _ in leaves} if len(leaves) >= 2 else ()
             for node in isns:  # (:529-538)
                 if node in grouped:
                     continue

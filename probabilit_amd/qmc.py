@@ -322,10 +322,11 @@ class ReferenceLHSSource(QuantileSource):
     reference's own LHS stream (modeling.py:480,488), opt-in with stream="reference".
 
     The engine's owned Generator is set up exactly as scipy does (engine_rng: a spawned child,
-    which also advances a caller Generator's seed sequence as scipy would); the n x d uniforms
-    come from the device PCG64 (pbh_pcg64_random) and the d Fisher-Yates shuffles, one
-    sequential stream by construction, from host threads inside pbh_lhs_reference.  The whole
-    matrix is generated at the first column (no row sharding: the shuffles are global)."""
+    which also advances a caller Generator's seed sequence as scipy would); pbh_lhs_reference
+    draws the n x d uniforms and decodes the d Fisher-Yates shuffles -- one sequential stream by
+    construction -- on the device (pbh_lhs_dev.hip).  The whole matrix is made at the first
+    column; a row shard (multi-GPU) makes it on its own GPU and keeps its rows, since every row
+    of a column depends on the whole shuffle."""
 
     def __init__(self, n, d, rng):
         super().__init__(n, d)
@@ -336,11 +337,6 @@ class ReferenceLHSSource(QuantileSource):
         self.has32, self.buf32 = int(st["has_uint32"]), int(st["uinteger"])
         self.q = None
 
-    def shard(self, row0, rows):
-        if (row0, rows) != (0, self.n):
-            raise NotImplementedError("the reference LHS stream is sequential: it cannot be row-sharded")
-        return self
-
     def matrix(self):
         if self.q is None and self.n > 0 and self.d > 0:
             lib = _lib.load()
@@ -350,10 +346,11 @@ class ReferenceLHSSource(QuantileSource):
             _lib.check(lib.pbh_lhs_reference(_lib.np_ptr(s), _lib.np_ptr(inc), self.has32, self.buf32, self.n, self.d,
                                              self.q.data_ptr(), self.n, ws.data_ptr(), ws.numel(), device.stream()),
                        "pbh_lhs_reference")
+            del ws
         return self.q
 
     def column(self, c):
-        return ("vector", self.matrix()[c], 1)
+        return ("vector", self.matrix()[c, self.row0:self.row0 + self.rows], 1)
 
 
 _DEFAULT_STREAM = os.environ.get("PBH_LHS_STREAM", "native")

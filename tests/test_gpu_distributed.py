@@ -149,6 +149,9 @@ def _dag(kind):
               Distribution("weibull_min", c=1.7), dists.PERT(1, 2, 9, gamma=10),
               Distribution("binom", n=12, p=0.6, loc=0.5)]  # non-integer loc: the exact count path
         return NoOp(*ds).correlate(*ds, corr_mat=_target(len(ds))), "lhs"
+    if kind == "refstream":  # the reference's own LHS stream: each rank decodes it whole, keeps its rows
+        ds = [Distribution("norm", loc=1.0, scale=2.0), Distribution("gamma", a=2.0), Distribution("beta", a=2.0, b=3.0)]
+        return NoOp(*ds), "lhs"
     r = 0
     for _ in range(20):  # README mutual-fund loop (BASELINE config 5)
         r = r * Distribution("norm", loc=1.11, scale=0.15) + 1200
@@ -163,9 +166,10 @@ def _dag_worker(rank, world, port, outdir):
     try:
         from probabilit_amd import device
 
-        for kind in ("correlated", "fund", "ext"):
+        for kind in ("correlated", "fund", "ext", "refstream"):
             root, method = _dag(kind)
-            out = root.sample_device(1 << 16, random_state=7, method=method, group=dist.group.WORLD)
+            out = root.sample_device(1 << 16, random_state=7, method=method, group=dist.group.WORLD,
+                                     stream="reference" if kind == "refstream" else None)
             if kind == "fund":
                 np.save(os.path.join(outdir, f"{kind}{rank}.npy"), device.to_host(out))
             else:
@@ -177,16 +181,17 @@ def _dag_worker(rank, world, port, outdir):
 
 def test_dag_row_sharded_world2_matches_one_process(gpu):
     """Node.sample_device(..., group=) with two ranks: every node's rows equal the same rows
-    of the one-process evaluation (Sobol and LHS counter-addressed by global row)."""
+    of the one-process evaluation (Sobol and LHS counter-addressed by global row; the reference
+    LHS stream decoded whole on each rank)."""
     import torch.multiprocessing as mp
 
     from probabilit_amd.distributed import shard_bounds
 
     n = 1 << 16
     refs = {}
-    for kind in ("correlated", "fund", "ext"):
+    for kind in ("correlated", "fund", "ext", "refstream"):
         root, method = _dag(kind)
-        out = root.sample(n, random_state=7, method=method)
+        out = root.sample(n, random_state=7, method=method, stream="reference" if kind == "refstream" else None)
         if kind == "fund":
             refs[kind] = out
         else:
@@ -196,7 +201,7 @@ def test_dag_row_sharded_world2_matches_one_process(gpu):
         b = shard_bounds(n, 2)
         for r in range(2):
             np.testing.assert_array_equal(np.load(os.path.join(d, f"fund{r}.npy")), refs["fund"][b[r]:b[r + 1]])
-            for kind in ("correlated", "ext"):
+            for kind in ("correlated", "ext", "refstream"):
                 for j, ref in enumerate(refs[kind]):
                     np.testing.assert_array_equal(np.load(os.path.join(d, f"{kind}{r}_v{j}.npy")), ref[b[r]:b[r + 1]])
 

@@ -247,3 +247,95 @@ def test_reference_lhs_correlated_dag_matches_reference_pipeline(gpu):
     Y = np.column_stack([x.samples_ for x in ds])
     ref = oic.iman_conover(ppf_columns(lhs_quantiles(n, d, seed), cfg_dists(d)), C)["Y"]
     assert_close(Y, ref, rtol=1e-10, what="reference-stream cfg3 DAG vs the reference pipeline")
+
+
+def _ref_stats():
+    import ctypes
+
+    from probabilit_amd import _lib
+
+    dev, att, amb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+    _lib.check(_lib.load().pbh_lhs_reference_stats(ctypes.byref(dev), ctypes.byref(att), ctypes.byref(amb)))
+    return dev.value, att.value, amb.value
+
+
+def _ref_lhs_direct(state, inc, has32, buf32, n, d):
+    """pbh_lhs_reference at an arbitrary PCG64 state (has32 / buf32 included)."""
+    import ctypes
+
+    from probabilit_amd import _lib, device
+    from probabilit_amd.qmc import _u128_words
+
+    lib = _lib.load()
+    nb = ctypes.c_size_t()
+    _lib.check(lib.pbh_lhs_reference_workspace_size(n, d, ctypes.byref(nb)))
+    ws = device.empty(int(nb.value), "uint8")
+    q = device.empty((d, n))
+    s, i = _u128_words(state), _u128_words(inc)
+    _lib.check(lib.pbh_lhs_reference(_lib.np_ptr(s), _lib.np_ptr(i), has32, buf32, n, d, q.data_ptr(), n,
+                                     ws.data_ptr(), ws.numel(), device.stream()), "pbh_lhs_reference")
+    return device.to_host(q).T
+
+
+def _ref_lhs_host(state, inc, has32, buf32, n, d):
+    """The same matrix from the host shuffles (pbh_lhs_reference_perms, pinned against numpy's
+    Generator.shuffle in test_streams_host.py) and numpy's own uniforms."""
+    import ctypes
+
+    from probabilit_amd import _lib
+    from probabilit_amd.qmc import _u128_words
+
+    g = np.random.Generator(np.random.PCG64())
+    g.bit_generator.state = {"bit_generator": "PCG64", "state": {"state": state, "inc": inc},
+                             "has_uint32": has32, "uinteger": buf32}
+    u = g.uniform(size=(n, d))
+    st = g.bit_generator.state
+    perms = np.empty((d, n), dtype=np.int32)
+    s, i = _u128_words(st["state"]["state"]), _u128_words(inc)
+    _lib.check(_lib.load().pbh_lhs_reference_perms(_lib.np_ptr(s), _lib.np_ptr(i), has32, buf32, n, d,
+                                                   _lib.np_ptr(perms), None))
+    return (perms.T - u) / n
+
+
+@pytest.mark.parametrize("n,d,has32", [(2, 3, 0), (3, 5, 1), (1000, 4, 1), (65_537, 3, 0), (1_000_003, 4, 1),
+                                       (3_000_000, 2, 0)])
+def test_reference_lhs_device_decode(gpu, n, d, has32):
+    """The shuffles decoded on the device (pbh_lhs_dev.hip: banded classification, host walk of
+    the ambiguous draws, every decision re-checked) equal the host shuffles bit for bit, from an
+    arbitrary PCG64 state with and without numpy's buffered 32-bit half, in one attempt."""
+    rng = np.random.default_rng(n + d)
+    state, inc = int(rng.integers(0, 2**63)) << 64 | int(rng.integers(0, 2**63)), (int(rng.integers(0, 2**62)) << 1) | 1
+    buf32 = int(rng.integers(0, 2**32)) if has32 else 0
+    got = _ref_lhs_direct(state, inc, has32, buf32, n, d)
+    dev, att, amb = _ref_stats()
+    np.testing.assert_array_equal(got, _ref_lhs_host(state, inc, has32, buf32, n, d))
+    assert dev == 1 and att == 1, (dev, att, amb)
+    print(f"n={n} d={d}: ambiguous draws walked on the host {amb} ({amb / d:.0f} per column)")
+
+
+def test_reference_lhs_device_decode_retry_and_fallback(gpu):
+    """A band too narrow for the walk fails the device check: the call retries with wider bands,
+    then falls back to the host shuffles; the result is the same matrix either way."""
+    import ctypes
+
+    from probabilit_amd import _lib
+
+    lib = _lib.load()
+    n, d, seed = 200_000, 3, 4
+    import scipy.stats
+
+    ref = scipy.stats.qmc.LatinHypercube(d=d, rng=seed).random(n)
+    from probabilit_amd import qmc
+
+    prev = ctypes.c_double()
+    _lib.check(lib.pbh_lhs_reference_band(1e-3, ctypes.byref(prev)))
+    try:
+        got = _src_matrix(qmc.make_source("lhs", n, d, seed, stream="reference"))
+        dev, att, amb = _ref_stats()
+    finally:
+        _lib.check(lib.pbh_lhs_reference_band(prev.value, None))
+    np.testing.assert_array_equal(got, ref)
+    assert att == 3 and dev == 0, (dev, att, amb)
+    got = _src_matrix(qmc.make_source("lhs", n, d, seed, stream="reference"))
+    np.testing.assert_array_equal(got, ref)
+    assert _ref_stats()[:2] == (1, 1)
