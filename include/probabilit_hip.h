@@ -177,6 +177,10 @@ int pbh_lhs_reference_perms(const uint64_t* state_host, const uint64_t* inc_host
  * retry doubles it); sigmas = 0 only reads it.  pbh_lhs_reference_stats: the last call's record
  * (device = 1: decoded on the device; attempts; ambiguous draws walked on the host). */
 int pbh_lhs_reference_band(double sigmas, double* previous);
+/* The process cache of inverse-CDF setup tables (gamma / beta guides, poisson / binom / nbinom CDF
+ * tables, keyed by their scalar parameters; pbh_table_cache.hip): tables held, their bytes, and
+ * the calls served from it. */
+int pbh_table_cache_stats(int64_t* entries, int64_t* bytes, int64_t* hits);
 int pbh_lhs_reference_stats(int32_t* device, int32_t* attempts, int64_t* ambiguous);
 
 /* Scrambled Halton points, bit-exact with scipy.stats.qmc.Halton(d, rng=...) (modeling.py:481,488):

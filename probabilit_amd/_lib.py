@@ -51,7 +51,7 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_pcg64_random", "pbh_halton_workspace_size", "pbh_fill_halton",
            "pbh_affine_workspace_size", "pbh_affine_rows", "pbh_table_ppf", "pbh_permcorr_workspace_size",
            "pbh_permcorr_climb", "pbh_sobol_ppf", "pbh_lhs_reference_workspace_size",
-           "pbh_lhs_reference", "pbh_lhs_reference_perms", "pbh_lhs_reference_band", "pbh_lhs_reference_stats", "pbh_hbm_copy", "pbh_dag_eval",
+           "pbh_lhs_reference", "pbh_lhs_reference_perms", "pbh_lhs_reference_band", "pbh_lhs_reference_stats", "pbh_table_cache_stats", "pbh_hbm_copy", "pbh_dag_eval",
            "pbh_lhs_sorted_counts", "pbh_sort_heads", "pbh_ic_owned_workspace_size", "pbh_ic_owned_create",
            "pbh_ic_owned_column", "pbh_ic_owned_finish", "pbh_lhs_values_at", "pbh_lhs_ppf_columns", "pbh_ic_owned_destroy", "pbh_event_create",
            "pbh_event_destroy", "pbh_event_record", "pbh_stream_wait_event", "pbh_event_synchronize",
@@ -180,6 +180,7 @@ def load():
         "pbh_lhs_reference_perms": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, vp], i32),
         "pbh_lhs_reference_band": ([ctypes.c_double, ctypes.POINTER(ctypes.c_double)], i32),
         "pbh_lhs_reference_stats": ([ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i64)], i32),
+        "pbh_table_cache_stats": ([ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
         "pbh_permcorr_climb": ([vp, vp, i64, ctypes.c_int32, i64, vp, vp, vp, vp, vp, vp, i64, dbl, vp, vp, vp, sz, vp],
                                i32),
         "pbh_lhs_sorted_counts": ([u64, i64, i64, i64, i32, i32, vp, i32, vp, vp, vp, ctypes.c_uint32, vp, i32, vp],

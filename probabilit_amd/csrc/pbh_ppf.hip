@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "pbh_error.h"
+#include "pbh_table_cache.h"
 #include "pbh_ppf_core.h"
 #include "pbh_ppf_ext.h"
 #include "pbh_rng.h"
@@ -1815,19 +1816,17 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
   *table = nullptr;
   if (dist == PBH_DIST_GAMMA && params[0].ptr == nullptr && params[0].value > 0.0 && isfinite(params[0].value)) {
     const double a = params[0].value;
-    const double z0 = sf::kGammaGuideZ0, h = sf::kGammaGuideH;
     const int m = sf::kGammaGuideM;
-    PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)4 * m * sizeof(double), s));
+    *table = gamma_guide_table(a, s);
+    if (!*table) {
+      set_error("gamma guide table for a = %g failed", a);
+      return PBH_ERR_HIP;
+    }
     double* tb = *table;
-    sf::GammaGuide T{tb, tb + m, tb + 2 * m, tb + 3 * m, m, z0, h, 1.0 / h};
-    const unsigned g = (unsigned)((m + 63) / 64);
-    hipLaunchKernelGGL(k_gamma_guide, dim3(g), dim3(64), 0, s, a, T, tb, tb + m, tb + 2 * m);
-    PBH_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_gamma_guide_check, dim3(g), dim3(64), 0, s, a, T, tb + 3 * m);
-    PBH_CHECK_LAUNCH();
     pt.has_gamma = 1;
     pt.aux = sf::gamma_aux(a);
-    pt.guide = T;
+    pt.guide = sf::GammaGuide{tb, tb + m, tb + 2 * m, tb + 3 * m, m, sf::kGammaGuideZ0, sf::kGammaGuideH,
+                              1.0 / sf::kGammaGuideH};
   }
   if (dist == PBH_DIST_POISSON && params[0].ptr == nullptr) {
     double mu = params[0].value;
@@ -1838,16 +1837,25 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
       int64_t k_hi = (int64_t)ceil(mu + 20.0 * sd + 40.0);
       int64_t len = k_hi - k_lo + 1;
       const int nb = 1 << kPoissonGuideBits;
-      PBH_CHECK_HIP(hipMallocAsync((void**)table, (size_t)2 * len * sizeof(double) + (size_t)nb * 4, s));
-      hipLaunchKernelGGL(k_poisson_table, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, mu, k_lo, len,
-                         *table, *table + len);
-      PBH_CHECK_LAUNCH();
-      int32_t* guide = (int32_t*)(*table + 2 * len);
-      hipLaunchKernelGGL(k_poisson_guide, dim3((unsigned)(nb / 256)), dim3(256), 0, s, *table, len, guide);
-      PBH_CHECK_LAUNCH();
+      const size_t bytes = (size_t)2 * len * sizeof(double) + (size_t)nb * 4;
+      auto build = [=](double* t, hipStream_t st) {
+        hipLaunchKernelGGL(k_poisson_table, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, mu, k_lo, len, t,
+                           t + len);
+        hipLaunchKernelGGL(k_poisson_guide, dim3((unsigned)(nb / 256)), dim3(256), 0, st, t, len,
+                           (int32_t*)(t + 2 * len));
+        return hipGetLastError() == hipSuccess;
+      };
+      *table = cached_table(kTabPoisson, &mu, 1, bytes, s, build);
+      if (!*table) {
+        PBH_CHECK_HIP(hipMallocAsync((void**)table, bytes, s));
+        if (!build(*table, s)) {
+          set_error("poisson table launch failed");
+          return PBH_ERR_HIP;
+        }
+      }
       pt.cdf = *table;
       pt.win = *table + len;
-      pt.cdf_guide = guide;
+      pt.cdf_guide = (int32_t*)(*table + 2 * len);
       pt.k_lo = k_lo;
       pt.len = len;
     }
@@ -1857,18 +1865,28 @@ int with_params(int dist, const pbh_param* params, int nparams, Params& prm, Poi
 
 }  // namespace
 
-// The gamma guide of shape a in a fresh stream-ordered allocation (4 x kGammaGuideM doubles: y, d1,
-// d2, ok; the layout with_params builds for gamma), for the extended distributions whose ppf is
-// gammaincinv (chi, maxwell, nakagami, chi2: pbh_ppf_ext.hip).  NULL for an invalid a.
+// The gamma guide of shape a (4 x kGammaGuideM doubles: y, d1, d2, ok), for gamma (with_params)
+// and the extended distributions whose ppf is gammaincinv (chi, maxwell, nakagami, chi2:
+// pbh_ppf_ext.hip): the process cache's (pbh_table_cache.hip), or a fresh stream-ordered
+// allocation when the cache is full; callers end with release_table.  NULL for an invalid a.
 double* gamma_guide_table(double a, hipStream_t s) {
   if (!(a > 0.0 && isfinite(a))) return nullptr;
   const int m = sf::kGammaGuideM;
+  auto build = [=](double* tb, hipStream_t st) {
+    sf::GammaGuide T{tb, tb + m, tb + 2 * m, tb + 3 * m, m, sf::kGammaGuideZ0, sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
+    const unsigned g = (unsigned)((m + 63) / 64);
+    hipLaunchKernelGGL(k_gamma_guide, dim3(g), dim3(64), 0, st, a, T, tb, tb + m, tb + 2 * m);
+    hipLaunchKernelGGL(k_gamma_guide_check, dim3(g), dim3(64), 0, st, a, T, tb + 3 * m);
+    return hipGetLastError() == hipSuccess;
+  };
+  const size_t bytes = (size_t)4 * m * sizeof(double);
+  if (double* t = cached_table(kTabGammaGuide, &a, 1, bytes, s, build)) return t;
   double* tb = nullptr;
-  if (hipMallocAsync((void**)&tb, (size_t)4 * m * sizeof(double), s) != hipSuccess) return nullptr;
-  sf::GammaGuide T{tb, tb + m, tb + 2 * m, tb + 3 * m, m, sf::kGammaGuideZ0, sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
-  const unsigned g = (unsigned)((m + 63) / 64);
-  hipLaunchKernelGGL(k_gamma_guide, dim3(g), dim3(64), 0, s, a, T, tb, tb + m, tb + 2 * m);
-  hipLaunchKernelGGL(k_gamma_guide_check, dim3(g), dim3(64), 0, s, a, T, tb + 3 * m);
+  if (hipMallocAsync((void**)&tb, bytes, s) != hipSuccess) return nullptr;
+  if (!build(tb, s)) {
+    (void)hipFreeAsync(tb, s);
+    return nullptr;
+  }
   return tb;
 }
 
@@ -1919,7 +1937,7 @@ int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* par
 
 void gen_destroy(GenColumn* g, hipStream_t s) {
   if (!g) return;
-  if (g->table) (void)hipFreeAsync(g->table, s);
+  release_table(g->table, s);
   if (g->rvals) (void)hipFreeAsync(g->rvals, s);
   delete g;
 }
@@ -2439,7 +2457,7 @@ extern "C" int pbh_ppf(int dist, const double* q, int64_t q_stride, int64_t n, c
   int st = with_params(dist, params, nparams, prm, pt, &table, s);
   if (st != PBH_OK) return st;
   st = launch_ppf(dist, q, q_stride, n, prm, pt, out, nonfinite_flag, s);
-  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));
+  release_table(table, s);
   return st;
 }
 
@@ -2458,7 +2476,7 @@ extern "C" int pbh_lhs_ppf(uint64_t seed, int64_t n, int64_t row0, int64_t nrows
   int st = with_params(dist, params, nparams, prm, pt, &table, s);
   if (st != PBH_OK) return st;
   st = launch_lhs_ppf(dist, seed, n, row0, nrows, (uint32_t)col, prm, pt, out, nonfinite_flag, s);
-  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));
+  release_table(table, s);
   return st;
 }
 
@@ -2608,6 +2626,6 @@ extern "C" int pbh_sobol_ppf(const uint32_t* sv_host, const uint32_t* shift_host
       break;
   }
   PBH_CHECK_LAUNCH();
-  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));
+  release_table(table, s);
   return PBH_OK;
 }

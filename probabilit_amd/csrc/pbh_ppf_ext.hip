@@ -17,6 +17,7 @@
 #include <math.h>
 
 #include "pbh_error.h"
+#include "pbh_table_cache.h"
 #include "pbh_ppf_ext.h"
 #include "pbh_rng.h"
 #include "pbh_special.h"
@@ -124,7 +125,8 @@ int discrete_table_len(int dist, const double* v) {
 // the setup table of `dist` with these parameters (stream-ordered allocation, NULL when the
 // distribution has none): beta with scalar, valid (a, b) -> its guide; chi / maxwell / nakagami /
 // chi2 with a scalar shape -> gammaincinv's guide (pbh_ppf.hip gamma_guide_table); binom /
-// bernoulli / nbinom with scalar parameters -> [len, CDF (len), complement (len)]
+// bernoulli / nbinom with scalar parameters -> [len, CDF (len), complement (len)]; the process
+// cache's (pbh_table_cache.hip) when it has room, callers end with release_table
 double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t s) {
   if (is_gamma_family(dist)) {
     if (dist != PBH_DIST_MAXWELL && (nparams < 1 || params[0].ptr)) return nullptr;
@@ -140,32 +142,49 @@ double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t 
     }
     const int len = discrete_table_len(dist, v);
     if (len <= 0) return nullptr;
+    auto build = [=](double* t, hipStream_t st) {
+      const double hdr = (double)len;
+      if (hipMemcpyAsync(t, &hdr, sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess) return false;
+      const dim3 g((unsigned)((len + 255) / 256)), b(256);
+      if (dist == PBH_DIST_BINOM)
+        hipLaunchKernelGGL(k_discrete_table<PBH_DIST_BINOM>, g, b, 0, st, v[0], v[1], len, t + 1, t + 1 + len);
+      else if (dist == PBH_DIST_BERNOULLI)
+        hipLaunchKernelGGL(k_discrete_table<PBH_DIST_BERNOULLI>, g, b, 0, st, v[0], v[1], len, t + 1, t + 1 + len);
+      else
+        hipLaunchKernelGGL(k_discrete_table<PBH_DIST_NBINOM>, g, b, 0, st, v[0], v[1], len, t + 1, t + 1 + len);
+      return hipGetLastError() == hipSuccess;
+    };
+    const size_t bytes = (size_t)(2 * len + 1) * sizeof(double);
+    const double key[3] = {(double)dist, v[0], v[1]};
+    if (double* t = cached_table(kTabDiscrete, key, 3, bytes, s, build)) return t;
     double* t = nullptr;
-    if (hipMallocAsync((void**)&t, (size_t)(2 * len + 1) * sizeof(double), s) != hipSuccess) return nullptr;
-    const double hdr = (double)len;
-    if (hipMemcpyAsync(t, &hdr, sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess) {
+    if (hipMallocAsync((void**)&t, bytes, s) != hipSuccess) return nullptr;
+    if (!build(t, s)) {
       (void)hipFreeAsync(t, s);
       return nullptr;
     }
-    const dim3 g((unsigned)((len + 255) / 256)), b(256);
-    if (dist == PBH_DIST_BINOM)
-      hipLaunchKernelGGL(k_discrete_table<PBH_DIST_BINOM>, g, b, 0, s, v[0], v[1], len, t + 1, t + 1 + len);
-    else if (dist == PBH_DIST_BERNOULLI)
-      hipLaunchKernelGGL(k_discrete_table<PBH_DIST_BERNOULLI>, g, b, 0, s, v[0], v[1], len, t + 1, t + 1 + len);
-    else
-      hipLaunchKernelGGL(k_discrete_table<PBH_DIST_NBINOM>, g, b, 0, s, v[0], v[1], len, t + 1, t + 1 + len);
     return t;
   }
   if (dist != PBH_DIST_BETA || nparams < 2 || params[0].ptr || params[1].ptr) return nullptr;
   const double a = params[0].value, b = params[1].value;
   if (!(a > 0.0 && b > 0.0 && isfinite(a) && isfinite(b))) return nullptr;
   constexpr int m = sfx::kBetaGuideM;
+  auto build = [=](double* t, hipStream_t st) {
+    const unsigned g = (unsigned)((m + 63) / 64);
+    hipLaunchKernelGGL(k_beta_guide, dim3(g), dim3(64), 0, st, a, b, sfx::lbeta(a, b), t, t + m, t + 2 * m);
+    const sfx::BetaGuide T{t, t + m, t + 2 * m, t + 3 * m};
+    hipLaunchKernelGGL(k_beta_guide_check, dim3(g), dim3(64), 0, st, a, b, T, t + 3 * m);
+    return hipGetLastError() == hipSuccess;
+  };
+  const size_t bytes = (size_t)4 * m * sizeof(double);
+  const double key[2] = {a, b};
+  if (double* t = cached_table(kTabBetaGuide, key, 2, bytes, s, build)) return t;
   double* t = nullptr;
-  if (hipMallocAsync((void**)&t, (size_t)4 * m * sizeof(double), s) != hipSuccess) return nullptr;
-  const unsigned g = (unsigned)((m + 63) / 64);
-  hipLaunchKernelGGL(k_beta_guide, dim3(g), dim3(64), 0, s, a, b, sfx::lbeta(a, b), t, t + m, t + 2 * m);
-  const sfx::BetaGuide T{t, t + m, t + 2 * m, t + 3 * m};
-  hipLaunchKernelGGL(k_beta_guide_check, dim3(g), dim3(64), 0, s, a, b, T, t + 3 * m);
+  if (hipMallocAsync((void**)&t, bytes, s) != hipSuccess) return nullptr;
+  if (!build(t, s)) {
+    (void)hipFreeAsync(t, s);
+    return nullptr;
+  }
   return t;
 }
 
@@ -585,7 +604,7 @@ int launch_ext(int dist, const double* q, int64_t q_stride, const LhsCol* lc, in
     else
       PBH_TIMED(kKPpf, s, hipLaunchKernelGGL((k_ppf_ext<D, false>), g, b, 0, s, q, q_stride, l, n, prm, out, flag));
   });
-  if (table) PBH_CHECK_HIP(hipFreeAsync(table, s));  // stream-ordered: after the kernel
+  release_table(table, s);  // stream-ordered: after the kernel (cached tables stay)
   if (!known) {
     set_error("ppf: unknown distribution id %d", dist);
     return PBH_ERR_UNSUPPORTED;

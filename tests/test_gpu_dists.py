@@ -438,3 +438,34 @@ def test_grouped_lhs_columns(gpu):
     one = D("beta", a=2.0, b=3.0)
     NoOp(one).sample(n, random_state=s, method="lhs")
     np.testing.assert_array_equal(one.samples_, native.lhs_ppf("beta", seed_from(s), n, 0, a=2.0, b=3.0))
+
+
+def test_setup_table_cache(gpu):
+    """Setup tables are kept per parameter set (pbh_table_cache.hip): a second sample with the
+    same parameters is served from the cache and gives the same values; other parameters get
+    tables of their own (no key collision)."""
+    import ctypes
+
+    from probabilit_amd import _lib, native
+
+    def stats():
+        e, b, h = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(_lib.load().pbh_table_cache_stats(ctypes.byref(e), ctypes.byref(b), ctypes.byref(h)))
+        return e.value, b.value, h.value
+
+    n = 20_000
+    cases = [("gamma", dict(a=3.3)), ("poisson", dict(mu=17.5)), ("beta", dict(a=1.7, b=4.2)), ("binom", dict(n=33, p=0.2)),
+             ("nbinom", dict(n=2.5, p=0.3)), ("chi", dict(df=4.5))]
+    for name, kw in cases:
+        first = native.lhs_ppf(name, 5, n, 1, **kw)
+        e0, _, h0 = stats()
+        again = native.lhs_ppf(name, 5, n, 1, **kw)
+        e1, _, h1 = stats()
+        np.testing.assert_array_equal(first, again, err_msg=name)
+        assert e1 == e0 and h1 > h0, (name, e0, e1, h0, h1)
+        bumped = dict(kw)
+        key = next(iter(kw))
+        bumped[key] = kw[key] * 1.25 if name not in ("binom",) else kw[key] + 1
+        other = native.lhs_ppf(name, 5, n, 1, **bumped)
+        assert stats()[0] == e1 + 1, name
+        assert not np.array_equal(other, first), name
