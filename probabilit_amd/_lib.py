@@ -9,8 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libprobabilit_hip.so")
-if os.environ.get("PBH_LIB_VARIANT"):  # A/B measurements: an in-tree variant built by build.py --variant
-    LIB_PATH = os.path.join(HERE, f"libprobabilit_hip_{os.environ['PBH_LIB_VARIANT']}.so")
+# (A/B measurements set LIB_PATH to a variant built by build.py --variant before the first load)
 
 # pbh_status
 OK, ERR_INVALID, ERR_HIP, ERR_NOT_PD, ERR_NONFINITE, ERR_WORKSPACE, ERR_UNSUPPORTED = range(7)

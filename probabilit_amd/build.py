@@ -52,8 +52,9 @@ def _stale(target, deps):
 
 
 def build(force=False, verbose=False, variant=None, defines=()):
-    """variant: build libprobabilit_hip_<variant>.so with extra -D `defines` (A/B measurements,
-    selected at run time by PBH_LIB_VARIANT); the default library is untouched."""
+    """variant: build libprobabilit_hip_<variant>.so with extra -D `defines` (A/B measurements:
+    a measuring tool points probabilit_amd._lib.LIB_PATH at it before the first load); the
+    default library is untouched."""
     bdir = BUILD if not variant else BUILD + "_" + variant
     lib_path = LIB if not variant else os.path.join(HERE, f"libprobabilit_hip_{variant}.so")
     os.makedirs(bdir, exist_ok=True)

@@ -877,11 +877,7 @@ int apply_decorrelate_correlate(double* S, int64_t n, int k, int64_t ld, const d
   dim3 g(grid_for(n, 256, 8192)), b(256);
   CodeMap c = cm ? *cm : CodeMap{};
   if (!cm) codes = nullptr;
-  static const bool vector_only = [] {
-    const char* e = getenv("PBH_APPLY");
-    return e && strcmp(e, "vector") == 0;
-  }();
-  if (k <= 32 && !vector_only) {
+  if (k <= 32) {
     double* M = nullptr;
     PBH_CHECK_HIP(hipMallocAsync((void**)&M, 32 * 32 * sizeof(double), s));
     hipLaunchKernelGGL(k_transform_matrix, dim3(1), dim3(64), 0, s, L, inv_diag, P, k, M);

@@ -43,25 +43,9 @@ constexpr int kBlock = 256;
 
 
 
-bool stream_enabled() {  // PBH_PPF_STREAM=0 selects the plain grid-stride k_ppf (A/B measurements)
-  static const bool on = [] {
-    const char* e = getenv("PBH_PPF_STREAM");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 unsigned compact_grid(int64_t n) { return grid_for(n, kCTile, 256 * 8); }
 
 bool scalar_params(const Params& prm) { return !prm.ptr[0] && !prm.ptr[1] && !prm.ptr[2]; }
-
-bool compaction_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("PBH_COMPACT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 
 // k_ppf / k_lhs_ppf for D in {norm, lognorm} with tail compaction.  Q(i) gives the quantile of
 // tile item i (a strided load, or the fused LHS generator).  SC: every parameter is a scalar
@@ -348,11 +332,7 @@ __global__ __launch_bounds__(kGBlock) void k_lhs_ppf_gamma_lds(uint64_t seed, in
 
 // scalar shape with a built guide, scalar loc / scale
 bool gamma_lds_ok(int dist, const Params& prm, const PoissonTable& pt) {
-  static const bool on = [] {
-    const char* e = getenv("PBH_GAMMA_LDS");
-    return !(e && e[0] == '0');
-  }();
-  return on && dist == PBH_DIST_GAMMA && pt.has_gamma && pt.guide.m == sf::kGammaGuideM && !prm.ptr[0] &&
+  return dist == PBH_DIST_GAMMA && pt.has_gamma && pt.guide.m == sf::kGammaGuideM && !prm.ptr[0] &&
          !prm.ptr[1] && !prm.ptr[2];
 }
 
@@ -428,11 +408,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_poisson_lds(uint64_t
 
 // dynamic LDS bytes of the poisson LDS kernels, or 0 when they do not apply
 size_t poisson_lds_bytes(int dist, const Params& prm, const PoissonTable& pt) {
-  static const bool on = [] {
-    const char* e = getenv("PBH_POISSON_LDS");
-    return !(e && e[0] == '0');
-  }();
-  if (!on || dist != PBH_DIST_POISSON || !pt.cdf || !pt.cdf_guide || pt.len <= 0 || pt.len > kPoissonLdsMaxLen ||
+  if (dist != PBH_DIST_POISSON || !pt.cdf || !pt.cdf_guide || pt.len <= 0 || pt.len > kPoissonLdsMaxLen ||
       prm.ptr[0] || prm.ptr[1])
     return 0;
   return (size_t)2 * pt.len * sizeof(double) + ((size_t)1 << kPoissonGuideBits) * sizeof(int32_t);
@@ -1691,7 +1667,7 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
   // unrolling gamma's / poisson's code kVU x 2 times measured 1.7x / 1.25x slower)
   const bool light = dist == PBH_DIST_UNIFORM || dist == PBH_DIST_TRIANG || dist == PBH_DIST_EXPON;
   const bool streamable = light && qs == 1 && !prm.ptr[0] && !prm.ptr[1] && !prm.ptr[2] &&
-                          ((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0 && stream_enabled();
+                          ((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0;
   dim3 gv(grid_for(n, kVTile, 256 * 8));
   if (gamma_lds_ok(dist, prm, pt)) {
     int st = PBH_OK;
@@ -1710,7 +1686,7 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
   switch (dist) {
 #define PBH_CASE(D) \
   case D:           \
-    if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
+    if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM))                                                  \
       PBH_TIMED(kKPpf, s, hipLaunchKernelGGL((scalar_params(prm) ? k_ppf_c<D, true> : k_ppf_c<D, false>),            \
                                              dim3(grid_for(n, kCTile, 8192)), b, 0, s, q, qs, n, prm, pt, out,  \
                                              flag));                                                            \
@@ -1756,7 +1732,7 @@ int launch_lhs_ppf(int dist, uint64_t seed, int64_t n, int64_t row0, int64_t nro
   switch (dist) {
 #define PBH_CASE(D) \
   case D:           \
-    if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                            \
+    if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM))                                                  \
       PBH_TIMED(kKLhsPpf, s,                                                                                    \
                 hipLaunchKernelGGL((scalar_params(prm) ? k_lhs_ppf_c<D, true> : k_lhs_ppf_c<D, false>),            \
                                    dim3(compact_grid(nrows)), b, 0, s, seed, n, row0, nrows, col, prm, pt, out, \
@@ -2605,7 +2581,7 @@ extern "C" int pbh_sobol_ppf(const uint32_t* sv_host, const uint32_t* shift_host
   switch (dist) {
 #define PBH_CASE(D)                                                                                               \
   case D:                                                                                                         \
-    if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM) && compaction_enabled())                                    \
+    if ((D == PBH_DIST_NORM || D == PBH_DIST_LOGNORM))                                                          \
       PBH_TIMED(kKPpf, s,                                                                                         \
                 hipLaunchKernelGGL((scalar_params(prm) ? k_sobol_ppf_c<D, true> : k_sobol_ppf_c<D, false>),         \
                                    dim3(compact_grid(nrows)), b, 0, s, sc, row0, nrows, prm, pt, out,             \

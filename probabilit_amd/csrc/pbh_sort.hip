@@ -370,21 +370,9 @@ __global__ __launch_bounds__(256) void k_place_bases(int64_t n, int shift, uint3
 // items (9216-key tiles: ~36 keys per digit bucket, whole 128-byte lines per burst; 72 KB of LDS,
 // 2 tiles per CU; 0.59 ms per 1e8-key pass against 0.62 with 32, 0.69 with 24); the 32-bit key +
 // 64-bit value passes of the row placement with 24
-// (72 KB, still 2 tiles per CU: 0.75 ms per 1e8-row pass against 0.91 with 16).  PBH_OS_IPT
-// (16 / 24 / 32 / 36) and PBH_PLACE_IPT (16 / 20 / 24) force either.
+// (72 KB, still 2 tiles per CU: 0.75 ms per 1e8-row pass against 0.91 with 16).
 int onesweep_items(size_t item_bytes_minus_key4) {
-  const size_t value_bytes = item_bytes_minus_key4;
-  static const int forced = [] {
-    const char* e = getenv("PBH_OS_IPT");
-    return e ? atoi(e) : 0;
-  }();
-  static const int forced_place = [] {
-    const char* e = getenv("PBH_PLACE_IPT");
-    return e ? atoi(e) : 0;
-  }();
-  if (value_bytes > 4 && (forced_place == 16 || forced_place == 20 || forced_place == 24)) return forced_place;
-  if (value_bytes <= 4 && (forced == 16 || forced == 24 || forced == 32 || forced == 36)) return forced;
-  return value_bytes <= 4 ? 36 : 24;  // item_bytes (key + value) 8 -> 36, 12 -> 24: ~79 KB of LDS either way
+  return item_bytes_minus_key4 <= 4 ? 36 : 24;  // item_bytes (key + value) 8 -> 36, 12 -> 24: ~79 KB of LDS either way
 }
 
 template <typename K, typename V, int IPT_>
@@ -398,21 +386,10 @@ void launch_onesweep_ipt(const K* kin, const V* vin, K* kout, V* vout, int64_t n
 template <typename K, typename V>
 void launch_onesweep(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
                      uint64_t* status, uint32_t* counter, hipStream_t s) {
-  switch (onesweep_items(sizeof(K) + sizeof(V) - 4)) {  // u64 key + u32 row sizes like u32 + f64
-    case 36: launch_onesweep_ipt<K, V, 36>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
-    case 32: launch_onesweep_ipt<K, V, 32>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
-    case 24: launch_onesweep_ipt<K, V, 24>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
-    case 20: launch_onesweep_ipt<K, V, 20>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
-    default: launch_onesweep_ipt<K, V, 16>(kin, vin, kout, vout, n, shift, bases, status, counter, s); break;
-  }
-}
-
-bool onesweep_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("PBH_SORT");
-    return !(e && strcmp(e, "classic") == 0);
-  }();
-  return on;
+  if (onesweep_items(sizeof(K) + sizeof(V) - 4) == 36)  // u64 key + u32 row sizes like u32 + f64
+    launch_onesweep_ipt<K, V, 36>(kin, vin, kout, vout, n, shift, bases, status, counter, s);
+  else
+    launch_onesweep_ipt<K, V, 24>(kin, vin, kout, vout, n, shift, bases, status, counter, s);
 }
 
 // ------------------------------------------------------------------ row placement
@@ -722,27 +699,12 @@ int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, in
   const double* vin = v;
   int cur = 0;
   for (int shift = kPlaceShift; shift < bits; shift += 8) {
-    if (onesweep_enabled()) {
-      hipLaunchKernelGGL(k_place_bases, dim3(1), dim3(256), 0, s, n, shift, pb.bases);
-      PBH_CHECK_LAUNCH();
-      PBH_CHECK_HIP(hipMemsetAsync(pb.status, 0, (size_t)nt * 256 * 8 + 256, s));  // words, counter, flag
-      PBH_TIMED(kKPlaceScatter, s,
-                launch_onesweep<uint32_t, double>(rin, vin, pb.rows[cur], pb.vals[cur], n, shift, pb.bases, pb.status,
-                                                  (uint32_t*)(pb.status + nt * 256), s));
-      PBH_CHECK_LAUNCH();
-      rin = pb.rows[cur];
-      vin = pb.vals[cur];
-      cur ^= 1;
-      continue;
-    }
-    PBH_TIMED(kKPlaceUpsweep, s,
-              hipLaunchKernelGGL(k_upsweep<uint32_t>, dim3((unsigned)nt), dim3(T), 0, s, rin, n, shift, pb.counts, nt));
+    hipLaunchKernelGGL(k_place_bases, dim3(1), dim3(256), 0, s, n, shift, pb.bases);
     PBH_CHECK_LAUNCH();
-    int st = exclusive_scan_u32(pb.counts, 256 * nt, pb.partials, s);
-    if (st != PBH_OK) return st;
+    PBH_CHECK_HIP(hipMemsetAsync(pb.status, 0, (size_t)nt * 256 * 8 + 256, s));  // words, counter, flag
     PBH_TIMED(kKPlaceScatter, s,
-              hipLaunchKernelGGL((k_scatter<uint32_t, double>), dim3((unsigned)nt), dim3(T), 0, s, rin, vin,
-                                 pb.rows[cur], pb.vals[cur], n, shift, pb.counts, nt));
+              launch_onesweep<uint32_t, double>(rin, vin, pb.rows[cur], pb.vals[cur], n, shift, pb.bases, pb.status,
+                                                (uint32_t*)(pb.status + nt * 256), s));
     PBH_CHECK_LAUNCH();
     rin = pb.rows[cur];
     vin = pb.vals[cur];
@@ -751,7 +713,7 @@ int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, in
   const int64_t nb = (n + kPlaceRows - 1) / kPlaceRows;
   PBH_TIMED(kKPlace, s, hipLaunchKernelGGL(k_place, dim3((unsigned)nb), dim3(T), 0, s, rin, vin, n, y, y_rs));
   PBH_CHECK_LAUNCH();
-  if (onesweep_enabled() && bits > kPlaceShift) {
+  if (bits > kPlaceShift) {
     uint32_t stuck = 0;
     PBH_CHECK_HIP(hipMemcpyAsync(&stuck, (uint32_t*)(pb.status + nt * 256) + 1, 4, hipMemcpyDeviceToHost, s));
     PBH_CHECK_HIP(hipStreamSynchronize(s));
@@ -767,7 +729,6 @@ bool code_buckets_enabled(int64_t n) {
   const char* e = getenv("PBH_STEP4");  // read per call: "buckets" forces, "lsd" disables
   if (e && strcmp(e, "buckets") == 0) return n >= 2 && n < ((int64_t)1 << 32);
   if (e && strcmp(e, "lsd") == 0) return false;
-  if (!onesweep_enabled()) return false;
   return n >= ((int64_t)1 << 22) && n <= (int64_t)110000000;  // mean bucket <= ~1700 of the 2048 cap
 }
 
@@ -895,44 +856,25 @@ int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, cons
   }
   if (npass == 0) passes[npass++] = 0;  // all keys equal: one pass yields the identity payload
   int cur = 0;
-  if (onesweep_enabled()) {
-    hipLaunchKernelGGL(k_digit_bases, dim3(NB), dim3(256), 0, s, b.hist, b.bases);
-    PBH_CHECK_LAUNCH();
-    PBH_CHECK_HIP(hipMemsetAsync(b.status + nt * 256, 0, 256, s));  // tile counter + stuck flag
-    for (int ip = 0; ip < npass; ++ip) {
-      const int shift = 8 * passes[ip];
-      PBH_CHECK_HIP(hipMemsetAsync(b.status, 0, (size_t)nt * 256 * 8 + 4, s));  // words + tile counter
-      PBH_TIMED(NB == 8 ? kKSortScatter : kKSortScatter32, s,
-                launch_onesweep<K, uint32_t>(ip == 0 ? first : keys[cur], ip == 0 ? nullptr : b.vals[cur],
-                                             keys[cur ^ 1], b.vals[cur ^ 1], n, shift, b.bases + passes[ip] * 256,
-                                             b.status, (uint32_t*)(b.status + nt * 256), s));
-      PBH_CHECK_LAUNCH();
-      cur ^= 1;
-    }
-    uint32_t stuck = 0;
-    PBH_CHECK_HIP(hipMemcpyAsync(&stuck, (uint32_t*)(b.status + nt * 256) + 1, 4, hipMemcpyDeviceToHost, s));
-    PBH_CHECK_HIP(hipStreamSynchronize(s));
-    if (stuck) {
-      set_error("radix sort: one-sweep look-back did not complete");
-      return PBH_ERR_HIP;
-    }
-    *out_buf = cur;
-    return PBH_OK;
-  }
+  hipLaunchKernelGGL(k_digit_bases, dim3(NB), dim3(256), 0, s, b.hist, b.bases);
+  PBH_CHECK_LAUNCH();
+  PBH_CHECK_HIP(hipMemsetAsync(b.status + nt * 256, 0, 256, s));  // tile counter + stuck flag
   for (int ip = 0; ip < npass; ++ip) {
     const int shift = 8 * passes[ip];
-    PBH_TIMED(NB == 8 ? kKSortUpsweep : kKSortUpsweep32, s,
-              hipLaunchKernelGGL(k_upsweep<K>, dim3((unsigned)nt), dim3(T), 0, s, ip == 0 ? first : keys[cur], n,
-                                 shift, b.counts, nt));
-    PBH_CHECK_LAUNCH();
-    int st = exclusive_scan_u32(b.counts, 256 * nt, b.partials, s);
-    if (st != PBH_OK) return st;
+    PBH_CHECK_HIP(hipMemsetAsync(b.status, 0, (size_t)nt * 256 * 8 + 4, s));  // words + tile counter
     PBH_TIMED(NB == 8 ? kKSortScatter : kKSortScatter32, s,
-              hipLaunchKernelGGL(k_scatter<K>, dim3((unsigned)nt), dim3(T), 0, s, ip == 0 ? first : keys[cur],
-                                 ip == 0 ? nullptr : b.vals[cur], keys[cur ^ 1], b.vals[cur ^ 1], n, shift, b.counts,
-                                 nt));
+              launch_onesweep<K, uint32_t>(ip == 0 ? first : keys[cur], ip == 0 ? nullptr : b.vals[cur],
+                                           keys[cur ^ 1], b.vals[cur ^ 1], n, shift, b.bases + passes[ip] * 256,
+                                           b.status, (uint32_t*)(b.status + nt * 256), s));
     PBH_CHECK_LAUNCH();
     cur ^= 1;
+  }
+  uint32_t stuck = 0;
+  PBH_CHECK_HIP(hipMemcpyAsync(&stuck, (uint32_t*)(b.status + nt * 256) + 1, 4, hipMemcpyDeviceToHost, s));
+  PBH_CHECK_HIP(hipStreamSynchronize(s));
+  if (stuck) {
+    set_error("radix sort: one-sweep look-back did not complete");
+    return PBH_ERR_HIP;
   }
   *out_buf = cur;
   return PBH_OK;

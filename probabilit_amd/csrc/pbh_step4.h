@@ -45,7 +45,6 @@ struct Step4Column {
   uint32_t* rows2;
   uint64_t* pairs[2];
   uint32_t* pcur[2];
-  uint32_t* segtp;  // tile map of the segmented finish output (k_seg_tiles)
 };
 
 size_t step4_gen_shared_bytes(int k);
@@ -53,8 +52,6 @@ size_t step4_gen_column_bytes(int64_t n);
 void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh);
 void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb);
 bool step4_gen_enabled(int64_t n);
-// the bucket finish scatters straight into the top row-placement level (PBH_STEP4_FUSED, default on)
-bool step4_fused();
 // columns of step 4 run concurrently on this many streams (PBH_STEP4_STREAMS, default 3, at
 // most kStep4MaxStreams), each with its own Step4Column staging, so that one column's VALU- or
 // latency-bound kernels (bucket finish, gen_place) overlap another's bandwidth-bound passes
@@ -66,7 +63,7 @@ extern int g_serial;  // pbh_set_serial (measurement mode: one lane, counts not 
 hipStream_t step4_side_stream(int i);
 void step4_sync_side_streams();
 // top-16 histograms, bucket starts and flatness of the code columns c0 .. c0 + kk - 1 (column c
-// at codes + (c - c0) * ldc).  With cs (column c at cs + (c - c0) * ldcs; PBH_ADAPT=0 disables),
+// at codes + (c - c0) * ldc).  With cs (column c at cs + (c - c0) * ldcs),
 // a column that is not flat is re-coded with its adaptive code map and counted again, all on
 // the device (the codes are rewritten in place); state / flags then hold the final verdict.
 int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,
@@ -75,8 +72,8 @@ int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs,
 // rare re-coded column's passes overlap the other lanes; ~6 launches that exit at once otherwise
 int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,
                     int c0, int kk, hipStream_t s);
-// code passes and bucket finish of column c: (row << 32 | p') pairs in cb.pairs[0], in position
-// order, or (step4_fused) grouped by the top row-placement level
+// code passes and bucket finish of column c: (row << 32 | p') pairs in cb.pairs[0], grouped by
+// the top row-placement level
 int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, const Step4Shared& sh,
                      const Step4Column& cb, hipStream_t s);
 // row-placement MSD passes on cb.pairs[0]; *out_buf = the pairs buffer grouped by 4096-row block

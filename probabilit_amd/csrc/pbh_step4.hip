@@ -39,19 +39,8 @@ constexpr int kIptP = 16;
 constexpr int kTileP = kT * kIptP;  // placement tiles: 4096 pairs (divides every group size 2^s >= 2^12)
 constexpr int kBucketCap2 = 2048;   // items per top-16 bucket a wave can finish
 constexpr int kRunCap = 16;         // longest run of equal codes the finish orders
-// Cursor spacing (u32 words) of the code-pass and finish cursors: atomics on neighbouring lines
-// also share a memory channel; PBH_CUR_PAD (power of two, default 16 = one 64-byte line) spreads
-// them further.
-static int cur_pad() {
-  static const int v = [] {
-    const char* e = getenv("PBH_CUR_PAD");
-    int x = e ? atoi(e) : 16;
-    int p = 1;
-    while (p < x && p < 4096) p <<= 1;
-    return p;
-  }();
-  return v;
-}
+// Cursor spacing (u32 words) of the code-pass and finish cursors: one 64-byte line each.
+static int cur_pad() { return 16; }
 
 __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh /* >= 256 + waves */) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -625,381 +614,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8))) void k_
   }
 }
 
-// ---------------------------------------------------------------- bucket finish
-// One wave per top-16 bucket: the low 16 bits and rows in registers (32 items per lane), a
-// non-stable LDS-atomic pass on the low byte and a stable ballot-ranked pass on the high byte
-// give the code order; runs of equal codes are put in CS order (exact ties flagged); every
-// position p then leaves as (row << 32 | p') with p' = the start of the bucket + p, or, inside a
-// group of exact ties [s, e], s + (e - s) / 2 (the int of the 'average' rank, minus one).
-constexpr int kWB = kBucketCap2 / 64;
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-struct WaveBucket2 {
-  uint16_t key[kBucketCap2];
-  uint32_t row[kBucketCap2];
-  uint8_t eq[kBucketCap2];
-  uint32_t cnt[256];
-  uint16_t runs[256];
-};
-
-__device__ __forceinline__ void wb_scan_counts(WaveBucket2& B) {
-  const int lane = threadIdx.x & 63;
-  uint32_t v[4], sum = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    v[q] = B.cnt[lane * 4 + q];
-    sum += v[q];
-  }
-  uint32_t incl = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
-  }
-  uint32_t run = incl - sum;
-  wave_sync();
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    B.cnt[lane * 4 + q] = run;
-    run += v[q];
-  }
-  wave_sync();
-}
-
-template <int R>
-__device__ __forceinline__ bool resolve_run2(WaveBucket2& B, int p, int L, const double* __restrict__ x) {
-  uint32_t rr[R];
-  double v[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    rr[j] = j < L ? B.row[p + j] : 0u;
-    v[j] = j < L ? x[rr[j]] : 0.0;
-  }
-  bool any_tie = false;
-#pragma unroll
-  for (int q = 0; q < R; ++q) {
-    int pos = 0;
-    bool tie = false;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const bool other = j < L && j != q;
-      pos += (other && (v[j] < v[q] || (v[j] == v[q] && j < q))) ? 1 : 0;
-      tie |= other && v[j] == v[q] && j < q;
-    }
-    if (q < L) {
-      B.row[p + pos] = rr[q];
-      B.eq[p + pos] = tie ? 1 : 0;
-      any_tie |= tie;
-    }
-  }
-  return any_tie;
-}
-
-constexpr int kBFWaves = 2;
-
-__global__ __launch_bounds__(64 * kBFWaves) void k_finish(const uint16_t* __restrict__ keys,
-                                                          const uint32_t* __restrict__ rows,
-                                                          const double* __restrict__ x,
-                                                          const uint32_t* __restrict__ start,
-                                                          uint64_t* __restrict__ out, int32_t* __restrict__ flags,
-                                                          const int32_t* __restrict__ state) {
-  if (*state) return;
-  __shared__ WaveBucket2 wb[kBFWaves];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  WaveBucket2& B = wb[w];
-  const int bkt = blockIdx.x * kBFWaves + w;
-  if (bkt >= 65536) return;
-  const int64_t s = start[bkt];
-  const int len = (int)((int64_t)start[bkt + 1] - s);  // <= kBucketCap2 (k_hist16_scan)
-  if (len == 0) return;
-  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  uint32_t k[kWB], r[kWB];
-#pragma unroll
-  for (int j = 0; j < kWB; ++j) {
-    const int p = j * 64 + lane;
-    k[j] = p < len ? (uint32_t)keys[s + p] : 0u;
-    r[j] = p < len ? rows[s + p] : 0u;
-  }
-  // pass 1, low byte: LDS atomics (not stable: equal low and high bytes = equal codes, a run)
-#pragma unroll
-  for (int q = 0; q < 4; ++q) B.cnt[lane * 4 + q] = 0;
-  wave_sync();
-  uint32_t rank[kWB];
-#pragma unroll
-  for (int j = 0; j < kWB; ++j) rank[j] = (j * 64 + lane < len) ? atomicAdd(&B.cnt[k[j] & 255u], 1u) : 0u;
-  wave_sync();
-  wb_scan_counts(B);
-#pragma unroll
-  for (int j = 0; j < kWB; ++j) {
-    if (j * 64 + lane < len) {
-      const uint32_t lp = B.cnt[k[j] & 255u] + rank[j];
-      B.key[lp] = (uint16_t)k[j];
-      B.row[lp] = r[j];
-    }
-  }
-  wave_sync();
-#pragma unroll
-  for (int j = 0; j < kWB; ++j) {
-    const int p = j * 64 + lane;
-    k[j] = p < len ? B.key[p] : 0u;
-    r[j] = p < len ? B.row[p] : 0u;
-  }
-  wave_sync();
-  // pass 2, high byte: stable (ballot peer matching against LDS digit counters)
-#pragma unroll
-  for (int q = 0; q < 4; ++q) B.cnt[lane * 4 + q] = 0;
-  wave_sync();
-#pragma unroll
-  for (int j = 0; j < kWB; ++j) {
-    const bool valid = j * 64 + lane < len;
-    const uint32_t d = (k[j] >> 8) & 255u;
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int bb = 0; bb < 8; ++bb) {
-      const uint64_t m = __ballot(valid && ((d >> bb) & 1u));
-      peers &= ((d >> bb) & 1u) ? m : ~m;
-    }
-    const uint32_t below = (uint32_t)__popcll(peers & lt);
-    const uint32_t c = valid ? B.cnt[d] : 0u;
-    rank[j] = c + below;
-    if (valid && below == 0) B.cnt[d] = c + (uint32_t)__popcll(peers);
-  }
-  wave_sync();
-  wb_scan_counts(B);
-#pragma unroll
-  for (int j = 0; j < kWB; ++j) {
-    if (j * 64 + lane < len) {
-      const uint32_t lp = B.cnt[(k[j] >> 8) & 255u] + rank[j];
-      B.key[lp] = (uint16_t)k[j];
-      B.row[lp] = r[j];
-    }
-  }
-  wave_sync();
-  // runs of equal codes, compacted into B.runs
-  int nrun = 0;
-#pragma unroll 4
-  for (int j = 0; j < kWB; ++j) {
-    const int p = j * 64 + lane;
-    bool st = false;
-    if (p < len) {
-      const uint16_t c = B.key[p];
-      st = p + 1 < len && B.key[p + 1] == c && (p == 0 || B.key[p - 1] != c);
-      B.eq[p] = 0;
-    }
-    const uint64_t m = __ballot(st);
-    const int slot = nrun + (int)__popcll(m & lt);
-    if (st && slot < 256) B.runs[slot] = (uint16_t)p;
-    nrun += (int)__popcll(m);
-  }
-  wave_sync();
-  if (nrun > 256) {
-    if (lane == 0) atomicOr(flags, 1);
-    return;
-  }
-  bool any_tie = false;
-  for (int i = lane; i < nrun; i += 64) {
-    const int p = B.runs[i];
-    const uint16_t c = B.key[p];
-    int L = 2;
-    while (p + L < len && B.key[p + L] == c && L <= kRunCap) ++L;
-    if (L > kRunCap) {
-      atomicOr(flags, 1);
-      continue;
-    }
-    if (L <= 4)
-      any_tie |= resolve_run2<4>(B, p, L, x);
-    else
-      any_tie |= resolve_run2<kRunCap>(B, p, L, x);
-  }
-  const bool ties = __ballot(any_tie) != 0ull;
-  wave_sync();
-#pragma unroll 4
-  for (int j = 0; j < kWB; ++j) {
-    const int p = j * 64 + lane;
-    if (p < len) {
-      int pp = p;
-      if (ties && (B.eq[p] || (p + 1 < len && B.eq[p + 1]))) {  // inside a group of exact ties
-        int a = p, e = p;
-        while (a > 0 && B.eq[a]) --a;
-        while (e + 1 < len && B.eq[e + 1]) ++e;
-        pp = a + (e - a) / 2;
-      }
-      out[s + p] = ((uint64_t)B.row[p] << 32) | (uint64_t)(uint32_t)(s + pp);
-    }
-  }
-}
-
 // ---------------------------------------------------------------- counting finish, fused row pass
-// One 256-thread block finishes kFBuckets consecutive top-16 buckets, one after the other, and
-// then scatters their (row << 32 | p') pairs straight into the groups of the first row-placement
-// level (row >> s_top; group g at positions [g << s_top, ...), closed form since the rows are a
+// One 512-thread block finishes two consecutive top-16 buckets, one after the other, and then
+// scatters their (row << 32 | p') pairs straight into the groups of the first row-placement level
+// (row >> s_top; group g at positions [g << s_top, ...), closed form since the rows are a
 // permutation), so the pairs never exist in position order.  Per bucket:
-//   * a non-stable LDS-atomic counting pass on the top 12 of the 16 low code bits (4096 bins,
-//     ~0.4 items per bin at 1500 items per bucket) puts every bin together;
+//   * a non-stable LDS-atomic counting pass on the top 11 of the 16 low code bits (2048 bins,
+//     ~0.75 items per bin at 1500 items per bucket) puts every bin together;
 //   * every item counts, inside its bin, the items below it: lt = #{smaller low bits} +
 //     #{equal code (a run), smaller CS value}, eq = #{equal code, equal CS} (exact ties);
 //   * p' = bucket start + bin start + lt + eq / 2: the sorted position, or for a group of exact
 //     ties [a, a + eq] its 'average' rank minus one, truncated (rankdata(...).astype(int) - 1).
 // No order inside a bin is ever materialised, so neither pass needs to be stable.  A bin above
-// kBinCap items (far from the ~0.4 expected: a discrete spike) flags the column for the
-// general path.
-constexpr int kFIpt = kBucketCap2 / kT;  // items per thread per bucket (8)
+// kBinCap items (far from the expected: a discrete spike) flags the column for the general path.
 constexpr int kBinCap = 32;
 
-template <int FB, int BINS>
-union FinishLds {
-  struct {
-    uint32_t cnt[BINS + 1];
-    uint16_t key[kBucketCap2];
-    uint32_t row[kBucketCap2];
-  } a;
-  uint64_t sv[FB * kBucketCap2];
-};
-
-// FB buckets per block (staging FB * kBucketCap2 pairs); BINS counting bins on the top
-// log2(BINS) of the 16 low code bits.  Kept for the segmented XCD-class output (PBH_FINISH_XCD=1);
-// the closed-form layout takes k_finish_q.
-template <int FB, int BINS>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void k_finish_fused(const uint16_t* __restrict__ keys,
-                                                     const uint32_t* __restrict__ rows,
-                                                     const double* __restrict__ x,
-                                                     const uint32_t* __restrict__ start, int s_top,
-                                                     uint32_t* __restrict__ gcur, int cpad, uint32_t segcap,
-                                                     uint64_t* __restrict__ out,
-                                                     int32_t* __restrict__ flags,
-                                                     const int32_t* __restrict__ state) {
-  if (*state) return;
-  constexpr int kShift = 16 - __builtin_ctz(BINS);  // bin = key >> kShift
-  constexpr int kPer = BINS / kT;                   // bins per thread in the scan
-  __shared__ FinishLds<FB, BINS> L;
-  __shared__ uint32_t gcnt[256], goff[264], gbase[256];
-  __shared__ int bad;
-  const int t = threadIdx.x;
-  if (t == 0) bad = 0;
-  gcnt[t] = 0;
-  uint64_t pr[FB * kFIpt];
-  uint32_t grk[FB * kFIpt];
-  int total = 0;
-  auto load = [&](int bkt, uint32_t* kk, uint32_t* rr) {
-    const int64_t s0 = start[bkt];
-    const int l0 = (int)((int64_t)start[bkt + 1] - s0);
-#pragma unroll
-    for (int j = 0; j < kFIpt; ++j) {
-      const int p = j * kT + t;
-      kk[j] = p < l0 ? (uint32_t)keys[s0 + p] : 0u;
-      rr[j] = p < l0 ? rows[s0 + p] : 0u;
-    }
-  };
-#pragma unroll
-  for (int bb = 0; bb < FB; ++bb) {
-    const int bkt = blockIdx.x * FB + bb;
-    const int64_t s = start[bkt];
-    const int len = (int)((int64_t)start[bkt + 1] - s);  // <= kBucketCap2 (k_hist16_scan)
-    for (int i = t; i <= BINS; i += kT) L.a.cnt[i] = 0;
-    uint32_t k[kFIpt], r[kFIpt], rk[kFIpt];
-    load(bkt, k, r);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kFIpt; ++j) rk[j] = (j * kT + t < len) ? atomicAdd(&L.a.cnt[k[j] >> kShift], 1u) : 0u;
-    __syncthreads();
-    // exclusive prefix over the bins: thread t owns bins kPer t .. kPer t + kPer - 1
-    uint32_t cb[kPer], sum = 0;
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-      cb[q] = L.a.cnt[kPer * t + q];
-      sum += cb[q];
-    }
-    uint32_t run = block_excl_scan256(sum, goff);
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-      L.a.cnt[kPer * t + q] = run;
-      run += cb[q];
-    }
-    if (t == kT - 1) L.a.cnt[BINS] = run;  // == len
-    __syncthreads();
-    uint32_t pos[kFIpt];
-#pragma unroll
-    for (int j = 0; j < kFIpt; ++j) {
-      if (j * kT + t < len) {
-        pos[j] = L.a.cnt[k[j] >> kShift] + rk[j];
-        L.a.key[pos[j]] = (uint16_t)k[j];
-        L.a.row[pos[j]] = r[j];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kFIpt; ++j) {
-      const int slot = bb * kFIpt + j;
-      if (j * kT + t >= len) {
-        pr[slot] = ~0ull;
-        continue;
-      }
-      const uint32_t bs = L.a.cnt[k[j] >> kShift], be = L.a.cnt[(k[j] >> kShift) + 1];
-      uint32_t lt = 0, eq = 0;
-      if (be - bs > 1) {
-        if (be - bs > (uint32_t)kBinCap) bad = 1;
-        bool have = false;
-        double xv = 0.0;
-        for (uint32_t m = bs; m < be; ++m) {
-          const uint32_t km = L.a.key[m];
-          lt += km < k[j];
-          if (km == k[j] && m != pos[j]) {  // a run of equal codes: order by the CS value
-            if (!have) {
-              xv = x[r[j]];
-              have = true;
-            }
-            const double xm = x[L.a.row[m]];
-            lt += xm < xv;
-            eq += xm == xv;
-          }
-        }
-      }
-      const uint32_t p = (uint32_t)s + bs + lt + eq / 2;
-      pr[slot] = ((uint64_t)r[j] << 32) | (uint64_t)p;
-      grk[slot] = atomicAdd(&gcnt[r[j] >> s_top], 1u);
-    }
-    total += len;
-    __syncthreads();  // the bucket's LDS is reused by the next one
-  }
-  // scatter into the row groups: one cursor add per (block, group)
-  const uint32_t my = gcnt[t];
-  const uint32_t ex = block_excl_scan256(my, goff);
-  goff[t] = ex;
-  if (segcap) {  // XCD-class segments: group t, class blockIdx.x mod 8 (see k_seg_tiles)
-    const uint32_t sg = ((uint32_t)t << 3) | (blockIdx.x & 7u);
-    uint32_t pos = my ? atomicAdd(&gcur[(int64_t)sg * cpad], my) : 0u;
-    if (my && pos + my > segcap) {  // past the segment's capacity: the column takes the general path
-      bad = 1;
-      gbase[t] = 0xFFFFFFFFu;
-    } else {
-      gbase[t] = sg * segcap + pos;
-    }
-  } else {
-    gbase[t] = my ? (uint32_t)(((uint64_t)t << s_top) + atomicAdd(&gcur[t * cpad], my)) : 0u;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int slot = 0; slot < FB * kFIpt; ++slot)
-    if (pr[slot] != ~0ull) L.sv[goff[(uint32_t)(pr[slot] >> (32 + s_top))] + grk[slot]] = pr[slot];
-  __syncthreads();
-  for (int p = t; p < total; p += kT) {
-    const uint64_t v = L.sv[p];
-    const uint32_t g = (uint32_t)(v >> (32 + s_top));
-    if (gbase[g] != 0xFFFFFFFFu) out[gbase[g] + ((uint32_t)p - goff[g])] = v;
-  }
-  __syncthreads();
-  if (t == 0 && bad) atomicOr(flags, 1);
-}
-
-// The counting finish over 512 threads (PBH_FINISH_CFG=29, the default): k_finish_ah's work with
-// 4 items of each bucket per thread instead of 8, so it fits 64 VGPRs and 8 waves per SIMD (the
-// 256-thread kernel needs ~100-120 VGPRs: 4 waves), which hides its latency far better (r3 A/B:
-// 23-24 against 28-30 ms per step).  The bin loop counts by code alone and marks the members of
+// The counting finish over 512 threads: 4 items of each bucket per thread, so it fits 64 VGPRs
+// and 8 waves per SIMD (the 256-thread form needed ~100-120 VGPRs: 4 waves), which hides its
+// latency far better (r3 A/B: 23-24 against 28-30 ms per step).  The bin loop counts by code alone and marks the members of
 // runs of equal codes; a second loop orders each run by CS value.  With Q the run members' CS
 // values are first loaded together into an LDS queue (one round trip per bucket instead of one
 // per item; a bucket whose runs hold more than kFQCap items reads the rest from global memory):
@@ -1188,135 +820,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
 // Input grouped by row >> s_in (closed-form groups: rows are a permutation of [0, n), so group
 // g occupies positions [g << s_in, ...)); tiles of kTileP never straddle a group.  Digit =
 // (row >> s_out) within the group; destination = positions (row >> s_out) << s_out.
-// SPLIT: the pairs staged as two 32-bit halves through one 16 KiB array.
-// seg != NULL: the input is the segmented output of k_finish_fused (XCD classes): segment i at
-// [i cap, i cap + min(segcur[i cpad], cap)), tiles of kTileP inside every segment, seg[i] = tiles
-// before segment i (seg[nseg] = all tiles); blocks past them exit.
-template <bool SPLIT>
-__global__ __launch_bounds__(kT) void k_place_msd(const uint64_t* __restrict__ in, int64_t n, int s_out,
-                                                  uint32_t* __restrict__ cur, uint64_t* __restrict__ out,
-                                                  const int32_t* __restrict__ state, const uint32_t* __restrict__ seg,
-                                                  const uint32_t* __restrict__ segcur, int cpad, uint32_t cap,
-                                                  int nseg) {
-  if (state && *state) return;
-  __shared__ uint32_t cnt[256], lst[264], gb[256];
-  __shared__ uint64_t sv[SPLIT ? 1 : kTileP];
-  __shared__ uint32_t sh32[SPLIT ? kTileP : 1];
-  __shared__ uint32_t gfirst;
-  __shared__ int64_t sbase;
-  __shared__ int sm;
-  const int t = threadIdx.x;
-  int64_t base;
-  int m;
-  if (seg) {
-    const uint32_t tile = blockIdx.x;
-    if (tile >= seg[nseg]) return;
-    if (t == 0) {  // the segment holding this tile: last i with seg[i] <= tile
-      int lo = 0, hi = nseg;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (seg[mid] <= tile)
-          lo = mid;
-        else
-          hi = mid - 1;
-      }
-      while (lo + 1 < nseg && seg[lo + 1] <= tile) ++lo;  // skip empty segments
-      const uint32_t len = min(segcur[(int64_t)lo * cpad], cap);
-      const uint32_t off = (tile - seg[lo]) * (uint32_t)kTileP;
-      sbase = (int64_t)lo * cap + off;
-      sm = (int)min(len - off, (uint32_t)kTileP);
-    }
-    __syncthreads();
-    base = sbase;
-    m = sm;
-  } else {
-    base = (int64_t)blockIdx.x * kTileP;
-    m = (int)((n - base) < kTileP ? (n - base) : kTileP);
-  }
-  cnt[t] = 0;
-  if (t == 0) gfirst = 0xFFFFFFFFu;
-  __syncthreads();
-  uint64_t v[kIptP];
-  uint32_t rk[kIptP], dg[kIptP];
-#pragma unroll
-  for (int j = 0; j < kIptP; ++j) {
-    const int p = j * kT + t;
-    v[j] = p < m ? in[base + p] : 0ull;
-    dg[j] = (uint32_t)(v[j] >> (32 + s_out));  // global destination id (row >> s_out)
-  }
-  // the tile's destinations span < 256 consecutive ids starting at its smallest
-  uint32_t mn = 0xFFFFFFFFu;
-#pragma unroll
-  for (int j = 0; j < kIptP; ++j)
-    if (j * kT + t < m) mn = dg[j] < mn ? dg[j] : mn;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t y = __shfl_xor(mn, o, 64);
-    mn = y < mn ? y : mn;
-  }
-  if ((t & 63) == 0) atomicMin(&gfirst, mn);
-  __syncthreads();
-  const uint32_t g0 = gfirst;
-#pragma unroll
-  for (int j = 0; j < kIptP; ++j) rk[j] = (j * kT + t < m) ? atomicAdd(&cnt[dg[j] - g0], 1u) : 0u;
-  __syncthreads();
-  const uint32_t my = cnt[t];
-  const uint32_t ex = block_excl_scan256(my, lst);
-  lst[t] = ex;
-  const uint32_t myb = my ? (uint32_t)(((uint64_t)(g0 + t) << s_out) + atomicAdd(&cur[g0 + t], my)) : 0u;
-  __syncthreads();  // (myb is stored to gb after the first scatter)
-  if constexpr (SPLIT) {
-    // round 1: the high halves (rows) give each slot's destination; round 2: the low halves
-    uint32_t dst[kIptP], hi[kIptP], slot[kIptP], lo[kIptP];
-#pragma unroll
-    for (int j = 0; j < kIptP; ++j) {
-      slot[j] = lst[dg[j] - g0] + rk[j];
-      lo[j] = (uint32_t)v[j];
-      if (j * kT + t < m) sh32[slot[j]] = (uint32_t)(v[j] >> 32);
-    }
-    gb[t] = myb;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kIptP; ++j) {
-      const int p = j * kT + t;
-      if (p < m) {
-        hi[j] = sh32[p];
-        const uint32_t d = (hi[j] >> s_out) - g0;
-        dst[j] = gb[d] + ((uint32_t)p - lst[d]);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kIptP; ++j)
-      if (j * kT + t < m) sh32[slot[j]] = lo[j];
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < kIptP; ++j) {
-      const int p = j * kT + t;
-      if (p < m) out[dst[j]] = ((uint64_t)hi[j] << 32) | sh32[p];
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < kIptP; ++j)
-      if (j * kT + t < m) sv[lst[dg[j] - g0] + rk[j]] = v[j];
-    gb[t] = myb;
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < kIptP; ++j) {
-      const int p = j * kT + t;
-      if (p < m) {
-        const uint64_t x = sv[p];
-        const uint32_t d = (uint32_t)(x >> (32 + s_out)) - g0;
-        out[gb[d] + ((uint32_t)p - lst[d])] = x;
-      }
-    }
-  }
-}
-
-// k_place_msd at 8 waves per SIMD (PBH_MSD_OCC=1, closed-form groups): the same 4096-pair tile
-// over 512 threads of 8 pairs each (k_place_msd<true>: 256 threads of 16, 100 VGPRs, 4 waves per
-// SIMD).  The low halves are staged first and read back in position order, then the high halves
-// (rows), which give the destination; the pair is written whole.
+// A 4096-pair tile over 512 threads of 8 pairs each, 8 waves per SIMD (the 256-thread form of 16
+// pairs needed 100 VGPRs: 4 waves; 13.4 against 13.1 ms per step).  The low halves are staged
+// first and read back in position order, then the high halves (rows), which give the
+// destination; the pair is written whole.
 constexpr int kTO = 512;
 constexpr int kIptO = kTileP / kTO;
 __global__ __launch_bounds__(kTO) __attribute__((amdgpu_waves_per_eu(8))) void k_place_msdo(
@@ -1386,34 +893,6 @@ __global__ __launch_bounds__(kTO) __attribute__((amdgpu_waves_per_eu(8))) void k
   }
 }
 
-// Tile map of the segmented finish output: tiles of kTileP in every segment (count = its cursor,
-// capped at cap; a segment past its capacity flags the column), exclusive prefix in seg[0..nseg].
-__global__ __launch_bounds__(256) void k_seg_tiles(const uint32_t* __restrict__ segcur, int cpad, uint32_t cap,
-                                                   int nseg, uint32_t* __restrict__ seg, int32_t* __restrict__ flags) {
-  __shared__ uint32_t sh[264];
-  const int t = threadIdx.x;
-  constexpr int kPer = 2048 / 256;  // nseg <= 8 x 256
-  uint32_t v[kPer], sum = 0;
-  bool over = false;
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const int i = t * kPer + q;
-    const uint32_t c = i < nseg ? segcur[(int64_t)i * cpad] : 0u;
-    over |= c > cap;
-    v[q] = ((c < cap ? c : cap) + kTileP - 1) / kTileP;
-    sum += v[q];
-  }
-  uint32_t run = block_excl_scan256(sum, sh);
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const int i = t * kPer + q;
-    if (i < nseg) seg[i] = run;
-    run += v[q];
-  }
-  if (t == 255) seg[nseg] = run;
-  if (over) atomicOr(flags, 1);
-}
-
 // p_out[row] = p of the pairs (row << 32 | p) of every 4096-row block, assembled in LDS and
 // written contiguously: a row-sharded run's owner sends these sorted positions back (4 bytes a
 // row instead of the 8 of Y; the row owner regenerates sort(X)[p], gen_values_at)
@@ -1448,8 +927,6 @@ int place_positions(const uint64_t* pairs, int64_t n, uint32_t* p_out, const int
   return PBH_OK;
 }
 
-static int64_t fin_slots(int64_t n);
-
 size_t step4_gen_shared_bytes(int k) {
   // per column: hist 65536 + start 65537 + cur1 8 x 256 * pad + cur2 65536 + curF 256 * pad +
   // cls 2048 + cstart 2048 + tpre 257 + seghist + amap (u32), state / flags / retry
@@ -1462,7 +939,7 @@ size_t step4_gen_column_bytes(int64_t n) {
   // keys32 + rows (msd1 out) | keys16 + rows (msd2 out) | pairs x 2 | placement cursors
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const int64_t ncur = (n >> kGenPlaceShift) + 2;
-  return al((size_t)n * 4) * 2 + al((size_t)n * 2) + al((size_t)n * 4) + al((size_t)fin_slots(n) * 8) +
+  return al((size_t)n * 4) * 2 + al((size_t)n * 2) + al((size_t)n * 4) + al((size_t)n * 8) +
          al((size_t)n * 8) + al((size_t)ncur * 4) * 2 + al(2049 * 4);
 }
 
@@ -1508,7 +985,7 @@ void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb) {
   cb.rows2 = (uint32_t*)p;
   p += al((size_t)n * 4);
   cb.pairs[0] = (uint64_t*)p;
-  p += al((size_t)fin_slots(n) * 8);
+  p += al((size_t)n * 8);
   cb.pairs[1] = (uint64_t*)p;
   p += al((size_t)n * 8);
   const int64_t ncur = (n >> kGenPlaceShift) + 2;
@@ -1516,7 +993,6 @@ void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb) {
   p += al((size_t)ncur * 4);
   cb.pcur[1] = (uint32_t*)p;
   p += al((size_t)ncur * 4);
-  cb.segtp = (uint32_t*)p;
 }
 
 int g_serial = 0;  // pbh_set_serial: one lane, no deferred counts (standalone kernel durations)
@@ -1571,13 +1047,6 @@ static int msd_tile_log() {
   return v;
 }
 
-bool step4_fused() {
-  static const bool v = [] {
-    const char* e = getenv("PBH_STEP4_FUSED");  // "0": position-order finish + every placement level
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
 
 
 // MSD levels of the row placement: shifts from kGenPlaceShift up, at most 8 bits per level
@@ -1596,31 +1065,6 @@ static int place_levels(int64_t n, int* shifts) {
   for (int sh = kGenPlaceShift; sh < bits; sh += 8) shifts[nl++] = sh;
   if (top && nl == 2 && bits - 8 > shifts[0]) shifts[1] = bits - 8;
   return nl;
-}
-
-// Segment capacity of the XCD-class finish output (PBH_FINISH_XCD=1; off by default: measured
-// 171.8 against 169.5 ms per step with the closed-form layout, profiles/r02 j11): two row-placement
-// levels (n <= 2^28), each group of 2^s rows split into 8 class segments of cap = 2^s / 8 +
-// 8 sqrt(2^s) + 256 slots (a class holds ~1/8 of its group, sd ~ sqrt(2^s) / 3: overflow is a
-// > 20-sigma event, and it is caught); 0 = the closed-form group layout.
-static uint32_t fin_segcap(int64_t n) {
-  const char* e = getenv("PBH_FINISH_XCD");  // read per call (the tests switch it)
-  const bool on = e && e[0] == '1';
-  int shifts[4];
-  if (!on || !step4_fused() || place_levels(n, shifts) != 2) return 0;
-  const double size = (double)((int64_t)1 << shifts[1]);
-  if (const char* e = getenv("PBH_FINISH_SEGCAP")) return (uint32_t)atoll(e);  // tests: force an overflow
-  return (uint32_t)(size / 8 + 8 * sqrt(size) + 256);
-}
-
-static int64_t fin_slots(int64_t n) {  // pair slots of the finish output buffer
-  const uint32_t cap = fin_segcap(n);
-  if (!cap) return n;
-  int shifts[4];
-  place_levels(n, shifts);
-  const int64_t groups = ((n - 1) >> shifts[1]) + 1;
-  const int64_t slots = groups * 8 * (int64_t)cap;
-  return slots > n ? slots : n;
 }
 
 bool step4_gen_enabled(int64_t n) {
@@ -1676,11 +1120,6 @@ int step4_gen_adapt(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs
                     int c0, int kk, hipStream_t s) {
   PBH_REQUIRE(c0 >= 0 && kk >= 1 && c0 + kk <= sh.k, "step4_gen_adapt: columns [%d, %d) outside [0, %d)", c0,
               c0 + kk, sh.k);
-  static const bool adapt = [] {
-    const char* e = getenv("PBH_ADAPT");  // "0": a column that is not flat goes to the general path
-    return !(e && e[0] == '0');
-  }();
-  if (!adapt) return PBH_OK;
   const int cpad = cur_pad();
   const size_t cw = (size_t)8 * 256 * cpad;
   uint32_t* hist = sh.hist + (int64_t)c0 * 65536;
@@ -1740,11 +1179,7 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
   const int32_t* state = sh.state + c;
   const int tlog = msd_tile_log();
   const int64_t t1 = (n + ((int64_t)1 << tlog) - 1) >> tlog;
-  static const bool xcd = [] {  // PBH_MSD1_XCD=0: one cursor per top byte for every tile
-    const char* e = getenv("PBH_MSD1_XCD");
-    return !(e && e[0] == '0');
-  }();
-  const uint32_t* cst = xcd ? sh.cstart + (int64_t)c * 2048 : nullptr;
+  const uint32_t* cst = sh.cstart + (int64_t)c * 2048;  // per tile class cursors (k_msd1x)
   uint32_t* cur1 = sh.cur1 + (int64_t)c * 8 * 256 * cur_pad();
   uint32_t* cur2 = sh.cur2 + (int64_t)c * 65536;
   const uint32_t* tp = sh.tpre + (int64_t)c * 257;
@@ -1766,47 +1201,18 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
                                  start, tp, cur2, cb.keys16, cb.rows2, state));
   }
   PBH_CHECK_LAUNCH();
-  if (step4_fused()) {
+  {
     int shifts[4];
     const int nl = place_levels(n, shifts);
     const int s_top = nl ? shifts[nl - 1] : kGenPlaceShift;
-    // PBH_FINISH_CFG (A/B measurements, profiles/r03/ and r04/README_ab.md): 31 (default) =
     // k_finish_q over 512 threads, 2048 bins, the run members' CS values read in pass 2 (r4s-r4u:
-    // 23.2-23.6 against 23.9-24.5 ms per step with 1024 bins, 29; 512 bins measured 25.7-26.2);
-    // 28 = 1024 bins with those reads queued through LDS; 30 = queued, 2048 bins; 26 = 256 threads
-    // (round 2's k_finish_ah).
-    // (Both buckets' phases merged into one pass, ~10 barriers instead of ~21: 23.7-24.1 against
-    // 24.1-24.3 ms per step, within run-to-run noise; not kept.)
-    // The segmented XCD-class output (PBH_FINISH_XCD=1) always takes k_finish_fused.
-    static const int cfg = [] {
-      const char* e = getenv("PBH_FINISH_CFG");
-      return e ? atoi(e) : 31;
-    }();
+    // 23.2-23.6 against 23.9-24.5 ms per step with 1024 bins; 512 bins 25.7-26.2; the 256-thread
+    // form, the LDS-queued CS reads, both buckets' phases in one pass and the XCD-class segmented
+    // output were measured and removed: profiles/r03/, r04/README_ab.md)
     uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
-    const int cpad = cur_pad();
-    const uint32_t segcap = fin_segcap(n);
-#define PBH_FINQ(BINS, NT, Q)                                                                                    \
-  PBH_TIMED(kKFinish, s,                                                                                         \
-            hipLaunchKernelGGL((k_finish_q<BINS, NT, Q>), dim3(65536 / 2), dim3(NT), 0, s, cb.keys16, cb.rows2, cs, \
-                               start, s_top, gc, cpad, cb.pairs[0], sh.flags + c, state))
-    if (segcap) {
-      PBH_TIMED(kKFinish, s,
-                hipLaunchKernelGGL((k_finish_fused<2, 4096>), dim3(65536 / 2), dim3(kT), 0, s, cb.keys16, cb.rows2, cs,
-                                   start, s_top, gc, cpad, segcap, cb.pairs[0], sh.flags + c, state));
-    } else {
-      switch (cfg) {
-        case 26: PBH_FINQ(1024, 256, false); break;
-        case 28: PBH_FINQ(1024, 512, true); break;
-        case 29: PBH_FINQ(1024, 512, false); break;
-        case 30: PBH_FINQ(2048, 512, true); break;
-        default: PBH_FINQ(2048, 512, false); break;
-      }
-    }
-#undef PBH_FINQ
-  } else {
     PBH_TIMED(kKFinish, s,
-              hipLaunchKernelGGL(k_finish, dim3(65536 / kBFWaves), dim3(64 * kBFWaves), 0, s, cb.keys16, cb.rows2, cs,
-                                 start, cb.pairs[0], sh.flags + c, state));
+              hipLaunchKernelGGL((k_finish_q<2048, 512, false>), dim3(65536 / 2), dim3(512), 0, s, cb.keys16,
+                                 cb.rows2, cs, start, s_top, gc, cur_pad(), cb.pairs[0], sh.flags + c, state));
   }
   PBH_CHECK_LAUNCH();
   return PBH_OK;
@@ -1817,40 +1223,16 @@ int step4_gen_place_passes(int c, int64_t n, const Step4Shared& sh, const Step4C
   int32_t* state = sh.flags + c;
   int shifts[4];
   int nl = place_levels(n, shifts);
-  if (step4_fused() && nl > 0) --nl;  // the finish scattered the top level
+  if (nl > 0) --nl;  // the finish scattered the top level
   int cur = 0;
   const int64_t tiles = (n + kTileP - 1) / kTileP;
-  const uint32_t segcap = fin_segcap(n);
-  const int cpad = cur_pad();
-  const uint32_t* segcur = sh.curF + (int64_t)c * 8 * 256 * cpad;
-  const int nseg = segcap ? (int)((((n - 1) >> shifts[1]) + 1) * 8) : 0;
-  if (segcap) {
-    hipLaunchKernelGGL(k_seg_tiles, dim3(1), dim3(256), 0, s, segcur, cpad, segcap, nseg, cb.segtp, state);
-    PBH_CHECK_LAUNCH();
-  }
   for (int l = nl - 1; l >= 0; --l) {
-    const bool sg = segcap && l == nl - 1;  // the first pass reads the finish's segments
-    const int64_t grid = sg ? tiles + nseg : tiles;
     const int64_t ncur = (n >> shifts[l]) + 1;
     uint32_t* cr = cb.pcur[l & 1];
     PBH_CHECK_HIP(hipMemsetAsync(cr, 0, (size_t)ncur * 4, s));
-    static const bool split = [] {  // PBH_PLACE_SPLIT=0: the pairs staged whole (32 KiB)
-      const char* e = getenv("PBH_PLACE_SPLIT");
-      return !(e && e[0] == '0');
-    }();
-    const uint32_t* segp = sg ? cb.segtp : nullptr;
-    if (!sg)  // 8 waves per SIMD (k_place_msd<true>: 4; 13.4 against 13.1 ms per step)
-      PBH_TIMED(kKPlaceMsd, s,
-                hipLaunchKernelGGL(k_place_msdo, dim3((unsigned)grid), dim3(kTO), 0, s, cb.pairs[cur], n, shifts[l], cr,
-                                   cb.pairs[cur ^ 1], state));
-    else if (split)
-      PBH_TIMED(kKPlaceMsd, s,
-                hipLaunchKernelGGL(k_place_msd<true>, dim3((unsigned)grid), dim3(kT), 0, s, cb.pairs[cur], n, shifts[l],
-                                   cr, cb.pairs[cur ^ 1], state, segp, segcur, cpad, segcap, nseg));
-    else
-      PBH_TIMED(kKPlaceMsd, s,
-                hipLaunchKernelGGL(k_place_msd<false>, dim3((unsigned)grid), dim3(kT), 0, s, cb.pairs[cur], n,
-                                   shifts[l], cr, cb.pairs[cur ^ 1], state, segp, segcur, cpad, segcap, nseg));
+    PBH_TIMED(kKPlaceMsd, s,
+              hipLaunchKernelGGL(k_place_msdo, dim3((unsigned)tiles), dim3(kTO), 0, s, cb.pairs[cur], n, shifts[l], cr,
+                                 cb.pairs[cur ^ 1], state));
     PBH_CHECK_LAUNCH();
     cur ^= 1;
   }

@@ -118,15 +118,9 @@ def test_generated_step4_run_heads_paths(gpu, monkeypatch, cap):
     assert_close(Y, ref["Y"], rtol=1e-10, what=f"poisson heads, cap={cap}")
 
 
-@pytest.mark.parametrize("env", [{}, {"PBH_FINISH_XCD": "1"}, {"PBH_FINISH_XCD": "1", "PBH_FINISH_SEGCAP": "100000"}])
-def test_generated_step4_finish_segments(gpu, monkeypatch, env):
-    """The bucket finish writes its (row, position) pairs into per-XCD-class segments of every
-    row group (PBH_FINISH_XCD=1, 2 placement levels: 2^20 < n <= 2^28), read back through a
-    tile map; the default is the closed-form group layout.  Either, and segments too small for
-    their class (PBH_FINISH_SEGCAP: the overflow flags every column, which the general path
-    redoes), give the same result, the oracle's."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+def test_generated_step4_two_placement_levels(gpu):
+    """2^20 < n <= 2^28: the bucket finish scatters into the top of two row-placement levels and
+    one MSD pass resolves the rest; indices and values are the oracle's."""
     from oracle.pipeline import cfg3_corr, cfg_dists
 
     n, d = 2**21 + 5, 3
@@ -134,7 +128,7 @@ def test_generated_step4_finish_segments(gpu, monkeypatch, env):
     Y, idx = _run(n, dists, 12, C)
     ref = _oracle(n, dists, 12, C)
     np.testing.assert_array_equal(idx, ref["idx"])
-    assert_close(Y, ref["Y"], rtol=1e-10, what=f"finish segments {env}")
+    assert_close(Y, ref["Y"], rtol=1e-10, what="two placement levels")
 
 
 def test_deferred_tie_check_redoes_the_call(gpu):
@@ -191,8 +185,7 @@ def _debug_run(n, dists, seed, C):
 @pytest.mark.timeout(900)
 def test_step4_variants_match_the_oracle(gpu, tmp_path):
     """Every A/B switch of the generated-column path, each in its own process (they are read
-    once): 4096-row code-pass tiles (PBH_MSD_TILE=4096), the 256-thread finish (PBH_FINISH_CFG=26),
-    the queued finish (28, 30), the 1024-bin finish (29; the default counts on 2048 bins), the whole gamma table in LDS
+    once): 4096-row code-pass tiles (PBH_MSD_TILE=4096), the whole gamma table in LDS
     (PBH_GAMMA_WIN=0), the placement levels' other split (PBH_PLACE_TOP=0), 64-row step-3 tiles
     (PBH_APPLY_ROWS=64), the poisson run heads from every stratum instead of the boundary search
     (PBH_DISCRETE_SCAN=1), the code histogram with the tile-class counts per code (PBH_HIST_CLASS=0),
@@ -211,8 +204,8 @@ def test_step4_variants_match_the_oracle(gpu, tmp_path):
     n, d, seed = 600_001, 8, 31
     dists, C = cfg_dists(d), cfg3_corr(d)
     ref = _oracle(n, dists, seed, C)
-    for env in ({"PBH_HIST_CLASS": "0"}, {"PBH_MSD_TILE": "4096", "PBH_FINISH_CFG": "26"}, {"PBH_FINISH_CFG": "28"}, {"PBH_FINISH_CFG": "29"},
-                {"PBH_FINISH_CFG": "30"}, {"PBH_GAMMA_WIN": "0"}, {"PBH_PLACE_TOP": "0"}, {"PBH_APPLY_ROWS": "64"},
+    for env in ({"PBH_HIST_CLASS": "0"}, {"PBH_MSD_TILE": "4096"}, {"PBH_GAMMA_WIN": "0"}, {"PBH_PLACE_TOP": "0"},
+                {"PBH_APPLY_ROWS": "64"},
                 {"PBH_DISCRETE_SCAN": "1"}, {"PBH_APPLY_W2": "0"}, {"PBH_APPLY_NT": "0"}, {"PBH_PLACE_RUNS": "0"}):
         dd = tmp_path / "_".join(f"{k}{v}" for k, v in env.items())
         dd.mkdir()

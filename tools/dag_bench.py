@@ -1,7 +1,7 @@
 """Fused-graph A/B timing: the cfg5 mutual fund (N=1e8, Sobol', gc_strategy None and [])
 through sample_device, wall time per call and the k_dag kernel's HIP-event time.
 
-    PBH_LIB_VARIANT=<v> python tools/dag_bench.py [--steps 3] [--rows 100000000]
+    python tools/dag_bench.py [--variant v] [--steps 3] [--rows 100000000]
 """
 
 import argparse
@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--variant", default="", help="load libprobabilit_hip_<variant>.so (build.py --variant)")
     a = ap.parse_args()
     import warnings
 
@@ -26,6 +27,9 @@ def main():
 
     from bench_configs import kernel_ms
     from probabilit_amd import _lib, dag, device
+
+    if a.variant:
+        _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), f"libprobabilit_hip_{a.variant}.so")
     from probabilit_amd.modeling import Distribution
 
     warnings.filterwarnings("ignore", message=".*balance properties of Sobol.*")
@@ -47,7 +51,7 @@ def main():
             pass
         if len(good) == a.steps + 1:
             break
-    out = {"variant": os.environ.get("PBH_LIB_VARIANT", ""), "dag": os.environ.get("PBH_DAG", "1"), "rows": a.rows}
+    out = {"variant": a.variant, "dag": os.environ.get("PBH_DAG", "1"), "rows": a.rows}
     for gc, label in [([], "gc_sink"), (None, "gc_none")]:
         sink = fund()
         sink.sample_device(a.rows, random_state=good[0], method="sobol", gc_strategy=gc)
