@@ -266,6 +266,19 @@ def _all_gather_varlen(t, group, world, sizes=None):
     return torch.cat([p[:s] for p, s in zip(parts, sizes)]).to(dev)
 
 
+def gather_block(block, n, group, world):
+    """The (K, n) block of every rank's row shard (block: this rank's (K, rows), shards by
+    shard_bounds), on every rank: the general correlators (Iman-Conover on materialised
+    quantiles, Cholesky, Permutation, a user class) then run on the whole block, identically on
+    every rank, and each keeps its rows."""
+    import torch
+
+    b = shard_bounds(n, world)
+    sizes = [b[r + 1] - b[r] for r in range(world)]
+    return torch.stack([_all_gather_varlen(block[j].contiguous(), group, world, sizes=sizes)
+                        for j in range(block.shape[0])])
+
+
 def _all_gather_rows(t, group, world):
     """(world, *t.shape) stack of every rank's `t` (same shape everywhere)."""
     import torch

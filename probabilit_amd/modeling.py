@@ -423,9 +423,6 @@ class Node(abc.ABC):
                      and all_set <= isn_set
                      and all(type(v) is Distribution and v.distr in _FUSED_LHS and v.is_leaf
                              for v in all_variables))
-        if world > 1 and correlations and not generated:
-            raise NotImplementedError("row-sharded evaluation correlates natively generated LHS columns of leaf "
-                                      "Distributions with Iman-Conover; evaluate this graph on one GPU")
         deferred = {}
         if correlations and all_set <= isn_set and not generated:
             block = device.empty((len(all_variables), size))
@@ -511,6 +508,24 @@ class Node(abc.ABC):
                     Y = inst._transform_generated(cols, size)
                     for j, var in enumerate(all_variables):
                         var._set_device(Y[j])
+                elif world > 1:
+                    # any other correlator on row shards: every rank gathers the whole correlated
+                    # block, runs the correlator on it as one process would (identically on every
+                    # rank: same inputs, same kernels, same seeds) and keeps its own rows
+                    from .distributed import gather_block
+
+                    assert block is not None  # every correlated variable is an ISN (checked above)
+                    full = gather_block(block, source.n, group, world)
+                    r0, r1 = source.row0, source.row0 + size
+                    if isinstance(inst, (ImanConover, Cholesky, PermutationCorrelator)):
+                        Yf = inst._transform_device(full, ev)
+                        for j, var in enumerate(all_variables):
+                            var._set_device(Yf[j, r0:r1].clone())
+                    else:  # a user correlator class: the reference's (N, K) ndarray protocol
+                        Yh = inst(device.to_host(full).T)
+                        for var, col in zip(all_variables, Yh.T):
+                            var.samples_ = np.copy(col[r0:r1])
+                    del full
                 elif isinstance(inst, (ImanConover, Cholesky, PermutationCorrelator)):
                     Y = inst._transform_device(block, ev)
                     for j, var in enumerate(all_variables):

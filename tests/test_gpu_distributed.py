@@ -149,6 +149,11 @@ def _dag(kind):
               Distribution("weibull_min", c=1.7), dists.PERT(1, 2, 9, gamma=10),
               Distribution("binom", n=12, p=0.6, loc=0.5)]  # non-integer loc: the exact count path
         return NoOp(*ds).correlate(*ds, corr_mat=_target(len(ds))), "lhs"
+    if kind in ("sobol_ic", "cholesky", "ref_ic"):  # correlators on materialised quantiles: gathered block
+        ds = [Distribution("norm", loc=1.0, scale=2.0), Distribution("gamma", a=2.0), Distribution("beta", a=2.0, b=3.0),
+              Distribution("poisson", mu=4.0)]
+        C = np.array([[1.0, 0.5, 0.3, 0.2], [0.5, 1.0, 0.4, 0.1], [0.3, 0.4, 1.0, 0.3], [0.2, 0.1, 0.3, 1.0]])
+        return NoOp(*ds).correlate(*ds, corr_mat=C), "sobol" if kind == "sobol_ic" else "lhs"
     if kind == "refstream":  # the reference's own LHS stream: each rank decodes it whole, keeps its rows
         ds = [Distribution("norm", loc=1.0, scale=2.0), Distribution("gamma", a=2.0), Distribution("beta", a=2.0, b=3.0)]
         return NoOp(*ds), "lhs"
@@ -156,6 +161,10 @@ def _dag(kind):
     for _ in range(20):  # README mutual-fund loop (BASELINE config 5)
         r = r * Distribution("norm", loc=1.11, scale=0.15) + 1200
     return r, "sobol"
+
+
+_DAG_KINDS = ("correlated", "fund", "ext", "refstream", "sobol_ic", "cholesky", "ref_ic")
+_DAG_KW = {"refstream": {"stream": "reference"}, "ref_ic": {"stream": "reference"}, "cholesky": {"correlator": "cholesky"}}
 
 
 def _dag_worker(rank, world, port, outdir):
@@ -166,10 +175,10 @@ def _dag_worker(rank, world, port, outdir):
     try:
         from probabilit_amd import device
 
-        for kind in ("correlated", "fund", "ext", "refstream"):
+        for kind in _DAG_KINDS:
             root, method = _dag(kind)
             out = root.sample_device(1 << 16, random_state=7, method=method, group=dist.group.WORLD,
-                                     stream="reference" if kind == "refstream" else None)
+                                     **_DAG_KW.get(kind, {}))
             if kind == "fund":
                 np.save(os.path.join(outdir, f"{kind}{rank}.npy"), device.to_host(out))
             else:
@@ -182,16 +191,17 @@ def _dag_worker(rank, world, port, outdir):
 def test_dag_row_sharded_world2_matches_one_process(gpu):
     """Node.sample_device(..., group=) with two ranks: every node's rows equal the same rows
     of the one-process evaluation (Sobol and LHS counter-addressed by global row; the reference
-    LHS stream decoded whole on each rank)."""
+    LHS stream decoded whole on each rank; Iman-Conover on Sobol' / reference-stream quantiles and
+    the Cholesky correlator on the gathered correlated block, identical on every rank)."""
     import torch.multiprocessing as mp
 
     from probabilit_amd.distributed import shard_bounds
 
     n = 1 << 16
     refs = {}
-    for kind in ("correlated", "fund", "ext", "refstream"):
+    for kind in _DAG_KINDS:
         root, method = _dag(kind)
-        out = root.sample(n, random_state=7, method=method, stream="reference" if kind == "refstream" else None)
+        out = root.sample(n, random_state=7, method=method, **_DAG_KW.get(kind, {}))
         if kind == "fund":
             refs[kind] = out
         else:
@@ -201,7 +211,7 @@ def test_dag_row_sharded_world2_matches_one_process(gpu):
         b = shard_bounds(n, 2)
         for r in range(2):
             np.testing.assert_array_equal(np.load(os.path.join(d, f"fund{r}.npy")), refs["fund"][b[r]:b[r + 1]])
-            for kind in ("correlated", "ext", "refstream"):
+            for kind in _DAG_KINDS[:1] + _DAG_KINDS[2:]:
                 for j, ref in enumerate(refs[kind]):
                     np.testing.assert_array_equal(np.load(os.path.join(d, f"{kind}{r}_v{j}.npy")), ref[b[r]:b[r + 1]])
 
