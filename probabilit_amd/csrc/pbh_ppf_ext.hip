@@ -97,9 +97,10 @@ __global__ void k_beta_guide_check(double a, double b, sfx::BetaGuide T, double*
 
 constexpr int kDiscreteTableMax = 1 << 16;  // CDF entries of a discrete distribution's table
 
-// the shape a of gammaincinv(a, q) behind chi (df / 2), maxwell (1.5), nakagami (nu), chi2 (df / 2)
+// the shape a of gammaincinv(a, q) behind chi (df / 2), maxwell (1.5), nakagami (nu), chi2 (df / 2),
+// and of gammainccinv(a, q) behind invgamma (a)
 inline double gamma_family_a(int dist, double s0) {
-  return dist == PBH_DIST_MAXWELL ? 1.5 : dist == PBH_DIST_NAKAGAMI ? s0 : 0.5 * s0;
+  return dist == PBH_DIST_MAXWELL ? 1.5 : (dist == PBH_DIST_NAKAGAMI || dist == PBH_DIST_INVGAMMA) ? s0 : 0.5 * s0;
 }
 constexpr bool is_gamma_family(int d) {
   return d == PBH_DIST_CHI || d == PBH_DIST_MAXWELL || d == PBH_DIST_NAKAGAMI || d == PBH_DIST_CHI2;
@@ -127,8 +128,16 @@ int discrete_table_len(int dist, const double* v) {
 // chi2 with a scalar shape -> gammaincinv's guide (pbh_ppf.hip gamma_guide_table); binom /
 // bernoulli / nbinom with scalar parameters -> [len, CDF (len), complement (len)]; the process
 // cache's (pbh_table_cache.hip) when it has room, callers end with release_table
+double* beta_guide_table(double a, double b, hipStream_t s);
+
 double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t s) {
-  if (is_gamma_family(dist)) {
+  if (dist == PBH_DIST_T) {  // stdtrit through I^-1(.; df / 2, 1 / 2): beta's guide of (df / 2, 1 / 2)
+    if (nparams < 1 || params[0].ptr) return nullptr;
+    const double df = params[0].value;
+    if (!(df > 0.0 && df < 1e5)) return nullptr;
+    return beta_guide_table(0.5 * df, 0.5, s);
+  }
+  if (is_gamma_family(dist) || dist == PBH_DIST_INVGAMMA) {
     if (dist != PBH_DIST_MAXWELL && (nparams < 1 || params[0].ptr)) return nullptr;
     return gamma_guide_table(gamma_family_a(dist, nparams ? params[0].value : 0.0), s);
   }
@@ -166,7 +175,10 @@ double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t 
     return t;
   }
   if (dist != PBH_DIST_BETA || nparams < 2 || params[0].ptr || params[1].ptr) return nullptr;
-  const double a = params[0].value, b = params[1].value;
+  return beta_guide_table(params[0].value, params[1].value, s);
+}
+
+double* beta_guide_table(double a, double b, hipStream_t s) {
   if (!(a > 0.0 && b > 0.0 && isfinite(a) && isfinite(b))) return nullptr;
   constexpr int m = sfx::kBetaGuideM;
   auto build = [=](double* t, hipStream_t st) {
@@ -196,9 +208,9 @@ sfx::BetaGuide guide_of(const double* t) {
 // Params4's view of build_table's table for `dist` (scalar parameters p.val)
 void attach_table(int dist, const double* t, Params4& p) {
   if (!t) return;
-  if (dist == PBH_DIST_BETA) {
+  if (dist == PBH_DIST_BETA || dist == PBH_DIST_T) {
     p.bg = guide_of(t);
-  } else if (is_gamma_family(dist)) {
+  } else if (is_gamma_family(dist) || dist == PBH_DIST_INVGAMMA) {
     const int m = sf::kGammaGuideM;
     const double a = gamma_family_a(dist, p.val[0]);
     p.gg = sf::GammaGuide{t, t + m, t + 2 * m, t + 3 * m, m, sf::kGammaGuideZ0, sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
@@ -448,6 +460,12 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
     if (!ok || !(q >= 0.0 && q <= 1.0)) return nan;
     if (q == 0.0) return lo * scale + loc;
     if (q == 1.0) return hi * scale + loc;
+    if constexpr (D == PBH_DIST_INVGAMMA) {
+      if (p.gg.y) return 1.0 / sf::igamci_guided(s0, q, &p.ga, p.gg) * scale + loc;  // 1 / gammainccinv
+    }
+    if constexpr (D == PBH_DIST_T) {
+      if (p.bg.z) return sfx::t_ppf_guided(q, s0, p.bg) * scale + loc;
+    }
     if constexpr (is_gamma_family(D)) {
       if (p.gg.y) {  // gammaincinv through the guide (igami_guided: within ~1e-12 of igami)
         const double g = sf::igami_guided(D == PBH_DIST_MAXWELL ? 1.5 : D == PBH_DIST_NAKAGAMI ? s0 : .5 * s0, q,

@@ -1123,6 +1123,26 @@ PBH_HD inline double igami_guided(double a, double p, const GammaAux* g, const G
   }
 }
 
+// igamci(a, q) = x with Q(a, x) = q through the same guide: P(a, x) = 1 - q has log-odds
+// log((1 - q) / q) = -w(q), exact without forming 1 - q, so the table needs no second copy; the
+// checked intervals' interpolant (~1e-12 in log x) or one Halley step on Q itself, else igamci.
+PBH_HD inline double igamci_guided(double a, double q, const GammaAux* g, const GammaGuide& T) {
+  if (!(q > 0.0 && q < 1.0)) return igamci(a, q);
+  const double w = -log_odds_at(q, &pbh_log_tab[0][0]);
+  const double u = (w - T.z0) * T.inv_h;
+  if (!(u >= 0.0 && u < (double)(T.m - 1))) return igamci(a, q);
+  const int j = (int)u;
+  const double y = guide_interp(T, j, u - (double)j);
+  if (!(y >= -680.0 && y <= 700.0)) return igamci(a, q);
+  const double x = exp_tab(y);
+  if (T.ok[j] != 0.0) return x;
+  const double fac = igam_fac(a, x, g);
+  if (fac == 0.0) return x;
+  const double f_fp = (igamc(a, x, g) - q) * x / (-fac);
+  const double fpp_fp = -1.0 + (a - 1) / x;
+  return isinf(fpp_fp) ? x - f_fp : x - f_fp / (1.0 - 0.5 * f_fp * fpp_fp);
+}
+
 // igami(a, p(w)), p(w) = 1 / (1 + e^-w); the upper half goes through the complement
 // Q = 1 / (1 + e^w) (igamci), which keeps every entry consistent with its w.  *p_out, *q_out:
 // p and 1 - p.

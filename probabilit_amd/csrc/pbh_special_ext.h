@@ -503,5 +503,21 @@ PBH_HD inline double t_ppf01(double q, double df) {
   return q < 0.5 ? -t : t;
 }
 
+// t_ppf01 with the incomplete-beta inverse of (df / 2, 1 / 2) read from beta's guide: z = logit x,
+// and t^2 = df (1 - x) / x = df e^-z for both of t_ppf01's branches (the upper one inverts the
+// complement, y = 1 - x, and y / (1 - y) is the same e^-z), so no 1 - x is ever formed.
+PBH_HD inline double t_ppf_guided(double q, double df, const BetaGuide& T) {
+  if (q == 0.5 || !(q > 0.0 && q < 1.0) || !(df > 0.0 && df < 1e5)) return t_ppf01(q, df);
+  const double pp = q < 0.5 ? 2.0 * q : 2.0 * (1.0 - q);
+  const double w = sf::log_odds_at(pp, &sf::pbh_log_tab[0][0]);
+  const double u = (w - kBetaGuideW0) * (1.0 / kBetaGuideH);
+  if (!(u >= 0.0 && u < (double)(kBetaGuideM - 1))) return t_ppf01(q, df);
+  const int j = (int)u;
+  if (T.ok[j] == 0.0) return t_ppf01(q, df);
+  const double z = sf::guide_interp_arr(T.z, T.d1, T.d2, kBetaGuideH, j, u - (double)j);
+  const double t = sqrt(df * exp(-z));
+  return q < 0.5 ? -t : t;
+}
+
 }  // namespace sfx
 }  // namespace pbh
