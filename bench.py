@@ -454,7 +454,19 @@ def reference_stream(root, seed, barrier, n=10_000_000, reps=2):
     d = root.num_distribution_nodes()
     dev, att, amb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
     _lib.check(_lib.load().pbh_lhs_reference_stats(ctypes.byref(dev), ctypes.byref(att), ctypes.byref(amb)))
+    # the stream alone: scipy's LatinHypercube(d, rng=seed).random(n) matrix, device-resident
+    from probabilit_amd import qmc
+
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(reps):
+        qmc.make_source("lhs", n, d, seed + 11 + i, stream="reference").matrix()
+    barrier()
+    ms_stream = (time.perf_counter() - t0) / reps * 1e3
     return {"value": round(n * d / (ms / 1e3) / 1e6, 2), "unit": "Msamples/s", "ms": round(ms, 1), "rows": n, "d": d,
+            "stream_only": {"value": round(n * d / (ms_stream / 1e3) / 1e6, 2), "unit": "Msamples/s",
+                            "ms": round(ms_stream, 1),
+                            "what": "LatinHypercube(d, rng=seed).random(n) alone (uniforms + shuffles + combine)"},
             "shuffles_on_device": bool(dev.value), "decode_attempts": att.value, "ambiguous_draws": amb.value,
             "what": "Node.sample_device(1e7, method='lhs', stream='reference'): same results as the reference on "
                     "the same seed (the shuffle stream decoded on the device), then ppf + Iman-Conover"}

@@ -26,8 +26,8 @@
 // the same target and M(q) = the first step to target position q from above, the value q held
 // before its own step is V(q) = V(M(q)), or q + 1 when nothing targeted it, and
 //   x[i] = V(S(i)) (or j_i + 1 when S(i) is none),   x[0] = V(M(0)) (or 1).
-// Counting sort of the steps by target, a sort of each (short) group, one pointer chase per
-// position: O(n) work, no sequential pass.
+// A stable radix sort of the steps by target (the library's one-sweep passes), one pass to link
+// each group, one pointer chase per position: O(n) work, no sequential pass.
 #include <math.h>
 #include <string.h>
 
@@ -37,6 +37,7 @@
 
 #include "pbh_error.h"
 #include "pbh_lhs_dev.h"
+#include "pbh_sort.h"
 #include "probabilit_hip.h"
 #include "pbh_timing.h"
 
@@ -127,38 +128,6 @@ __global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* __restrict_
     run += v;
   }
   if (t == 1023) out[m] = run;
-}
-
-__global__ __launch_bounds__(kT) void k_scan_blocksum(const uint32_t* __restrict__ in, int64_t m,
-                                                      uint32_t* __restrict__ bsum) {
-  __shared__ uint32_t sh[kT / 64];
-  const int64_t e0 = (int64_t)blockIdx.x * kBlk + (int64_t)threadIdx.x * kPer;
-  uint32_t s = 0;
-  for (int j = 0; j < kPer; ++j) s += e0 + j < m ? in[e0 + j] : 0u;
-  uint32_t tot;
-  (void)scan256(s, sh, &tot);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(kT) void k_scan_apply(const uint32_t* __restrict__ in, int64_t m,
-                                                   const uint32_t* __restrict__ bpre, int64_t nb,
-                                                   uint32_t* __restrict__ out) {
-  __shared__ uint32_t sh[kT / 64];
-  const int64_t e0 = (int64_t)blockIdx.x * kBlk + (int64_t)threadIdx.x * kPer;
-  uint32_t v[kPer], s = 0;
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    v[j] = e0 + j < m ? in[e0 + j] : 0u;
-    s += v[j];
-  }
-  uint32_t tot;
-  uint32_t run = bpre[blockIdx.x] + scan256(s, sh, &tot);
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    if (e0 + j < m) out[e0 + j] = run;
-    run += v[j];
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) out[m] = bpre[nb];
 }
 
 // ---------------------------------------------------------------- decode
@@ -396,49 +365,25 @@ __global__ void k_dec_seal(const int32_t* __restrict__ err, const int64_t* __res
 }
 
 // ---------------------------------------------------------------- targets -> permutation
-// One column at a time (its n targets J, 4 n-word arrays: resident in the 256 MB Infinity Cache
-// at n = 1e7), skipped unless the column's decode was sealed.
-__global__ __launch_bounds__(256) void k_perm_count(const int32_t* __restrict__ J, int64_t n,
-                                                    uint32_t* __restrict__ cnt, const int32_t* __restrict__ ok) {
+// One column at a time, skipped unless the column's decode was sealed.  The steps 1 .. n-1 are
+// sorted by target with the library's stable one-sweep radix passes (radix_sort_keys32_async:
+// within a target the steps stay ascending), so each target's group is contiguous and in time
+// order: S(step) = the next step of its group, M(q) = the group's first step above q.
+__global__ __launch_bounds__(256) void k_perm_links(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ idx,
+                                                    int64_t m, int32_t* __restrict__ S, int32_t* __restrict__ M,
+                                                    const int32_t* __restrict__ ok) {
   if (!*ok) return;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    if (i >= 1) atomicAdd(&cnt[J[i]], 1u);
-}
-
-__global__ __launch_bounds__(256) void k_perm_scatter(const int32_t* __restrict__ J, int64_t n,
-                                                      const uint32_t* __restrict__ off, uint32_t* __restrict__ cnt,
-                                                      int32_t* __restrict__ L, const int32_t* __restrict__ ok) {
-  if (!*ok) return;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    if (i >= 1) {
-      const int32_t g = J[i];
-      L[off[g] + atomicSub(&cnt[g], 1u) - 1u] = (int32_t)i;
-    }
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < m; k += (int64_t)gridDim.x * 256) {
+    const uint32_t t = keys[k];
+    const int32_t st = (int32_t)idx[k] + 1;  // key k is J[1 + k]
+    const int32_t nx = (k + 1 < m && keys[k + 1] == t) ? (int32_t)idx[k + 1] + 1 : -1;
+    S[st] = nx;
+    if (k == 0 || keys[k - 1] != t) M[t] = st != (int32_t)t ? st : nx;
   }
 }
 
-// each target's steps ascending; S (next step with the same target, in time = the next larger
-// index) and M (the first step to target q from above)
-__global__ __launch_bounds__(256) void k_perm_groups(const uint32_t* __restrict__ off, int32_t* __restrict__ L,
-                                                     int64_t n, int32_t* __restrict__ S, int32_t* __restrict__ M,
-                                                     const int32_t* __restrict__ ok) {
-  if (!*ok) return;
-  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
-    const uint32_t a = off[p], b = off[p + 1];
-    for (uint32_t k = a + 1; k < b; ++k) {  // insertion sort: groups hold ~ln(n / p) steps
-      const int32_t x = L[k];
-      uint32_t r = k;
-      while (r > a && L[r - 1] > x) {
-        L[r] = L[r - 1];
-        --r;
-      }
-      L[r] = x;
-    }
-    for (uint32_t k = a; k < b; ++k) S[L[k]] = k + 1 < b ? L[k + 1] : -1;
-    int32_t first = -1;
-    if (b > a) first = L[a] != (int32_t)p ? L[a] : (b - a > 1 ? L[a + 1] : -1);
-    M[p] = first;
-  }
+__global__ void k_flag_if(const uint32_t* __restrict__ word, int32_t* __restrict__ err, int32_t bit) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && *word) atomicOr(err, bit);
 }
 
 __global__ __launch_bounds__(256) void k_perm_values(const int32_t* __restrict__ M, int64_t n,
@@ -616,34 +561,30 @@ struct SideJoin {
 };
 
 struct PermBufs {
-  uint32_t *cnt, *off, *bsum, *bpre;
-  int32_t *L, *M;
+  SortBuffers sb;
+  int32_t *S, *V, *M;
 };
 
 // column c's permutation from its targets (J: n words), combined into q[0 .. n) (u on entry);
-// every kernel exits at once unless ok[0] (k_dec_seal)
-int column_to_q(const int32_t* J, int64_t n, const PermBufs& pb, const int32_t* ok, double* q, hipStream_t s) {
+// every kernel past the sort exits at once unless ok[0] (k_dec_seal)
+int column_to_q(const int32_t* J, int64_t n, PermBufs& pb, const int32_t* ok, int32_t* err, double* q,
+                hipStream_t s) {
+  const int64_t m = n - 1;  // steps 1 .. n-1
+  int bits = 1;
+  while (bits < 32 && ((int64_t)1 << bits) < n) ++bits;  // targets < n
+  int cur = 0;
+  uint32_t* stuck = nullptr;
+  if (int st = radix_sort_keys32_async(pb.sb, m, (bits + 7) / 8, s, &cur, (const uint32_t*)(J + 1), &stuck)) return st;
+  hipLaunchKernelGGL(k_flag_if, dim3(1), dim3(64), 0, s, stuck, err, 4);
+  PBH_CHECK_LAUNCH();
+  PBH_CHECK_HIP(hipMemsetAsync(pb.M, 0xFF, (size_t)n * 4, s));  // -1: no step targets q from above
   const unsigned grid = grid_for(n, 256, 1 << 16);
-  const unsigned gb = (unsigned)((n + kBlk - 1) / kBlk);
-  PBH_CHECK_HIP(hipMemsetAsync(pb.cnt, 0, (size_t)n * 4, s));
-  hipLaunchKernelGGL(k_perm_count, dim3(grid), dim3(256), 0, s, J, n, pb.cnt, ok);
+  hipLaunchKernelGGL(k_perm_links, dim3(grid), dim3(256), 0, s, (const uint32_t*)pb.sb.keys[cur], pb.sb.vals[cur], m,
+                     pb.S, pb.M, ok);
   PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_scan_blocksum, dim3(gb), dim3(kT), 0, s, pb.cnt, n, pb.bsum);
+  hipLaunchKernelGGL(k_perm_values, dim3(grid), dim3(256), 0, s, pb.M, n, pb.V, ok);
   PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, pb.bsum, (int64_t)gb, (int64_t)gb, pb.bpre,
-                     (int64_t)gb + 1);
-  PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_scan_apply, dim3(gb), dim3(kT), 0, s, pb.cnt, n, pb.bpre, (int64_t)gb, pb.off);
-  PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_perm_scatter, dim3(grid), dim3(256), 0, s, J, n, pb.off, pb.cnt, pb.L, ok);
-  PBH_CHECK_LAUNCH();
-  int32_t* S = reinterpret_cast<int32_t*>(pb.cnt);  // cnt is all zero again
-  int32_t* V = reinterpret_cast<int32_t*>(pb.off);  // off is read by k_perm_groups only
-  hipLaunchKernelGGL(k_perm_groups, dim3(grid), dim3(256), 0, s, pb.off, pb.L, n, S, pb.M, ok);
-  PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_perm_values, dim3(grid), dim3(256), 0, s, pb.M, n, V, ok);
-  PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_perm_combine, dim3(grid), dim3(256), 0, s, J, S, V, pb.M, n, q, ok);
+  hipLaunchKernelGGL(k_perm_combine, dim3(grid), dim3(256), 0, s, J, pb.S, pb.V, pb.M, n, q, ok);
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
@@ -662,7 +603,6 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
   pr.nb = pr.tcap / kBlk;
   pr.nband = (int64_t)band.size() / 2;
   const int64_t cap = std::min<int64_t>(pr.tcap, (int64_t)1 << 22);
-  const int64_t gbn = (n + kBlk - 1) / kBlk;
   DevBufs b{s};
   uint32_t *W, *tot, *pre, *tot2, *pre2;
   uint8_t *cls, *dec;
@@ -672,14 +612,16 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
   int32_t *err, *okc;
   u128* pcg_ws;
   PermBufs pb;
+  char* sort_ws;
   int st;
   if ((st = b.get(&W, pr.tcap)) || (st = b.get(&cls, pr.tcap)) || (st = b.get(&tot, 2 * pr.nb)) ||
       (st = b.get(&pre, 2 * (pr.nb + 1))) || (st = b.get(&tot2, pr.nb)) || (st = b.get(&pre2, pr.nb + 1)) ||
       (st = b.get(&list, cap)) || (st = b.get(&dec, cap)) || (st = b.get(&band_dev, pr.nband)) ||
       (st = b.get(&P, d + 1)) || (st = b.get(&err, 1)) || (st = b.get(&okc, d)) || (st = b.get(&pcg_ws, 128)) ||
-      (st = b.get(&pb.cnt, n)) || (st = b.get(&pb.off, n + 1)) || (st = b.get(&pb.bsum, gbn)) ||
-      (st = b.get(&pb.bpre, gbn + 1)) || (st = b.get(&pb.L, n)) || (st = b.get(&pb.M, n)))
+      (st = b.get(&pb.S, n)) || (st = b.get(&pb.V, n)) || (st = b.get(&pb.M, n)) ||
+      (st = b.get(&sort_ws, sort_workspace_bytes(n))))
     return st;
+  sort_carve(sort_ws, n, pb.sb);
   const hipStream_t side = perm_stream(s);
   SideJoin join{side, s};
   hipEvent_t ev = nullptr;
@@ -750,7 +692,11 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
       PBH_CHECK_HIP(hipEventRecord(ev, s));
       PBH_CHECK_HIP(hipStreamWaitEvent(side, ev, 0));
     }
-    if ((st = column_to_q(Jc, n, pb, okc + c, q + (int64_t)c * ldq, side))) return st;
+    if ((st = column_to_q(Jc, n, pb, okc + c, err, q + (int64_t)c * ldq, side))) return st;
+  }
+  if (side != s) {  // the permutations' look-back checks land in err before it is read
+    PBH_CHECK_HIP(hipEventRecord(ev, side));
+    PBH_CHECK_HIP(hipStreamWaitEvent(s, ev, 0));
   }
   int64_t tail = -1;
   int32_t e = 0;

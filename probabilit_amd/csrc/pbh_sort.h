@@ -47,6 +47,11 @@ int exclusive_scan_u32(uint32_t* a, int64_t m, uint32_t* partials, hipStream_t s
 // The same on uint32 keys stored in b.keys[0] (reinterpreted), or read from `in` (left
 // unmodified): at most 4 passes.
 int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, const uint32_t* in = nullptr);
+// The stable LSD passes of radix_sort_keys32 over the low npass bytes of the keys read from `in`
+// (payload: their index), with no host synchronisation: every pass runs (a constant byte is a
+// copy), and *stuck points at the device word a failed look-back sets (the caller checks it).
+int radix_sort_keys32_async(SortBuffers& b, int64_t n, int npass, hipStream_t s, int* out_buf, const uint32_t* in,
+                            uint32_t** stuck);
 // Step 4's code sort for 2^22 <= n <= 2^27 (see k_code_buckets): codes -> rows in final rank
 // order in b.vals[*out_buf] plus eqprev / flags exactly as resolve_code_runs leaves them (flags
 // bit 0: fall back to 64-bit keys; bit 1: exact ties).  flags must be zeroed by the caller.

@@ -880,6 +880,32 @@ int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, cons
   return PBH_OK;
 }
 
+int radix_sort_keys32_async(SortBuffers& b, int64_t n, int npass, hipStream_t s, int* out_buf, const uint32_t* in,
+                            uint32_t** stuck) {
+  PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32) && npass >= 1 && npass <= 4 && in,
+              "radix_sort_keys32_async: bad arguments");
+  const int64_t nt = sort_tiles(n);
+  uint32_t* keys[2] = {(uint32_t*)b.keys[0], (uint32_t*)b.keys[1]};
+  PBH_CHECK_HIP(hipMemsetAsync(b.hist, 0, 8 * 256 * 4, s));
+  hipLaunchKernelGGL(k_digit_hist<uint32_t>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, in, n, b.hist);
+  PBH_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_digit_bases, dim3(4), dim3(256), 0, s, b.hist, b.bases);
+  PBH_CHECK_LAUNCH();
+  PBH_CHECK_HIP(hipMemsetAsync(b.status + nt * 256, 0, 256, s));  // tile counter + stuck flag
+  int cur = 0;
+  for (int ip = 0; ip < npass; ++ip) {
+    PBH_CHECK_HIP(hipMemsetAsync(b.status, 0, (size_t)nt * 256 * 8 + 4, s));  // words + tile counter
+    launch_onesweep<uint32_t, uint32_t>(ip == 0 ? in : keys[cur], ip == 0 ? nullptr : b.vals[cur], keys[cur ^ 1],
+                                        b.vals[cur ^ 1], n, 8 * ip, b.bases + ip * 256, b.status,
+                                        (uint32_t*)(b.status + nt * 256), s);
+    PBH_CHECK_LAUNCH();
+    cur ^= 1;
+  }
+  *out_buf = cur;
+  *stuck = (uint32_t*)(b.status + nt * 256) + 1;
+  return PBH_OK;
+}
+
 int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
   return radix_sort_impl<uint64_t>(b, n, s, out_buf);
 }

@@ -307,3 +307,30 @@ def test_poisson_table_every_boundary(gpu, mu, near):
         "mu": mu, "quantiles": int(q.size), "scipy_below_definition": int(np.count_nonzero(exp < definition)),
         "device_differs_from_scipy": int(diff.sum()), "of_which_within_near": int(np.count_nonzero(off < near)),
         "of_which_scipy_deep_tail": int(np.count_nonzero(tail & ~(off < near))), "near": near})
+
+
+@pytest.mark.parametrize("name,kw,q0", [("norm", dict(loc=2.0, scale=3.0), None), ("norm", dict(loc=-5.0, scale=0.5), None),
+                                        ("lognorm", dict(s=0.5, loc=-1.0, scale=1.0), 0.5),
+                                        ("lognorm", dict(s=2.0, loc=-3.0, scale=0.7), None)])
+def test_norm_lognorm_cancellation_guard(gpu, name, kw, q0):
+    """Where loc + scale·z (norm) or loc + scale·exp(s·z) (lognorm) cancels to near zero, a
+    1e-15 difference in z becomes ~1e-9 relative in x: there the kernels take Cephes' ndtri, bit
+    for bit with scipy, instead of PPND16 (normal_guard, pbh_ppf_core.h).  Quantiles packed around
+    the zero crossing, plain and fused-LHS paths, within 1e-10 relative of scipy."""
+    import scipy.stats
+
+    from probabilit_amd import native
+
+    dist = getattr(scipy.stats, name)(**kw)
+    if q0 is None:
+        q0 = float(dist.cdf(0.0))
+    offs = np.concatenate([-np.logspace(-15, -3, 400), [0.0], np.logspace(-15, -3, 400)])
+    q = np.clip(q0 + offs, 1e-300, 1 - 2.0**-53)
+    q = np.concatenate([q, np.nextafter(q0, 0.0) - np.arange(50) * 2.0**-54, np.nextafter(q0, 1.0) + np.arange(50) * 2.0**-53])
+    ref = dist.ppf(q)
+    got = native.ppf(name, q, **kw)
+    # norm: bit for bit there.  lognorm: z is Cephes' bit for bit, but exp(s z) ~ 1 comes from the
+    # device's exp, within 1 ulp of libm's, and loc + scale exp(s z) keeps that ulp absolutely
+    # (x ~ 1e-15 next to the crossing of lognorm(0.5, loc=-1): one ulp of 1 is 6% of x)
+    atol = 0.0 if name == "norm" else 4 * np.spacing(abs(kw["loc"]))
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=atol)
