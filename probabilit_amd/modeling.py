@@ -211,6 +211,13 @@ def _unary(op, a, n, flag=None):
 # =============================================================================
 # COMPUTATIONAL GRAPH AND MODELING LANGUAGE
 # =============================================================================
+class _GraphPlan:
+    __slots__ = ("G", "all_nodes", "isns", "order", "n_dist")
+
+    def __init__(self, G, all_nodes, isns, order, n_dist):
+        self.G, self.all_nodes, self.isns, self.order, self.n_dist = G, all_nodes, isns, order, n_dist
+
+
 class Node(abc.ABC):
     """A node in the computational graph (modeling.py:335-680)."""
 
@@ -279,6 +286,7 @@ class Node(abc.ABC):
         for node in nx.topological_sort(self.to_graph()):
             dup = copy.copy(node)
             dup.__dict__ = dict(node.__dict__)
+            dup.__dict__.pop("_plan_cache", None)  # it names the original's nodes
             new[dup._id] = dup
             dev = dup.__dict__.get("_smp")
             if dev is not None and not isinstance(dev, _Broadcast):
@@ -307,7 +315,27 @@ class Node(abc.ABC):
             stack.extend(node.get_parents())
 
     def num_distribution_nodes(self):
-        return sum(1 for node in set(self.nodes()) if isinstance(node, AbstractDistribution))
+        return self._plan().n_dist
+
+    def _plan(self):
+        """The graph analysis of an evaluation (networkx graph, topological order, ISNs), kept on
+        the node between calls: the reference redoes it on every .sample() (modeling.py:499-538),
+        ~1 ms of Python for cfg3's 33 nodes.  It is reused only while a walk over the ancestors
+        finds the same node objects with the same correlation counts (a node's parents are fixed
+        at construction; correlate() appends), so a changed graph is always analysed again."""
+        fp = tuple((id(n), len(n._correlations)) for n in self.nodes())
+        cached = self.__dict__.get("_plan_cache")
+        if cached is not None and cached[0] == fp:
+            return cached[1]
+        G = self.to_graph()
+        assert nx.is_directed_acyclic_graph(G)
+        all_nodes = set(G.nodes) if G.number_of_nodes() else {self}
+        plan = _GraphPlan(G, all_nodes, sorted({n for n in all_nodes if n._is_initial_sampling_node()},
+                                               key=lambda n: n._id),
+                          list(nx.topological_sort(G)),
+                          sum(1 for node in all_nodes if isinstance(node, AbstractDistribution)))
+        self.__dict__["_plan_cache"] = (fp, plan)
+        return plan
 
     def to_graph(self):
         """networkx MultiDiGraph of the expression (modeling.py:663-680)."""
@@ -377,10 +405,10 @@ class Node(abc.ABC):
         return self._evaluate(source, correlator, gc_strategy, to_host=False, group=group)
 
     def _evaluate(self, source, correlator, gc_strategy, to_host, group=None):
-        G = self.to_graph()
-        assert nx.is_directed_acyclic_graph(G)
+        plan = self._plan()
+        G = plan.G
         n_dim = source.d
-        assert n_dim == self.num_distribution_nodes()
+        assert n_dim == plan.n_dist
         world, rank = 1, 0
         if group is not None:
             import torch.distributed as tdist
@@ -396,13 +424,13 @@ class Node(abc.ABC):
         if isinstance(correlator, str):
             correlator = {"imanconover": ImanConover, "cholesky": Cholesky}[correlator.lower()]
 
-        all_nodes = set(G.nodes) if G.number_of_nodes() else {self}
+        all_nodes = plan.all_nodes
         for node in all_nodes:
             if "_smp" in node.__dict__:
                 del node.samples_
 
         gc = GarbageCollector(strategy=gc_strategy).set_sink(self)
-        isns = sorted({n for n in all_nodes if n._is_initial_sampling_node()}, key=lambda n: n._id)
+        isns = plan.isns
         isn_set = set(isns)
         ev = _Evaluation(size, list(G.nodes))
 
@@ -429,7 +457,7 @@ class Node(abc.ABC):
             block_row = {v: j for j, v in enumerate(all_variables)}
 
         # a graph of leaf draws, constants and float64 transforms runs as one kernel
-        fused = not correlations and dag.try_evaluate(list(nx.topological_sort(G)), isns, source, ev, gc)
+        fused = not correlations and dag.try_evaluate(list(plan.order), isns, source, ev, gc)
         if not fused:
             # the ISNs' quantile columns in the reference's order (:529-538); native-LHS leaves with
             # plain-number parameters are then drawn together by one call (pbh_lhs_ppf_columns: their
@@ -537,7 +565,7 @@ class Node(abc.ABC):
                         var.samples_ = np.copy(col)
 
             # the per-node loop, or all of it as one fused kernel (probabilit_amd.dag)
-            order = list(nx.topological_sort(G))
+            order = list(plan.order)
             if correlations and dag.try_evaluate(order, isns, source, ev, gc):
                 order = []
             for node in order:  # (:586-612)
