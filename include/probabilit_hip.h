@@ -171,6 +171,12 @@ int pbh_pcg64_random(const uint64_t* state_host, const uint64_t* inc_host, int64
 int pbh_lhs_reference_workspace_size(int64_t n, int32_t d, size_t* bytes);
 int pbh_lhs_reference(const uint64_t* state_host, const uint64_t* inc_host, int32_t has32, uint32_t buf32, int64_t n,
                       int32_t d, double* q, int64_t ldq, void* ws, size_t ws_bytes, void* stream);
+/* As pbh_lhs_reference, and strata (device int32, column c at strata + c * lds, lds >= n; may be
+ * NULL) receives each row's stratum: strata[c][r] = perms[r, c] - 1, so q[c][r] lies in
+ * (strata / n, (strata + 1) / n] -- the rank - 1 of q[c][r] in its column. */
+int pbh_lhs_reference_strata(const uint64_t* state_host, const uint64_t* inc_host, int32_t has32, uint32_t buf32,
+                             int64_t n, int32_t d, double* q, int64_t ldq, int32_t* strata, int64_t lds, void* ws,
+                             size_t ws_bytes, void* stream);
 int pbh_lhs_reference_perms(const uint64_t* state_host, const uint64_t* inc_host, int32_t has32, uint32_t buf32,
                             int64_t n, int32_t d, int32_t* perms_host, uint64_t* state_out_host);
 /* The device decode's band half-width in standard deviations of the steps done (default 6; each
@@ -265,6 +271,13 @@ typedef struct pbh_ic_args {
   double* cscores_out;
   int32_t* idx_out;
   double* corr_host_out; /* optional K x K host buffer: E = corrcoef(S) */
+  /* optional (X only): host array of k device pointers, NULL entries allowed.  strata[c][r] =
+   * rank - 1 of row r in column c when known (an LHS column's strata, e.g. the reference
+   * stream's decoded shuffles, pbh_lhs_reference_strata): step 1 then puts X[:, c] in order by
+   * one scatter instead of a sort, and keeps it only if the result is certified sorted (no
+   * inversion, no stratum missed); otherwise the column is sorted as usual.  Results are the
+   * same either way. */
+  const int32_t* const* strata;
 } pbh_ic_args;
 
 int pbh_ic_workspace_size(int64_t n, int32_t k, size_t* bytes);

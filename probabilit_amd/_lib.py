@@ -50,7 +50,7 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_pcg64_random", "pbh_halton_workspace_size", "pbh_fill_halton",
            "pbh_affine_workspace_size", "pbh_affine_rows", "pbh_table_ppf", "pbh_permcorr_workspace_size",
            "pbh_permcorr_climb", "pbh_sobol_ppf", "pbh_lhs_reference_workspace_size",
-           "pbh_lhs_reference", "pbh_lhs_reference_perms", "pbh_lhs_reference_band", "pbh_lhs_reference_stats", "pbh_table_cache_stats", "pbh_hbm_copy", "pbh_dag_eval",
+           "pbh_lhs_reference", "pbh_lhs_reference_strata", "pbh_lhs_reference_perms", "pbh_lhs_reference_band", "pbh_lhs_reference_stats", "pbh_table_cache_stats", "pbh_hbm_copy", "pbh_dag_eval",
            "pbh_lhs_sorted_counts", "pbh_sort_heads", "pbh_ic_owned_workspace_size", "pbh_ic_owned_create",
            "pbh_ic_owned_column", "pbh_ic_owned_finish", "pbh_lhs_values_at", "pbh_lhs_ppf_columns", "pbh_ic_owned_destroy", "pbh_event_create",
            "pbh_event_destroy", "pbh_event_record", "pbh_stream_wait_event", "pbh_event_synchronize",
@@ -84,7 +84,8 @@ class ICArgs(ctypes.Structure):
                 ("x_cs", ctypes.c_int64), ("target_chol_host", ctypes.c_void_p), ("Y", ctypes.c_void_p),
                 ("y_rs", ctypes.c_int64), ("y_cs", ctypes.c_int64), ("ws", ctypes.c_void_p),
                 ("ws_bytes", ctypes.c_size_t), ("scores_out", ctypes.c_void_p), ("cscores_out", ctypes.c_void_p),
-                ("idx_out", ctypes.c_void_p), ("corr_host_out", ctypes.c_void_p)]
+                ("idx_out", ctypes.c_void_p), ("corr_host_out", ctypes.c_void_p),
+                ("strata", ctypes.c_void_p)]
 
 
 class DagOp(ctypes.Structure):  # pbh_dag_op
@@ -173,6 +174,8 @@ def load():
         "pbh_permcorr_workspace_size": ([ctypes.c_int32, ctypes.POINTER(sz)], i32),
         "pbh_lhs_reference_workspace_size": ([i64, ctypes.c_int32, ctypes.POINTER(sz)], i32),
         "pbh_lhs_reference": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, i64, vp, sz, vp], i32),
+        "pbh_lhs_reference_strata": ([vp, vp, ctypes.c_int32, ctypes.c_uint32, i64, ctypes.c_int32, vp, i64, vp, i64, vp,
+                                      sz, vp], i32),
         "pbh_hbm_copy": ([vp, vp, sz, i32, vp], i32),
         "pbh_dag_eval": ([ctypes.POINTER(DagOp), i32, ctypes.POINTER(DagSource), i32, ctypes.POINTER(vp), i32, i64, i64,
                           vp, vp], i32),

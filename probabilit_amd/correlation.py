@@ -268,7 +268,7 @@ class ImanConover(Correlator):
         super().set_target(correlation_matrix)
         return self
 
-    def _run(self, X, n, k, x_rs, x_cs, Y, y_rs, y_cs, debug=None, columns=None):
+    def _run(self, X, n, k, x_rs, x_cs, Y, y_rs, y_cs, debug=None, columns=None, strata=None):
         lib = _lib.load()
         ws_bytes = ctypes.c_size_t()
         _lib.check(lib.pbh_ic_workspace_size(n, k, ctypes.byref(ws_bytes)))
@@ -282,6 +282,14 @@ class ImanConover(Correlator):
         args.target_chol_host = P.ctypes.data
         args.Y, args.y_rs, args.y_cs = Y.data_ptr(), y_rs, y_cs
         args.ws, args.ws_bytes = ws.data_ptr(), ws_bytes.value
+        if strata is not None and any(t is not None for t in strata):
+            import torch
+
+            for t in strata:
+                if t is not None and (t.dtype != torch.int32 or t.numel() != n or not t.is_contiguous()):
+                    raise ValueError("strata: contiguous int32 device vectors of n entries")
+            sptr = (ctypes.c_void_p * k)(*[t.data_ptr() if t is not None else None for t in strata])
+            args.strata = ctypes.cast(sptr, ctypes.c_void_p)
         if debug is not None:  # intermediates for parity tests; "idx" selects the gather form of step 4
             if "S" in debug:
                 args.scores_out = debug["S"].data_ptr()
@@ -309,12 +317,17 @@ class ImanConover(Correlator):
         self._run(Xd, N, K, K, 1, Y, K, 1)
         return Y if on_device else device.to_host(Y)
 
-    def _transform_device(self, block, ev=None):
-        """block: (K, N) contiguous device tensor of the correlated variables (DAG path)."""
+    def _transform_device(self, block, ev=None, strata=None, debug=None):
+        """block: (K, N) contiguous device tensor of the correlated variables (DAG path).
+        strata: optional list of K entries, each None or row j's known ranks - 1 (an int32
+        device vector: an LHS column's strata, which a monotone inverse CDF keeps); step 1 then
+        orders that column by a scatter instead of a sort, after checking it on the device."""
         K, N = block.shape
         self._validate_X(block.T)
+        if strata is not None and len(strata) != K:
+            raise ValueError(f"strata: {len(strata)} entries for {K} columns")
         Y = device.empty((K, N))
-        self._run(block, N, K, 1, N, Y, 1, N)
+        self._run(block, N, K, 1, N, Y, 1, N, strata=strata, debug=debug)
         return Y
 
     def _transform_generated(self, columns, n, debug=None):

@@ -399,11 +399,45 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     for (int c = 0; c < k; ++c)
       if (deferred[c]) cnt_host[2 * c] = cnt_host[2 * c + 1] = 0;  // assumed; checked before step 4
   }
+  // Materialised columns with known strata (a->strata[c]: each row's rank - 1, e.g. the
+  // reference LHS stream's decoded shuffles): sort(X[:, c]) by one scatter, certified by its
+  // tie / inversion counts (one readback for all of them); an inversion (a ppf not monotone on
+  // the grid, a NaN, strata that are not a permutation) leaves the column to the sort below.
+  std::vector<char> by_strata(k, 0);
+  std::vector<unsigned long long> scnt(2 * (size_t)k, 0);
+  if (a->strata && a->X && !a->columns) {
+    bool any = false;
+    for (int c = 0; c < k; ++c) {
+      if (!a->strata[c]) continue;
+      st = strata_sorted(a->X + (int64_t)c * a->x_cs, a->x_rs, a->strata[c], n, L.sorted_x + (int64_t)c * n,
+                         L.counts + 2 * c, s);
+      if (st) return st;
+      by_strata[c] = any = true;
+    }
+    if (any) {
+      PBH_CHECK_HIP(hipMemcpyAsync(scnt.data(), L.counts, 16 * (size_t)k, hipMemcpyDeviceToHost, s));
+      PBH_CHECK_HIP(hipStreamSynchronize(s));
+    }
+  }
   for (int c = 0; c < k; ++c) {
     double* S_c = L.S + (int64_t)c * n;
     double* sx_c = L.sorted_x + (int64_t)c * n;
     const double* x_c = a->X ? a->X + (int64_t)c * a->x_cs : nullptr;
     int64_t x_stride = a->x_rs;
+    if (by_strata[c] && scnt[2 * c + 1] == 0) {
+      uint32_t* heads = nullptr;
+      int64_t nheads = 0;
+      if (scnt[2 * c] != 0) {  // ties: 'average' ranks from the runs of the sorted column
+        heads = (uint32_t*)L.tmp;
+        st = run_heads(sx_c, n, 0, false, heads, &nheads, L.heads_ws, s);
+        if (st) return st;
+      }
+      st = strata_scores(a->strata[c], n, heads, nheads, S_c, s);
+      if (st) return st;
+      all_generated = false;
+      have_sx[c] = 1;
+      continue;
+    }
     if (a->columns) {
       // generated LHS column: sorted order straight from the inverse permutation
       const pbh_ic_column& g = a->columns[c];

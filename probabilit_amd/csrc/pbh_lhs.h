@@ -21,6 +21,14 @@ int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, 
                 int64_t nheads, double* S, hipStream_t s, double* partial = nullptr);
 // number of partial sums perm_scores writes for nrows rows
 unsigned perm_scores_blocks(int64_t nrows);
+// perm_scores for a materialised column whose strata (rank - 1 of each row, a permutation of
+// [0, n)) are known: S[r] = ndtri(rank / (n + 1)), rank = strata[r] + 1 or its run's average.
+int strata_scores(const int32_t* strata, int64_t n, const uint32_t* heads, int64_t nheads, double* S, hipStream_t s);
+// sorted[strata[r]] = x[r * stride], then the tie / inversion counts of sorted (counts: 2 device
+// u64, as check_sorted).  counts[1] == 0 certifies that sorted is sort(x) and strata its ranks
+// (a stratum no row names stays NaN and counts as an inversion).
+int strata_sorted(const double* x, int64_t stride, const int32_t* strata, int64_t n, double* sorted,
+                  unsigned long long* counts, hipStream_t s);
 // Run heads of a sorted segment x[0..m) (see k_heads_write); *count = number written (syncs).
 size_t run_heads_ws_bytes(int64_t m);
 int run_heads(const double* x, int64_t m, int64_t t0, bool first_is_prev, uint32_t* heads, int64_t* count,

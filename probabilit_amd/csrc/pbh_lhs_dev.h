@@ -14,8 +14,10 @@ namespace pbh {
 // uniforms; has32 / buf32: the 32-bit buffer of next_uint32), combined into q (column-major,
 // ldq) as (perms.T - u) / n, the whole thing on the device.  targets: d * n int32 of scratch.
 // *done = false: the decode failed its own check at every band width; q then holds nothing
-// usable (the caller draws u again and shuffles on the host).
+// usable (the caller draws u again and shuffles on the host).  strata (optional, column c at
+// strata + c * lds): each row's stratum perms - 1.
 int lhs_reference_device(const uint64_t* state_host, const uint64_t* inc_host, bool has32, uint32_t buf32, int64_t n,
-                         int d, double* q, int64_t ldq, int32_t* targets, hipStream_t s, bool* done);
+                         int d, double* q, int64_t ldq, int32_t* targets, hipStream_t s, bool* done,
+                         int32_t* strata = nullptr, int64_t lds = 0);
 
 }  // namespace pbh

@@ -396,11 +396,11 @@ __global__ __launch_bounds__(256) void k_perm_values(const int32_t* __restrict__
   }
 }
 
-// q = (perm - u) / n for one column (u in q on entry)
+// q = (perm - u) / n for one column (u in q on entry); strata (optional) = perm - 1
 __global__ __launch_bounds__(256) void k_perm_combine(const int32_t* __restrict__ J, const int32_t* __restrict__ S,
                                                       const int32_t* __restrict__ V, const int32_t* __restrict__ M,
                                                       int64_t n, double* __restrict__ q,
-                                                      const int32_t* __restrict__ ok) {
+                                                      const int32_t* __restrict__ ok, int32_t* __restrict__ strata) {
   if (!*ok) return;
   const double dn = (double)n;
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
@@ -413,6 +413,7 @@ __global__ __launch_bounds__(256) void k_perm_combine(const int32_t* __restrict_
       v = nx >= 0 ? V[nx] : J[r] + 1;
     }
     q[r] = ((double)v - q[r]) / dn;  // (perms - samples) / n: subtract, then divide
+    if (strata) strata[r] = v - 1;
   }
 }
 
@@ -568,7 +569,7 @@ struct PermBufs {
 // column c's permutation from its targets (J: n words), combined into q[0 .. n) (u on entry);
 // every kernel past the sort exits at once unless ok[0] (k_dec_seal)
 int column_to_q(const int32_t* J, int64_t n, PermBufs& pb, const int32_t* ok, int32_t* err, double* q,
-                hipStream_t s) {
+                int32_t* strata, hipStream_t s) {
   const int64_t m = n - 1;  // steps 1 .. n-1
   int bits = 1;
   while (bits < 32 && ((int64_t)1 << bits) < n) ++bits;  // targets < n
@@ -584,7 +585,7 @@ int column_to_q(const int32_t* J, int64_t n, PermBufs& pb, const int32_t* ok, in
   PBH_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_perm_values, dim3(grid), dim3(256), 0, s, pb.M, n, pb.V, ok);
   PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_perm_combine, dim3(grid), dim3(256), 0, s, J, pb.S, pb.V, pb.M, n, q, ok);
+  hipLaunchKernelGGL(k_perm_combine, dim3(grid), dim3(256), 0, s, J, pb.S, pb.V, pb.M, n, q, ok, strata);
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
@@ -593,8 +594,8 @@ int column_to_q(const int32_t* J, int64_t n, PermBufs& pb, const int32_t* ok, in
 // stream and, once sealed, its permutation on the side stream (overlapping the next column's
 // host walk).  *ok: every column passed the check (q complete); otherwise q is to be redone.
 int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint64_t* inc_host, const u128* jt_dev,
-                   int d, double ksig, double* q, int64_t ldq, int32_t* J, hipStream_t s, bool* ok,
-                   int64_t* ambiguous) {
+                   int d, double ksig, double* q, int64_t ldq, int32_t* J, int32_t* strata, int64_t lds,
+                   hipStream_t s, bool* ok, int64_t* ambiguous) {
   *ok = false;
   DecParams pr = base;
   const int64_t n = pr.n, N1 = n - 1;
@@ -692,7 +693,9 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
       PBH_CHECK_HIP(hipEventRecord(ev, s));
       PBH_CHECK_HIP(hipStreamWaitEvent(side, ev, 0));
     }
-    if ((st = column_to_q(Jc, n, pb, okc + c, err, q + (int64_t)c * ldq, side))) return st;
+    if ((st = column_to_q(Jc, n, pb, okc + c, err, q + (int64_t)c * ldq, strata ? strata + (int64_t)c * lds : nullptr,
+                          side)))
+      return st;
   }
   if (side != s) {  // the permutations' look-back checks land in err before it is read
     PBH_CHECK_HIP(hipEventRecord(ev, side));
@@ -716,7 +719,8 @@ __global__ void k_single_row(double* __restrict__ q, int64_t ldq, int d) {
 }  // namespace
 
 int lhs_reference_device(const uint64_t* state_host, const uint64_t* inc_host, bool has32, uint32_t buf32, int64_t n,
-                         int d, double* q, int64_t ldq, int32_t* targets, hipStream_t s, bool* done) {
+                         int d, double* q, int64_t ldq, int32_t* targets, hipStream_t s, bool* done, int32_t* strata,
+                         int64_t lds) {
   *done = false;
   g_last_attempts = 0;
   g_last_device = 0;
@@ -733,6 +737,8 @@ int lhs_reference_device(const uint64_t* state_host, const uint64_t* inc_host, b
     if ((st = pbh_pcg64_random(state_host, inc_host, 0, 1, d, q, ldq, pcg_ws, 128 * sizeof(u128), s))) return st;
     hipLaunchKernelGGL(k_single_row, dim3(1), dim3(256), 0, s, q, ldq, d);
     PBH_CHECK_LAUNCH();
+    if (strata)
+      for (int c = 0; c < d; ++c) PBH_CHECK_HIP(hipMemsetAsync(strata + (int64_t)c * lds, 0, 4, s));
   } else {
     std::vector<u128> table(128);
     pcg::jump_table(inc, table.data());
@@ -754,7 +760,8 @@ int lhs_reference_device(const uint64_t* state_host, const uint64_t* inc_host, b
     for (int a = 0; a < kAttempts && !ok; ++a, ksig *= 2.0) {
       int64_t amb = 0;
       ++g_last_attempts;
-      if ((st = decode_attempt(pr, state_host, inc_host, jt, d, ksig, q, ldq, targets, s, &ok, &amb))) return st;
+      if ((st = decode_attempt(pr, state_host, inc_host, jt, d, ksig, q, ldq, targets, strata, lds, s, &ok, &amb)))
+        return st;
       g_last_ambiguous = amb;
     }
     if (!ok) return PBH_OK;  // q is to be redone by the caller

@@ -106,13 +106,15 @@ int worker_count(int d) {
 }
 
 __global__ __launch_bounds__(256) void k_lhs_combine(const int32_t* __restrict__ perms, double* __restrict__ q,
-                                                     int64_t n, int d, int64_t ldq) {
+                                                     int64_t n, int d, int64_t ldq, int32_t* __restrict__ strata,
+                                                     int64_t lds) {
   const double dn = (double)n;
   const int64_t total = n * (int64_t)d;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int64_t c = e / n, r = e - c * n;
     double* p = q + c * ldq + r;
     *p = ((double)perms[e] - *p) / dn;  // (perms - samples) / n: subtract, then divide
+    if (strata) strata[c * lds + r] = perms[e] - 1;
   }
 }
 
@@ -164,7 +166,14 @@ extern "C" int pbh_lhs_reference_workspace_size(int64_t n, int32_t d, size_t* by
 extern "C" int pbh_lhs_reference(const uint64_t* state_host, const uint64_t* inc_host, int32_t has32, uint32_t buf32,
                                  int64_t n, int32_t d, double* q, int64_t ldq, void* ws, size_t ws_bytes,
                                  void* stream) {
-  PBH_REQUIRE(state_host && inc_host && n >= 1 && n < ((int64_t)1 << 31) && d >= 1 && q && ldq >= n && ws,
+  return pbh_lhs_reference_strata(state_host, inc_host, has32, buf32, n, d, q, ldq, nullptr, 0, ws, ws_bytes, stream);
+}
+
+extern "C" int pbh_lhs_reference_strata(const uint64_t* state_host, const uint64_t* inc_host, int32_t has32,
+                                        uint32_t buf32, int64_t n, int32_t d, double* q, int64_t ldq, int32_t* strata,
+                                        int64_t lds, void* ws, size_t ws_bytes, void* stream) {
+  PBH_REQUIRE(state_host && inc_host && n >= 1 && n < ((int64_t)1 << 31) && d >= 1 && q && ldq >= n && ws &&
+                  (!strata || lds >= n),
               "pbh_lhs_reference: bad arguments");
   size_t need = 0;
   pbh_lhs_reference_workspace_size(n, d, &need);
@@ -179,7 +188,8 @@ extern "C" int pbh_lhs_reference(const uint64_t* state_host, const uint64_t* inc
   // the shuffles on the host: draws 0 .. n d - 1 row-major into q's column-major layout; the
   // shuffles continue the stream after the n d doubles (uniform() leaves the 32-bit buffer)
   bool done = false;
-  int st = lhs_reference_device(state_host, inc_host, has32 != 0, buf32, n, d, q, ldq, perms_dev, s, &done);
+  int st = lhs_reference_device(state_host, inc_host, has32 != 0, buf32, n, d, q, ldq, perms_dev, s, &done, strata,
+                                lds);
   if (st || done) return st;
   st = pbh_pcg64_random(state_host, inc_host, 0, n, d, q, ldq, pcg_ws, 128 * sizeof(u128), stream);
   if (st) return st;
@@ -195,7 +205,7 @@ extern "C" int pbh_lhs_reference(const uint64_t* state_host, const uint64_t* inc
   PBH_CHECK_HIP(hipMemcpyAsync(perms_dev, perms.data(), perms.size() * 4, hipMemcpyHostToDevice, s));
   PBH_TIMED(kKStreams, s,
             hipLaunchKernelGGL(k_lhs_combine, dim3(grid_for(n * (int64_t)d, 256, 65536)), dim3(256), 0, s, perms_dev,
-                               q, n, (int)d, ldq));
+                               q, n, (int)d, ldq, strata, lds));
   PBH_CHECK_LAUNCH();
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // `perms` is pageable and goes out of scope
   return PBH_OK;

@@ -45,6 +45,13 @@ constexpr int kBlock = 256;
 
 unsigned compact_grid(int64_t n) { return grid_for(n, kCTile, 256 * 8); }
 
+// Blocks of the gamma slow-list kernels (grid-stride over the list; a few thousand items at a
+// time in practice): a grid this size schedules in one wave of the chip even next to the other
+// step-4 lanes' kernels.
+#ifndef PBH_SLOW_GRID
+#define PBH_SLOW_GRID 1024
+#endif
+
 bool scalar_params(const Params& prm) { return !prm.ptr[0] && !prm.ptr[1] && !prm.ptr[2]; }
 
 // k_ppf / k_lhs_ppf for D in {norm, lognorm} with tail compaction.  Q(i) gives the quantile of
@@ -1182,7 +1189,7 @@ bool launch_gamma_w(const double* q, int64_t qs, int64_t n, const GammaLhs* lc, 
     return true;
   }
   const GammaLhs l = lc ? *lc : GammaLhs{0, 1, 0, 0};
-  const unsigned gw = grid_for(n, kGSweepPer * kGSBlock, 256 * 3 * 512 / kGSBlock), gs = 256 * 4;
+  const unsigned gw = grid_for(n, kGSweepPer * kGSBlock, 256 * 3 * 512 / kGSBlock), gs = PBH_SLOW_GRID;
   if (lc) {
     PBH_TIMED(kKLhsPpf, s, {
       hipLaunchKernelGGL(k_ppf_gamma_w<true>, dim3(gw), dim3(kGSBlock), 0, s, q, qs, n, l, prm, pt, out, flag, j0, jn,
@@ -1417,10 +1424,14 @@ constexpr int64_t kLdsHeads = 4096;  // run heads staged in LDS by k_perm_scores
 // the queue order is the lanes' order (ballots, no atomics), so the result is deterministic.
 constexpr int kWaveQ = 576;  // a wave's tail stack: at most 63 left over + 8 x 64 pushed in a step
 
+// STRATA: the strata come from an array (strata[row0 + i], a materialised LHS column's known
+// permutation, e.g. the reference stream's decoded shuffles) instead of the Feistel permutation.
+template <bool STRATA>
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, int64_t n, uint32_t col, int64_t row0,
                                                           int64_t nrows, const uint32_t* __restrict__ heads,
                                                           int64_t nheads, double* __restrict__ S,
-                                                          double* __restrict__ partial) {
+                                                          double* __restrict__ partial,
+                                                          const int32_t* __restrict__ strata) {
   __shared__ double qarg[kBlock / 64][kWaveQ];
   __shared__ uint32_t qrow[kBlock / 64][kWaveQ];
   extern __shared__ uint32_t lheads[];
@@ -1441,14 +1452,22 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_perm_scores(uint64_t seed, i
   const int64_t gw = (int64_t)blockIdx.x * (kBlock / 64) + w, W = (int64_t)gridDim.x * (kBlock / 64);
   for (int64_t base = gw * 512; base < nrows; base += W * 512) {
     uint64_t tt[8];
+    if constexpr (STRATA) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t i = base + j * 64 + lane;
-      tt[j] = n > 1 && i < nrows ? fp.round_trip((uint64_t)(row0 + i)) : 0;
+      for (int j = 0; j < 8; ++j) {
+        const int64_t i = base + j * 64 + lane;
+        tt[j] = i < nrows ? (uint64_t)(uint32_t)strata[row0 + i] : 0;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t i = base + j * 64 + lane;
+        tt[j] = n > 1 && i < nrows ? fp.round_trip((uint64_t)(row0 + i)) : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        while (tt[j] >= (uint64_t)n) tt[j] = fp.round_trip(tt[j]);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      while (tt[j] >= (uint64_t)n) tt[j] = fp.round_trip(tt[j]);
 #pragma unroll 2
     for (int j = 0; j < 8; ++j) {
       const int64_t i = base + j * 64 + lane;
@@ -2257,7 +2276,7 @@ static int place_launch(const GenColumn* g, const uint64_t* pairs, const uint32_
                                  dim3(kGWBlock), 0, s, pairs, pidx, rows, n, g->seed, g->col, g->prm, g->pt, y, y_rs,
                                  idx, state, j0, jn, slow, cap));
     PBH_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_place_gen_gamma_slow<BYROW>, dim3(1024), dim3(256), 0, s, pairs, pidx, rows, n, g->seed,
+    hipLaunchKernelGGL(k_place_gen_gamma_slow<BYROW>, dim3(PBH_SLOW_GRID), dim3(256), 0, s, pairs, pidx, rows, n, g->seed,
                        g->col, g->prm, g->pt, y, y_rs, state, slow, cap);
     PBH_CHECK_LAUNCH();
     PBH_CHECK_HIP(hipFreeAsync(slow, s));
@@ -2381,10 +2400,40 @@ int perm_scores(uint64_t seed, int64_t n, int col, int64_t row0, int64_t nrows, 
   if (nrows == 0) return PBH_OK;
   const size_t lds = heads && nheads <= kLdsHeads ? (size_t)nheads * 4 : 0;
   PBH_TIMED(kKPermScores, s,
-            hipLaunchKernelGGL(k_perm_scores, dim3(scores_grid(nrows)), dim3(kBlock), lds, s, seed, n, (uint32_t)col,
-                               row0, nrows, heads, nheads, S, partial));
+            hipLaunchKernelGGL(k_perm_scores<false>, dim3(scores_grid(nrows)), dim3(kBlock), lds, s, seed, n,
+                               (uint32_t)col, row0, nrows, heads, nheads, S, partial, nullptr));
   PBH_CHECK_LAUNCH();
   return PBH_OK;
+}
+
+int strata_scores(const int32_t* strata, int64_t n, const uint32_t* heads, int64_t nheads, double* S, hipStream_t s) {
+  if (n == 0) return PBH_OK;
+  const size_t lds = heads && nheads <= kLdsHeads ? (size_t)nheads * 4 : 0;
+  PBH_TIMED(kKPermScores, s,
+            hipLaunchKernelGGL(k_perm_scores<true>, dim3(scores_grid(n)), dim3(kBlock), lds, s, 0ull, n, 0u, 0ll, n,
+                               heads, nheads, S, nullptr, strata));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+// sorted[strata[r]] = x[r * stride]: a materialised column put in order by its known strata
+// (sorted is NaN-filled first, so a stratum no row names reads as an inversion in check_sorted)
+__global__ __launch_bounds__(kBlock) void k_strata_scatter(const double* __restrict__ x, int64_t stride,
+                                                           const int32_t* __restrict__ strata, int64_t n,
+                                                           double* __restrict__ sorted) {
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n; r += (int64_t)gridDim.x * kBlock) {
+    const uint32_t t = (uint32_t)strata[r];
+    if (t < (uint64_t)n) sorted[t] = x[r * stride];
+  }
+}
+
+int strata_sorted(const double* x, int64_t stride, const int32_t* strata, int64_t n, double* sorted,
+                  unsigned long long* counts, hipStream_t s) {
+  PBH_CHECK_HIP(hipMemsetAsync(sorted, 0xFF, (size_t)n * 8, s));  // all-ones: a NaN
+  hipLaunchKernelGGL(k_strata_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, x, stride, strata, n,
+                     sorted);
+  PBH_CHECK_LAUNCH();
+  return check_sorted(sorted, n, counts, s);
 }
 
 size_t run_heads_ws_bytes(int64_t m) {

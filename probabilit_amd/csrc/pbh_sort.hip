@@ -469,6 +469,7 @@ __device__ __forceinline__ void wave_radix_pass(uint32_t (&k)[kWBItems], uint32_
   uint32_t rank[kWBItems];
 #pragma unroll
   for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 >= len) break;  // wave-uniform: a small bucket skips the empty item slots
     const bool valid = j * 64 + lane < len;
     const uint32_t d = (k[j] >> shift) & 255u;
     uint64_t peers = __ballot(valid);
@@ -506,6 +507,7 @@ __device__ __forceinline__ void wave_radix_pass(uint32_t (&k)[kWBItems], uint32_
   wave_sync();
 #pragma unroll
   for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 >= len) break;  // wave-uniform: a small bucket skips the empty item slots
     if (j * 64 + lane < len) {
       const uint32_t lp = B.cnt[(k[j] >> shift) & 255u] + rank[j];
       B.key[lp] = (uint16_t)k[j];
@@ -526,8 +528,10 @@ __device__ __forceinline__ void wave_count_pass(uint32_t (&k)[kWBItems], uint32_
   wave_sync();
   uint32_t rank[kWBItems];
 #pragma unroll
-  for (int j = 0; j < kWBItems; ++j)
+  for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 >= len) break;
     rank[j] = (j * 64 + lane < len) ? atomicAdd(&B.cnt[k[j] & 255u], 1u) : 0u;
+  }
   wave_sync();
   uint32_t v[4], sum = 0;
 #pragma unroll
@@ -551,6 +555,7 @@ __device__ __forceinline__ void wave_count_pass(uint32_t (&k)[kWBItems], uint32_
   wave_sync();
 #pragma unroll
   for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 >= len) break;  // wave-uniform: a small bucket skips the empty item slots
     if (j * 64 + lane < len) {
       const uint32_t lp = B.cnt[k[j] & 255u] + rank[j];
       B.key[lp] = (uint16_t)k[j];
@@ -621,10 +626,11 @@ __global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* 
     if (lane == 0) atomicOr(flags, 1);
     return;
   }
-  const int len = (int)(e - s);
+  const int len = __builtin_amdgcn_readfirstlane((int)(e - s));
   uint32_t k[kWBItems], r[kWBItems];
 #pragma unroll
   for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 >= len) break;  // wave-uniform: a small bucket skips the empty item slots
     const int p = j * 64 + lane;
     k[j] = p < len ? (keys[s + p] & 0xFFFFu) : 0u;
     r[j] = p < len ? rows[s + p] : 0u;
@@ -632,6 +638,7 @@ __global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* 
   wave_count_pass(k, r, len, B);
 #pragma unroll
   for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 >= len) break;  // wave-uniform: a small bucket skips the empty item slots
     const int p = j * 64 + lane;
     k[j] = p < len ? B.key[p] : 0u;
     r[j] = p < len ? B.row[p] : 0u;
@@ -643,6 +650,7 @@ __global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* 
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll 4
   for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 >= len) break;  // wave-uniform: a small bucket skips the empty item slots
     const int p = j * 64 + lane;
     bool st = false;
     if (p < len) {
@@ -679,6 +687,7 @@ __global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* 
   wave_sync();
 #pragma unroll 4
   for (int j = 0; j < kWBItems; ++j) {
+    if (j * 64 >= len) break;  // wave-uniform: a small bucket skips the empty item slots
     const int p = j * 64 + lane;
     if (p < len) {
       rows[s + p] = B.row[p];

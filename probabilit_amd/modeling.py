@@ -462,7 +462,12 @@ class Node(abc.ABC):
             # the ISNs' quantile columns in the reference's order (:529-538); native-LHS leaves with
             # plain-number parameters are then drawn together by one call (pbh_lhs_ppf_columns: their
             # inverse-CDF setups overlap), the rest one by one
-            columns = {node: source.next_column() for node in isns}
+            if correlations and block is not None and isinstance(source, qmc.ReferenceLHSSource) and world == 1:
+                source.keep_strata = True  # the correlated leaves' ranks (step 1 of Iman-Conover)
+            columns, col_index = {}, {}
+            for node in isns:
+                col_index[node] = source._next
+                columns[node] = source.next_column()
             leaves = []
             if isinstance(source, qmc.LHSSource):
                 leaves = [node for node in isns
@@ -554,6 +559,17 @@ class Node(abc.ABC):
                         for var, col in zip(all_variables, Yh.T):
                             var.samples_ = np.copy(col[r0:r1])
                     del full
+                elif isinstance(inst, ImanConover) and getattr(source, "strata", None) is not None:
+                    # leaves with plain-number parameters: their ranks are their LHS strata
+                    # (checked on the device; a column that fails the check is sorted)
+                    strata = [source.strata_of(col_index[v])
+                              if type(v) is Distribution and v.is_leaf
+                              and all(not isinstance(p, Node) and np.ndim(p) == 0
+                                      for p in _parse_scipy_args(v.distr, v.args, v.kwargs)) else None
+                              for v in all_variables]
+                    Y = inst._transform_device(block, ev, strata=strata)
+                    for j, var in enumerate(all_variables):
+                        var._set_device(Y[j])
                 elif isinstance(inst, (ImanConover, Cholesky, PermutationCorrelator)):
                     Y = inst._transform_device(block, ev)
                     for j, var in enumerate(all_variables):

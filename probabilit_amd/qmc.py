@@ -336,21 +336,35 @@ class ReferenceLHSSource(QuantileSource):
         self.state, self.inc = int(st["state"]["state"]), int(st["state"]["inc"])
         self.has32, self.buf32 = int(st["has_uint32"]), int(st["uinteger"])
         self.q = None
+        self.keep_strata = False  # set before the first column: keep each row's stratum as well
+        self.strata = None
 
     def matrix(self):
         if self.q is None and self.n > 0 and self.d > 0:
             lib = _lib.load()
             ws = _workspace(lib.pbh_lhs_reference_workspace_size, self.n, self.d)
             self.q = device.empty((self.d, self.n))
+            if self.keep_strata:
+                self.strata = device.empty((self.d, self.n), "int32")
             s, inc = _u128_words(self.state), _u128_words(self.inc)
-            _lib.check(lib.pbh_lhs_reference(_lib.np_ptr(s), _lib.np_ptr(inc), self.has32, self.buf32, self.n, self.d,
-                                             self.q.data_ptr(), self.n, ws.data_ptr(), ws.numel(), device.stream()),
+            _lib.check(lib.pbh_lhs_reference_strata(_lib.np_ptr(s), _lib.np_ptr(inc), self.has32, self.buf32, self.n,
+                                                    self.d, self.q.data_ptr(), self.n,
+                                                    self.strata.data_ptr() if self.strata is not None else None,
+                                                    self.n, ws.data_ptr(), ws.numel(), device.stream()),
                        "pbh_lhs_reference")
             del ws
         return self.q
 
     def column(self, c):
         return ("vector", self.matrix()[c, self.row0:self.row0 + self.rows], 1)
+
+    def strata_of(self, c):
+        """Column c's strata (each row's rank - 1 in the whole column: int32 device vector), when
+        kept (keep_strata) and this process holds every row; else None.  A monotone inverse CDF
+        keeps these ranks, which lets Iman-Conover order the column without sorting it."""
+        if self.strata is None or self.row0 != 0 or self.rows != self.n:
+            return None
+        return self.strata[c]
 
 
 _DEFAULT_STREAM = os.environ.get("PBH_LHS_STREAM", "native")

@@ -339,3 +339,84 @@ def test_reference_lhs_device_decode_retry_and_fallback(gpu):
     got = _src_matrix(qmc.make_source("lhs", n, d, seed, stream="reference"))
     np.testing.assert_array_equal(got, ref)
     assert _ref_stats()[:2] == (1, 1)
+
+
+def _ref_lhs_strata(state, inc, has32, buf32, n, d):
+    """pbh_lhs_reference_strata: the matrix and each row's stratum."""
+    import ctypes
+
+    from probabilit_amd import _lib, device
+    from probabilit_amd.qmc import _u128_words
+
+    lib = _lib.load()
+    nb = ctypes.c_size_t()
+    _lib.check(lib.pbh_lhs_reference_workspace_size(n, d, ctypes.byref(nb)))
+    ws = device.empty(int(nb.value), "uint8")
+    q, t = device.empty((d, n)), device.empty((d, n), "int32")
+    s, i = _u128_words(state), _u128_words(inc)
+    _lib.check(lib.pbh_lhs_reference_strata(_lib.np_ptr(s), _lib.np_ptr(i), has32, buf32, n, d, q.data_ptr(), n,
+                                            t.data_ptr(), n, ws.data_ptr(), ws.numel(), device.stream()),
+               "pbh_lhs_reference_strata")
+    return device.to_host(q).T, device.to_host(t).T
+
+
+@pytest.mark.parametrize("narrow", [False, True])
+def test_reference_lhs_strata(gpu, narrow):
+    """The strata beside the matrix (device decode, and the host-shuffle fallback a too-narrow
+    band forces): perms - 1 of the host shuffles, so every q lies in its stratum's interval."""
+    import ctypes
+
+    from probabilit_amd import _lib
+
+    n, d, has32 = 100_003, 3, 1
+    rng = np.random.default_rng(5)
+    state, inc = int(rng.integers(0, 2**63)) << 64 | int(rng.integers(0, 2**63)), (int(rng.integers(0, 2**62)) << 1) | 1
+    buf32 = int(rng.integers(0, 2**32))
+    lib = _lib.load()
+    prev = ctypes.c_double()
+    _lib.check(lib.pbh_lhs_reference_band(1e-3 if narrow else 0.0, ctypes.byref(prev)))
+    try:
+        q, t = _ref_lhs_strata(state, inc, has32, buf32, n, d)
+        dev = _ref_stats()[0]
+    finally:
+        _lib.check(lib.pbh_lhs_reference_band(prev.value, None))
+    assert dev == (0 if narrow else 1)
+    np.testing.assert_array_equal(q, _ref_lhs_host(state, inc, has32, buf32, n, d))
+    np.testing.assert_array_equal(np.sort(t, axis=0), np.tile(np.arange(n, dtype=np.int32)[:, None], (1, d)))
+    assert np.all(q > t / n) and np.all(q <= (t + 1) / n)
+
+
+def test_iman_conover_strata_equals_sort(gpu):
+    """Iman-Conover given the columns' strata (step 1 by scatter, certified on the device) equals
+    Iman-Conover sorting them: Y, the scores and E identical.  Covered: continuous columns,
+    discrete ones (ties: average ranks from the runs), and hints the check must reject (a
+    decreasing transform of the column, strata that are not a permutation): those columns are
+    sorted instead, with the same result."""
+    import scipy.stats
+
+    from oracle.pipeline import cfg3_corr, cfg_dists
+    from probabilit_amd import device, qmc
+    from probabilit_amd.correlation import ImanConover
+
+    n, d, seed = 50_000, 8, 7
+    src = qmc.make_source("lhs", n, d, seed, stream="reference")
+    src.keep_strata = True
+    q = device.to_host(src.matrix())
+    strata = [src.strata_of(c) for c in range(d)]
+    dists = cfg_dists(d)
+    X = np.stack([getattr(scipy.stats, nm)(**kw).ppf(q[c]) for c, (nm, kw) in enumerate(dists)])
+    X[5] = -X[5]  # decreasing: the strata are not its ranks (inversions) -> sorted
+    bad = device.to_host(strata[6]).copy()
+    bad[10] = bad[11]  # not a permutation: a stratum left NaN -> sorted
+    strata[6] = device.to_device(bad)
+    strata[7] = None  # no hint
+    block = device.to_device(X).contiguous()
+    ic = ImanConover().set_target(cfg3_corr(d))
+    dbg_a = {"S": device.empty((d, n)), "E": np.zeros((d, d))}
+    dbg_b = {"S": device.empty((d, n)), "E": np.zeros((d, d))}
+    Ya = device.to_host(ic._transform_device(block, strata=strata, debug=dbg_a))
+    Yb = device.to_host(ic._transform_device(block, debug=dbg_b))
+    np.testing.assert_array_equal(device.to_host(dbg_a["S"]), device.to_host(dbg_b["S"]))
+    np.testing.assert_array_equal(dbg_a["E"], dbg_b["E"])
+    np.testing.assert_array_equal(Ya, Yb)
+    assert any(nm == "poisson" for nm, _ in dists)  # a tied column took the heads branch

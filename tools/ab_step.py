@@ -1,0 +1,56 @@
+"""Interleaved A/B of bench.py's cfg3 step (N = 1e8, d = 32, LHS + ppf + Iman-Conover) across library
+variants built by `python -m probabilit_amd.build --variant NAME -D ...`: each variant runs in
+its own process (the library loads once), alternating, and prints its ms per step.
+python tools/ab_step.py [--rounds 2] [--steps 4] default sg128 ..."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r"""
+import os, sys, time, json
+sys.path.insert(0, {root!r})
+from probabilit_amd import _lib
+if {variant!r} != "default":
+    _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), "libprobabilit_hip_{variant}.so")
+import torch
+import numpy as np
+import probabilit_amd  # noqa: F401
+from probabilit_amd import device
+from probabilit_amd.modeling import Distribution, NoOp
+dev = device.device()
+base = [("norm", {{"loc": 0.0, "scale": 1.0}}), ("gamma", {{"a": 2.0}}), ("triang", {{"c": 0.3}}),
+        ("poisson", {{"mu": 4.0}}), ("norm", {{"loc": 5.0, "scale": 2.0}}), ("gamma", {{"a": 0.7, "scale": 3.0}}),
+        ("triang", {{"c": 0.8, "loc": 1.0, "scale": 2.0}}), ("poisson", {{"mu": 30.0}})]
+dists = (base * 4)[:32]
+A = np.random.default_rng(0).normal(size=(64, 32))
+C = 0.9 * np.corrcoef(A, rowvar=False) + 0.1 * np.eye(32)
+ds = [Distribution(name, **kw) for name, kw in dists]
+root = NoOp(*ds).correlate(*ds, corr_mat=C)
+root.sample_device(100_000_000, random_state=0, method="lhs")
+torch.cuda.synchronize(dev)
+t = time.perf_counter()
+for i in range({steps}):
+    root.sample_device(100_000_000, random_state=1 + i, method="lhs")
+torch.cuda.synchronize(dev)
+print(json.dumps({{"variant": {variant!r}, "ms": round(1e3 * (time.perf_counter() - t) / {steps}, 2)}}), flush=True)
+"""
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rounds", type=int, default=2)
+ap.add_argument("--steps", type=int, default=4)
+ap.add_argument("variants", nargs="+")
+a = ap.parse_args()
+out = []
+for r in range(a.rounds):
+    for v in a.variants:
+        p = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, variant=v, steps=a.steps)],
+                           capture_output=True, text=True, timeout=600)
+        if p.returncode != 0:
+            print(p.stderr[-2000:], file=sys.stderr)
+            sys.exit(p.returncode)
+        out.append(json.loads(p.stdout.strip().splitlines()[-1]))
+        print(json.dumps(out[-1]), flush=True)
+print(json.dumps({"runs": out}))
