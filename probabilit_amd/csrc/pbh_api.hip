@@ -681,14 +681,52 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
       PBH_CHECK_HIP(hipMemcpyAsync(hists_host.data(), hists, (size_t)k * 1024 * 4, hipMemcpyDeviceToHost, s));
       PBH_CHECK_HIP(hipStreamSynchronize(s));
     }
-    for (int c = 0; c < k && st == PBH_OK; ++c) {
-      st = materialise(c);
-      if (st) break;
-      const uint32_t* hc = hists ? hists + (size_t)c * 1024 : nullptr;
-      const int flat = hists ? (code_hist_flat(hists_host.data() + (size_t)c * 1024, n) ? 1 : 0) : 1;
-      st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
-                          a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n, hc,
-                          flat);
+    // Materialised columns (X given) on the step-4 lanes, each lane with its own reorder
+    // workspace carved from the generated path's per-lane staging (unused here): a column's code
+    // sort waits for its run flags on the host (its lane only), while the other lanes go on with
+    // the placements queued before it; the placements' look-back checks land in one device word
+    // read once at the end.  (About half of a column's step 4 at 1e7 rows is latency: the
+    // one-sweep look-back chains and the per-column readback.)
+    const int nts = step4_streams();
+    const bool lanes_on = !a->columns && nts > 1 && reorder_ws_bytes(n) <= step4_gen_column_bytes(n);
+    if (lanes_on) {
+      Step4Lanes lanes(n, L.s4column, nullptr, s);
+      std::vector<ReorderWs> lrw(lanes.ns);
+      for (int i = 0; i < lanes.ns && st == PBH_OK; ++i)
+        st = reorder_carve((char*)L.s4column + (size_t)i * step4_gen_column_bytes(n), n, lrw[i], s);
+      if (st) return st;
+      int32_t* err = L.flag + 1;
+      PBH_CHECK_HIP(hipMemsetAsync(err, 0, sizeof(int32_t), s));
+      sync_on_exit.side = true;
+      if ((st = lanes.begin())) return st;
+      for (int c = 0; c < k && st == PBH_OK; ++c) {
+        const int i = lanes.next();
+        const uint32_t* hc = hists ? hists + (size_t)c * 1024 : nullptr;
+        const int flat = hists ? (code_hist_flat(hists_host.data() + (size_t)c * 1024, n) ? 1 : 0) : 1;
+        st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs,
+                            a->y_rs, a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, lrw[i], lanes.ss[i],
+                            L.codes + (int64_t)c * n, hc, flat, err);
+      }
+      const int sj = lanes.join();  // s (and the histograms' free on it) after every lane
+      if (st) return st;
+      if (sj) return sj;
+      int32_t e = 0;
+      PBH_CHECK_HIP(hipMemcpyAsync(&e, err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      PBH_CHECK_HIP(hipStreamSynchronize(s));
+      if (e) {
+        set_error("row placement: one-sweep look-back did not complete");
+        return PBH_ERR_HIP;
+      }
+    } else {
+      for (int c = 0; c < k && st == PBH_OK; ++c) {
+        st = materialise(c);
+        if (st) break;
+        const uint32_t* hc = hists ? hists + (size_t)c * 1024 : nullptr;
+        const int flat = hists ? (code_hist_flat(hists_host.data() + (size_t)c * 1024, n) ? 1 : 0) : 1;
+        st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs,
+                            a->y_rs, a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n,
+                            hc, flat);
+      }
     }
     if (st) return st;
   }

@@ -118,8 +118,10 @@ int reorder_carve(void* ws, int64_t n, ReorderWs& w, hipStream_t s);
 // codes (optional): code_of(cs) already computed (by the step-3 kernel); not modified.
 // code_hist (optional): the codes' byte histograms on the device with the host's decision
 // `code_flat` (code_hist_flat), so that the bucket path needs no sync of its own.
+// err (optional, device): the placement's look-back failure is OR-ed into *err instead of being
+// read back (no host synchronisation after the placement: columns pipelined over streams).
 int reorder_column(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx,
                    ReorderWs& w, hipStream_t s, const uint32_t* codes = nullptr, const uint32_t* code_hist = nullptr,
-                   int code_flat = 1);
+                   int code_flat = 1, int32_t* err = nullptr);
 
 }  // namespace pbh

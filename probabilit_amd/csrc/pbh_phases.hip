@@ -110,7 +110,8 @@ int reorder_carve(void* ws, int64_t n, ReorderWs& w, hipStream_t s) {
 // rank - 1 of row r is its sorted position, and Y is written by the LDS row placement; exact
 // ties use the tie-aware gather, and a run longer than kMaxRun the 64-bit sort.
 int reorder_column(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx,
-                   ReorderWs& w, hipStream_t s, const uint32_t* codes, const uint32_t* code_hist, int code_flat) {
+                   ReorderWs& w, hipStream_t s, const uint32_t* codes, const uint32_t* code_hist, int code_flat,
+                   int32_t* err) {
   SortBuffers& sb = w.sb;
   RankOut out = {};
   out.sorted_src = sorted_src;
@@ -157,7 +158,7 @@ int reorder_column(const double* cs, int64_t n, const double* sorted_src, double
     pb.partials = sb.partials;
     pb.status = sb.status;
     pb.bases = sb.bases;
-    return place_by_row(sb.vals[buf], vals, n, y, y_rs, pb, s);
+    return place_by_row(sb.vals[buf], vals, n, y, y_rs, pb, s, err);
   }
   if (!(run_flags & 1)) return rank_finish(kModeGather, nullptr, sb.vals[buf], n, w.tb, out, s, w.eqprev);
   st = load_keys(cs, 1, n, sb.keys[0], nullptr, s);

@@ -1344,13 +1344,27 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_place_gen_runs(const uint64_
 }
 
 // counts[0] += #(x[t] == x[t+1]), counts[1] += #(x[t] > x[t+1] or unordered)
+// (kCheckU pairs per thread and step, their loads issued together: one pair per step left each
+// wave a single load in flight, 111 us per 1e7)
+constexpr int kCheckU = 4;
 __global__ __launch_bounds__(kBlock) void k_check_sorted(const double* __restrict__ x, int64_t n,
                                                          unsigned long long* counts) {
   unsigned long long ties = 0, inv = 0;
-  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t + 1 < n; t += (int64_t)gridDim.x * kBlock) {
-    double a = x[t], b = x[t + 1];
-    ties += (a == b);
-    inv += !(a <= b);
+  for (int64_t base = (int64_t)blockIdx.x * kBlock * kCheckU; base + 1 < n;
+       base += (int64_t)gridDim.x * kBlock * kCheckU) {
+    double a[kCheckU], b[kCheckU];
+#pragma unroll
+    for (int u = 0; u < kCheckU; ++u) {
+      const int64_t t = base + u * kBlock + threadIdx.x;
+      const bool in = t + 1 < n;
+      a[u] = in ? x[t] : 0.0;
+      b[u] = in ? x[t + 1] : 1.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kCheckU; ++u) {
+      ties += (a[u] == b[u]);
+      inv += !(a[u] <= b[u]);
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -2385,7 +2399,7 @@ int sort_heads(uint32_t* heads, int64_t nh, hipStream_t s) {
 
 int check_sorted(const double* x, int64_t n, unsigned long long* counts, hipStream_t s) {
   PBH_CHECK_HIP(hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), s));
-  hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, x, n, counts);
+  hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(n, kBlock * kCheckU, 4096)), dim3(kBlock), 0, s, x, n, counts);
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }

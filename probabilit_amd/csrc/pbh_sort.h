@@ -79,7 +79,9 @@ struct PlaceBuffers {
   uint64_t* status;    // one-sweep look-back words
   uint32_t* bases;     // 256 digit bases
 };
+// err (optional, device): a look-back failure is OR-ed into *err on the stream instead of being
+// read back with a synchronisation
 int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, int64_t y_rs, const PlaceBuffers& pb,
-                 hipStream_t s);
+                 hipStream_t s, int32_t* err = nullptr);
 
 }  // namespace pbh

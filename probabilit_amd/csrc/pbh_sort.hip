@@ -393,6 +393,10 @@ void launch_onesweep(const K* kin, const V* vin, K* kout, V* vout, int64_t n, in
 }
 
 // ------------------------------------------------------------------ row placement
+__global__ void k_or_flag(const uint32_t* __restrict__ word, int32_t* __restrict__ err) {
+  if (threadIdx.x == 0 && *word) atomicOr(err, 1);
+}
+
 // Bucket b = rows [b * kPlaceRows, (b + 1) * kPlaceRows).  Because `rows` is a permutation,
 // after the bucket passes bucket b occupies exactly positions [b * kPlaceRows, ...) of the
 // staging arrays; one workgroup assembles its bucket in LDS and writes it out contiguously.
@@ -699,7 +703,7 @@ __global__ __launch_bounds__(64 * kCBWaves) void k_code_buckets(const uint32_t* 
 }  // namespace
 
 int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, int64_t y_rs, const PlaceBuffers& pb,
-                 hipStream_t s) {
+                 hipStream_t s, int32_t* err) {
   PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "place_by_row: n out of range");
   int bits = 0;
   while (((int64_t)1 << bits) < n) ++bits;
@@ -722,7 +726,10 @@ int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, in
   const int64_t nb = (n + kPlaceRows - 1) / kPlaceRows;
   PBH_TIMED(kKPlace, s, hipLaunchKernelGGL(k_place, dim3((unsigned)nb), dim3(T), 0, s, rin, vin, n, y, y_rs));
   PBH_CHECK_LAUNCH();
-  if (bits > kPlaceShift) {
+  if (bits > kPlaceShift && err) {
+    hipLaunchKernelGGL(k_or_flag, dim3(1), dim3(64), 0, s, (const uint32_t*)(pb.status + nt * 256) + 1, err);
+    PBH_CHECK_LAUNCH();
+  } else if (bits > kPlaceShift) {
     uint32_t stuck = 0;
     PBH_CHECK_HIP(hipMemcpyAsync(&stuck, (uint32_t*)(pb.status + nt * 256) + 1, 4, hipMemcpyDeviceToHost, s));
     PBH_CHECK_HIP(hipStreamSynchronize(s));

@@ -1,5 +1,6 @@
 """Interleaved A/B of bench.py's cfg3 step (N = 1e8, d = 32, LHS + ppf + Iman-Conover) across library
-variants built by `python -m probabilit_amd.build --variant NAME -D ...`: each variant runs in
+variants built by `python -m probabilit_amd.build --variant NAME -D ...` (--refstream: bench.py's
+reference_stream workload, the same graph at 1e7 rows on stream="reference"): each variant runs in
 its own process (the library loads once), alternating, and prints its ms per step.
 python tools/ab_step.py [--rounds 2] [--steps 4] default sg128 ..."""
 import argparse
@@ -29,11 +30,13 @@ A = np.random.default_rng(0).normal(size=(64, 32))
 C = 0.9 * np.corrcoef(A, rowvar=False) + 0.1 * np.eye(32)
 ds = [Distribution(name, **kw) for name, kw in dists]
 root = NoOp(*ds).correlate(*ds, corr_mat=C)
-root.sample_device(100_000_000, random_state=0, method="lhs")
+kw = dict(method="lhs", stream="reference") if {ref!r} else dict(method="lhs")
+rows = 10_000_000 if {ref!r} else 100_000_000
+root.sample_device(rows, random_state=0, **kw)
 torch.cuda.synchronize(dev)
 t = time.perf_counter()
 for i in range({steps}):
-    root.sample_device(100_000_000, random_state=1 + i, method="lhs")
+    root.sample_device(rows, random_state=1 + i, **kw)
 torch.cuda.synchronize(dev)
 print(json.dumps({{"variant": {variant!r}, "ms": round(1e3 * (time.perf_counter() - t) / {steps}, 2)}}), flush=True)
 """
@@ -41,12 +44,13 @@ print(json.dumps({{"variant": {variant!r}, "ms": round(1e3 * (time.perf_counter(
 ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--steps", type=int, default=4)
+ap.add_argument("--refstream", action="store_true", help="the reference-stream side figure (1e7 rows) instead")
 ap.add_argument("variants", nargs="+")
 a = ap.parse_args()
 out = []
 for r in range(a.rounds):
     for v in a.variants:
-        p = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, variant=v, steps=a.steps)],
+        p = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, variant=v, steps=a.steps, ref=a.refstream)],
                            capture_output=True, text=True, timeout=600)
         if p.returncode != 0:
             print(p.stderr[-2000:], file=sys.stderr)
