@@ -194,8 +194,8 @@ struct Step4Lanes {
   Step4Column cb[kStep4MaxStreams];
   uint32_t* codes[kStep4MaxStreams];
   std::vector<hipEvent_t> events;
-  Step4Lanes(int64_t n, void* column_ws, void* codes_ws, hipStream_t s_) : s(s_) {
-    ns = step4_streams();
+  Step4Lanes(int64_t n, void* column_ws, void* codes_ws, hipStream_t s_, int max_lanes = kStep4MaxStreams) : s(s_) {
+    ns = step4_streams() < max_lanes ? step4_streams() : max_lanes;
     for (int i = 0; i < ns; ++i) {
       step4_gen_carve_column((char*)column_ws + (size_t)i * step4_gen_column_bytes(n), n, cb[i]);
       codes[i] = codes_ws ? (uint32_t*)((char*)codes_ws + (size_t)i * align256((size_t)n * 4)) : nullptr;
@@ -686,11 +686,12 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     // sort waits for its run flags on the host (its lane only), while the other lanes go on with
     // the placements queued before it; the placements' look-back checks land in one device word
     // read once at the end.  (About half of a column's step 4 at 1e7 rows is latency: the
-    // one-sweep look-back chains and the per-column readback.)
+    // one-sweep look-back chains and the per-column readback.)  Two lanes: 75.7-76.3 ms per
+    // reference-stream call at 1e7 x 32 against 77.2-78.5 with three (profiles/r05/ab_step_lanes_r5zd_refstream.log).
     const int nts = step4_streams();
     const bool lanes_on = !a->columns && nts > 1 && reorder_ws_bytes(n) <= step4_gen_column_bytes(n);
     if (lanes_on) {
-      Step4Lanes lanes(n, L.s4column, nullptr, s);
+      Step4Lanes lanes(n, L.s4column, nullptr, s, 2);
       std::vector<ReorderWs> lrw(lanes.ns);
       for (int i = 0; i < lanes.ns && st == PBH_OK; ++i)
         st = reorder_carve((char*)L.s4column + (size_t)i * step4_gen_column_bytes(n), n, lrw[i], s);

@@ -50,11 +50,13 @@ a = ap.parse_args()
 out = []
 for r in range(a.rounds):
     for v in a.variants:
-        p = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, variant=v, steps=a.steps, ref=a.refstream)],
-                           capture_output=True, text=True, timeout=600)
+        lib, *envs = v.split("+")  # "NAME+VAR=VALUE+...": library variant NAME with those env settings
+        env = dict(os.environ, **dict(e.split("=", 1) for e in envs))
+        p = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, variant=lib, steps=a.steps, ref=a.refstream)],
+                           capture_output=True, text=True, timeout=600, env=env)
         if p.returncode != 0:
             print(p.stderr[-2000:], file=sys.stderr)
             sys.exit(p.returncode)
-        out.append(json.loads(p.stdout.strip().splitlines()[-1]))
+        out.append(dict(json.loads(p.stdout.strip().splitlines()[-1]), variant=v))
         print(json.dumps(out[-1]), flush=True)
 print(json.dumps({"runs": out}))
