@@ -15,9 +15,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--variant", default=None, help="load libprobabilit_hip_<variant>.so (build.py --variant)")
     a = ap.parse_args()
     import bench
     from probabilit_amd import _lib, device
+
+    if a.variant:
+        _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), f"libprobabilit_hip_{a.variant}.so")
 
     device.device()
     base = [("norm", {"loc": 0.0, "scale": 1.0}), ("gamma", {"a": 2.0}), ("triang", {"c": 0.3}),
