@@ -468,8 +468,11 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
     }
     if constexpr (is_gamma_family(D)) {
       if (p.gg.y) {  // gammaincinv through the guide (igami_guided: within ~1e-12 of igami)
-        const double g = sf::igami_guided(D == PBH_DIST_MAXWELL ? 1.5 : D == PBH_DIST_NAKAGAMI ? s0 : .5 * s0, q,
-                                          &p.ga, p.gg);
+        // the fallbacks behind a call (COLD): inline, with a runtime shape they cost registers
+        // and occupancy: chi / nakagami / chi2 0.24 -> 0.14 ms per 1e7 (maxwell, whose shape
+        // is a constant, was already 0.14; profiles/r05/ext_cold_ab_r5zh/)
+        const double g = sf::igami_guided<true>(D == PBH_DIST_MAXWELL ? 1.5 : D == PBH_DIST_NAKAGAMI ? s0 : .5 * s0, q,
+                                                &p.ga, p.gg);
         double x;
         if constexpr (D == PBH_DIST_CHI2)
           x = 2.0 * g;

@@ -1,7 +1,9 @@
 """Inverse-CDF sweep times of the extended distributions (pbh_ppf over an HBM-resident quantile
 column, HIP events via pbh_timing, best of 3 after a warm call) and the correlated-PERT fast
-path end to end: python tools/ext_sweep.py [rows]"""
+path end to end: python tools/ext_sweep.py [rows [variant]] (variant: a library built by
+build.py --variant)"""
 import json
+import os
 import sys
 import time
 
@@ -10,6 +12,9 @@ import numpy as np
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 import probabilit_amd  # noqa: E402,F401
 from probabilit_amd import _lib, device, native  # noqa: E402
+
+if len(sys.argv) > 2:
+    _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), f"libprobabilit_hip_{sys.argv[2]}.so")
 
 
 def main():
