@@ -100,6 +100,16 @@ PBH_HD inline double truncnorm_ppf01(double q, double a, double b) {  // scipy t
   if (a < 0.0) return ndtri_exp(log_sum(log_ndtr(a), log(q) + log_gauss_mass(a, b)));
   return -ndtri_exp(log_sum(log_ndtr(-b), log1p(-q) + log_gauss_mass(a, b)));
 }
+// The same with the terms that depend on (a, b) alone evaluated once (scalar parameters):
+// c0 = log_ndtr(a) for a < 0, else log_ndtr(-b); c1 = log_gauss_mass(a, b)
+PBH_HD inline void truncnorm_consts(double a, double b, double* c0, double* c1) {
+  *c0 = a < 0.0 ? log_ndtr(a) : log_ndtr(-b);
+  *c1 = log_gauss_mass(a, b);
+}
+PBH_HD inline double truncnorm_ppf01_c(double q, double a, double c0, double c1) {
+  if (a < 0.0) return ndtri_exp(log_sum(c0, log(q) + c1));
+  return -ndtri_exp(log_sum(c0, log1p(-q) + c1));
+}
 
 // ---------------------------------------------------------------- incomplete beta (Cephes)
 PBH_HD inline double lbeta(double a, double b) { return lgam(a) + lgam(b) - lgam(a + b); }
