@@ -27,7 +27,8 @@
 // before its own step is V(q) = V(M(q)), or q + 1 when nothing targeted it, and
 //   x[i] = V(S(i)) (or j_i + 1 when S(i) is none),   x[0] = V(M(0)) (or 1).
 // A stable radix sort of the steps by target (the library's one-sweep passes), one pass to link
-// each group, one pointer chase per position: O(n) work, no sequential pass.
+// each group, then per row one pointer chase from the position it reads: O(n) work, no
+// sequential pass.
 #include <math.h>
 #include <string.h>
 
@@ -386,31 +387,30 @@ __global__ void k_flag_if(const uint32_t* __restrict__ word, int32_t* __restrict
   if (threadIdx.x == 0 && blockIdx.x == 0 && *word) atomicOr(err, bit);
 }
 
-__global__ __launch_bounds__(256) void k_perm_values(const int32_t* __restrict__ M, int64_t n,
-                                                     int32_t* __restrict__ V, const int32_t* __restrict__ ok) {
-  if (!*ok) return;
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256) {
-    int32_t x = (int32_t)q, y;
-    while ((y = M[x]) >= 0) x = y;  // M(x) > x: the chain ends
-    V[q] = x + 1;
-  }
+// V(x) = V(M(x)), or x + 1 at the end of the chain (M(x) > x: it ends)
+__device__ __forceinline__ int32_t perm_value(const int32_t* __restrict__ M, int32_t x) {
+  int32_t y;
+  while ((y = M[x]) >= 0) x = y;
+  return x + 1;
 }
 
-// q = (perm - u) / n for one column (u in q on entry); strata (optional) = perm - 1
+// q = (perm - u) / n for one column (u in q on entry); strata (optional) = perm - 1.  V is
+// followed along M only from the positions a row needs (S(r), or M(0) for row 0) instead of
+// being tabulated for every position first (a separate pass of its own, 0.14 ms per 1e7).
 __global__ __launch_bounds__(256) void k_perm_combine(const int32_t* __restrict__ J, const int32_t* __restrict__ S,
-                                                      const int32_t* __restrict__ V, const int32_t* __restrict__ M,
-                                                      int64_t n, double* __restrict__ q,
-                                                      const int32_t* __restrict__ ok, int32_t* __restrict__ strata) {
+                                                      const int32_t* __restrict__ M, int64_t n,
+                                                      double* __restrict__ q, const int32_t* __restrict__ ok,
+                                                      int32_t* __restrict__ strata) {
   if (!*ok) return;
   const double dn = (double)n;
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
     int32_t v;
     if (r == 0) {
       const int32_t f = M[0];
-      v = f >= 0 ? V[f] : 1;
+      v = f >= 0 ? perm_value(M, f) : 1;
     } else {
       const int32_t nx = S[r];
-      v = nx >= 0 ? V[nx] : J[r] + 1;
+      v = nx >= 0 ? perm_value(M, nx) : J[r] + 1;
     }
     q[r] = ((double)v - q[r]) / dn;  // (perms - samples) / n: subtract, then divide
     if (strata) strata[r] = v - 1;
@@ -563,7 +563,7 @@ struct SideJoin {
 
 struct PermBufs {
   SortBuffers sb;
-  int32_t *S, *V, *M;
+  int32_t *S, *M;
 };
 
 // column c's permutation from its targets (J: n words), combined into q[0 .. n) (u on entry);
@@ -583,9 +583,7 @@ int column_to_q(const int32_t* J, int64_t n, PermBufs& pb, const int32_t* ok, in
   hipLaunchKernelGGL(k_perm_links, dim3(grid), dim3(256), 0, s, (const uint32_t*)pb.sb.keys[cur], pb.sb.vals[cur], m,
                      pb.S, pb.M, ok);
   PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_perm_values, dim3(grid), dim3(256), 0, s, pb.M, n, pb.V, ok);
-  PBH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_perm_combine, dim3(grid), dim3(256), 0, s, J, pb.S, pb.V, pb.M, n, q, ok, strata);
+  hipLaunchKernelGGL(k_perm_combine, dim3(grid), dim3(256), 0, s, J, pb.S, pb.M, n, q, ok, strata);
   PBH_CHECK_LAUNCH();
   return PBH_OK;
 }
@@ -619,7 +617,7 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
       (st = b.get(&pre, 2 * (pr.nb + 1))) || (st = b.get(&tot2, pr.nb)) || (st = b.get(&pre2, pr.nb + 1)) ||
       (st = b.get(&list, cap)) || (st = b.get(&dec, cap)) || (st = b.get(&band_dev, pr.nband)) ||
       (st = b.get(&P, d + 1)) || (st = b.get(&err, 1)) || (st = b.get(&okc, d)) || (st = b.get(&pcg_ws, 128)) ||
-      (st = b.get(&pb.S, n)) || (st = b.get(&pb.V, n)) || (st = b.get(&pb.M, n)) ||
+      (st = b.get(&pb.S, n)) || (st = b.get(&pb.M, n)) ||
       (st = b.get(&sort_ws, sort_workspace_bytes(n))))
     return st;
   sort_carve(sort_ws, n, pb.sb);
