@@ -61,7 +61,7 @@ PMC_NAMES = {"k_scatter<u32>": ["k_onesweep<unsigned int, unsigned int, 36>", "k
                                   "k_scatter<unsigned int, double>"],
              "k_code_runs": ["k_code_buckets", "k_runs_resolve"], "k_gram": ["k_gram_mfma", "k_gram"],
              "k_apply": ["k_apply_mfma_w2<true>", "k_apply_mfma_w2<false>", "k_apply_mfma", "k_apply<32>"], "k_digit_hist<u32>": ["k_digit_hist<unsigned int>"],
-             "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores"],
+             "k_place": ["k_place"], "k_perm_scores": ["k_perm_scores<false>", "k_perm_scores"],
              "k_finish": ["k_finish_q<2048, 512, false>", "k_finish_q<1024, 512, false>", "k_finish_q<1024, 512, true>", "k_finish_q<2048, 512, true>",
                           "k_finish_q<1024, 256, true>", "k_finish_ah<2048>", "k_finish_ah<1024>", "k_finish_ah<4096>", "k_finish_fused<2, 4096>", "k_finish_fused<2, 4096, false>",
                           "k_finish_fused<2, 4096, true>", "k_finish_fused<1, 4096>", "k_finish_fused<2, 2048>",
