@@ -527,9 +527,26 @@ struct LhsCol {
   uint32_t col;
 };
 
+// binom / bernoulli / nbinom with scalar parameters: a CDF table of at most kExtLdsTab entries
+// (and its complement) is staged in LDS, so the binary search reads LDS instead of a cached
+// global line per step
+constexpr int kExtLdsTab = 512;
+template <int D>
+constexpr bool ext_table_discrete() {
+  return D == PBH_DIST_BINOM || D == PBH_DIST_BERNOULLI || D == PBH_DIST_NBINOM;
+}
+
 template <int D, bool LHS>
 __global__ __launch_bounds__(256) void k_ppf_ext(const double* __restrict__ q, int64_t q_stride, LhsCol lc, int64_t n,
                                                  Params4 prm, double* __restrict__ out, int32_t* flag) {
+  if constexpr (ext_table_discrete<D>()) {
+    __shared__ double tab[2 * kExtLdsTab];
+    if (prm.dt && prm.dlen <= kExtLdsTab) {  // block-uniform
+      for (int k = threadIdx.x; k < 2 * prm.dlen; k += 256) tab[k] = prm.dt[k];
+      __syncthreads();
+      prm.dt = tab;
+    }
+  }
   Philox ph(lc.seed);
   FeistelPerm fp(ph, (uint64_t)(LHS ? lc.n : 1), lc.col);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
