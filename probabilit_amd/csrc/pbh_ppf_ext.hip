@@ -802,6 +802,14 @@ __global__ __launch_bounds__(256) void k_ext_place(const uint64_t* __restrict__ 
                                                    const int32_t* __restrict__ state) {
   if (state && *state) return;
   __shared__ double buf[kExtGenRows];
+  if constexpr (ext_table_discrete<D>()) {  // as k_ppf_ext: the small CDF tables from LDS
+    __shared__ double tab[2 * kExtLdsTab];
+    if (prm.dt && prm.dlen <= kExtLdsTab) {  // block-uniform
+      for (int k = threadIdx.x; k < 2 * prm.dlen; k += 256) tab[k] = prm.dt[k];
+      __syncthreads();
+      prm.dt = tab;
+    }
+  }
   Philox ph(seed);
   for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < rows; b += gridDim.x) {
     const int64_t r0 = b << kGenPlaceShift;
