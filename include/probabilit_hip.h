@@ -185,8 +185,12 @@ int pbh_lhs_reference_perms(const uint64_t* state_host, const uint64_t* inc_host
 int pbh_lhs_reference_band(double sigmas, double* previous);
 /* The process cache of inverse-CDF setup tables (gamma / beta guides, poisson / binom / nbinom CDF
  * tables, keyed by their scalar parameters; pbh_table_cache.hip): tables held, their bytes, and
- * the calls served from it. */
+ * the calls served from it.  The cache holds at most 1 GiB and 4 096 tables of <= 64 MiB each
+ * (larger ones are built per call); when full, the least recently used table no call holds is
+ * evicted.  pbh_table_cache_clear frees every table no call holds (after the kernels that read
+ * them), reporting how many it freed and kept; safe between calls. */
 int pbh_table_cache_stats(int64_t* entries, int64_t* bytes, int64_t* hits);
+int pbh_table_cache_clear(int64_t* freed, int64_t* kept);
 int pbh_lhs_reference_stats(int32_t* device, int32_t* attempts, int64_t* ambiguous);
 
 /* Scrambled Halton points, bit-exact with scipy.stats.qmc.Halton(d, rng=...) (modeling.py:481,488):
@@ -347,6 +351,13 @@ int pbh_ic_apply(double* S, int64_t n, int32_t k, int64_t ld, const double* L_ho
 int pbh_ic_reorder_workspace_size(int64_t n, size_t* bytes);
 int pbh_ic_reorder(const double* cs, int64_t n, const double* sorted_src, double* y, int64_t y_rs, int32_t* idx_out,
                    void* ws, size_t ws_bytes, void* stream);
+/* Step 1 for one materialised column on its owner (correlation.py:394-395): scores[r] =
+ * ndtri(rankdata(x)[r] / (n + 1)) and, when sorted_x is not NULL, sorted_x = np.sort(x) (the
+ * sort(X[:, k]) of :423, kept for the owner's pbh_ic_reorder).  Same kernels as a materialised
+ * column of pbh_iman_conover; a NaN in x sets *nonfinite_flag (device, optional).
+ * ws >= pbh_rank_workspace_size(n).  Synchronises the stream. */
+int pbh_ic_column_scores(const double* x, int64_t stride, int64_t n, double* scores, double* sorted_x,
+                         int32_t* nonfinite_flag, void* ws, size_t ws_bytes, void* stream);
 
 /* Step 4 of the columns a rank owns in a row-sharded run (correlation.py:418-423 for the column
  * owner): m generated columns (as pbh_iman_conover's `columns`) of an

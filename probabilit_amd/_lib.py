@@ -50,11 +50,11 @@ SYMBOLS = ["pbh_version", "pbh_last_error", "pbh_init", "pbh_fill_lhs", "pbh_fil
            "pbh_pcg64_random", "pbh_halton_workspace_size", "pbh_fill_halton",
            "pbh_affine_workspace_size", "pbh_affine_rows", "pbh_table_ppf", "pbh_permcorr_workspace_size",
            "pbh_permcorr_climb", "pbh_sobol_ppf", "pbh_lhs_reference_workspace_size",
-           "pbh_lhs_reference", "pbh_lhs_reference_strata", "pbh_lhs_reference_perms", "pbh_lhs_reference_band", "pbh_lhs_reference_stats", "pbh_table_cache_stats", "pbh_hbm_copy", "pbh_dag_eval",
+           "pbh_lhs_reference", "pbh_lhs_reference_strata", "pbh_lhs_reference_perms", "pbh_lhs_reference_band", "pbh_lhs_reference_stats", "pbh_table_cache_stats", "pbh_table_cache_clear", "pbh_hbm_copy", "pbh_dag_eval",
            "pbh_lhs_sorted_counts", "pbh_sort_heads", "pbh_ic_owned_workspace_size", "pbh_ic_owned_create",
            "pbh_ic_owned_column", "pbh_ic_owned_finish", "pbh_lhs_values_at", "pbh_lhs_ppf_columns", "pbh_ic_owned_destroy", "pbh_event_create",
            "pbh_event_destroy", "pbh_event_record", "pbh_stream_wait_event", "pbh_event_synchronize",
-           "pbh_set_serial"]
+           "pbh_set_serial", "pbh_ic_column_scores"]
 
 # kernel ids of pbh_kernel_name / pbh_timing_read (csrc/pbh_timing.h)
 KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_rank_finish<scores>",
@@ -183,6 +183,8 @@ def load():
         "pbh_lhs_reference_band": ([ctypes.c_double, ctypes.POINTER(ctypes.c_double)], i32),
         "pbh_lhs_reference_stats": ([ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i64)], i32),
         "pbh_table_cache_stats": ([ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
+        "pbh_table_cache_clear": ([ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
+        "pbh_ic_column_scores": ([vp, i64, i64, vp, vp, vp, vp, sz, vp], i32),
         "pbh_permcorr_climb": ([vp, vp, i64, ctypes.c_int32, i64, vp, vp, vp, vp, vp, vp, i64, dbl, vp, vp, vp, sz, vp],
                                i32),
         "pbh_lhs_sorted_counts": ([u64, i64, i64, i64, i32, i32, vp, i32, vp, vp, vp, ctypes.c_uint32, vp, i32, vp],

@@ -217,12 +217,16 @@ class Cholesky(Correlator):
         Y = self._transform_device(block).t()
         return Y.contiguous() if on_device else device.to_host(Y)
 
-    def _transform_device(self, block, ev=None):
+    def _transform_device(self, block, ev=None, stats=None, n=None):
+        """block: (K, rows) device tensor.  stats / n (row-sharded runs): the column means and
+        centered Gram matrix over all n rows (distributed.block_stats); default: this block's."""
         import scipy.linalg
 
         K, N = block.shape
-        self._validate_X(block.T)
-        mean, G = _block_stats(block)
+        if n is not None:
+            N = n
+        self._validate_X(block.T if n is None else np.lib.stride_tricks.as_strided(np.zeros(1), (N, K), (0, 0)))
+        mean, G = _block_stats(block) if stats is None else stats
         std = np.sqrt(np.diag(G) / N)                        # np.std(X, axis=0)
         with np.errstate(divide="ignore", invalid="ignore"):
             cov = G / N / np.outer(std, std)                 # np.cov(X_n, rowvar=False, ddof=0)

@@ -341,3 +341,38 @@ extern "C" int pbh_ic_reorder(const double* cs, int64_t n, const double* sorted_
   if (st) return st;
   return reorder_column(cs, n, sorted_src, y, y_rs, idx_out, w, s);
 }
+
+// Step 1 of one materialised column on its owner (row-sharded Iman-Conover on materialised
+// quantiles, probabilit_amd/distributed.py iman_conover_block): the same load / radix sort /
+// rank_finish sequence pbh_iman_conover runs for a column of X, so the scores and sort(X) equal
+// the single call's bit for bit.
+extern "C" int pbh_ic_column_scores(const double* x, int64_t stride, int64_t n, double* scores, double* sorted_x,
+                                    int32_t* nonfinite_flag, void* ws, size_t ws_bytes, void* stream) {
+  PBH_REQUIRE(x && scores && ws, "pbh_ic_column_scores: null pointer");
+  PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "pbh_ic_column_scores: n out of range");
+  const size_t sb_bytes = align256(sort_workspace_bytes(n));
+  const size_t need = sb_bytes + align256(tie_workspace_bytes(n));
+  if (ws_bytes < need) {
+    set_error("pbh_ic_column_scores: workspace %zu < %zu bytes", ws_bytes, need);
+    return PBH_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  SortBuffers sb;
+  sort_carve(ws, n, sb);
+  TieBuffers tb;
+  tie_carve((char*)ws + sb_bytes, n, tb);
+  uint32_t hist_host[8 * 256];
+  sb.hist_host = hist_host;
+  int st = load_keys(x, stride, n, sb.keys[0], nonfinite_flag, s);
+  if (st) return st;
+  int buf = 0;
+  st = radix_sort_keys(sb, n, s, &buf);
+  if (st) return st;
+  RankOut out = {};
+  out.scores = scores;
+  out.sorted_x = sorted_x;
+  st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+  if (st) return st;
+  PBH_CHECK_HIP(hipStreamSynchronize(s));  // hist_host is read by the sort's copies
+  return PBH_OK;
+}

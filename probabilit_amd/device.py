@@ -153,5 +153,20 @@ def synchronize():
     _torch().cuda.synchronize(device())
 
 
+def clear_table_cache():
+    """Free the process cache of inverse-CDF setup tables (gamma / beta guides, poisson / binom /
+    nbinom CDF tables kept between calls, pbh_table_cache.hip): every table no call holds, after
+    the kernels that read it.  Returns (freed, kept).  The cache is bounded anyway (1 GiB, LRU,
+    tables over 64 MiB never kept); this returns its HBM to the caller between workloads."""
+    import ctypes
+
+    from . import _lib
+
+    device()
+    freed, kept = ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(_lib.load().pbh_table_cache_clear(ctypes.byref(freed), ctypes.byref(kept)), "pbh_table_cache_clear")
+    return freed.value, kept.value
+
+
 _TORCH = {"float64": "float64", "int64": "int64", "bool": "bool", "int32": "int32", "uint8": "uint8",
           "uint32": "int32"}

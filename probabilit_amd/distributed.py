@@ -225,6 +225,27 @@ class HipPhases:
         _lib.check(self.lib.pbh_lhs_values_at(ctypes.byref(c), n, p.data_ptr(), p.shape[0], y.data_ptr(), 1,
                                               device.stream()), "pbh_lhs_values_at")
 
+    # -- materialised columns on their owner (iman_conover_block) --------------------------
+    def column_scores(self, x, s_out, sx_out, flag):
+        """Step 1 of a whole materialised column: s_out = ndtri(rankdata(x) / (n + 1)),
+        sx_out = np.sort(x); a NaN sets flag."""
+        n = x.shape[0]
+        nbytes = ctypes.c_size_t()
+        _lib.check(self.lib.pbh_rank_workspace_size(n, ctypes.byref(nbytes)))
+        ws = self._ws(nbytes.value)
+        _lib.check(self.lib.pbh_ic_column_scores(x.data_ptr(), 1, n, s_out.data_ptr(), sx_out.data_ptr(),
+                                                 flag.data_ptr(), ws.data_ptr(), nbytes.value, device.stream()),
+                   "pbh_ic_column_scores")
+
+    def reorder(self, cs, sx, y):
+        """Step 4 of a whole column: y = sx[rankdata(cs).astype(int) - 1]."""
+        n = cs.shape[0]
+        nbytes = ctypes.c_size_t()
+        _lib.check(self.lib.pbh_ic_reorder_workspace_size(n, ctypes.byref(nbytes)))
+        ws = self._ws(nbytes.value)
+        _lib.check(self.lib.pbh_ic_reorder(cs.data_ptr(), n, sx.data_ptr(), y.data_ptr(), 1, None, ws.data_ptr(),
+                                           nbytes.value, device.stream()), "pbh_ic_reorder")
+
 
 def _solo(world):
     """world == 1 skips the collectives -- unless PBH_FORCE_COLLECTIVES=1, which runs them on a
@@ -264,19 +285,6 @@ def _all_gather_varlen(t, group, world, sizes=None):
     parts = [torch.empty_like(padded) for _ in range(world)]
     dist.all_gather(parts, padded, group=group)
     return torch.cat([p[:s] for p, s in zip(parts, sizes)]).to(dev)
-
-
-def gather_block(block, n, group, world):
-    """The (K, n) block of every rank's row shard (block: this rank's (K, rows), shards by
-    shard_bounds), on every rank: the general correlators (Iman-Conover on materialised
-    quantiles, Cholesky, Permutation, a user class) then run on the whole block, identically on
-    every rank, and each keeps its rows."""
-    import torch
-
-    b = shard_bounds(n, world)
-    sizes = [b[r + 1] - b[r] for r in range(world)]
-    return torch.stack([_all_gather_varlen(block[j].contiguous(), group, world, sizes=sizes)
-                        for j in range(block.shape[0])])
 
 
 def _all_gather_rows(t, group, world):
@@ -544,6 +552,161 @@ def _iman_conover_lhs(columns, P, n, group, world, rank, phases, flags, defer):
             raise _Redo()
     _all_reduce_flags(flags, group, world)
     return Y
+
+
+def _world(group):
+    if group is not None or _dist_initialized():
+        import torch.distributed as dist
+
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def _column_exchanges(n, K, world, rank, phases):
+    """The two all-to-all directions of a column-owner exchange over K row-sharded columns:
+    to_owner(i, src, dst): every rank's rows of each owner's i-th column (src[c]: this shard's
+    rows of column c) land in the owner's whole-column buffer dst[i]; from_owner(i, src, dst) is
+    the way back (src[i]: the owner's whole column, dst[c]: this shard's rows of column c)."""
+    rb, cb = shard_bounds(n, world), shard_bounds(K, world)
+    own = [cb[o + 1] - cb[o] for o in range(world)]
+    k_own = own[rank]
+
+    def to_owner(i, src, dst, nothing):
+        send = [src[cb[o] + i] if i < own[o] else nothing for o in range(world)]
+        recv = [dst[i][rb[s]:rb[s + 1]] if i < k_own else nothing for s in range(world)]
+        return recv, send
+
+    def from_owner(i, src, dst, nothing):
+        send = [src[i][rb[s]:rb[s + 1]] if i < k_own else nothing for s in range(world)]
+        recv = [dst[cb[o] + i] if i < own[o] else nothing for o in range(world)]
+        return recv, send
+
+    return to_owner, from_owner, k_own, max(own)
+
+
+def iman_conover_block(block, P, n, group=None, phases=None):
+    """Iman-Conover (correlation.py:368-425) of a row-sharded MATERIALISED block: block is this
+    rank's rows (K, rows) of X (shards by shard_bounds), the result this rank's rows of Y.  The
+    correlators' other sources -- Sobol', Halton, MT19937 / PCG64 quantiles, the reference LHS
+    stream, composite parameters -- take this path (natively generated LHS columns take
+    iman_conover_lhs).  Rank r owns columns [K r / R, K (r + 1) / R):
+
+        step 1  X's owned columns to their owner (all-to-all, 8 B a row); the owner ranks each
+                whole column ('average' ties) into its scores and keeps np.sort(X[:, k])
+                (pbh_ic_column_scores); the scores back to the row shards (8 B a row)
+        step 2  column sums and the centered Gram matrix all-reduced; E, L on every host
+        step 3  CS = S L^-T P^T on the local rows
+        step 4  CS's owned columns to their owner (8 B); the owner reorders its sorted X by the
+                ranks of CS (pbh_ic_reorder); Y's rows back to the row shards (8 B)
+
+    No rank holds more than its owned columns whole (K / R x N), and no correlator work is
+    replicated.  Raises ValueError exactly where ImanConover.__call__ does (NaN input, rank
+    correlation not positive definite)."""
+    world, rank = _world(group)
+    phases = phases or HipPhases()
+    K, nrows = block.shape
+    if n <= K:
+        raise ValueError(f"The matrix X must have rows > columns. Got shape: {(n, K)}")
+    if not 1 <= K <= 128:
+        raise ValueError(f"Iman-Conover on the device takes 1 to 128 variables, got {K}")
+    to_owner, from_owner, k_own, m = _column_exchanges(n, K, world, rank, phases)
+    nothing = phases.empty(0)
+
+    # ---- step 1 on the owners -------------------------------------------------------------
+    whole = [phases.empty(n) for _ in range(k_own)]
+    for i in range(m):
+        _exchange(*to_owner(i, block, whole, nothing), group, world, phases).wait()
+    sx = [phases.empty(n) for _ in range(k_own)]
+    flag = phases.zeros(1, "int32")
+    for i in range(k_own):  # the scores overwrite X's column in place (it is sorted into sx first)
+        phases.column_scores(whole[i], whole[i], sx[i], flag)
+    if int(_all_reduce(flag, group, world, op="max").cpu()[0]):
+        from .correlation import _NOT_PD_MSG
+
+        raise ValueError(_NOT_PD_MSG)  # NaN ranks: corrcoef -> NaN -> not PD (correlation.py:399-403)
+    S = phases.empty((K, nrows))
+    for i in range(m):
+        _exchange(*from_owner(i, whole, S, nothing), group, world, phases).wait()
+
+    # ---- steps 2 and 3 on the row shards ----------------------------------------------------
+    sums = _all_reduce(phases.column_sums(S), group, world)
+    gram = _all_reduce(phases.centered_gram(S, sums / float(n)), group, world)
+    try:
+        _, L = phases.factor(gram.cpu().numpy(), n)
+    except ValueError:
+        from .correlation import _NOT_PD_MSG
+
+        raise ValueError(_NOT_PD_MSG) from None
+    phases.apply(S, L, np.asarray(P, dtype=np.float64))
+
+    # ---- step 4 on the owners ---------------------------------------------------------------
+    for i in range(m):
+        _exchange(*to_owner(i, S, whole, nothing), group, world, phases).wait()
+    del S
+    ys = [phases.empty(n) for _ in range(k_own)]
+    for i in range(k_own):
+        phases.reorder(whole[i], sx[i], ys[i])
+    del whole, sx
+    Y = phases.empty((K, nrows))
+    for i in range(m):
+        _exchange(*from_owner(i, ys, Y, nothing), group, world, phases).wait()
+    return Y
+
+
+def block_stats(block, n, group=None, phases=None):
+    """Column means and the centered Gram matrix sum_r (x_r - mean)(x_r - mean)^T of a
+    row-sharded block over all n rows (the np.mean / np.cov inputs of the Cholesky correlator,
+    correlation.py:255-285, and of decorrelate): two all-reduces, no rows exchanged."""
+    world, _ = _world(group)
+    phases = phases or HipPhases()
+    sums = _all_reduce(phases.column_sums(block), group, world)
+    mean = sums / float(n)
+    gram = _all_reduce(phases.centered_gram(block, mean), group, world)
+    return mean.cpu().numpy(), gram.cpu().numpy()
+
+
+def gather_to_root(block, n, group, root=0):
+    """The whole (K, n) block on rank `root` (None elsewhere): one all-to-all in which every
+    rank sends its rows to the root only.  For correlators whose result depends on state a rank
+    cannot share by construction (an unseeded PermutationCorrelator's rng, a user class): they
+    run once, on the root, and scatter_from_root hands every rank its rows."""
+    world, rank = _world(group)
+    phases = HipPhases() if block.is_cuda else _HostPhases()
+    rb = shard_bounds(n, world)
+    K = block.shape[0]
+    full = phases.empty((K, n)) if rank == root else None
+    nothing = phases.empty(0)
+    for j in range(K):
+        send = [block[j] if d == root else nothing for d in range(world)]
+        recv = [full[j][rb[s]:rb[s + 1]] if rank == root else nothing for s in range(world)]
+        _exchange(recv, send, group, world, phases).wait()
+    return full
+
+
+def scatter_from_root(full, K, n, group, like, root=0):
+    """Every rank's rows (K, rows) of the root's (K, n) block `full` (the inverse of gather_to_root)."""
+    world, rank = _world(group)
+    phases = HipPhases() if like.is_cuda else _HostPhases()
+    rb = shard_bounds(n, world)
+    out = phases.empty((K, rb[rank + 1] - rb[rank]))
+    nothing = phases.empty(0)
+    for j in range(K):
+        send = [full[j][rb[d]:rb[d + 1]] if rank == root else nothing for d in range(world)]
+        recv = [out[j] if s == root else nothing for s in range(world)]
+        _exchange(recv, send, group, world, phases).wait()
+    return out
+
+
+class _HostPhases:
+    """Allocation and (no-op) stream ordering for CPU tensors (gloo tests of the root exchanges)."""
+
+    def empty(self, shape, dtype="float64"):
+        import torch
+
+        return torch.empty(shape, dtype=getattr(torch, dtype))
+
+    def wait(self, ev, stream=None):
+        pass
 
 
 class _nullcontext:

@@ -542,23 +542,35 @@ class Node(abc.ABC):
                     for j, var in enumerate(all_variables):
                         var._set_device(Y[j])
                 elif world > 1:
-                    # any other correlator on row shards: every rank gathers the whole correlated
-                    # block, runs the correlator on it as one process would (identically on every
-                    # rank: same inputs, same kernels, same seeds) and keeps its own rows
-                    from .distributed import gather_block
+                    # any other correlator on row shards
+                    from . import distributed as _dist
 
                     assert block is not None  # every correlated variable is an ISN (checked above)
-                    full = gather_block(block, source.n, group, world)
-                    r0, r1 = source.row0, source.row0 + size
-                    if isinstance(inst, (ImanConover, Cholesky, PermutationCorrelator)):
-                        Yf = inst._transform_device(full, ev)
-                        for j, var in enumerate(all_variables):
-                            var._set_device(Yf[j, r0:r1].clone())
-                    else:  # a user correlator class: the reference's (N, K) ndarray protocol
-                        Yh = inst(device.to_host(full).T)
-                        for var, col in zip(all_variables, Yh.T):
-                            var.samples_ = np.copy(col[r0:r1])
-                    del full
+                    K = len(all_variables)
+                    if isinstance(inst, ImanConover):
+                        # sharded: each column ranked on its owner, Gram all-reduced, no replica
+                        inst._validate_X(np.lib.stride_tricks.as_strided(np.zeros(1), (source.n, K), (0, 0)))
+                        Y = _dist.iman_conover_block(block, inst.P, source.n, group=group)
+                    elif isinstance(inst, Cholesky):
+                        # row-local given the global means and Gram matrix: two all-reduces
+                        stats = _dist.block_stats(block, source.n, group=group)
+                        Y = inst._transform_device(block, ev, stats=stats, n=source.n)
+                    else:
+                        # state no rank can share by construction (an unseeded PermutationCorrelator's
+                        # rng, a user class): the correlator runs once, on rank 0, over the whole
+                        # block gathered there, and every rank receives its rows
+                        full = _dist.gather_to_root(block, source.n, group)
+                        Yf = None
+                        if rank == 0:
+                            if isinstance(inst, PermutationCorrelator):
+                                Yf = inst._transform_device(full, ev)
+                            else:  # a user correlator class: the reference's (N, K) ndarray protocol
+                                Yf = device.to_device(np.ascontiguousarray(np.asarray(inst(device.to_host(full).T),
+                                                                                      dtype=np.float64).T))
+                        del full
+                        Y = _dist.scatter_from_root(Yf, K, source.n, group, like=block)
+                    for j, var in enumerate(all_variables):
+                        var._set_device(Y[j])
                 elif isinstance(inst, ImanConover) and getattr(source, "strata", None) is not None:
                     # leaves with plain-number parameters: their ranks are their LHS strata
                     # (checked on the device; a column that fails the check is sorted)

@@ -159,3 +159,16 @@ class CpuPhases:
 
     def values_at(self, col, n, p, y):
         y.copy_(torch.from_numpy(self._sorted(col, n, p.numpy().astype(np.int64))))
+
+    # -- materialised columns on their owner (distributed.iman_conover_block)
+    def column_scores(self, x, s_out, sx_out, flag):
+        xv = x.numpy().copy()  # s_out may be x itself
+        if np.isnan(xv).any():
+            flag |= 1
+        r = rankdata_average(xv)
+        sx_out.copy_(torch.from_numpy(np.sort(xv)))
+        s_out.copy_(torch.from_numpy(scipy.special.ndtri(r / (len(xv) + 1))))
+
+    def reorder(self, cs, sx, y):
+        idx = rankdata_average(cs.numpy()).astype(int) - 1
+        y.copy_(torch.from_numpy(sx.numpy()[idx]))

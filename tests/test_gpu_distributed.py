@@ -135,6 +135,34 @@ def _worker(rank, world, port, outdir, spec="cfg2", backend="gloo"):
         dist.destroy_process_group()
 
 
+class SeededPermutation:
+    """correlator=PermutationCorrelator with a fixed seed (the DAG calls correlator() without
+    arguments): the one-process result is reproducible, so every rank's rows can be compared."""
+
+    def __new__(cls):
+        from probabilit_amd.correlation import PermutationCorrelator
+
+        return PermutationCorrelator(seed=11, iterations=40)
+
+
+class UnseededPermutation:
+    def __new__(cls):
+        from probabilit_amd.correlation import PermutationCorrelator
+
+        return PermutationCorrelator(iterations=40)  # seed=None: a fresh rng per instance
+
+
+class ReverseRows:
+    """A user correlator class (the reference's (N, K) ndarray protocol): reverses the rows."""
+
+    def set_target(self, C):
+        self.C = C
+        return self
+
+    def __call__(self, X):
+        return X[::-1].copy()
+
+
 def _dag(kind):
     from oracle.pipeline import cfg_dists
     from probabilit_amd.modeling import Distribution, NoOp
@@ -149,7 +177,7 @@ def _dag(kind):
               Distribution("weibull_min", c=1.7), dists.PERT(1, 2, 9, gamma=10),
               Distribution("binom", n=12, p=0.6, loc=0.5)]  # non-integer loc: the exact count path
         return NoOp(*ds).correlate(*ds, corr_mat=_target(len(ds))), "lhs"
-    if kind in ("sobol_ic", "cholesky", "ref_ic"):  # correlators on materialised quantiles: gathered block
+    if kind in ("sobol_ic", "cholesky", "ref_ic", "permcorr", "permcorr_unseeded", "user"):  # materialised block
         ds = [Distribution("norm", loc=1.0, scale=2.0), Distribution("gamma", a=2.0), Distribution("beta", a=2.0, b=3.0),
               Distribution("poisson", mu=4.0)]
         C = np.array([[1.0, 0.5, 0.3, 0.2], [0.5, 1.0, 0.4, 0.1], [0.3, 0.4, 1.0, 0.3], [0.2, 0.1, 0.3, 1.0]])
@@ -163,8 +191,11 @@ def _dag(kind):
     return r, "sobol"
 
 
-_DAG_KINDS = ("correlated", "fund", "ext", "refstream", "sobol_ic", "cholesky", "ref_ic")
-_DAG_KW = {"refstream": {"stream": "reference"}, "ref_ic": {"stream": "reference"}, "cholesky": {"correlator": "cholesky"}}
+_DAG_KINDS = ("correlated", "fund", "ext", "refstream", "sobol_ic", "cholesky", "ref_ic", "permcorr", "user",
+              "permcorr_unseeded")
+_DAG_KW = {"refstream": {"stream": "reference"}, "ref_ic": {"stream": "reference"}, "cholesky": {"correlator": "cholesky"},
+           "permcorr": {"correlator": SeededPermutation}, "permcorr_unseeded": {"correlator": UnseededPermutation},
+           "user": {"correlator": ReverseRows}}
 
 
 def _dag_worker(rank, world, port, outdir):
@@ -191,8 +222,12 @@ def _dag_worker(rank, world, port, outdir):
 def test_dag_row_sharded_world2_matches_one_process(gpu):
     """Node.sample_device(..., group=) with two ranks: every node's rows equal the same rows
     of the one-process evaluation (Sobol and LHS counter-addressed by global row; the reference
-    LHS stream decoded whole on each rank; Iman-Conover on Sobol' / reference-stream quantiles and
-    the Cholesky correlator on the gathered correlated block, identical on every rank)."""
+    LHS stream decoded whole on each rank; Iman-Conover on Sobol' / reference-stream quantiles
+    sharded by column owners (distributed.iman_conover_block), the Cholesky correlator from
+    all-reduced statistics, a seeded PermutationCorrelator and a user class run once on rank 0
+    and scattered).  An unseeded PermutationCorrelator cannot equal another process's run; its
+    ranks' rows together must still be a permutation of each marginal (every rank
+    used to climb with its own rng)."""
     import torch.multiprocessing as mp
 
     from probabilit_amd.distributed import shard_bounds
@@ -211,9 +246,12 @@ def test_dag_row_sharded_world2_matches_one_process(gpu):
         b = shard_bounds(n, 2)
         for r in range(2):
             np.testing.assert_array_equal(np.load(os.path.join(d, f"fund{r}.npy")), refs["fund"][b[r]:b[r + 1]])
-            for kind in _DAG_KINDS[:1] + _DAG_KINDS[2:]:
+            for kind in _DAG_KINDS[:1] + _DAG_KINDS[2:-1]:
                 for j, ref in enumerate(refs[kind]):
                     np.testing.assert_array_equal(np.load(os.path.join(d, f"{kind}{r}_v{j}.npy")), ref[b[r]:b[r + 1]])
+        for j, ref in enumerate(refs["permcorr_unseeded"]):
+            got = np.concatenate([np.load(os.path.join(d, f"permcorr_unseeded{r}_v{j}.npy")) for r in range(2)])
+            np.testing.assert_array_equal(np.sort(got), np.sort(ref))
 
 
 @pytest.mark.parametrize("spec", sorted(SPECS))
