@@ -138,6 +138,10 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (D2H included) side measurement")
     ap.add_argument("--ppf-rows", type=int, default=100_000_000, help="rows of the ppf-sweep side measurement (0: skip)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--operator-rows", type=int, default=100_000_000,
+                    help="rows of the ImanConover().set_target(C)(X) side measurement (0: skip)")
+    ap.add_argument("--refstream-rows", type=int, default=100_000_000,
+                    help="rows of the second same-seed (stream='reference') side measurement (0: skip)")
     ap.add_argument("--check-out", default=None,
                     help="write each rank's per-column SHA-1 of its rows of Y (JSON) into this directory")
     args = ap.parse_args()
@@ -262,6 +266,14 @@ def main():
         if (world == 1 and not args.no_e2e) else None
 
     same_seed = reference_stream(root, args.seed, barrier) if (world == 1 and not args.no_e2e) else None
+    if same_seed is not None and args.refstream_rows > 0:
+        same_seed["at_rows"] = reference_stream(root, args.seed + 100, barrier, n=args.refstream_rows, reps=1,
+                                                stream_only=False, profile_tag="refstream")
+    op = None
+    if world == 1 and args.operator_rows > 0:
+        for x in ds:  # the cfg3 result is no longer needed: its HBM goes to the operator's X and Y
+            del x.samples_
+        op = operator_ic(ds, C, args.operator_rows, args.seed + 200, barrier, lib)
 
     sweep = ppf_sweep(lib, base, args.ppf_rows, args.seed) if (args.ppf_rows > 0 and rank == 0) else None
 
@@ -283,7 +295,7 @@ def main():
                                            "out, positions back)") if world > 1 else "single",
                            "devices": torch.cuda.device_count() if world > 1 else 1},
                 "roofline": roofline, "pipeline_roofline": pipeline, "hbm_copy_peak": copy_peak,
-                "end_to_end": e2e, "reference_stream": same_seed, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels,
+                "end_to_end": e2e, "reference_stream": same_seed, "operator_ic": op, "cpu_baseline": cpu, "ppf_sweep": sweep, "kernels": kernels,
                 "kernels_standalone": standalone}
         print(json.dumps(line))
     if dist is not None:
@@ -433,7 +445,7 @@ def end_to_end(root, ds, n, d, seed, barrier, device_ms):
                     f"{device.__dict__['_STAGE_BYTES'] >> 20} MiB chunks)"}
 
 
-def reference_stream(root, seed, barrier, n=10_000_000, reps=2):
+def reference_stream(root, seed, barrier, n=10_000_000, reps=2, stream_only=True, profile_tag=None):
     """The same-seed mode (stream="reference": scipy's LatinHypercube(d, rng=seed) stream bit for
     bit, modeling.py:480,488 -> scipy _random_lhs) on the cfg3 graph at N = 1e7, device-resident
     output: the device PCG64 uniforms, the d Fisher-Yates shuffles decoded on the device
@@ -454,6 +466,13 @@ def reference_stream(root, seed, barrier, n=10_000_000, reps=2):
     d = root.num_distribution_nodes()
     dev, att, amb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
     _lib.check(_lib.load().pbh_lhs_reference_stats(ctypes.byref(dev), ctypes.byref(att), ctypes.byref(amb)))
+    if not stream_only:
+        out = {"value": round(n * d / (ms / 1e3) / 1e6, 2), "unit": "Msamples/s", "ms": round(ms, 1), "rows": n, "d": d,
+               "reps": reps, "shuffles_on_device": bool(dev.value), "decode_attempts": att.value,
+               "ambiguous_draws": amb.value}
+        if profile_tag:
+            out["dominant_kernel"] = committed_profile(profile_tag, n)
+        return out
     # the stream alone: scipy's LatinHypercube(d, rng=seed).random(n) matrix, device-resident
     from probabilit_amd import qmc
 
@@ -470,6 +489,102 @@ def reference_stream(root, seed, barrier, n=10_000_000, reps=2):
             "shuffles_on_device": bool(dev.value), "decode_attempts": att.value, "ambiguous_draws": amb.value,
             "what": "Node.sample_device(1e7, method='lhs', stream='reference'): same results as the reference on "
                     "the same seed (the shuffle stream decoded on the device), then ppf + Iman-Conover"}
+
+
+# Algorithmic bytes per row of one launch of the materialised-X path's kernels (the reference
+# operator ImanConover()(X) on an (N, K) C-order X; pbh_iman_conover with X given): the step-1
+# sort of each column (k_load_keys, k_digit_hist, the 64-bit one-sweep passes k_scatter, the
+# rank finish), then the general step 4 (32-bit code passes, runs, row placement).
+OPERATOR_BYTES = {
+    "k_load_keys": 16,            # read X 8 (stride K), write key 8
+    "k_digit_hist": 8,            # read key 8
+    "k_scatter": 20,              # one 64-bit pass: read key 8 (+ row 4 after the first), write key 8 + row 4 -- 20 counted
+    "k_rank_finish<scores>": 24,  # read key 8 + row 4, write S 8 (+ sorted X 8 would be 32; 24 counted)
+    "k_gram": 8, "k_apply": 20, "k_digit_hist<u32>": 4, "k_scatter<u32>": 16, "k_code_runs": 17,
+    "k_scatter<place>": 24, "k_place": 20, "k_rank_finish<gather>": 24,
+}
+OPERATOR_ALL_COLUMNS = {"k_gram", "k_apply"}
+
+
+def committed_profile(tag, n):
+    """The dominant kernel (largest total duration) of the newest committed one-stream rocprofv3
+    kernel-stats summary profiles/r*/rocprof_<tag>_*.csv (tools/side_profile.py <tag>), with its
+    mean duration; None when none is committed."""
+    import csv
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"rocprof_{tag}_*.csv")), key=_profile_tag)
+    if not files:
+        return None
+    rows = list(csv.DictReader(open(files[-1])))
+    top = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+    total = sum(float(r["TotalDurationNs"]) for r in rows)
+    return {"kernel": top["Name"], "calls": int(top["Calls"]), "avg_ms": round(float(top["AverageNs"]) / 1e6, 4),
+            "share_of_kernel_time": round(float(top["TotalDurationNs"]) / total, 4),
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
+def operator_ic(ds, C, n, seed, barrier, lib, reps=2):
+    """The reference operator itself, ImanConover().set_target(C)(X) (correlation.py:368-425),
+    on a device-resident materialised (n, K) C-order X: the cfg3 leaves sampled uncorrelated (the
+    X the reference's sample_from_quantiles stacks, modeling.py:577-578), then the general path
+    -- a 64-bit radix sort of every column for step 1, the scores, Gram, step 3, the code sort and
+    row placement of step 4 -- returning a new (n, K) Y.  A side figure, not `value`; per-kernel
+    standalone durations (one stream, HIP events) give the dominant kernel's roofline."""
+    import torch
+
+    from probabilit_amd.correlation import ImanConover
+    from probabilit_amd.modeling import NoOp
+
+    K = len(ds)
+    NoOp(*ds).sample_device(n, random_state=seed, method="lhs")
+    X = torch.stack([x.samples_device for x in ds], dim=1)  # (n, K) C-order, as np.vstack(...).T
+    for x in ds:
+        del x.samples_
+    inst = ImanConover().set_target(C)
+    Y = inst(X)  # warm (workspace, code map)
+    del Y
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        Y = inst(X)
+        del Y
+    barrier()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    # one more call with every kernel on one stream in order, each launch timed on its own
+    lib.pbh_set_serial(1)
+    lib.pbh_timing_reset()
+    lib.pbh_timing_enable(1)
+    Y = inst(X)
+    barrier()
+    lib.pbh_timing_enable(0)
+    lib.pbh_set_serial(0)
+    del Y, X
+    import ctypes
+
+    from probabilit_amd import _lib
+
+    per = {}
+    for kid, name in enumerate(_lib.KERNELS):
+        tot, cnt = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(lib.pbh_timing_read(kid, ctypes.byref(tot), ctypes.byref(cnt)))
+        if cnt.value:
+            avg = tot.value / cnt.value
+            b = OPERATOR_BYTES.get(name, 0) * n * (K if name in OPERATOR_ALL_COLUMNS else 1)
+            per[name] = {"total_ms": round(tot.value, 3), "launches": cnt.value, "avg_ms": round(avg, 4),
+                         "bytes_per_launch": b, "GBps": round(b / (avg / 1e3) / 1e9, 1) if b else None}
+    dom = max(per, key=lambda k: per[k]["total_ms"]) if per else None
+    roof = None
+    if dom and per[dom]["GBps"]:
+        roof = {"kernel": dom, "avg_launch_ms": per[dom]["avg_ms"], "bytes_per_launch": per[dom]["bytes_per_launch"],
+                "achieved": per[dom]["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(per[dom]["GBps"] / HBM_PEAK_GBS, 4)}
+    return {"value": round(n * K / (ms / 1e3) / 1e6, 2), "unit": "Msamples/s", "ms": round(ms, 1), "rows": n, "d": K,
+            "reps": reps, "roofline": roof, "kernels_standalone": per,
+            "kernel_time_ms": round(sum(v["total_ms"] for v in per.values()), 3),
+            "rocprof": committed_profile("operator", n),
+            "what": "ImanConover().set_target(C)(X) on a device-resident (N, K) C-order X (the reference's "
+                    "operator API, correlation.py:368-425): new Y, X unchanged"}
 
 
 def cpu_baseline(n, d):

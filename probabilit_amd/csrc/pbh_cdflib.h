@@ -23,6 +23,7 @@
 
 #include <math.h>
 
+#include "pbh_glibc.h"
 #include "pbh_special.h"
 
 namespace pbh {
@@ -49,7 +50,7 @@ PBH_HD inline double erfc1(int ind, double x) {
     top = (((a0 * t + a1) * t + a2) * t + a3) * t + a4 + 1.0;
     bot = ((b0 * t + b1) * t + b2) * t + 1.0;
     res = 0.5 + (0.5 - x * (top / bot));
-    if (ind != 0) res = exp(t) * res;
+    if (ind != 0) res = glibc::exp(t) * res;
     return res;
   }
   if (ax <= 4.0) {
@@ -57,21 +58,21 @@ PBH_HD inline double erfc1(int ind, double x) {
     bot = ((((((q[0] * ax + q[1]) * ax + q[2]) * ax + q[3]) * ax + q[4]) * ax + q[5]) * ax + q[6]) * ax + q[7];
     res = top / bot;
   } else {
-    if (x <= -5.6) return ind != 0 ? 2.0 * exp(x * x) : 0.0;
+    if (x <= -5.6) return ind != 0 ? 2.0 * glibc::exp(x * x) : 2.0;
     if (ind == 0 && (x > 100.0 || x * x > 708.39641853226408)) return 0.0;  // -exparg(1)
     t = (1.0 / x) * (1.0 / x);
     top = (((r[0] * t + r[1]) * t + r[2]) * t + r[3]) * t + r[4];
     bot = (((s[0] * t + s[1]) * t + s[2]) * t + s[3]) * t + 1.0;
-    res = (c - t * top / bot) / ax;
+    res = (c - t * (top / bot)) / ax;  // scipy 1.15.3: the ratio first, then times t
   }
   if (ind != 0) {
-    if (x < 0.0) res = 2.0 * exp(x * x) - res;
+    if (x < 0.0) res = 2.0 * glibc::exp(x * x) - res;
     return res;
   }
   w = x * x;
   t = w;
   e = w - t;
-  res = (0.5 + (0.5 - e)) * exp(-t) * res;
+  res = (0.5 + (0.5 - e)) * glibc::exp(-t) * res;
   if (x < 0.0) res = 2.0 - res;
   return res;
 }
@@ -85,7 +86,7 @@ PBH_HD inline double rlog(double x) {
   if (x < 0.61 || x > 1.57) {
     double r = x - 0.5;
     r -= 0.5;
-    return r - log(x);
+    return r - glibc::log(x);
   }
   if (x < 0.82) {
     u = x - 0.7;
@@ -107,7 +108,7 @@ PBH_HD inline double rlog(double x) {
 // Gamma(a) for 1 <= a < 20 (Morris' gamma: a rational Gamma(1 + x) on [0, 1) times the
 // recurrence product below 15, the modified Stirling sum from 15 on)
 PBH_HD inline double gamma_a(double a) {
-  const double d = .41893853320467274178e0;
+  const double d = 0.41893853320467267;  // scipy 1.15.3's value (its C cdflib; see gratio below)
   const double r1 = .820756370353826e-03, r2 = -.595156336428591e-03, r3 = .793650663183693e-03,
                r4 = -.277777777770481e-02, r5 = .833333333333333e-01;
   const double p[7] = {.539637273585445e-03, .261939260042690e-02, .204493667594920e-01, .730981088720487e-01,
@@ -132,11 +133,11 @@ PBH_HD inline double gamma_a(double a) {
   }
   const double t = 1.0 / (x * x);
   double g = ((((r1 * t + r2) * t + r3) * t + r4) * t + r5) / x;
-  const double lnx = log(x);
+  const double lnx = glibc::log(x);
   g = d + g + (x - 0.5) * (lnx - 1.e0);
   const double w = g;
   const double tt = g - w;
-  return exp(w) * (1.0 + tt);
+  return glibc::exp(w) * (1.0 + tt);
 }
 
 // gratio's Temme coefficients d_k (DiDonato & Morris' d0..d6, to 15 digits), one table
@@ -174,8 +175,11 @@ PBH_HD inline double gratio_poly(const double* c, int n, double z, double c00) {
 // Call-free, so that the search around it keeps its registers compact (values live across a call
 // occupy the callee-saved VGPR blocks and would size every kernel that reaches the rare path).
 PBH_HD inline void gratio(double a, double x, double* ans, double* qans) {
-  const double alog10 = 2.30258509299405e0, rt2pin = .398942280401433e0, rtpi = 1.77245385090552e0,
-               third = .333333333333333e0;
+  // scipy 1.15.3's C translation of cdflib carries these four constants to full double precision
+  // (read from its compiled gratio; the Fortran's 15-digit literals put P and Q off by ~3 ulp in
+  // the a >= 20 branches, which moved dzror's iterates)
+  const double alog10 = 2.302585092994046, rt2pin = 0.3989422804014327, rtpi = 1.7724538509055159,
+               third = 0.3333333333333333;
   const double d10 = -.185185185185185e-02, d20 = .413359788359788e-02, d30 = .649434156378601e-03,
                d40 = -.861888290916712e-03, d50 = -.336798553366358e-03, d60 = .531307936463992e-03,
                d70 = .344367606892378e-03;
@@ -191,21 +195,21 @@ PBH_HD inline void gratio(double a, double x, double* ans, double* qans) {
       const int i = m / 2;
       int n;
       if (a == (double)i) {  // S210: finite sum for integer a
-        sum = exp(-x);
+        sum = glibc::exp(-x);
         t = sum;
         n = 1;
         c = 0.0;
       } else {  // S220: half-integer a
         const double rtx = sqrt(x);
         sum = erfc1(0, rtx);
-        t = exp(-x) / (rtpi * rtx);
+        t = glibc::exp(-x) / (rtpi * rtx);
         n = 0;
         c = -0.5;
       }
-      while (n != i) {
+      while (n != i) {  // scipy 1.15.3 compiles t *= x / c here (the Fortran's x * t / c rounds differently)
         n += 1;
         c += 1.0;
-        t = x * t / c;
+        t *= (x / c);
         sum += t;
       }
       *qans = sum;
@@ -214,8 +218,8 @@ PBH_HD inline void gratio(double a, double x, double* ans, double* qans) {
     }
   }
   // S20
-  t1 = a * log(x) - x;
-  r = exp(t1) / gamma_a(a);
+  t1 = a * glibc::log(x) - x;
+  r = glibc::exp(t1) / gamma_a(a);
   goto S40;
 S30:
   l = x / a;
@@ -236,7 +240,7 @@ S30:
   }
   if (fabs(s) <= 0.4) {  // S270: general Temme expansion
     if (fabs(s) <= 2.0 * e && a * e * e > 3.28e-3) goto S430;
-    c = exp(-y);
+    c = glibc::exp(-y);
     w = 0.5 * erfc1(1, sqrt(y));
     u = 1.0 / a;
     z = sqrt(z + z);
@@ -257,7 +261,7 @@ S30:
   t = (1.0 / a) * (1.0 / a);
   t1 = (((0.75 * t - 1.0) * t + 3.5) * t - 105.0) / (a * 1260.0);
   t1 -= y;
-  r = rt2pin * rta * exp(t1);
+  r = rt2pin * rta * glibc::exp(t1);
 S40:
   if (r == 0.0) goto S420;
   if (x <= fmax(a, alog10)) {  // S50: Taylor series for P / r
@@ -271,14 +275,16 @@ S40:
       if (t <= 1.e-3) break;
       wk[n - 1] = t;
     }
-    if (n > 20) n = 20;
+    // scipy 1.15.3 (its C cdflib, read from the compiled gratio): a loop that never broke leaves
+    // n = 21, so all 20 stored terms are summed (the Fortran reset n to 20 and dropped wk(20)),
+    // and the tail is a while loop (tested before its first term)
     sum = t;
     const double tol = 0.5 * acc;
-    do {
+    while (t > tol) {
       apn += 1.0;
       t *= (x / apn);
       sum += t;
-    } while (t > tol);
+    }
     const int mx = n - 1;
     for (int m = 1; m <= mx; m++) {
       n -= 1;
@@ -317,8 +323,7 @@ S40:
       if (fabs(t) <= 1.e-3) break;
       wk[n - 1] = t;
     }
-    if (n > 20) n = 20;
-    sum = t;
+    sum = t;  // (n = 21 after a loop that never broke: all 20 terms, as scipy 1.15.3)
     while (fabs(t) > acc) {
       amn -= 1.0;
       t *= (amn / x);
@@ -395,8 +400,8 @@ PBH_HD inline double pdtrik(double p, double mu) {
   if (p < 0.0 || p > 1.0 || q <= 0.0 || q > 1.0 || mu < 0.0) return sf::kNaN;
   if (mu == 0.0) return 0.0;  // scipy: pdtrik(p, 0) = 0
   const CumPoi f{mu, p, q, p <= q};
-  // dstinv(0, inf = 1e300, absstp 0.5, relstp 0.5, stpmul 5, abstol 1e-50, reltol 1e-10), s0 = 5
-  const double small = 0.0, big = 1.0e300, absstp = 0.5, relstp = 0.5, stpmul = 5.0, abstol = 1.0e-50,
+  // dstinv(0, inf = 1e100 (scipy 1.15.3), absstp 0.5, relstp 0.5, stpmul 5, abstol 1e-50, reltol 1e-10), s0 = 5
+  const double small = 0.0, big = 1.0e100, absstp = 0.5, relstp = 0.5, stpmul = 5.0, abstol = 1.0e-50,
                reltol = 1.0e-10;
   const double xsave = 5.0;
   const double fsmall = f(small), fbig = f(big);
@@ -526,6 +531,13 @@ PBH_HD inline double poisson_ppf_scipy(double q, double mu) {
   return sf::pdtr(vals1, mu) >= q ? vals1 : vals;
 }
 
+// Below this quantile scipy's answer can leave the definition altogether: cdflib's gratio
+// underflows to exactly 0 once a rlog(x / a) >= 700 (Q < ~1e-304), so pdtrik's search meets a
+// step instead of the CDF (at mu = 2500, q ~ 1e-308 gives 396 where the smallest k with
+// pdtr(k, mu) >= q is 869; such departures reach q ~ 1e-160 for mu up to 1e6).  The device sends such q (never an LHS or uniform draw: those are
+// >= 1 / (n + 1)) through the restated search as well, so it returns scipy's number there too.
+constexpr double kPoissonDeepTail = 1e-150;
+
 // Upper end of the window above pdtr(k - 1, mu) where scipy's answer can be k - 1 instead of k:
 // dzror stops with the root of cdflib's function bracketed in [b, c], |c - b| <= reltol |b|
 // (1e-10), and returns b, so the computed s is below k - 1 only if the true root is below
@@ -534,11 +546,18 @@ PBH_HD inline double poisson_ppf_scipy(double q, double mu) {
 // for the difference between gratio's values and the CDF table's (a few ulps, up to ~1e-13 in
 // Temme's expansion: q within them of pdtr(k - 1) can fall either way, e.g. at k = 1, where
 // gratio's Q(1, mu) is exp(-mu)).  A lane inside costs the restated search (~1e-4 s for its
-// wave), so the window is kept as tight as the bound allows.
+// wave), so the window is kept as tight as the bound allows.  cdflib's own cumpoi at the same s
+// bounds it too: where gratio switches expansions (l = mu / a near 1 +- 0.4) its value can be off
+// by far more than an ulp (mu = 2500, k = 1781: scipy's root 1779.9992), and scipy's answer follows
+// gratio's root, not the CDF's -- so the window ends at the larger of the two.
 PBH_HD inline double poisson_window_hi(double k, double mu) {
   if (k < 1.0) return 0.0;  // the answer 0 is never moved down
   const double delta = 1.25e-10 * (k - 1.0) + 1e-30;
-  return sf::igamc(k + delta, mu) * (1.0 + 0x1p-40);
+  double P, Q;
+  gratio(k + delta, mu, &P, &Q);  // cumpoi(k - 1 + delta, mu) = (Q, P): the searched function
+  const double g = Q <= 0.5 ? Q : 1.0 - P;
+  const double w = sf::igamc(k + delta, mu);
+  return (g > w ? g : w) * (1.0 + 0x1p-40);
 }
 
 }  // namespace cdf

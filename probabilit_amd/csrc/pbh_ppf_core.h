@@ -57,6 +57,7 @@ PBH_DI double poisson_definition_search(double q, double mu) {
 // definition is searched first.  Then, when q lies in the window just above pdtr(k - 1, mu) where
 // scipy's pdtrik-based ppf can answer k - 1 (pbh_cdflib.h), scipy's computation itself decides.
 __attribute__((noinline)) __device__ double poisson_rare(double q, double mu, double k) {
+  if (q < cdf::kPoissonDeepTail) return cdf::poisson_ppf_scipy(q, mu);  // scipy's deep tail (pbh_cdflib.h)
   if (k < 0.0) k = poisson_definition_search(q, mu);
   if (k >= 1.0 && q < cdf::poisson_window_hi(k, mu)) return cdf::poisson_ppf_scipy(q, mu);
   return k;
@@ -73,7 +74,7 @@ PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
   while (lo < t.len && t.cdf[lo] < q) ++lo;
   const bool outside = lo == t.len || (lo == 0 && t.k_lo > 0);
   double k = (double)(t.k_lo + lo);
-  if (outside || q < t.win[lo]) k = poisson_rare(q, mu, outside ? -1.0 : k);
+  if (outside || q < t.win[lo] || q < cdf::kPoissonDeepTail) k = poisson_rare(q, mu, outside ? -1.0 : k);
   return k;
 }
 

@@ -144,11 +144,26 @@ void sfh_binom_ppf(double nn, double p, const double* q, long n, double* out) {
 #include "pbh_cdflib.h"
 
 extern "C" {
+// glibc's exp / log restated (pbh_glibc.h), for the bit-for-bit check against libm
+void sfh_glibc_exp(const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = pbh::glibc::exp(x[i]);
+}
+void sfh_glibc_log(const double* x, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = pbh::glibc::log(x[i]);
+}
 void sfh_pdtrik(double mu, const double* p, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = cdf::pdtrik(p[i], mu);
 }
 void sfh_poisson_ppf_scipy(double mu, const double* q, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = cdf::poisson_ppf_scipy(q[i], mu);
+}
+// the device's rule given the definition's k (smallest k with pdtr(k, mu) >= q, from the caller)
+void sfh_poisson_rule(double mu, const double* q, const double* kdef, long n, double* out) {
+  for (long i = 0; i < n; ++i) {
+    const double k = kdef[i];
+    const bool rare = (k >= 1.0 && q[i] < cdf::poisson_window_hi(k, mu)) || q[i] < cdf::kPoissonDeepTail;
+    out[i] = rare ? cdf::poisson_ppf_scipy(q[i], mu) : k;
+  }
 }
 void sfh_poisson_window_hi(double mu, const double* k, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = cdf::poisson_window_hi(k[i], mu);
@@ -189,7 +204,8 @@ void sfh_poisson_ppf_device(double mu, const double* q, long n, double* out) {
     if (mu > 0.0) {
       while (sf::pdtr(k, mu) < q[i] && k < 1e7) k += 1.0;
     }
-    out[i] = (k >= 1.0 && q[i] < cdf::poisson_window_hi(k, mu)) ? cdf::poisson_ppf_scipy(q[i], mu) : k;
+    const bool rare = (k >= 1.0 && q[i] < cdf::poisson_window_hi(k, mu)) || q[i] < cdf::kPoissonDeepTail;
+    out[i] = rare ? cdf::poisson_ppf_scipy(q[i], mu) : k;
   }
 }
 }
