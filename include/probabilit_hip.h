@@ -100,7 +100,25 @@ typedef enum pbh_dist {
   PBH_DIST_RANDINT = 56,      /* low, high, loc (discrete)  ceil(q (high - low) + low) - 1, one step down */
   PBH_DIST_NBINOM = 57,       /* n, p, loc (discrete)  smallest k: I_p(n, k + 1) >= q (Boost) */
   PBH_DIST_INVGAMMA = 58,     /* a        1 / gammainccinv(a, q) */
-  PBH_DIST_T = 59             /* df       stdtrit(df, q), through the incomplete beta */
+  PBH_DIST_T = 59,            /* df       stdtrit(df, q), through the incomplete beta */
+  /* round 6: more scipy.stats names; trapz is trapezoid (PBH_DIST_TRAPEZOID) */
+  PBH_DIST_JOHNSONSU = 60,    /* a, b     sinh((ndtri(q) - a) / b) */
+  PBH_DIST_JOHNSONSB = 61,    /* a, b     expit(1 / b (ndtri(q) - a)) */
+  PBH_DIST_POWERNORM = 62,    /* c        -ndtri(pow(1 - q, 1 / c)) */
+  PBH_DIST_LAPLACE_ASYMMETRIC = 63, /* kappa  two log branches at kappa / (kappa + 1 / kappa) */
+  PBH_DIST_MIELKE = 64,       /* k, s     pow(q^(s/k) / (1 - q^(s/k)), 1 / s) */
+  PBH_DIST_TRUNCPARETO = 65,  /* b, c     pow(1 - (1 - c^-b) q, -1 / b) */
+  PBH_DIST_TUKEYLAMBDA = 66,  /* lam      boxcox(q, lam) - boxcox1p(-q, lam) */
+  PBH_DIST_GENGAMMA = 67,     /* a, c     (c > 0 ? gammaincinv : gammainccinv)(a, q)^(1 / c) */
+  PBH_DIST_LOGGAMMA = 68,     /* c        log(gammaincinv(c, q)), the one-term tail below DBL_MIN */
+  PBH_DIST_DGAMMA = 69,       /* a        +-gammaincinv / gammainccinv of 2 q - 1 / 2 q */
+  PBH_DIST_F = 70,            /* dfn, dfd dfd w / (dfn (1 - w)), w = I^-1(q; dfn / 2, dfd / 2) */
+  PBH_DIST_RDIST = 71,        /* c        2 I^-1(q; c / 2, c / 2) - 1 */
+  PBH_DIST_SEMICIRCULAR = 72, /*          rdist with c = 3 */
+  PBH_DIST_BETAPRIME = 73,    /* a, b     r / (1 - r), r = I^-1(q; a, b); 1 / isf - 1 near r = 1 */
+  PBH_DIST_DLAPLACE = 74,     /* a, loc (discrete)   log branches, one step down by its cdf */
+  PBH_DIST_PLANCK = 75,       /* lambda, loc (discrete)   ceil(-log1p(-q) / lambda - 1), one step down */
+  PBH_DIST_BOLTZMANN = 76     /* lambda, N, loc (discrete) the truncated planck */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

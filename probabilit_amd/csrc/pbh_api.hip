@@ -661,6 +661,45 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
       st = general(c);  // not flat, not regenerable, or a run of equal codes beyond the finish
       if (st) return st;
     }
+  } else if (!a->columns && step4_mat_enabled(n)) {
+    // materialised columns (X given: the operator API, the reference LHS stream) through the same
+    // MSD code passes, bucket finish and row placement as the generated ones, Y[row] = sort(X)[p]
+    // gathered from the sorted column (place_sorted); a column the finish rejects is redone by the
+    // general path after the one verdict readback
+    Step4Shared sh;
+    step4_gen_carve_shared(L.s4shared, k, sh);
+    Step4Lanes lanes(n, L.s4column, nullptr, s);
+    sync_on_exit.side = sync_on_exit.side || lanes.ns > 1;
+    st = step4_gen_hist(L.codes, n, nullptr, n, n, sh, 0, k, s);
+    if (st) return st;
+    PBH_CHECK_HIP(hipMemcpyAsync(state.data(), sh.state, (size_t)k * 4, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+    if ((st = lanes.begin())) return st;
+    for (int c = 0; c < k; ++c) {
+      const int i = lanes.next();
+      hipStream_t cs_ = lanes.ss[i];
+      if (state[c]) {
+        st = step4_gen_adapt(L.codes + (int64_t)c * n, n, L.S + (int64_t)c * n, n, n, sh, c, 1, cs_);
+        if (st) return st;
+      }
+      st = step4_gen_column(c, L.codes + (int64_t)c * n, L.S + (int64_t)c * n, n, sh, lanes.cb[i], cs_);
+      if (st) return st;
+      int buf = 0;
+      st = step4_gen_place_passes(c, n, sh, lanes.cb[i], cs_, &buf);
+      if (st) return st;
+      st = place_sorted(L.sorted_x + (int64_t)c * n, lanes.cb[i].pairs[buf], n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
+                        a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, sh.flags + c, cs_);
+      if (st) return st;
+    }
+    if ((st = lanes.join())) return st;
+    std::vector<int32_t> verdict(2 * (size_t)k);
+    PBH_CHECK_HIP(hipMemcpyAsync(verdict.data(), sh.state, 8 * (size_t)k, hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+    for (int c = 0; c < k; ++c) {
+      if (verdict[c] == 0 && verdict[k + c] == 0) continue;
+      st = general(c);
+      if (st) return st;
+    }
   } else {
     // The code histograms of all columns up front, one readback for the bucket-path decisions.
     struct AsyncBuf {  // freed on every return (stream-ordered, before the guard's final sync)

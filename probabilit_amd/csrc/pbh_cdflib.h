@@ -528,7 +528,7 @@ PBH_HD inline double pdtrik(double p, double mu) {
 PBH_HD inline double poisson_ppf_scipy(double q, double mu) {
   const double vals = ceil(pdtrik(q, mu));
   const double vals1 = fmax(vals - 1.0, 0.0);
-  return sf::pdtr(vals1, mu) >= q ? vals1 : vals;
+  return sf::pdtr<glibc::Math>(vals1, mu) >= q ? vals1 : vals;
 }
 
 // Below this quantile scipy's answer can leave the definition altogether: cdflib's gratio
@@ -556,7 +556,7 @@ PBH_HD inline double poisson_window_hi(double k, double mu) {
   double P, Q;
   gratio(k + delta, mu, &P, &Q);  // cumpoi(k - 1 + delta, mu) = (Q, P): the searched function
   const double g = Q <= 0.5 ? Q : 1.0 - P;
-  const double w = sf::igamc(k + delta, mu);
+  const double w = sf::igamc<glibc::Math>(k + delta, mu);
   return (g > w ? g : w) * (1.0 + 0x1p-40);
 }
 

@@ -14,9 +14,18 @@
 // Plain IEEE operations and __builtin_fma only, so host and device give the same doubles.
 #pragma once
 
+#include <math.h>
 #include <stdint.h>
 
-#include "pbh_special.h"
+#include "pbh_common.h"
+
+#ifndef PBH_TABLE
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PBH_TABLE static __constant__ const
+#else
+#define PBH_TABLE static const
+#endif
+#endif
 
 namespace pbh {
 namespace glibc {
@@ -137,6 +146,91 @@ PBH_HD inline double log(double x) {
   const double y = __builtin_fma(r3, q, lo);
   return y + hi;
 }
+
+// pow's log: log(x) as y + tail with ~15 extra bits (e_pow.c log_inline, FMA build)
+PBH_HD inline double pow_log(uint64_t ix, double* tail) {
+  const double Ln2hi = kGlibcPowHead[0], Ln2lo = kGlibcPowHead[1];
+  const double* A = kGlibcPowHead + 2;  // A0 = -0.5 .. A6
+  const uint64_t tmp = ix - 0x3fe6955500000000ull;
+  const int i = (int)((tmp >> 45) & 0x7f);
+  const int k = (int)((int64_t)tmp >> 52);
+  const double z = from_bits(ix - (tmp & 0xfff0000000000000ull));
+  const double kd = (double)k;
+  const double invc = kGlibcPowTab[3 * i], logc = kGlibcPowTab[3 * i + 1], logctail = kGlibcPowTab[3 * i + 2];
+  const double t1 = __builtin_fma(kd, Ln2hi, logc);
+  const double r = __builtin_fma(z, invc, -1.0);
+  const double ar = r * A[0];
+  const double lo1 = __builtin_fma(kd, Ln2lo, logctail);
+  const double p12 = __builtin_fma(r, A[2], A[1]);
+  const double p34 = __builtin_fma(r, A[4], A[3]);
+  const double t2 = r + t1;
+  const double ar2 = r * ar;
+  const double ar3 = r * ar2;
+  const double lo3 = __builtin_fma(ar, r, -ar2);
+  const double lo2 = (t1 - t2) + r;
+  double p56 = __builtin_fma(r, A[6], A[5]);
+  const double hi = t2 + ar2;
+  p56 = __builtin_fma(p56, ar2, p34);
+  const double lo4 = (t2 - hi) + ar2;
+  const double p = __builtin_fma(ar2, p56, p12);
+  double lo = ((lo1 + lo2) + lo3) + lo4;
+  lo = __builtin_fma(ar3, p, lo);
+  const double y = hi + lo;
+  *tail = (hi - y) + lo;
+  return y;
+}
+
+// pow's exp: exp(x + xtail) (e_pow.c exp_inline, sign_bias 0, FMA build)
+PBH_HD inline double pow_exp(double x, double xtail) {
+  const double InvLn2N = kGlibcExpHead[0], Shift = kGlibcExpHead[1], NegLn2hiN = kGlibcExpHead[2],
+               NegLn2loN = kGlibcExpHead[3], C2 = kGlibcExpHead[4], C3 = kGlibcExpHead[5], C4 = kGlibcExpHead[6],
+               C5 = kGlibcExpHead[7];
+  uint32_t abstop = (uint32_t)(bits(x) >> 52) & 0x7ff;
+  if (abstop - 0x3c9u > 0x3eu) {
+    if ((int32_t)(abstop - 0x3c9u) < 0) return x + 1.0;
+    if (abstop > 0x408u) return (bits(x) >> 63) ? 0.0 : __builtin_inf();
+    abstop = 0;
+  }
+  const double kz = __builtin_fma(x, InvLn2N, Shift);
+  const uint64_t ki = bits(kz);
+  const double kd = kz - Shift;
+  double r = __builtin_fma(kd, NegLn2hiN, x);
+  r = __builtin_fma(kd, NegLn2loN, r);
+  r = xtail + r;
+  const uint64_t idx = 2 * (ki & 0x7f);
+  const uint64_t sbits = kGlibcExpTab[idx + 1] + (ki << 45);
+  const double p23 = __builtin_fma(r, C3, C2);
+  const double tr = r + from_bits(kGlibcExpTab[idx]);
+  const double r2 = r * r;
+  const double p45 = __builtin_fma(r, C5, C4);
+  const double t = __builtin_fma(p23, r2, tr);
+  const double tmp = __builtin_fma(r2 * r2, p45, t);
+  if (abstop == 0) return exp_special(tmp, sbits, ki);
+  const double scale = from_bits(sbits);
+  return __builtin_fma(tmp, scale, scale);
+}
+
+// pow(x, y) for x a positive normal double and y with 2^-65 <= |y| < 2^63 (the main path of
+// glibc's __pow_fma); any other argument takes the device pow (never reached by the cdflib /
+// Cephes restatements that use this: x / fac > 0, 0 < a < 200)
+PBH_HD inline double pow(double x, double y) {
+  const uint64_t ix = bits(x), iy = bits(y);
+  const uint32_t topx = (uint32_t)(ix >> 52), topy = (uint32_t)(iy >> 52) & 0x7ff;
+  if (topx - 1u > 0x7fdu || topy - 0x3beu > 0x7fu) return ::pow(x, y);
+  double tail;
+  const double hi = pow_log(ix, &tail);
+  const double ehi = y * hi;
+  const double elo = __builtin_fma(y, tail, __builtin_fma(hi, y, -ehi));
+  return pow_exp(ehi, elo);
+}
+
+// the math of the reference's L0 (scipy's compiled Cephes / cdflib over glibc's libm), for the
+// sf:: templates that take a math policy (pbh_special.h)
+struct Math {
+  PBH_HD static double exp(double x) { return glibc::exp(x); }
+  PBH_HD static double log(double x) { return glibc::log(x); }
+  PBH_HD static double pow(double x, double y) { return glibc::pow(x, y); }
+};
 
 }  // namespace glibc
 }  // namespace pbh

@@ -157,6 +157,7 @@ int reorder_column(const double* cs, int64_t n, const double* sorted_src, double
     pb.counts = sb.counts;
     pb.partials = sb.partials;
     pb.status = sb.status;
+    pb.sweep = &sb.sweep;
     pb.bases = sb.bases;
     return place_by_row(sb.vals[buf], vals, n, y, y_rs, pb, s, err);
   }

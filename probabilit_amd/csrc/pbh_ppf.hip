@@ -1593,7 +1593,7 @@ __global__ void k_gamma_guide_check(double a, sf::GammaGuide T, double* ok) {
 __global__ void k_poisson_table(double mu, int64_t k_lo, int64_t len, double* cdf, double* win) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j < len) {
-    cdf[j] = sf::pdtr((double)(k_lo + j), mu);
+    cdf[j] = sf::pdtr<glibc::Math>((double)(k_lo + j), mu);  // scipy's pdtr bit for bit (pbh_glibc.h)
     win[j] = cdf::poisson_window_hi((double)(k_lo + j), mu);
   }
 }

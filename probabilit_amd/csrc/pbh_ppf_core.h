@@ -42,12 +42,12 @@ PBH_DI double poisson_definition_search(double q, double mu) {
   if (!(g >= 0.0)) g = 0.0;
   if (g > 9.0e15) g = 9.0e15;
   double k = g;
-  if (sf::pdtr(k, mu) >= q) {
-    while (k > 0.0 && sf::pdtr(k - 1.0, mu) >= q) k -= 1.0;
+  if (sf::pdtr<glibc::Math>(k, mu) >= q) {
+    while (k > 0.0 && sf::pdtr<glibc::Math>(k - 1.0, mu) >= q) k -= 1.0;
   } else {
     do {
       k += 1.0;
-    } while (sf::pdtr(k, mu) < q && k < 1.0e18);
+    } while (sf::pdtr<glibc::Math>(k, mu) < q && k < 1.0e18);
   }
   return k;
 }

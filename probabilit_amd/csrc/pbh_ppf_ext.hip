@@ -233,14 +233,20 @@ void attach_table(int dist, const double* t, Params4& p) {
 }
 
 constexpr bool is_closed(int d) {
-  return (d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID) || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T;
+  return (d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID) || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T ||
+         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME);
 }
-// discrete distributions beyond binom / bernoulli (round 5): p, loc / low, high, loc / n, p, loc
-constexpr bool is_discrete2(int d) { return d == PBH_DIST_GEOM || d == PBH_DIST_RANDINT || d == PBH_DIST_NBINOM; }
+// discrete distributions beyond binom / bernoulli (round 5): p, loc / low, high, loc / n, p, loc;
+// round 6: a, loc (dlaplace) / lambda, loc (planck) / lambda, N, loc (boltzmann)
+constexpr bool is_discrete2(int d) {
+  return d == PBH_DIST_GEOM || d == PBH_DIST_RANDINT || d == PBH_DIST_NBINOM || d == PBH_DIST_DLAPLACE ||
+         d == PBH_DIST_PLANCK || d == PBH_DIST_BOLTZMANN;
+}
 
 constexpr int closed_shapes(int d) {
   return (d == PBH_DIST_LOGUNIFORM || d == PBH_DIST_BURR || d == PBH_DIST_BURR12 || d == PBH_DIST_EXPONWEIB ||
-          d == PBH_DIST_TRAPEZOID)
+          d == PBH_DIST_TRAPEZOID || d == PBH_DIST_JOHNSONSU || d == PBH_DIST_JOHNSONSB || d == PBH_DIST_MIELKE ||
+          d == PBH_DIST_TRUNCPARETO || d == PBH_DIST_GENGAMMA || d == PBH_DIST_F || d == PBH_DIST_BETAPRIME)
              ? 2
          : (d == PBH_DIST_WEIBULL_MIN || d == PBH_DIST_WEIBULL_MAX || d == PBH_DIST_PARETO || d == PBH_DIST_LOMAX ||
             d == PBH_DIST_GENEXTREME || d == PBH_DIST_GOMPERTZ || d == PBH_DIST_CHI2 || d == PBH_DIST_POWERLAW ||
@@ -248,7 +254,9 @@ constexpr int closed_shapes(int d) {
             d == PBH_DIST_INVWEIBULL || d == PBH_DIST_LOGLAPLACE || d == PBH_DIST_TRUNCEXPON || d == PBH_DIST_CHI ||
             d == PBH_DIST_NAKAGAMI || d == PBH_DIST_DWEIBULL || d == PBH_DIST_KAPPA3 ||
             d == PBH_DIST_GENHALFLOGISTIC || d == PBH_DIST_ALPHA || d == PBH_DIST_FATIGUELIFE ||
-            d == PBH_DIST_GENLOGISTIC || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T)
+            d == PBH_DIST_GENLOGISTIC || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T || d == PBH_DIST_POWERNORM ||
+            d == PBH_DIST_LAPLACE_ASYMMETRIC || d == PBH_DIST_TUKEYLAMBDA || d == PBH_DIST_LOGGAMMA ||
+            d == PBH_DIST_DGAMMA || d == PBH_DIST_RDIST)
              ? 1
              : 0;
 }
@@ -260,6 +268,16 @@ __device__ __forceinline__ double boxcox1p(double x, double lmbda) {
   if (fabs(lmbda) < 1e-19 || (fabs(lgx) < 1e-289 && fabs(lmbda) < 1e273)) return lgx;
   return expm1(lmbda * lgx) / lmbda;
 }
+
+// scipy.special.boxcox (scipy _boxcox.pxd): log(x) for a vanishing lambda, else
+// expm1(lambda log(x)) / lambda
+__device__ __forceinline__ double boxcox(double x, double lmbda) {
+  if (fabs(lmbda) < 1e-19) return log(x);
+  return expm1(lmbda * log(x)) / lmbda;
+}
+
+// scipy.special.expit (xsf): 1 / (1 + exp(-x))
+__device__ __forceinline__ double expit(double x) { return 1.0 / (1.0 + exp(-x)); }
 
 // scipy.special.powm1 (Boost powm1) for x > 0: expm1(y log x) when that is the accurate form,
 // else pow(x, y) - 1
@@ -322,6 +340,35 @@ __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo,
   if constexpr (D == PBH_DIST_TRUNCEXPON) hi = s0;  // support [0, b]
   if constexpr (D == PBH_DIST_GENHALFLOGISTIC) hi = 1.0 / s0;  // support [0, 1 / c]
   if constexpr (D == PBH_DIST_TRAPEZOID) return s0 >= 0.0 && s0 <= 1.0 && s1 >= 0.0 && s1 <= 1.0 && s1 >= s0;
+  // round 6
+  if constexpr (D == PBH_DIST_JOHNSONSU || D == PBH_DIST_JOHNSONSB) {  // _argcheck (b > 0) & (a == a)
+    if constexpr (D == PBH_DIST_JOHNSONSB) {
+      lo = 0.0;
+      hi = 1.0;
+    }
+    return s1 > 0.0 && s0 == s0;
+  }
+  if constexpr (D == PBH_DIST_MIELKE || D == PBH_DIST_F || D == PBH_DIST_BETAPRIME) lo = 0.0;
+  if constexpr (D == PBH_DIST_TRUNCPARETO) {  // _argcheck (b > 0) & (c > 1), support [1, c]
+    lo = 1.0;
+    hi = s1;
+    return s0 > 0.0 && s1 > 1.0;
+  }
+  if constexpr (D == PBH_DIST_TUKEYLAMBDA) {  // _argcheck isfinite(lam); support +-1 / lam for lam > 0
+    if (s0 > 0.0) {
+      lo = -1.0 / s0;
+      hi = 1.0 / s0;
+    }
+    return isfinite(s0);
+  }
+  if constexpr (D == PBH_DIST_GENGAMMA) {  // _argcheck (a > 0) & (c != 0), support [0, inf)
+    lo = 0.0;
+    return s0 > 0.0 && s1 != 0.0;
+  }
+  if constexpr (D == PBH_DIST_RDIST || D == PBH_DIST_SEMICIRCULAR) {
+    lo = -1.0;
+    hi = 1.0;
+  }
   if constexpr (closed_shapes(D) == 1) return s0 > 0.0;
   if constexpr (closed_shapes(D) == 2) return s0 > 0.0 && s1 > 0.0;
   return true;
@@ -413,6 +460,42 @@ __device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
     if (q <= qd) return 0.5 * q * (1 + d - c) + 0.5 * c;
     return 1 - sqrt((1 - q) * (d - c + 1) * (1 - d));
   }
+  // round 6 (scipy 1.15 _continuous_distns.py _ppf bodies, operation for operation)
+  if constexpr (D == PBH_DIST_JOHNSONSU) return sinh((sf::ndtri(q) - s0) / s1);
+  if constexpr (D == PBH_DIST_JOHNSONSB) return expit(1.0 / s1 * (sf::ndtri(q) - s0));
+  if constexpr (D == PBH_DIST_POWERNORM) return -sf::ndtri(pow(1.0 - q, 1.0 / s0));
+  if constexpr (D == PBH_DIST_LAPLACE_ASYMMETRIC) {
+    const double kapinv = 1 / s0, kappkapinv = s0 + kapinv;
+    return q >= s0 / kappkapinv ? -log((1 - q) * kappkapinv * s0) * kapinv : log(q * kappkapinv / s0) * s0;
+  }
+  if constexpr (D == PBH_DIST_MIELKE) {
+    const double qsk = pow(q, s1 * 1.0 / s0);
+    return pow(qsk / (1.0 - qsk), 1.0 / s1);
+  }
+  if constexpr (D == PBH_DIST_TRUNCPARETO) return pow(1 - (1 - 1 / pow(s1, s0)) * q, -1 / s0);
+  if constexpr (D == PBH_DIST_TUKEYLAMBDA) return boxcox(q, s0) - boxcox1p(-q, s0);
+  if constexpr (D == PBH_DIST_GENGAMMA) return pow(s1 > 0.0 ? sf::igami(s0, q) : sf::igamci(s0, q), 1.0 / s1);
+  if constexpr (D == PBH_DIST_LOGGAMMA) {
+    const double g = sf::igami(s0, q);
+    return g < 2.2250738585072014e-308 ? (log(q) + sf::lgam(s0 + 1)) / s0 : log(g);  // _XMIN = finfo.tiny
+  }
+  if constexpr (D == PBH_DIST_DGAMMA) return q > 0.5 ? sf::igami(s0, 2 * q - 1) : -sf::igamci(s0, 2 * q);
+  if constexpr (D == PBH_DIST_F) {  // fdtri: w = I^-1(q; dfn / 2, dfd / 2), its complement by symmetry
+    const double a = 0.5 * s0, b = 0.5 * s1;
+    if (q <= 0.5) {
+      const double w = sfx::beta_ppf01(q, a, b);
+      return s1 * w / (s0 * (1.0 - w));
+    }
+    const double v = sfx::beta_ppf01(1.0 - q, b, a);  // 1 - w, exact for q >= 0.5
+    return s1 * (1.0 - v) / (s0 * v);
+  }
+  if constexpr (D == PBH_DIST_RDIST) return 2 * sfx::beta_ppf01(q, s0 / 2, s0 / 2) - 1;
+  if constexpr (D == PBH_DIST_SEMICIRCULAR) return 2 * sfx::beta_ppf01(q, 1.5, 1.5) - 1;  // rdist._ppf(q, 3)
+  if constexpr (D == PBH_DIST_BETAPRIME) {  // r / (1 - r); 1 / beta._isf(p, b, a) - 1 for r > 0.9999
+    const double r = sfx::beta_ppf01(q, s0, s1);
+    if (r > 0.9999) return 1 / sfx::beta_ppf01(1.0 - q, s1, s0) - 1;
+    return r / (1 - r);
+  }
   return sf::kNaN;
 }
 
@@ -449,6 +532,24 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
         return nan;
       if (q == 1.0) return high - 1.0 + loc;
       return sfx::randint_ppf01(q, low, high) + loc;
+    } else if constexpr (D == PBH_DIST_DLAPLACE) {  // support (-inf, inf), _argcheck a > 0
+      const double a = p.at(0, i), loc = p.at(1, i);
+      if (q == 0.0) return -sf::kInf + loc;
+      if (!(a > 0.0 && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
+      if (q == 1.0) return inf + loc;
+      return sfx::dlaplace_ppf01(q, a) + loc;
+    } else if constexpr (D == PBH_DIST_PLANCK) {  // support [0, inf), _argcheck lambda > 0
+      const double lam = p.at(0, i), loc = p.at(1, i);
+      if (q == 0.0) return -1.0 + loc;
+      if (!(lam > 0.0 && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
+      if (q == 1.0) return inf + loc;
+      return sfx::planck_ppf01(q, lam) + loc;
+    } else if constexpr (D == PBH_DIST_BOLTZMANN) {  // support [0, N - 1], _argcheck lambda > 0, N > 0 integral
+      const double lam = p.at(0, i), N = p.at(1, i), loc = p.at(2, i);
+      if (q == 0.0) return -1.0 + loc;
+      if (!(lam > 0.0 && N > 0.0 && N == floor(N) && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
+      if (q == 1.0) return N - 1.0 + loc;
+      return sfx::boltzmann_ppf01(q, lam, N) + loc;
     } else {  // nbinom
       const double n = p.at(0, i), pp = p.at(1, i), loc = p.at(2, i);
       if (q == 0.0) return -1.0 + loc;
@@ -623,6 +724,23 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_NBINOM)
     PBH_EXT(PBH_DIST_INVGAMMA)
     PBH_EXT(PBH_DIST_T)
+    PBH_EXT(PBH_DIST_JOHNSONSU)
+    PBH_EXT(PBH_DIST_JOHNSONSB)
+    PBH_EXT(PBH_DIST_POWERNORM)
+    PBH_EXT(PBH_DIST_LAPLACE_ASYMMETRIC)
+    PBH_EXT(PBH_DIST_MIELKE)
+    PBH_EXT(PBH_DIST_TRUNCPARETO)
+    PBH_EXT(PBH_DIST_TUKEYLAMBDA)
+    PBH_EXT(PBH_DIST_GENGAMMA)
+    PBH_EXT(PBH_DIST_LOGGAMMA)
+    PBH_EXT(PBH_DIST_DGAMMA)
+    PBH_EXT(PBH_DIST_F)
+    PBH_EXT(PBH_DIST_RDIST)
+    PBH_EXT(PBH_DIST_SEMICIRCULAR)
+    PBH_EXT(PBH_DIST_BETAPRIME)
+    PBH_EXT(PBH_DIST_DLAPLACE)
+    PBH_EXT(PBH_DIST_PLANCK)
+    PBH_EXT(PBH_DIST_BOLTZMANN)
 #undef PBH_EXT
     default:
       return false;
@@ -881,8 +999,10 @@ Params4 scalar_params(int dist, const double* val, int np, const double* table) 
 }  // namespace
 
 int ext_nparams(int dist) {
-  if (dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_GEOM) return 2;
-  if (dist == PBH_DIST_BINOM || dist == PBH_DIST_RANDINT || dist == PBH_DIST_NBINOM) return 3;
+  if (dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_GEOM || dist == PBH_DIST_DLAPLACE || dist == PBH_DIST_PLANCK)
+    return 2;
+  if (dist == PBH_DIST_BINOM || dist == PBH_DIST_RANDINT || dist == PBH_DIST_NBINOM || dist == PBH_DIST_BOLTZMANN)
+    return 3;
   if (dist == PBH_DIST_BETA || dist == PBH_DIST_TRUNCNORM) return 4;
   if (is_closed(dist)) return closed_shapes(dist) + 2;
   return -1;
@@ -919,6 +1039,18 @@ void discrete_span(int dist, const double* val, double* span, double* loc) {
     case PBH_DIST_NBINOM:
       if (val[0] > 0.0 && val[1] > 0.0 && val[1] <= 1.0 && val[0] < 1e6 && val[1] > 1e-6)
         *span = sfx::nbinom_ppf01(top, val[0], val[1]) + 1.0;
+      *loc = val[2];
+      break;
+    case PBH_DIST_DLAPLACE:
+      if (val[0] > 0.0) *span = sfx::dlaplace_ppf01(top, val[0]) - sfx::dlaplace_ppf01(0x1p-53, val[0]) + 1.0;
+      *loc = val[1];
+      break;
+    case PBH_DIST_PLANCK:
+      if (val[0] > 0.0) *span = sfx::planck_ppf01(top, val[0]) + 1.0;
+      *loc = val[1];
+      break;
+    case PBH_DIST_BOLTZMANN:
+      if (val[0] > 0.0 && val[1] > 0.0) *span = val[1];
       *loc = val[2];
       break;
     default:

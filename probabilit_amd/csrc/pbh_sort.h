@@ -15,6 +15,14 @@
 
 namespace pbh {
 
+// the one-sweep look-back words' pass state (host side, one per workspace): the words carry the
+// pass's epoch, so they are cleared once (the first pass) rather than before every pass
+struct SweepState {
+  uint32_t epoch;      // of the last pass; 0: the words are not cleared yet
+  uint32_t tile_base;  // the tile counter's value before the next pass
+  size_t bytes;        // the words, the tile counter and the stuck flag
+};
+
 struct SortBuffers {
   uint64_t* keys[2];
   uint32_t* vals[2];
@@ -24,6 +32,7 @@ struct SortBuffers {
   uint32_t* hist_host; // pinned host mirror of hist (8 * 256)
   uint64_t* status;    // one-sweep look-back words (256 * ntiles) + tile counter
   uint32_t* bases;     // one-sweep global digit bases (8 * 256)
+  SweepState sweep;    // set by sort_carve
 };
 
 constexpr int kSortThreads = 256;
@@ -78,6 +87,7 @@ struct PlaceBuffers {
   uint32_t* partials;  // scan partials
   uint64_t* status;    // one-sweep look-back words
   uint32_t* bases;     // 256 digit bases
+  SweepState* sweep;   // the SortBuffers' pass state whose status words these are
 };
 // err (optional, device): a look-back failure is OR-ed into *err on the stream instead of being
 // read back with a synchronisation

@@ -229,13 +229,19 @@ __global__ __launch_bounds__(T) void k_scatter(const K* __restrict__ kin, const 
 // as in Adinets & Merrill's Onesweep).  Global digit bases come from the one up-front
 // histogram.  Tile ids are taken from an atomic counter, so a tile only ever waits on tiles
 // that started before it: the look-back always terminates.
-constexpr uint64_t kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62, kCountMask = (1ull << 62) - 1;
+// Every word carries its pass's epoch (bits 40..61): a word left by an earlier pass reads as "not
+// yet published", so the words are cleared once per workspace (sweep_begin) instead of by a fill
+// before every pass, and the tile counter runs on across passes (tile = counter - tile_base).
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62, kFlagMask = 3ull << 62;
+constexpr uint64_t kCountMask = (1ull << 40) - 1;
+constexpr int kEpochShift = 40;
+constexpr uint32_t kEpochMax = (1u << 22) - 1;
 
 template <typename K, typename V, int IPTT>
 __global__ __launch_bounds__(T) void k_onesweep(const K* __restrict__ kin, const V* __restrict__ vin,
                                                K* __restrict__ kout, V* __restrict__ vout, int64_t n, int shift,
                                                const uint32_t* __restrict__ digit_base, uint64_t* status,
-                                               uint32_t* tile_counter) {
+                                               uint32_t* tile_counter, uint32_t epoch, uint32_t tile_base) {
   constexpr int IPT = IPTT;
   constexpr int TILE = T * IPTT;
   __shared__ K skeys[TILE];
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(T) void k_onesweep(const K* __restrict__ kin, const
   __shared__ uint32_t tile_sh;
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t == 0) tile_sh = atomicAdd(tile_counter, 1u);
+  if (t == 0) tile_sh = atomicAdd(tile_counter, 1u) - tile_base;
 #pragma unroll
   for (int q = 0; q < 4; ++q) wcnt[w][lane + 64 * q] = 0;
   __syncthreads();
@@ -286,10 +292,11 @@ __global__ __launch_bounds__(T) void k_onesweep(const K* __restrict__ kin, const
   const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
   const uint32_t tot = c0 + c1 + c2 + c3;
   uint64_t* my = status + tile * 256 + t;
+  const uint64_t etag = (uint64_t)epoch << kEpochShift;
   if (tile == 0)
-    __hip_atomic_store(my, kFlagInc | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(my, kFlagInc | etag | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else
-    __hip_atomic_store(my, kFlagAgg | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(my, kFlagAgg | etag | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t ex = block_exclusive_scan_256(tot, dstart, nullptr);
   uint64_t excl = 0;
   if (tile > 0) {
@@ -297,8 +304,8 @@ __global__ __launch_bounds__(T) void k_onesweep(const K* __restrict__ kin, const
     uint32_t spins = 0;
     while (true) {
       const uint64_t sv = __hip_atomic_load(status + tp * 256 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t flag = sv & ~kCountMask;
-      if (flag == 0) {  // tile tp has not published yet
+      const uint64_t flag = (sv & ~kFlagMask & ~kCountMask) == etag ? sv & kFlagMask : 0ull;
+      if (flag == 0) {  // tile tp has not published in this pass yet
         if (++spins > (1u << 26)) {  // cannot happen (see above); never hang the device on a bug
           atomicOr(tile_counter + 1, 1u);
           break;
@@ -309,7 +316,7 @@ __global__ __launch_bounds__(T) void k_onesweep(const K* __restrict__ kin, const
       if (flag == kFlagInc) break;
       --tp;
     }
-    __hip_atomic_store(my, kFlagInc | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(my, kFlagInc | etag | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   dstart[t] = ex;
   wcnt[0][t] = 0;
@@ -375,21 +382,38 @@ int onesweep_items(size_t item_bytes_minus_key4) {
   return item_bytes_minus_key4 <= 4 ? 36 : 24;  // item_bytes (key + value) 8 -> 36, 12 -> 24: ~79 KB of LDS either way
 }
 
+// The next pass's epoch and tile base; the words and the counter are cleared (one fill) on a
+// workspace's first pass and when the epoch or the counter would wrap.
+int sweep_begin(SweepState& sw, uint64_t* status, int64_t nt, hipStream_t s, uint32_t* epoch, uint32_t* tile_base) {
+  if (sw.epoch == 0 || sw.epoch >= kEpochMax || (uint64_t)sw.tile_base + (uint64_t)nt >= (1ull << 31)) {
+    PBH_CHECK_HIP(hipMemsetAsync(status, 0, sw.bytes, s));  // words, tile counter, stuck flag
+    sw.epoch = 0;
+    sw.tile_base = 0;
+  }
+  *epoch = ++sw.epoch;
+  *tile_base = sw.tile_base;
+  sw.tile_base += (uint32_t)nt;
+  return PBH_OK;
+}
+
+// counter: the tile counter (the stuck flag is the word after it), at status + 256 * sort_tiles(n)
 template <typename K, typename V, int IPT_>
-void launch_onesweep_ipt(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
-                         uint64_t* status, uint32_t* counter, hipStream_t s) {
+int launch_onesweep_ipt(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
+                        uint64_t* status, uint32_t* counter, SweepState& sw, hipStream_t s) {
   const int64_t nt = (n + T * IPT_ - 1) / (T * IPT_);
+  uint32_t epoch = 0, tile_base = 0;
+  if (int st = sweep_begin(sw, status, nt, s, &epoch, &tile_base)) return st;
   hipLaunchKernelGGL((k_onesweep<K, V, IPT_>), dim3((unsigned)nt), dim3(T), 0, s, kin, vin, kout, vout, n, shift,
-                     bases, status, counter);
+                     bases, status, counter, epoch, tile_base);
+  return PBH_OK;
 }
 
 template <typename K, typename V>
-void launch_onesweep(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
-                     uint64_t* status, uint32_t* counter, hipStream_t s) {
+int launch_onesweep(const K* kin, const V* vin, K* kout, V* vout, int64_t n, int shift, const uint32_t* bases,
+                    uint64_t* status, uint32_t* counter, SweepState& sw, hipStream_t s) {
   if (onesweep_items(sizeof(K) + sizeof(V) - 4) == 36)  // u64 key + u32 row sizes like u32 + f64
-    launch_onesweep_ipt<K, V, 36>(kin, vin, kout, vout, n, shift, bases, status, counter, s);
-  else
-    launch_onesweep_ipt<K, V, 24>(kin, vin, kout, vout, n, shift, bases, status, counter, s);
+    return launch_onesweep_ipt<K, V, 36>(kin, vin, kout, vout, n, shift, bases, status, counter, sw, s);
+  return launch_onesweep_ipt<K, V, 24>(kin, vin, kout, vout, n, shift, bases, status, counter, sw, s);
 }
 
 // ------------------------------------------------------------------ row placement
@@ -714,10 +738,11 @@ int place_by_row(const uint32_t* rows, const double* v, int64_t n, double* y, in
   for (int shift = kPlaceShift; shift < bits; shift += 8) {
     hipLaunchKernelGGL(k_place_bases, dim3(1), dim3(256), 0, s, n, shift, pb.bases);
     PBH_CHECK_LAUNCH();
-    PBH_CHECK_HIP(hipMemsetAsync(pb.status, 0, (size_t)nt * 256 * 8 + 256, s));  // words, counter, flag
+    int st = PBH_OK;
     PBH_TIMED(kKPlaceScatter, s,
-              launch_onesweep<uint32_t, double>(rin, vin, pb.rows[cur], pb.vals[cur], n, shift, pb.bases, pb.status,
-                                                (uint32_t*)(pb.status + nt * 256), s));
+              st = launch_onesweep<uint32_t, double>(rin, vin, pb.rows[cur], pb.vals[cur], n, shift, pb.bases,
+                                                     pb.status, (uint32_t*)(pb.status + nt * 256), *pb.sweep, s));
+    if (st) return st;
     PBH_CHECK_LAUNCH();
     rin = pb.rows[cur];
     vin = pb.vals[cur];
@@ -786,15 +811,16 @@ int code_sort_buckets(SortBuffers& b, int64_t n, const uint32_t* codes, const do
   }
   hipLaunchKernelGGL(k_digit_bases, dim3(4), dim3(256), 0, s, hist_dev, b.bases);
   PBH_CHECK_LAUNCH();
-  PBH_CHECK_HIP(hipMemsetAsync(b.status + nt * 256, 0, 256, s));
   int cur = 0;
   for (int ip = 0; ip < 2; ++ip) {
     const int byte = 2 + ip;
-    PBH_CHECK_HIP(hipMemsetAsync(b.status, 0, (size_t)nt * 256 * 8 + 4, s));
+    int st = PBH_OK;
     PBH_TIMED(kKSortScatter32, s,
-              launch_onesweep<uint32_t, uint32_t>(ip == 0 ? codes : keys[cur], ip == 0 ? nullptr : b.vals[cur],
-                                                  keys[cur ^ 1], b.vals[cur ^ 1], n, 8 * byte, b.bases + byte * 256,
-                                                  b.status, (uint32_t*)(b.status + nt * 256), s));
+              st = launch_onesweep<uint32_t, uint32_t>(ip == 0 ? codes : keys[cur], ip == 0 ? nullptr : b.vals[cur],
+                                                       keys[cur ^ 1], b.vals[cur ^ 1], n, 8 * byte,
+                                                       b.bases + byte * 256, b.status,
+                                                       (uint32_t*)(b.status + nt * 256), b.sweep, s));
+    if (st) return st;
     PBH_CHECK_LAUNCH();
     cur ^= 1;
   }
@@ -847,6 +873,7 @@ void sort_carve(void* ws, int64_t n, SortBuffers& sb) {
   sb.partials = (uint32_t*)take((size_t)scan_partials_count(m) * 4);
   sb.hist = (uint32_t*)take(8 * 256 * 4);
   sb.status = (uint64_t*)take((size_t)m * 8 + 256);
+  sb.sweep = SweepState{0, 0, (size_t)m * 8 + 256};  // cleared by the first pass (sweep_begin)
   sb.bases = (uint32_t*)take(8 * 256 * 4);
 }
 
@@ -874,14 +901,14 @@ int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, cons
   int cur = 0;
   hipLaunchKernelGGL(k_digit_bases, dim3(NB), dim3(256), 0, s, b.hist, b.bases);
   PBH_CHECK_LAUNCH();
-  PBH_CHECK_HIP(hipMemsetAsync(b.status + nt * 256, 0, 256, s));  // tile counter + stuck flag
   for (int ip = 0; ip < npass; ++ip) {
     const int shift = 8 * passes[ip];
-    PBH_CHECK_HIP(hipMemsetAsync(b.status, 0, (size_t)nt * 256 * 8 + 4, s));  // words + tile counter
+    int st = PBH_OK;
     PBH_TIMED(NB == 8 ? kKSortScatter : kKSortScatter32, s,
-              launch_onesweep<K, uint32_t>(ip == 0 ? first : keys[cur], ip == 0 ? nullptr : b.vals[cur],
-                                           keys[cur ^ 1], b.vals[cur ^ 1], n, shift, b.bases + passes[ip] * 256,
-                                           b.status, (uint32_t*)(b.status + nt * 256), s));
+              st = launch_onesweep<K, uint32_t>(ip == 0 ? first : keys[cur], ip == 0 ? nullptr : b.vals[cur],
+                                                keys[cur ^ 1], b.vals[cur ^ 1], n, shift, b.bases + passes[ip] * 256,
+                                                b.status, (uint32_t*)(b.status + nt * 256), b.sweep, s));
+    if (st) return st;
     PBH_CHECK_LAUNCH();
     cur ^= 1;
   }
@@ -907,13 +934,12 @@ int radix_sort_keys32_async(SortBuffers& b, int64_t n, int npass, hipStream_t s,
   PBH_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_digit_bases, dim3(4), dim3(256), 0, s, b.hist, b.bases);
   PBH_CHECK_LAUNCH();
-  PBH_CHECK_HIP(hipMemsetAsync(b.status + nt * 256, 0, 256, s));  // tile counter + stuck flag
   int cur = 0;
   for (int ip = 0; ip < npass; ++ip) {
-    PBH_CHECK_HIP(hipMemsetAsync(b.status, 0, (size_t)nt * 256 * 8 + 4, s));  // words + tile counter
-    launch_onesweep<uint32_t, uint32_t>(ip == 0 ? in : keys[cur], ip == 0 ? nullptr : b.vals[cur], keys[cur ^ 1],
-                                        b.vals[cur ^ 1], n, 8 * ip, b.bases + ip * 256, b.status,
-                                        (uint32_t*)(b.status + nt * 256), s);
+    if (int st = launch_onesweep<uint32_t, uint32_t>(ip == 0 ? in : keys[cur], ip == 0 ? nullptr : b.vals[cur],
+                                                     keys[cur ^ 1], b.vals[cur ^ 1], n, 8 * ip, b.bases + ip * 256,
+                                                     b.status, (uint32_t*)(b.status + nt * 256), b.sweep, s))
+      return st;
     PBH_CHECK_LAUNCH();
     cur ^= 1;
   }

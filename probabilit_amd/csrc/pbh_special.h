@@ -409,19 +409,31 @@ PBH_HD inline double ppnd16(double p) {
   return ppnd16_takes_tail(p) ? ppnd16_tail(p) : ppnd16_centre(p);
 }
 
+// Math policy of the incomplete-gamma family below: the device's libm (default), or glibc's
+// restated (pbh_glibc.h glibc::Math) where a result must equal scipy's compiled Cephes bit for bit
+// (the poisson CDF, pdtr<glibc::Math>: its tables decide integers at q = a CDF value).
+struct DevMath {
+  PBH_HD static double exp(double x) { return ::exp(x); }
+  PBH_HD static double log(double x) { return ::log(x); }
+  PBH_HD static double pow(double x, double y) { return ::pow(x, y); }
+};
+
 // ---------------------------------------------------------------- erf / erfc (for Temme)
+template <class M = DevMath>
 PBH_HD inline double erfc_(double a);
+template <class M = DevMath>
 PBH_HD inline double erf_(double x) {
   const double T[5] = {9.60497373987051638749e0, 9.00260197203842689217e1, 2.23200534594684319226e3,
                        7.00332514112805075473e3, 5.55923013010394962768e4};
   const double U[5] = {3.35617141647503099647e1, 5.21357949780152679795e2, 4.59432382970980127987e3,
                        2.26290000613890934246e4, 4.92673942608635921086e4};
   if (isnan(x)) return kNaN;
-  if (x < 0.0) return -erf_(-x);
-  if (fabs(x) > 1.0) return 1.0 - erfc_(x);
+  if (x < 0.0) return -erf_<M>(-x);
+  if (fabs(x) > 1.0) return 1.0 - erfc_<M>(x);
   double z = x * x;
   return x * polevl(z, T, 4) / p1evl(z, U, 5);
 }
+template <class M>
 PBH_HD inline double erfc_(double a) {
   const double P[9] = {2.46196981473530512524e-10, 5.64189564831068821977e-1, 7.46321056442269912687e0,
                        4.86371970985681366614e1, 1.96520832956077098242e2, 5.26445194995477358631e2,
@@ -435,10 +447,10 @@ PBH_HD inline double erfc_(double a) {
                        1.70814450747565897222e1, 9.60896809063285878198e0, 3.36907645100081516050e0};
   if (isnan(a)) return kNaN;
   double x = a < 0.0 ? -a : a;
-  if (x < 1.0) return 1.0 - erf_(a);
+  if (x < 1.0) return 1.0 - erf_<M>(a);
   double z = -a * a;
   if (z < -kMaxLog) return a < 0 ? 2.0 : 0.0;
-  z = exp(z);
+  z = M::exp(z);
   double p, q;
   if (x < 8.0) {
     p = polevl(x, P, 8);
@@ -454,6 +466,7 @@ PBH_HD inline double erfc_(double a) {
 }
 
 // ---------------------------------------------------------------- log1p / expm1 / log1pmx
+template <class M = DevMath>
 PBH_HD inline double log1p_(double x) {
   const double LP[7] = {4.5270000862445199635215e-5, 4.9854102823193375972212e-1, 6.5787325942061044846969e0,
                         2.9911919328553073277375e1, 6.0949667980987787057556e1, 5.7112963590585538103336e1,
@@ -461,12 +474,13 @@ PBH_HD inline double log1p_(double x) {
   const double LQ[6] = {1.5062909083469192043167e1, 8.3047565967967209469434e1, 2.2176239823732856465394e2,
                         3.0909872225312059774938e2, 2.1642788614495947685003e2, 6.0118660497603843919306e1};
   double z = 1.0 + x;
-  if ((z < 0.70710678118654752440) || (z > 1.41421356237309504880)) return log(z);
+  if ((z < 0.70710678118654752440) || (z > 1.41421356237309504880)) return M::log(z);
   z = x * x;
   z = -0.5 * z + x * (z * polevl(x, LP, 6) / p1evl(x, LQ, 6));
   return x + z;
 }
 
+template <class M = DevMath>
 PBH_HD inline double expm1_(double x) {
   const double EP[3] = {1.2617719307481059087798e-4, 3.0299440770744196129956e-2, 9.9999999999999999991025e-1};
   const double EQ[4] = {3.0019850513866445504159e-6, 2.5244834034968410419224e-3, 2.2726554820815502876593e-1,
@@ -475,7 +489,7 @@ PBH_HD inline double expm1_(double x) {
     if (isnan(x)) return x;
     return x > 0 ? x : -1.0;
   }
-  if ((x < -0.5) || (x > 0.5)) return exp(x) - 1.0;
+  if ((x < -0.5) || (x > 0.5)) return M::exp(x) - 1.0;
   double xx = x * x;
   double r = x * polevl(xx, EP, 2);
   r = r / (polevl(xx, EQ, 3) - r);
@@ -486,6 +500,7 @@ PBH_HD inline double expm1_(double x) {
 // subnormal arguments are not flushed by the device implementation.
 PBH_HD inline double log1p_libm(double x) { return fabs(x) < 0x1p-54 ? x : log1p(x); }
 
+template <class M = DevMath>
 PBH_HD inline double log1pmx(double x) {  // log(1 + x) - x
   if (fabs(x) < 0.5) {
     double xfac = x, res = 0.0;
@@ -497,7 +512,7 @@ PBH_HD inline double log1pmx(double x) {  // log(1 + x) - x
     }
     return res;
   }
-  return log1p_(x) - x;
+  return log1p_<M>(x) - x;
 }
 
 // ---------------------------------------------------------------- Gamma / lgamma
@@ -585,6 +600,7 @@ small:
   return z / ((1.0 + 0.5772156649015329 * x) * x);
 }
 
+template <class M = DevMath>
 PBH_HD inline double lgam(double x) {
   const double A[5] = {8.11614167470508450300e-4, -5.95061904284301438324e-4, 7.93650340457716943945e-4,
                        -2.77777777730099687205e-3, 8.33333333333331927722e-2};
@@ -595,7 +611,7 @@ PBH_HD inline double lgam(double x) {
   if (!isfinite(x)) return x;
   if (x < -34.0) {
     double q = -x;
-    double w = lgam(q);
+    double w = lgam<M>(q);
     double p = floor(q);
     if (p == q) return kInf;
     double z = q - p;
@@ -605,7 +621,7 @@ PBH_HD inline double lgam(double x) {
     }
     z = q * sinpi_(z);
     if (z == 0.0) return kInf;
-    return kLogPi - log(z) - w;
+    return kLogPi - M::log(z) - w;
   }
   if (x < 13.0) {
     double z = 1.0, p = 0.0, u = x;
@@ -621,21 +637,21 @@ PBH_HD inline double lgam(double x) {
       u = x + p;
     }
     if (z < 0.0) z = -z;
-    if (u == 2.0) return log(z);
+    if (u == 2.0) return M::log(z);
     p -= 2.0;
     x = x + p;
     p = x * polevl(x, B, 5) / p1evl(x, C, 6);
-    return log(z) + p;
+    return M::log(z) + p;
   }
   if (x > 2.556348e305) return kInf;
   if (x >= 1000.0) {
-    double q = (x - 0.5) * log(x) - x + kLogSqrt2Pi;
+    double q = (x - 0.5) * M::log(x) - x + kLogSqrt2Pi;
     if (x > 1.0e8) return q;
     double p = 1.0 / (x * x);
     p = ((7.9365079365079365079365e-4 * p - 2.7777777777777777777778e-3) * p + 0.0833333333333333333333) / x;
     return q + p;
   }
-  double q = (x - 0.5) * log(x) - x + kLogSqrt2Pi;
+  double q = (x - 0.5) * M::log(x) - x + kLogSqrt2Pi;
   double p = 1.0 / (x * x);
   return q + polevl(p, A, 4) / x;
 }
@@ -653,10 +669,11 @@ PBH_HD inline double lgam1p_taylor(double x) {
   return res;
 }
 
+template <class M = DevMath>
 PBH_HD inline double lgam1p(double x) {  // lgamma(1 + x)
   if (fabs(x) <= 0.5) return lgam1p_taylor(x);
-  if (fabs(x - 1) < 0.5) return log(x) + lgam1p_taylor(x - 1);
-  return lgam(x + 1);
+  if (fabs(x - 1) < 0.5) return M::log(x) + lgam1p_taylor(x - 1);
+  return lgam<M>(x + 1);
 }
 
 // Lanczos approximation pieces (g = 6.0246800407767295...), rational evaluation "ratevl"
@@ -719,26 +736,28 @@ struct GammaAux {
 
 PBH_HD inline GammaAux gamma_aux(double a);
 
+template <class M = DevMath>
 PBH_HD inline double igam_fac(double a, double x, const GammaAux* g = nullptr) {
   if (fabs(a - x) > 0.4 * fabs(a)) {
-    double ax = a * log(x) - x - (g ? g->lga : lgam(a));
+    double ax = a * M::log(x) - x - (g ? g->lga : lgam<M>(a));
     if (ax < -kMaxLog) return 0.0;
-    return exp(ax);
+    return M::exp(ax);
   }
   double fac = a + kLanczosG - 0.5;
-  double res = sqrt(fac / exp(1.0)) / (g ? g->lanczos : lanczos_sum_expg_scaled(a));
+  double res = sqrt(fac / M::exp(1.0)) / (g ? g->lanczos : lanczos_sum_expg_scaled(a));
   if ((a < 200) && (x < 200)) {
-    res *= exp(a - x) * pow(x / fac, a);
+    res *= M::exp(a - x) * M::pow(x / fac, a);
   } else {
     double num = x - a - kLanczosG + 0.5;
-    res *= exp(a * log1pmx(num / fac) + x * (0.5 - kLanczosG) / fac);
+    res *= M::exp(a * log1pmx<M>(num / fac) + x * (0.5 - kLanczosG) / fac);
   }
   return res;
 }
 
+template <class M = DevMath>
 PBH_HD inline double igamc_cf(double a, double x, const GammaAux* g = nullptr) {  // DLMF 8.9.2
   const double big = 4.503599627370496e15, biginv = 2.22044604925031308085e-16;
-  double ax = igam_fac(a, x, g);
+  double ax = igam_fac<M>(a, x, g);
   if (ax == 0.0) return 0.0;
   double y = 1.0 - a, z = x + y + 1.0, c = 0.0;
   double pkm2 = 1.0, qkm2 = x, pkm1 = x + 1.0, qkm1 = z * x;
@@ -772,8 +791,9 @@ PBH_HD inline double igamc_cf(double a, double x, const GammaAux* g = nullptr) {
   return ans * ax;
 }
 
+template <class M = DevMath>
 PBH_HD inline double igam_series(double a, double x, const GammaAux* g = nullptr) {  // DLMF 8.11.4
-  double ax = igam_fac(a, x, g);
+  double ax = igam_fac<M>(a, x, g);
   if (ax == 0.0) return 0.0;
   double r = a, c = 1.0, ans = 1.0;
   for (int i = 0; i < 2000; ++i) {
@@ -785,6 +805,7 @@ PBH_HD inline double igam_series(double a, double x, const GammaAux* g = nullptr
   return ans * ax / a;
 }
 
+template <class M = DevMath>
 PBH_HD inline double igamc_series(double a, double x, const GammaAux* g = nullptr) {  // DLMF 8.7.3
   double fac = 1, sum = 0;
   for (int n = 1; n < 2000; ++n) {
@@ -793,12 +814,13 @@ PBH_HD inline double igamc_series(double a, double x, const GammaAux* g = nullpt
     sum += term;
     if (fabs(term) <= kMachEp * fabs(sum)) break;
   }
-  double logx = log(x);
-  double term = -expm1_(a * logx - (g ? g->lg1pa : lgam1p(a)));
-  return term - exp(a * logx - (g ? g->lga : lgam(a))) * sum;
+  double logx = M::log(x);
+  double term = -expm1_<M>(a * logx - (g ? g->lg1pa : lgam1p<M>(a)));
+  return term - M::exp(a * logx - (g ? g->lga : lgam<M>(a))) * sum;
 }
 
 // Temme uniform asymptotic expansion, DLMF 8.12.3 / 8.12.4; igam when upper == false.
+template <class M = DevMath>
 PBH_HD inline double igam_asymptotic(double a, double x, bool upper) {
   const int K = 25, N = 25;
   double lambda = x / a, sigma = (x - a) / a, eta;
@@ -808,12 +830,12 @@ PBH_HD inline double igam_asymptotic(double a, double x, bool upper) {
   double sum = 0, afac = 1, absoldterm = kInf;
   int sgn = upper ? 1 : -1;
   if (lambda > 1)
-    eta = sqrt(-2 * log1pmx(sigma));
+    eta = sqrt(-2 * log1pmx<M>(sigma));
   else if (lambda < 1)
-    eta = -sqrt(-2 * log1pmx(sigma));
+    eta = -sqrt(-2 * log1pmx<M>(sigma));
   else
     eta = 0;
-  double res = 0.5 * erfc_(sgn * eta * sqrt(a / 2));
+  double res = 0.5 * erfc_<M>(sgn * eta * sqrt(a / 2));
   for (int k = 0; k < K; ++k) {
     double ck = pbh_temme_d[k][0];
     for (int n = 1; n < N; ++n) {
@@ -833,12 +855,14 @@ PBH_HD inline double igam_asymptotic(double a, double x, bool upper) {
     absoldterm = absterm;
     afac /= a;
   }
-  res += sgn * exp(-0.5 * a * eta * eta) * sum / sqrt(2 * kPi * a);
+  res += sgn * M::exp(-0.5 * a * eta * eta) * sum / sqrt(2 * kPi * a);
   return res;
 }
 
+template <class M = DevMath>
 PBH_HD inline double igamc(double a, double x, const GammaAux* g = nullptr);
 
+template <class M = DevMath>
 PBH_HD inline double igam(double a, double x, const GammaAux* g = nullptr) {  // regularized lower P(a, x)
   if (x < 0 || a < 0) return kNaN;
   if (a == 0) return x > 0 ? 1.0 : kNaN;
@@ -846,12 +870,13 @@ PBH_HD inline double igam(double a, double x, const GammaAux* g = nullptr) {  //
   if (isinf(a)) return isinf(x) ? kNaN : 0.0;
   if (isinf(x)) return 1.0;
   double absxma_a = fabs(x - a) / a;
-  if ((a > 20) && (a < 200) && (absxma_a < 0.3)) return igam_asymptotic(a, x, false);
-  if ((a > 200) && (absxma_a < 4.5 / sqrt(a))) return igam_asymptotic(a, x, false);
-  if ((x > 1.0) && (x > a)) return 1.0 - igamc(a, x, g);
-  return igam_series(a, x, g);
+  if ((a > 20) && (a < 200) && (absxma_a < 0.3)) return igam_asymptotic<M>(a, x, false);
+  if ((a > 200) && (absxma_a < 4.5 / sqrt(a))) return igam_asymptotic<M>(a, x, false);
+  if ((x > 1.0) && (x > a)) return 1.0 - igamc<M>(a, x, g);
+  return igam_series<M>(a, x, g);
 }
 
+template <class M>
 PBH_HD inline double igamc(double a, double x, const GammaAux* g) {  // regularized upper Q(a, x)
   if (x < 0 || a < 0) return kNaN;
   if (a == 0) return x > 0 ? 0.0 : kNaN;
@@ -859,18 +884,18 @@ PBH_HD inline double igamc(double a, double x, const GammaAux* g) {  // regulari
   if (isinf(a)) return isinf(x) ? kNaN : 1.0;
   if (isinf(x)) return 0.0;
   double absxma_a = fabs(x - a) / a;
-  if ((a > 20) && (a < 200) && (absxma_a < 0.3)) return igam_asymptotic(a, x, true);
-  if ((a > 200) && (absxma_a < 4.5 / sqrt(a))) return igam_asymptotic(a, x, true);
+  if ((a > 20) && (a < 200) && (absxma_a < 0.3)) return igam_asymptotic<M>(a, x, true);
+  if ((a > 200) && (absxma_a < 4.5 / sqrt(a))) return igam_asymptotic<M>(a, x, true);
   if (x > 1.1) {
-    if (x < a) return 1.0 - igam_series(a, x, g);
-    return igamc_cf(a, x, g);
+    if (x < a) return 1.0 - igam_series<M>(a, x, g);
+    return igamc_cf<M>(a, x, g);
   }
   if (x <= 0.5) {
-    if (-0.4 / log(x) < a) return 1.0 - igam_series(a, x, g);
-    return igamc_series(a, x, g);
+    if (-0.4 / M::log(x) < a) return 1.0 - igam_series<M>(a, x, g);
+    return igamc_series<M>(a, x, g);
   }
-  if (x * 1.1 < a) return 1.0 - igam_series(a, x, g);
-  return igamc_series(a, x, g);
+  if (x * 1.1 < a) return 1.0 - igam_series<M>(a, x, g);
+  return igamc_series<M>(a, x, g);
 }
 
 PBH_HD inline GammaAux gamma_aux(double a) { return GammaAux{lgam(a), lgam1p(a), lanczos_sum_expg_scaled(a)}; }
@@ -1186,10 +1211,11 @@ PBH_HD inline double gamma_guide_check(double a, const GammaGuide& T, int j) {
 }
 
 // Poisson CDF P[X <= k] = Q(k + 1, m) for integer k >= 0 (scipy.special.pdtr).
+template <class M = DevMath>
 PBH_HD inline double pdtr(double k, double m) {
   if (k < 0 || m < 0) return kNaN;
   if (m == 0.0) return 1.0;
-  return igamc(floor(k) + 1, m);
+  return igamc<M>(floor(k) + 1, m);
 }
 
 }  // namespace sf

@@ -442,6 +442,42 @@ PBH_HD inline double randint_ppf01(double q, double low, double high) {
   return temp >= q ? vals1 : vals;
 }
 
+// ---- round 6: dlaplace, planck, boltzmann (scipy 1.15 _discrete_distns.py _ppf / _cdf bodies)
+
+// dlaplace._ppf(q, a): const = 1 + exp(a); vals = ceil(q < 1 / (1 + exp(-a)) ? log(q const) / a - 1
+// : -log((1 - q) const) / a); one step down where _cdf(vals - 1, a) >= q, with
+// _cdf(k) = 1 - exp(-a k) / (exp(a) + 1) for k >= 0, exp(a (k + 1)) / (exp(a) + 1) below
+PBH_HD inline double dlaplace_cdf(double x, double a) {
+  const double k = floor(x);
+  return k >= 0.0 ? 1.0 - exp(-a * k) / (exp(a) + 1) : exp(a * (k + 1)) / (exp(a) + 1);
+}
+PBH_HD inline double dlaplace_ppf01(double q, double a) {
+  const double cst = 1 + exp(a);
+  const double vals = ceil(q < 1.0 / (1 + exp(-a)) ? log(q * cst) / a - 1 : -log((1 - q) * cst) / a);
+  const double vals1 = vals - 1;
+  return dlaplace_cdf(vals1, a) >= q ? vals1 : vals;
+}
+
+// planck._ppf(q, lambda): vals = ceil(-1 / lambda log1p(-q) - 1); vals1 = max(vals - 1, 0);
+// _cdf(vals1) = -expm1(-lambda (floor(vals1) + 1)) >= q ? vals1 : vals
+PBH_HD inline double planck_ppf01(double q, double lam) {
+  const double vals = ceil(-1.0 / lam * log1p(-q) - 1);
+  const double vals1 = fmax(vals - 1, 0.0);
+  const double temp = -expm1(-lam * (floor(vals1) + 1));
+  return temp >= q ? vals1 : vals;
+}
+
+// boltzmann._ppf(q, lambda, N): the truncated planck, qnew = q (1 - exp(-lambda N)); vals =
+// ceil(-1 / lambda log(1 - qnew) - 1); vals1 = max(vals - 1, 0); _cdf(vals1) = (1 - exp(-lambda
+// (floor(vals1) + 1))) / (1 - exp(-lambda N)) >= q ? vals1 : vals
+PBH_HD inline double boltzmann_ppf01(double q, double lam, double N) {
+  const double qnew = q * (1 - exp(-lam * N));
+  const double vals = ceil(-1.0 / lam * log(1 - qnew) - 1);
+  const double vals1 = fmax(vals - 1, 0.0);
+  const double temp = (1 - exp(-lam * (floor(vals1) + 1))) / (1 - exp(-lam * N));
+  return temp >= q ? vals1 : vals;
+}
+
 // negative binomial CDF P(X <= k) = I_p(n, k + 1) and its complement I_{1-p}(k + 1, n) (Boost's
 // nbinom cdf, the incomplete beta ratio; Cephes incbet restated above)
 PBH_HD inline double nbdtr(double k, double n, double p) {

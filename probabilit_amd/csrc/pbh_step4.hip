@@ -915,7 +915,60 @@ __global__ __launch_bounds__(256) void k_place_positions(const uint64_t* __restr
   }
 }
 
+// Y[row] = sorted[p] for the pairs (row << 32 | p) of every 4096-row block: the final placement of a
+// MATERIALISED column (X given: the operator API, the reference LHS stream) through the same
+// passes as a generated one -- sort(X)[p] read from the sorted column instead of regenerated.  The
+// reads are a gather (p is random inside a block); the block is assembled in LDS and written out
+// contiguously.  idx (optional): idx[row] = p.
+constexpr int kPSIpt = 8;
+__global__ __launch_bounds__(512) void k_place_sorted(const uint64_t* __restrict__ pairs, int64_t n,
+                                                      const double* __restrict__ sorted, double* __restrict__ y,
+                                                      int64_t y_rs, int32_t* __restrict__ idx,
+                                                      const int32_t* __restrict__ state) {
+  if (state && *state) return;
+  constexpr int kRows = 1 << kGenPlaceShift;
+  __shared__ double buf[kRows];
+  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
+    const int64_t r0 = b << kGenPlaceShift;
+    const int cnt = (int)((n - r0) < kRows ? (n - r0) : kRows);
+    uint64_t pa[kPSIpt];
+    double v[kPSIpt];
+#pragma unroll
+    for (int j = 0; j < kPSIpt; ++j) {
+      const int p = j * 512 + threadIdx.x;
+      pa[j] = p < cnt ? pairs[r0 + p] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kPSIpt; ++j) v[j] = j * 512 + (int)threadIdx.x < cnt ? sorted[(uint32_t)pa[j]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < kPSIpt; ++j) {
+      if (j * 512 + (int)threadIdx.x >= cnt) continue;
+      const int64_t row = (int64_t)(pa[j] >> 32);
+      if (idx) idx[row] = (int32_t)(uint32_t)pa[j];
+      buf[row - r0] = v[j];
+    }
+    __syncthreads();
+    if (y_rs == 1) {
+      for (int p = threadIdx.x; p < cnt; p += 512) y[r0 + p] = buf[p];
+    } else {
+      for (int p = threadIdx.x; p < cnt; p += 512) y[(r0 + p) * y_rs] = buf[p];
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
+
+int place_sorted(const double* sorted, const uint64_t* pairs, int64_t n, double* y, int64_t y_rs, int32_t* idx,
+                 const int32_t* state, hipStream_t s) {
+  const int64_t blocks = (n + (1 << kGenPlaceShift) - 1) >> kGenPlaceShift;
+  if (blocks <= 0) return PBH_OK;
+  PBH_TIMED(kKPlaceGen, s,
+            hipLaunchKernelGGL(k_place_sorted, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(512), 0, s,
+                               pairs, n, sorted, y, y_rs, idx, state));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
 
 int place_positions(const uint64_t* pairs, int64_t n, uint32_t* p_out, const int32_t* state, hipStream_t s) {
   const int64_t blocks = (n + (1 << kGenPlaceShift) - 1) >> kGenPlaceShift;
@@ -1071,6 +1124,14 @@ bool step4_gen_enabled(int64_t n) {
   const char* e = getenv("PBH_STEP4");  // "lsd" / "legacy": the general path for every column
   if (e && (strcmp(e, "lsd") == 0 || strcmp(e, "legacy") == 0)) return false;
   return n >= 2 && n < ((int64_t)1 << 32);
+}
+
+bool step4_mat_enabled(int64_t n) {
+  const char* e = getenv("PBH_STEP4_MAT");  // "general": the per-column code sort + row placement; "msd": forced
+  if (e && strcmp(e, "general") == 0) return false;
+  if (!step4_gen_enabled(n)) return false;
+  if (e && strcmp(e, "msd") == 0) return true;
+  return n >= ((int64_t)1 << 20);  // below, the 32 768 finish blocks per column outweigh the rows
 }
 
 int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,

@@ -39,7 +39,8 @@ import numpy as np
 from . import _lib, device
 
 HEADS_CAP = 16384  # run heads a discrete column's shard may append (kHeadsCap, pbh_step4.h)
-DISCRETE = {_lib.DIST_IDS[d] for d in ("poisson", "binom", "bernoulli", "geom", "randint", "nbinom")}  # sorted columns with runs
+DISCRETE = {_lib.DIST_IDS[d] for d in ("poisson", "binom", "bernoulli", "geom", "randint", "nbinom", "dlaplace",
+                                        "planck", "boltzmann")}  # sorted columns with runs
 
 
 def shard_bounds(n, world):

@@ -705,8 +705,14 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "loglaplace": ("c",), "truncexpon": ("b",), "chi": ("df",), "maxwell": (), "nakagami": ("nu",),
                 "dweibull": ("c",), "kappa3": ("a",), "genhalflogistic": ("c",), "alpha": ("a",),
                 "fatiguelife": ("c",), "genlogistic": ("c",), "trapezoid": ("c", "d"),
-                "geom": ("p",), "randint": ("low", "high"), "nbinom": ("n", "p"), "invgamma": ("a",), "t": ("df",)}
-_DISCRETE = {"poisson", "binom", "bernoulli", "geom", "randint", "nbinom"}
+                "geom": ("p",), "randint": ("low", "high"), "nbinom": ("n", "p"), "invgamma": ("a",), "t": ("df",),
+                # round 6
+                "trapz": ("c", "d"), "johnsonsu": ("a", "b"), "johnsonsb": ("a", "b"), "powernorm": ("c",),
+                "laplace_asymmetric": ("kappa",), "mielke": ("k", "s"), "truncpareto": ("b", "c"),
+                "tukeylambda": ("lam",), "gengamma": ("a", "c"), "loggamma": ("c",), "dgamma": ("a",),
+                "f": ("dfn", "dfd"), "rdist": ("c",), "semicircular": (), "betaprime": ("a", "b"),
+                "dlaplace": ("a",), "planck": ("lambda_",), "boltzmann": ("lambda_", "N")}
+_DISCRETE = {"poisson", "binom", "bernoulli", "geom", "randint", "nbinom", "dlaplace", "planck", "boltzmann"}
 # distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so
 # that Iman-Conover takes them as generated columns (pbh_ppf.hip k_lhs_sorted_ppf / k_place_gen;
 # the extended set pbh_ppf_ext.hip k_ext_sorted / k_ext_place): every distribution with a kernel

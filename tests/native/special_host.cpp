@@ -4,6 +4,7 @@
 // are checked separately by tests/test_gpu_ppf.py (libm vs device math may differ by ulps).
 #include <vector>
 
+#include "pbh_glibc.h"
 #include "pbh_special.h"
 
 using namespace pbh;
@@ -71,7 +72,7 @@ void sfh_igami(double a, const double* p, long n, double* out) {
 }
 
 void sfh_pdtr(const double* k, double mu, long n, double* out) {
-  for (long i = 0; i < n; ++i) out[i] = sf::pdtr(k[i], mu);
+  for (long i = 0; i < n; ++i) out[i] = sf::pdtr<pbh::glibc::Math>(k[i], mu);
 }
 
 // gamma ppf through the scalar-shape guide table, exactly as the device kernels use it.
@@ -151,6 +152,9 @@ void sfh_glibc_exp(const double* x, long n, double* out) {
 void sfh_glibc_log(const double* x, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = pbh::glibc::log(x[i]);
 }
+void sfh_glibc_pow(const double* x, const double* y, long n, double* out) {
+  for (long i = 0; i < n; ++i) out[i] = pbh::glibc::pow(x[i], y[i]);
+}
 void sfh_pdtrik(double mu, const double* p, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = cdf::pdtrik(p[i], mu);
 }
@@ -202,7 +206,7 @@ void sfh_poisson_ppf_device(double mu, const double* q, long n, double* out) {
   for (long i = 0; i < n; ++i) {
     double k = 0.0;
     if (mu > 0.0) {
-      while (sf::pdtr(k, mu) < q[i] && k < 1e7) k += 1.0;
+      while (sf::pdtr<pbh::glibc::Math>(k, mu) < q[i] && k < 1e7) k += 1.0;
     }
     const bool rare = (k >= 1.0 && q[i] < cdf::poisson_window_hi(k, mu)) || q[i] < cdf::kPoissonDeepTail;
     out[i] = rare ? cdf::poisson_ppf_scipy(q[i], mu) : k;

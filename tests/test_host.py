@@ -123,7 +123,7 @@ def test_distribution_table_matches_header_and_scipy():
     text = open(f"{ROOT}/include/probabilit_hip.h").read()
     enum = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"PBH_DIST_(\w+) = (\d+)", text)}
     for name, shapes in _DIST_SHAPES.items():
-        alias = {"reciprocal": "loguniform", "erlang": "gamma"}.get(name)  # the same _ppf as another id
+        alias = {"reciprocal": "loguniform", "erlang": "gamma", "trapz": "trapezoid"}.get(name)  # the same _ppf as another id
         assert _lib.DIST_IDS[name] == enum.get(name, enum.get(alias)), name
         sc = getattr(scipy.stats, name).shapes
         assert (tuple(x.strip() for x in sc.split(",")) if sc else ()) == shapes, name

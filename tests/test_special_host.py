@@ -28,7 +28,7 @@ def sfh():
         pytest.skip("hipcc not available")
     deps = [SRC] + [os.path.join(ROOT, "probabilit_amd", "csrc", f) for f in ("pbh_special.h", "pbh_special_ext.h", "pbh_common.h",
                                                                             "pbh_tables.inc", "pbh_cdflib.h",
-                                                                            "pbh_glibc.h", "pbh_glibc_tables.inc")]
+                                                                            "pbh_glibc.h", "pbh_glibc_tables.inc", "pbh_special.h")]
     if not os.path.exists(OUT) or any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
         subprocess.run([hipcc, "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
@@ -321,6 +321,16 @@ def test_glibc_exp_log_bit_exact(sfh):
     want_l = np.array([libm.log(float(v)) for v in xl])
     np.testing.assert_array_equal(_call(sfh, "sfh_glibc_exp", xe), want_e)
     np.testing.assert_array_equal(_call(sfh, "sfh_glibc_log", xl), want_l)
+    # pow on the arguments the Cephes incomplete gamma gives it (igam_fac: (x / fac)^a, a < 200)
+    # and beyond
+    libm.pow.restype = ctypes.c_double
+    libm.pow.argtypes = [ctypes.c_double, ctypes.c_double]
+    px = np.concatenate([rng.uniform(0.5, 1.5, 100000), 10.0 ** rng.uniform(-300, 300, 50000)])
+    py = np.concatenate([rng.uniform(0.5, 200.0, 100000), rng.uniform(-1.0, 1.0, 50000)])
+    got = np.empty_like(px)
+    P = ctypes.c_void_p
+    sfh.sfh_glibc_pow(P(px.ctypes.data), P(py.ctypes.data), ctypes.c_long(px.size), P(got.ctypes.data))
+    np.testing.assert_array_equal(got, np.array([libm.pow(float(a), float(b)) for a, b in zip(px, py)]))
 
 
 @pytest.mark.parametrize("mu", [1e-3, 0.5, 1.0, 2.0, 3.0, 4.0, 17.3, 30.0, 250.0, 2500.0, 1e5])
