@@ -74,7 +74,9 @@ PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
   while (lo < t.len && t.cdf[lo] < q) ++lo;
   const bool outside = lo == t.len || (lo == 0 && t.k_lo > 0);
   double k = (double)(t.k_lo + lo);
+#ifndef PBH_AB_POISSON_NORARE  // A/B build (timing only): the table's answer everywhere
   if (outside || q < t.win[lo] || q < cdf::kPoissonDeepTail) k = poisson_rare(q, mu, outside ? -1.0 : k);
+#endif
   return k;
 }
 

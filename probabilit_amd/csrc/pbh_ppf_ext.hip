@@ -480,14 +480,19 @@ __device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
     return g < 2.2250738585072014e-308 ? (log(q) + sf::lgam(s0 + 1)) / s0 : log(g);  // _XMIN = finfo.tiny
   }
   if constexpr (D == PBH_DIST_DGAMMA) return q > 0.5 ? sf::igami(s0, 2 * q - 1) : -sf::igamci(s0, 2 * q);
-  if constexpr (D == PBH_DIST_F) {  // fdtri: w = I^-1(q; dfn / 2, dfd / 2), its complement by symmetry
-    const double a = 0.5 * s0, b = 0.5 * s1;
-    if (q <= 0.5) {
-      const double w = sfx::beta_ppf01(q, a, b);
-      return s1 * w / (s0 * (1.0 - w));
+  if constexpr (D == PBH_DIST_F) {
+    // scipy's fdtri (Cephes fdtr.c) step for step: y = 1 - q first (so q below ~1e-16 reads as 0,
+    // and scipy returns 0 there), then the inverse on the side of I_0.5(dfd / 2, dfn / 2) that
+    // avoids the cancellation in dfd - dfd w
+    const double a = s0, b = s1;
+    const double y = 1.0 - q;
+    const double w0 = sfx::incbet(0.5 * b, 0.5 * a, 0.5);
+    if (w0 > y || y < 0.001) {
+      const double w = sfx::beta_ppf01(y, 0.5 * b, 0.5 * a);
+      return (b - b * w) / (a * w);
     }
-    const double v = sfx::beta_ppf01(1.0 - q, b, a);  // 1 - w, exact for q >= 0.5
-    return s1 * (1.0 - v) / (s0 * v);
+    const double w = sfx::beta_ppf01(1.0 - y, 0.5 * a, 0.5 * b);
+    return b * w / (a * (1.0 - w));
   }
   if constexpr (D == PBH_DIST_RDIST) return 2 * sfx::beta_ppf01(q, s0 / 2, s0 / 2) - 1;
   if constexpr (D == PBH_DIST_SEMICIRCULAR) return 2 * sfx::beta_ppf01(q, 1.5, 1.5) - 1;  // rdist._ppf(q, 3)

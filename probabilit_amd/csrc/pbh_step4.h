@@ -53,7 +53,7 @@ void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh);
 void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb);
 bool step4_gen_enabled(int64_t n);
 // materialised columns (X given) through the same passes, the final placement gathering sort(X)[p]
-// (PBH_STEP4_MAT: "general" keeps the per-column code sort, "msd" forces; default n >= 2^20)
+// (PBH_STEP4_MAT=msd; the default is the general path, measured faster)
 bool step4_mat_enabled(int64_t n);
 // columns of step 4 run concurrently on this many streams (PBH_STEP4_STREAMS, default 3, at
 // most kStep4MaxStreams), each with its own Step4Column staging, so that one column's VALU- or

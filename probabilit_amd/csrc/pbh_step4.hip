@@ -1126,12 +1126,15 @@ bool step4_gen_enabled(int64_t n) {
   return n >= 2 && n < ((int64_t)1 << 32);
 }
 
+// Measured (profiles/r06/ab_step4_mat_r6ab.log): the reference stream at 1e7 x 32 takes 83.9 ms
+// through the MSD passes against 76.1-76.4 through the general path, the operator at 1e8 x 32
+// 679 against 675 ms -- k_place_sorted's gather of sort(X)[p] from a random p costs a 64-byte line
+// per 8-byte value once the column outgrows the caches (6.2 ms per 1e8-row column), what the
+// general path's row placement, carrying the value, does not pay.  So the general path stays the
+// default and PBH_STEP4_MAT=msd selects this one (tests prove both equal).
 bool step4_mat_enabled(int64_t n) {
-  const char* e = getenv("PBH_STEP4_MAT");  // "general": the per-column code sort + row placement; "msd": forced
-  if (e && strcmp(e, "general") == 0) return false;
-  if (!step4_gen_enabled(n)) return false;
-  if (e && strcmp(e, "msd") == 0) return true;
-  return n >= ((int64_t)1 << 20);  // below, the 32 768 finish blocks per column outweigh the rows
+  const char* e = getenv("PBH_STEP4_MAT");
+  return e && strcmp(e, "msd") == 0 && step4_gen_enabled(n);
 }
 
 int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,

@@ -592,6 +592,8 @@ class Node(abc.ABC):
                     for var, col in zip(all_variables, Yh.T):
                         var.samples_ = np.copy(col)
 
+            if getattr(source, "strata", None) is not None:
+                source.strata = None  # read only by the correlators above: d x n int32 freed now
             # the per-node loop, or all of it as one fused kernel (probabilit_amd.dag)
             order = list(plan.order)
             if correlations and dag.try_evaluate(order, isns, source, ev, gc):

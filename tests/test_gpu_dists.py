@@ -504,6 +504,13 @@ def test_round6_distributions_ppf(gpu, name, kw):
     if name in ("dlaplace", "planck", "boltzmann"):
         np.testing.assert_array_equal(got, ref)
     else:
+        if name == "mielke":
+            # q = 1 - 2^-53: q^(s/k) is 1 - 4.9e-17, which rounds to 1.0 (glibc's pow and the device's
+            # give 1.0, so qsk / (1 - qsk) = inf); numpy's SIMD power returns the double below 1, one
+            # ulp off, and scipy's finite value follows from that ulp alone.  Either is accepted there.
+            at = q == 1 - 2.0**-53
+            assert np.all((got[at] == ref[at]) | np.isinf(got[at]))
+            got, ref = got[~at], ref[~at]
         assert_close(got, ref, rtol=1e-10, atol=1e-13, what=f"{name} {kw}")
 
 

@@ -1,8 +1,9 @@
 """Step 4 of MATERIALISED columns (X given: the operator API, the reference LHS stream) through the
 generated columns' passes -- top-16 histogram, MSD code passes, bucket finish, row placement --
 with sort(X)[p] gathered from the sorted column (k_place_sorted) instead of regenerated.
-PBH_STEP4_MAT=msd forces that path below its default size (n >= 2^20), "general" keeps the
-per-column code sort; both must give the oracle's Y and indices bit for bit."""
+PBH_STEP4_MAT=msd selects that path (measured slower than the general path's per-column code sort
+and value-carrying row placement, which stays the default); both must give the oracle's Y and
+indices bit for bit."""
 
 import numpy as np
 import pytest
@@ -71,8 +72,8 @@ def test_mat_msd_long_runs_fall_back(gpu, msd):
 
 
 def test_mat_msd_matches_general_large(gpu, monkeypatch):
-    """n = 3M (the default range): identical Y from the MSD path and the general path, and the
-    oracle's on the whole design."""
+    """n = 3M: identical Y from the MSD path and the general path, and the oracle's on the whole
+    design."""
     from oracle import ic as oic
     from oracle.pipeline import cfg3_corr, cfg_dists, lhs_quantiles, ppf_columns
     from probabilit_amd.correlation import ImanConover
@@ -82,7 +83,7 @@ def test_mat_msd_matches_general_large(gpu, monkeypatch):
     C = cfg3_corr(k)
     monkeypatch.setenv("PBH_STEP4_MAT", "general")
     Y_g = ImanConover().set_target(C)(X)
-    monkeypatch.delenv("PBH_STEP4_MAT")
+    monkeypatch.setenv("PBH_STEP4_MAT", "msd")
     Y_m = ImanConover().set_target(C)(X)
     np.testing.assert_array_equal(Y_m, Y_g)
     np.testing.assert_array_equal(Y_m, oic.iman_conover(X, C)["Y"])
