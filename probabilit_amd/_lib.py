@@ -66,7 +66,7 @@ KERNELS = ["k_lhs_ppf", "k_ppf", "k_scatter", "k_upsweep", "k_digit_hist", "k_ra
            "k_make_codes", "k_scatter<u32>", "k_upsweep<u32>", "k_digit_hist<u32>",
            "k_upsweep<place>", "k_scatter<place>", "k_place", "k_streams", "k_affine", "k_table_ppf",
            "k_permcorr", "k_hbm_copy", "k_hist16", "k_msd1", "k_msd2", "k_finish", "k_place_msd",
-           "k_place_gen", "k_dag"]
+           "k_place_gen", "k_dag", "k_transpose"]
 
 
 class Param(ctypes.Structure):

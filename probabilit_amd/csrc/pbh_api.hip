@@ -399,6 +399,27 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     for (int c = 0; c < k; ++c)
       if (deferred[c]) cnt_host[2 * c] = cnt_host[2 * c + 1] = 0;  // assumed; checked before step 4
   }
+  // The operator API's row-major X (n, k) (correlation.py:368, numpy C order): every phase reads
+  // whole columns, a 64-byte line per 8-byte value when strided, so the block is transposed once into
+  // S (k x n; step 1 reads column c there before it writes c's scores over it) and Y is assembled
+  // column-major in S (step 4 writes column c's values last, over its dead CS) and transposed back
+  // (PBH_IC_TRANSPOSE=0: strided, the comparator)
+  static const bool transpose_on = [] {
+    const char* e = getenv("PBH_IC_TRANSPOSE");
+    return !(e && e[0] == '0');
+  }();
+  const bool x_rows = transpose_on && a->X && !a->columns && k > 1 && a->x_cs == 1 && a->x_rs >= k;
+  const bool y_rows = transpose_on && !a->columns && k > 1 && a->y_cs == 1 && a->y_rs >= k;
+  const double* Xb = a->X;
+  int64_t xb_rs = a->x_rs, xb_cs = a->x_cs;
+  if (x_rows) {
+    if ((st = rows_to_columns(a->X, a->x_rs, n, k, L.S, s))) return st;
+    Xb = L.S;
+    xb_rs = 1;
+    xb_cs = n;
+  }
+  double* const Yb = y_rows ? L.S : a->Y;
+  const int64_t yb_rs = y_rows ? 1 : a->y_rs, yb_cs = y_rows ? n : a->y_cs;
   // Materialised columns with known strata (a->strata[c]: each row's rank - 1, e.g. the
   // reference LHS stream's decoded shuffles): sort(X[:, c]) by one scatter, certified by its
   // tie / inversion counts (one readback for all of them); an inversion (a ppf not monotone on
@@ -409,7 +430,7 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     bool any = false;
     for (int c = 0; c < k; ++c) {
       if (!a->strata[c]) continue;
-      st = strata_sorted(a->X + (int64_t)c * a->x_cs, a->x_rs, a->strata[c], n, L.sorted_x + (int64_t)c * n,
+      st = strata_sorted(Xb + (int64_t)c * xb_cs, xb_rs, a->strata[c], n, L.sorted_x + (int64_t)c * n,
                          L.counts + 2 * c, s);
       if (st) return st;
       by_strata[c] = any = true;
@@ -422,8 +443,8 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
   for (int c = 0; c < k; ++c) {
     double* S_c = L.S + (int64_t)c * n;
     double* sx_c = L.sorted_x + (int64_t)c * n;
-    const double* x_c = a->X ? a->X + (int64_t)c * a->x_cs : nullptr;
-    int64_t x_stride = a->x_rs;
+    const double* x_c = Xb ? Xb + (int64_t)c * xb_cs : nullptr;
+    int64_t x_stride = xb_rs;
     if (by_strata[c] && scnt[2 * c + 1] == 0) {
       uint32_t* heads = nullptr;
       int64_t nheads = 0;
@@ -661,45 +682,6 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
       st = general(c);  // not flat, not regenerable, or a run of equal codes beyond the finish
       if (st) return st;
     }
-  } else if (!a->columns && step4_mat_enabled(n)) {
-    // materialised columns (X given: the operator API, the reference LHS stream) through the same
-    // MSD code passes, bucket finish and row placement as the generated ones, Y[row] = sort(X)[p]
-    // gathered from the sorted column (place_sorted); a column the finish rejects is redone by the
-    // general path after the one verdict readback
-    Step4Shared sh;
-    step4_gen_carve_shared(L.s4shared, k, sh);
-    Step4Lanes lanes(n, L.s4column, nullptr, s);
-    sync_on_exit.side = sync_on_exit.side || lanes.ns > 1;
-    st = step4_gen_hist(L.codes, n, nullptr, n, n, sh, 0, k, s);
-    if (st) return st;
-    PBH_CHECK_HIP(hipMemcpyAsync(state.data(), sh.state, (size_t)k * 4, hipMemcpyDeviceToHost, s));
-    PBH_CHECK_HIP(hipStreamSynchronize(s));
-    if ((st = lanes.begin())) return st;
-    for (int c = 0; c < k; ++c) {
-      const int i = lanes.next();
-      hipStream_t cs_ = lanes.ss[i];
-      if (state[c]) {
-        st = step4_gen_adapt(L.codes + (int64_t)c * n, n, L.S + (int64_t)c * n, n, n, sh, c, 1, cs_);
-        if (st) return st;
-      }
-      st = step4_gen_column(c, L.codes + (int64_t)c * n, L.S + (int64_t)c * n, n, sh, lanes.cb[i], cs_);
-      if (st) return st;
-      int buf = 0;
-      st = step4_gen_place_passes(c, n, sh, lanes.cb[i], cs_, &buf);
-      if (st) return st;
-      st = place_sorted(L.sorted_x + (int64_t)c * n, lanes.cb[i].pairs[buf], n, a->Y + (int64_t)c * a->y_cs, a->y_rs,
-                        a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, sh.flags + c, cs_);
-      if (st) return st;
-    }
-    if ((st = lanes.join())) return st;
-    std::vector<int32_t> verdict(2 * (size_t)k);
-    PBH_CHECK_HIP(hipMemcpyAsync(verdict.data(), sh.state, 8 * (size_t)k, hipMemcpyDeviceToHost, s));
-    PBH_CHECK_HIP(hipStreamSynchronize(s));
-    for (int c = 0; c < k; ++c) {
-      if (verdict[c] == 0 && verdict[k + c] == 0) continue;
-      st = general(c);
-      if (st) return st;
-    }
   } else {
     // The code histograms of all columns up front, one readback for the bucket-path decisions.
     struct AsyncBuf {  // freed on every return (stream-ordered, before the guard's final sync)
@@ -743,8 +725,8 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
         const int i = lanes.next();
         const uint32_t* hc = hists ? hists + (size_t)c * 1024 : nullptr;
         const int flat = hists ? (code_hist_flat(hists_host.data() + (size_t)c * 1024, n) ? 1 : 0) : 1;
-        st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs,
-                            a->y_rs, a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, lrw[i], lanes.ss[i],
+        st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, Yb + (int64_t)c * yb_cs, yb_rs,
+                            a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, lrw[i], lanes.ss[i],
                             L.codes + (int64_t)c * n, hc, flat, err);
       }
       const int sj = lanes.join();  // s (and the histograms' free on it) after every lane
@@ -763,12 +745,13 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
         if (st) break;
         const uint32_t* hc = hists ? hists + (size_t)c * 1024 : nullptr;
         const int flat = hists ? (code_hist_flat(hists_host.data() + (size_t)c * 1024, n) ? 1 : 0) : 1;
-        st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, a->Y + (int64_t)c * a->y_cs,
-                            a->y_rs, a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n,
+        st = reorder_column(L.S + (int64_t)c * n, n, L.sorted_x + (int64_t)c * n, Yb + (int64_t)c * yb_cs, yb_rs,
+                            a->idx_out ? a->idx_out + (int64_t)c * n : nullptr, rw, s, L.codes + (int64_t)c * n,
                             hc, flat);
       }
     }
     if (st) return st;
+    if (y_rows && (st = columns_to_rows(L.S, n, k, a->Y, a->y_rs, s))) return st;
   }
   if (any_deferred && side && defer >= 2 && !(a->columns && any_regen && step4_gen_enabled(n))) {
     st = check_counts();  // (checked with the step-4 verdicts above on the generated path)

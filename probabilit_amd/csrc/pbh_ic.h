@@ -75,6 +75,10 @@ int resolve_code_runs(const uint32_t* codes, uint32_t* rows, const double* x, in
 
 // dst = src, then dst[p] = src[s + (e - s) / 2] inside every tie run [s, e] flagged by eqprev:
 // the value every member of a tie run receives in step 4 (int of the 'average' rank).
+// out (k x n, column-major) = X (n rows of k values, row stride x_rs >= k), and back: Y[r * y_rs + c] =
+// in[c * n + r] (tiled through LDS; the operator API's row-major X / Y, k <= 128)
+int rows_to_columns(const double* X, int64_t x_rs, int64_t n, int k, double* out, hipStream_t s);
+int columns_to_rows(const double* in, int64_t n, int k, double* Y, int64_t y_rs, hipStream_t s);
 int tie_fix_values(const uint8_t* eqprev, int64_t n, const double* src, double* dst, hipStream_t s);
 
 // out[c] = (sum of column c) / divisor, k columns of length n (column stride ld), fixed order.

@@ -1132,4 +1132,72 @@ int resolve_code_runs(const uint32_t* codes, uint32_t* rows, const double* x, in
   return PBH_OK;
 }
 
+// ---------------------------------------------------------------- row-major <-> column-major
+// The operator API's X and Y are (n, k) row-major (correlation.py:368: numpy C order); every phase
+// reads and writes whole columns.  Read strided, a column costs a 64-byte line per 8-byte value
+// (k_load_keys 2.7 ms per 1e8-row column at k = 32); one tiled transpose of the whole block costs
+// ~2 x 8 n k bytes, once.  A tile of kTRows rows x k columns passes through LDS (row pitch k + 1:
+// conflict-free both ways): rows read contiguously, columns written contiguously.
+constexpr int kTRows = 64;
+
+__global__ __launch_bounds__(256) void k_rows_to_columns(const double* __restrict__ X, int64_t x_rs, int64_t n, int k,
+                                                         double* __restrict__ out) {
+  extern __shared__ double tile[];
+  const int pitch = k + 1;
+  for (int64_t r0 = (int64_t)blockIdx.x * kTRows; r0 < n; r0 += (int64_t)gridDim.x * kTRows) {
+    const int rows = (int)((n - r0) < kTRows ? (n - r0) : kTRows);
+    const int m = rows * k;
+    for (int e = threadIdx.x; e < m; e += 256) {
+      const int r = e / k, c = e - r * k;
+      tile[r * pitch + c] = X[(r0 + r) * x_rs + c];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kTRows * k; e += 256) {
+      const int c = e / kTRows, r = e - c * kTRows;
+      if (r < rows) out[(int64_t)c * n + r0 + r] = tile[r * pitch + c];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_columns_to_rows(const double* __restrict__ in, int64_t n, int k,
+                                                         double* __restrict__ Y, int64_t y_rs) {
+  extern __shared__ double tile[];
+  const int pitch = k + 1;
+  for (int64_t r0 = (int64_t)blockIdx.x * kTRows; r0 < n; r0 += (int64_t)gridDim.x * kTRows) {
+    const int rows = (int)((n - r0) < kTRows ? (n - r0) : kTRows);
+    for (int e = threadIdx.x; e < kTRows * k; e += 256) {
+      const int c = e / kTRows, r = e - c * kTRows;
+      if (r < rows) tile[r * pitch + c] = in[(int64_t)c * n + r0 + r];
+    }
+    __syncthreads();
+    const int m = rows * k;
+    for (int e = threadIdx.x; e < m; e += 256) {
+      const int r = e / k, c = e - r * k;
+      Y[(r0 + r) * y_rs + c] = tile[r * pitch + c];
+    }
+    __syncthreads();
+  }
+}
+
+int rows_to_columns(const double* X, int64_t x_rs, int64_t n, int k, double* out, hipStream_t s) {
+  PBH_REQUIRE(k >= 1 && k <= 128 && x_rs >= k, "rows_to_columns: bad shape");
+  const size_t lds = (size_t)kTRows * (k + 1) * sizeof(double);
+  PBH_TIMED(kKTranspose, s,
+            hipLaunchKernelGGL(k_rows_to_columns, dim3(grid_for(n, kTRows, 8192)), dim3(256), lds, s, X, x_rs, n, k,
+                               out));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
+int columns_to_rows(const double* in, int64_t n, int k, double* Y, int64_t y_rs, hipStream_t s) {
+  PBH_REQUIRE(k >= 1 && k <= 128 && y_rs >= k, "columns_to_rows: bad shape");
+  const size_t lds = (size_t)kTRows * (k + 1) * sizeof(double);
+  PBH_TIMED(kKTranspose, s,
+            hipLaunchKernelGGL(k_columns_to_rows, dim3(grid_for(n, kTRows, 8192)), dim3(256), lds, s, in, n, k, Y,
+                               y_rs));
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
 }  // namespace pbh

@@ -368,9 +368,25 @@ PBH_DI PoissonTable stage_poisson(const PoissonTable& pt, double* lds) {
   return local;
 }
 
+// one atomic per wave: the lanes with sl set append index i to the global list (slow[0] = count)
+__device__ __forceinline__ void append_slow(bool sl, int64_t i, unsigned long long* slow, uint32_t cap) {
+  const uint64_t m = __ballot(sl);
+  if (!m) return;  // wave-uniform
+  const int lane = threadIdx.x & 63, leader = __builtin_ctzll(m);
+  unsigned long long b0 = 0;
+  if (lane == leader) b0 = atomicAdd(&slow[0], (unsigned long long)__popcll(m));
+  b0 = __shfl(b0, leader, 64);
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const unsigned long long k = b0 + (unsigned long long)__popcll(m & below);
+  if (sl && k < cap) slow[1 + k] = (unsigned long long)i;
+}
+
+// The table lookup only (poisson_ppf_fast); the rare lanes -- scipy's windows, outside the table,
+// the deep tail -- go to the slow list for k_ppf_poisson_slow
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_poisson_lds(const double* __restrict__ q, int64_t q_stride,
                                                             int64_t n, Params prm, PoissonTable pt,
-                                                            double* __restrict__ out, int32_t* flag) {
+                                                            double* __restrict__ out, int32_t* flag,
+                                                            unsigned long long* __restrict__ slow, uint32_t cap) {
   extern __shared__ double plds[];
   const PoissonTable T = stage_poisson(pt, plds);
   // 4 items per thread per step, their loads issued together (4 independent chains, as in
@@ -385,13 +401,17 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_poisson_lds(const double
       qv[j] = i < n ? q[i * q_stride] : 0.5;
     }
     double x[kPer];
+    bool ok[kPer];
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) x[j] = ppf_one<PBH_DIST_POISSON>(qv[j], prm.val[0], prm.val[1], prm.val[2], T);
+    for (int j = 0; j < kPer; ++j) ok[j] = poisson_ppf_fast(qv[j], prm.val[0], prm.val[1], T, &x[j]);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int64_t i = b + j * kBlock + threadIdx.x;
-      if (i < n) out[i] = x[j];
-      bad |= i < n && !isfinite(x[j]);
+      if (i < n && ok[j]) {
+        out[i] = x[j];
+        bad |= !isfinite(x[j]);
+      }
+      append_slow(i < n && !ok[j], i, slow, cap);
     }
   }
   flag_nonfinite(flag, bad);
@@ -400,17 +420,29 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_poisson_lds(const double
 __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_poisson_lds(uint64_t seed, int64_t n, int64_t row0,
                                                                 int64_t nrows, uint32_t col, Params prm,
                                                                 PoissonTable pt, double* __restrict__ out,
-                                                                int32_t* flag) {
+                                                                int32_t* flag, unsigned long long* __restrict__ slow,
+                                                                uint32_t cap) {
   extern __shared__ double plds[];
   const PoissonTable T = stage_poisson(pt, plds);
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
-    const double q = lhs_quantile(ph, fp, (uint64_t)(row0 + i), col);
-    const double x = ppf_one<PBH_DIST_POISSON>(q, prm.val[0], prm.val[1], prm.val[2], T);
-    out[i] = x;
-    flag_nonfinite(flag, !isfinite(x));
+  bool bad = false;
+  for (int64_t i0 = (int64_t)blockIdx.x * kBlock; i0 < nrows; i0 += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = i0 + threadIdx.x;
+    const bool valid = i < nrows;
+    double x = 0.0;
+    bool ok = true;
+    if (valid) {
+      const double q = lhs_quantile(ph, fp, (uint64_t)(row0 + i), col);
+      ok = poisson_ppf_fast(q, prm.val[0], prm.val[1], T, &x);
+      if (ok) {
+        out[i] = x;
+        bad |= !isfinite(x);
+      }
+    }
+    append_slow(valid && !ok, i, slow, cap);
   }
+  flag_nonfinite(flag, bad);
 }
 
 // dynamic LDS bytes of the poisson LDS kernels, or 0 when they do not apply
@@ -1167,6 +1199,69 @@ __global__ __launch_bounds__(256) void k_ppf_gamma_slow(const double* __restrict
   flag_nonfinite(flag, bad);
 }
 
+// The poisson sweeps' slow list: ppf_one (poisson_rare included) on the global table for the listed
+// rows, or every row when the list overflowed -- the same function as the table lookup, so the same
+// values.  LHS: the fused native-LHS column (the quantile of row row0 + i regenerated).
+template <bool LHS>
+__global__ __launch_bounds__(256) void k_ppf_poisson_slow(const double* __restrict__ q, int64_t q_stride, int64_t n,
+                                                          GammaLhs lc, Params prm, PoissonTable pt,
+                                                          double* __restrict__ out, int32_t* flag,
+                                                          const unsigned long long* __restrict__ slow, uint32_t cap) {
+  const unsigned long long count = slow[0];
+  if (count == 0) return;
+  const bool all = count > cap;
+  const int64_t m = all ? n : (int64_t)count;
+  Philox ph(lc.seed);
+  FeistelPerm fp(ph, (uint64_t)(LHS ? lc.n : 1), lc.col);
+  bool bad = false;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < m; k += (int64_t)gridDim.x * 256) {
+    const int64_t i = all ? k : (int64_t)slow[1 + k];
+    double qi;
+    if constexpr (LHS)
+      qi = lhs_quantile(ph, fp, (uint64_t)(lc.row0 + i), lc.col);
+    else
+      qi = q[i * q_stride];
+    const double x = ppf_one<PBH_DIST_POISSON>(qi, prm.val[0], prm.val[1], prm.val[2], pt);
+    out[i] = x;
+    bad |= !isfinite(x);
+  }
+  flag_nonfinite(flag, bad);
+}
+
+// The poisson LDS sweep and its slow list (pbh_ppf: q given; pbh_lhs_ppf: lc, the fused LHS)
+int launch_poisson_lds(const double* q, int64_t qs, int64_t n, const GammaLhs* lc, size_t pl, const Params& prm,
+                       const PoissonTable& pt, double* out, int32_t* flag, hipStream_t s) {
+  if (n <= 0) return PBH_OK;
+  const uint32_t cap = (uint32_t)((n >> 10) + 4096 < (1u << 30) ? (n >> 10) + 4096 : (1u << 30));
+  unsigned long long* slow = nullptr;
+  PBH_CHECK_HIP(hipMallocAsync((void**)&slow, ((size_t)cap + 1) * 8, s));
+  struct Free {
+    unsigned long long* p;
+    hipStream_t s;
+    ~Free() { (void)hipFreeAsync(p, s); }  // stream-ordered: after the slow kernel
+  } fr{slow, s};
+  PBH_CHECK_HIP(hipMemsetAsync(slow, 0, 8, s));
+  const GammaLhs l = lc ? *lc : GammaLhs{0, 1, 0, 0};
+  const dim3 b(kBlock);
+  if (lc) {
+    PBH_TIMED(kKLhsPpf, s, {
+      hipLaunchKernelGGL(k_lhs_ppf_poisson_lds, dim3(grid_for(n, kBlock, 256 * 8)), b, pl, s, l.seed, l.n, l.row0, n,
+                         l.col, prm, pt, out, flag, slow, cap);
+      hipLaunchKernelGGL(k_ppf_poisson_slow<true>, dim3(PBH_SLOW_GRID), dim3(256), 0, s, q, qs, n, l, prm, pt, out,
+                         flag, slow, cap);
+    });
+  } else {
+    PBH_TIMED(kKPpf, s, {
+      hipLaunchKernelGGL(k_ppf_poisson_lds, dim3(grid_for(n, kBlock, 256 * 8)), b, pl, s, q, qs, n, prm, pt, out,
+                         flag, slow, cap);
+      hipLaunchKernelGGL(k_ppf_poisson_slow<false>, dim3(PBH_SLOW_GRID), dim3(256), 0, s, q, qs, n, l, prm, pt, out,
+                         flag, slow, cap);
+    });
+  }
+  PBH_CHECK_LAUNCH();
+  return PBH_OK;
+}
+
 // The windowed gamma sweep (pbh_ppf / pbh_lhs_ppf with scalar a, loc, scale): false when it does not
 // apply (PBH_GAMMA_WIN=0, no guide, a window wider than kGWin)
 bool launch_gamma_w(const double* q, int64_t qs, int64_t n, const GammaLhs* lc, const Params& prm,
@@ -1710,12 +1805,7 @@ int launch_ppf(int dist, const double* q, int64_t qs, int64_t n, const Params& p
     PBH_CHECK_LAUNCH();
     return PBH_OK;
   }
-  if (const size_t pl = poisson_lds_bytes(dist, prm, pt)) {
-    PBH_TIMED(kKPpf, s, hipLaunchKernelGGL(k_ppf_poisson_lds, dim3(grid_for(n, kBlock, 256 * 8)), b, pl, s, q, qs,
-                                           n, prm, pt, out, flag));
-    PBH_CHECK_LAUNCH();
-    return PBH_OK;
-  }
+  if (const size_t pl = poisson_lds_bytes(dist, prm, pt)) return launch_poisson_lds(q, qs, n, nullptr, pl, prm, pt, out, flag, s);
   switch (dist) {
 #define PBH_CASE(D) \
   case D:           \
@@ -1757,10 +1847,8 @@ int launch_lhs_ppf(int dist, uint64_t seed, int64_t n, int64_t row0, int64_t nro
     return PBH_OK;
   }
   if (const size_t pl = poisson_lds_bytes(dist, prm, pt)) {
-    PBH_TIMED(kKLhsPpf, s, hipLaunchKernelGGL(k_lhs_ppf_poisson_lds, dim3(grid_for(nrows, kBlock, 256 * 8)), b, pl,
-                                              s, seed, n, row0, nrows, col, prm, pt, out, flag));
-    PBH_CHECK_LAUNCH();
-    return PBH_OK;
+    const GammaLhs lc{seed, n, row0, col};
+    return launch_poisson_lds(nullptr, 0, nrows, &lc, pl, prm, pt, out, flag, s);
   }
   switch (dist) {
 #define PBH_CASE(D) \

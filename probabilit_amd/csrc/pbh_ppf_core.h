@@ -74,10 +74,21 @@ PBH_DI double poisson_from_table(double q, double mu, const PoissonTable& t) {
   while (lo < t.len && t.cdf[lo] < q) ++lo;
   const bool outside = lo == t.len || (lo == 0 && t.k_lo > 0);
   double k = (double)(t.k_lo + lo);
-#ifndef PBH_AB_POISSON_NORARE  // A/B build (timing only): the table's answer everywhere
   if (outside || q < t.win[lo] || q < cdf::kPoissonDeepTail) k = poisson_rare(q, mu, outside ? -1.0 : k);
-#endif
   return k;
+}
+
+// poisson_from_table without poisson_rare: false when the lane needs it (outside the table, inside
+// a window, the deep tail).  The sweep kernels list such lanes for k_ppf_poisson_slow instead of
+// calling it, so no call -- and no stack frame for cdflib's search -- sits in their loop (the call
+// alone took the 1e8-row sweep at mu = 30 from 0.375 to 0.504 ms, profiles/r06/ppf_sweep_ab_r6pa.log).
+PBH_DI bool poisson_table_fast(double q, const PoissonTable& t, double* k) {
+  int64_t lo = t.cdf_guide[(int)(q * (double)(1 << kPoissonGuideBits))];
+  while (lo < t.len && t.cdf[lo] < q) ++lo;
+  const bool outside = lo == t.len || (lo == 0 && t.k_lo > 0);
+  if (outside || q < t.win[lo] || q < cdf::kPoissonDeepTail) return false;
+  *k = (double)(t.k_lo + lo);
+  return true;
 }
 
 // log_tab's table staged in LDS without its padding column (3 KiB): ndtri's tail reads two random
@@ -118,6 +129,24 @@ PBH_DI bool normal_guard(double v, double m, double loc) {
 // for the compacted kernels that know which one an element takes.
 // COLD_GAMMA: igami_guided's fallbacks as a call (see igami_guided)
 // lt: for PART 2, log_tab's table in LDS with entry stride 3 (stage_log3), else the global table
+// ppf_one<PBH_DIST_POISSON> (below) on the table alone: false leaves *x unset and sends the element
+// to the slow list (then ppf_one itself evaluates it: the same value)
+PBH_DI bool poisson_ppf_fast(double q, double mu, double loc, const PoissonTable& t, double* x) {
+  const bool cond0 = (mu >= 0.0) && (loc == loc);
+  if (q == 0.0) {
+    *x = -1.0 + loc;
+  } else if (cond0 && q == 1.0) {
+    *x = kInf + loc;
+  } else if (cond0 && q > 0.0 && q < 1.0) {
+    double k;
+    if (!poisson_table_fast(q, t, &k)) return false;
+    *x = k + loc;
+  } else {
+    *x = kNaN;
+  }
+  return true;
+}
+
 template <int D, int PART = 0, bool COLD_GAMMA = false>
 PBH_DI double ppf_one(double q, double p0, double p1, double p2, const PoissonTable& pt, const double* lt = nullptr) {
   if constexpr (D == PBH_DIST_POISSON) {

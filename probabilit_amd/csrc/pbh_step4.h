@@ -52,9 +52,6 @@ size_t step4_gen_column_bytes(int64_t n);
 void step4_gen_carve_shared(void* ws, int k, Step4Shared& sh);
 void step4_gen_carve_column(void* ws, int64_t n, Step4Column& cb);
 bool step4_gen_enabled(int64_t n);
-// materialised columns (X given) through the same passes, the final placement gathering sort(X)[p]
-// (PBH_STEP4_MAT=msd; the default is the general path, measured faster)
-bool step4_mat_enabled(int64_t n);
 // columns of step 4 run concurrently on this many streams (PBH_STEP4_STREAMS, default 3, at
 // most kStep4MaxStreams), each with its own Step4Column staging, so that one column's VALU- or
 // latency-bound kernels (bucket finish, gen_place) overlap another's bandwidth-bound passes
@@ -131,10 +128,5 @@ int gen_set_runs(GenColumn* g, const uint32_t* heads, int64_t nh, hipStream_t s)
 // assembled in LDS and written contiguously (the owner's step-4 output of a row-sharded run);
 // state (optional device word): skip when non-zero
 int place_positions(const uint64_t* pairs, int64_t n, uint32_t* p_out, const int32_t* state, hipStream_t s);
-// y[row * y_rs] = sorted[p] for every pair (row << 32 | p) of `pairs` grouped by 4096-row block: the
-// final placement of a materialised column (sorted = sort(X[:, c])); idx[row] = p when idx != NULL;
-// state (optional device word): skip when non-zero
-int place_sorted(const double* sorted, const uint64_t* pairs, int64_t n, double* y, int64_t y_rs, int32_t* idx,
-                 const int32_t* state, hipStream_t s);
 
 }  // namespace pbh

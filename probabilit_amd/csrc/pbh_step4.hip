@@ -915,60 +915,7 @@ __global__ __launch_bounds__(256) void k_place_positions(const uint64_t* __restr
   }
 }
 
-// Y[row] = sorted[p] for the pairs (row << 32 | p) of every 4096-row block: the final placement of a
-// MATERIALISED column (X given: the operator API, the reference LHS stream) through the same
-// passes as a generated one -- sort(X)[p] read from the sorted column instead of regenerated.  The
-// reads are a gather (p is random inside a block); the block is assembled in LDS and written out
-// contiguously.  idx (optional): idx[row] = p.
-constexpr int kPSIpt = 8;
-__global__ __launch_bounds__(512) void k_place_sorted(const uint64_t* __restrict__ pairs, int64_t n,
-                                                      const double* __restrict__ sorted, double* __restrict__ y,
-                                                      int64_t y_rs, int32_t* __restrict__ idx,
-                                                      const int32_t* __restrict__ state) {
-  if (state && *state) return;
-  constexpr int kRows = 1 << kGenPlaceShift;
-  __shared__ double buf[kRows];
-  for (int64_t b = blockIdx.x; (b << kGenPlaceShift) < n; b += gridDim.x) {
-    const int64_t r0 = b << kGenPlaceShift;
-    const int cnt = (int)((n - r0) < kRows ? (n - r0) : kRows);
-    uint64_t pa[kPSIpt];
-    double v[kPSIpt];
-#pragma unroll
-    for (int j = 0; j < kPSIpt; ++j) {
-      const int p = j * 512 + threadIdx.x;
-      pa[j] = p < cnt ? pairs[r0 + p] : 0ull;
-    }
-#pragma unroll
-    for (int j = 0; j < kPSIpt; ++j) v[j] = j * 512 + (int)threadIdx.x < cnt ? sorted[(uint32_t)pa[j]] : 0.0;
-#pragma unroll
-    for (int j = 0; j < kPSIpt; ++j) {
-      if (j * 512 + (int)threadIdx.x >= cnt) continue;
-      const int64_t row = (int64_t)(pa[j] >> 32);
-      if (idx) idx[row] = (int32_t)(uint32_t)pa[j];
-      buf[row - r0] = v[j];
-    }
-    __syncthreads();
-    if (y_rs == 1) {
-      for (int p = threadIdx.x; p < cnt; p += 512) y[r0 + p] = buf[p];
-    } else {
-      for (int p = threadIdx.x; p < cnt; p += 512) y[(r0 + p) * y_rs] = buf[p];
-    }
-    __syncthreads();
-  }
-}
-
 }  // namespace
-
-int place_sorted(const double* sorted, const uint64_t* pairs, int64_t n, double* y, int64_t y_rs, int32_t* idx,
-                 const int32_t* state, hipStream_t s) {
-  const int64_t blocks = (n + (1 << kGenPlaceShift) - 1) >> kGenPlaceShift;
-  if (blocks <= 0) return PBH_OK;
-  PBH_TIMED(kKPlaceGen, s,
-            hipLaunchKernelGGL(k_place_sorted, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(512), 0, s,
-                               pairs, n, sorted, y, y_rs, idx, state));
-  PBH_CHECK_LAUNCH();
-  return PBH_OK;
-}
 
 int place_positions(const uint64_t* pairs, int64_t n, uint32_t* p_out, const int32_t* state, hipStream_t s) {
   const int64_t blocks = (n + (1 << kGenPlaceShift) - 1) >> kGenPlaceShift;
@@ -1126,16 +1073,6 @@ bool step4_gen_enabled(int64_t n) {
   return n >= 2 && n < ((int64_t)1 << 32);
 }
 
-// Measured (profiles/r06/ab_step4_mat_r6ab.log): the reference stream at 1e7 x 32 takes 83.9 ms
-// through the MSD passes against 76.1-76.4 through the general path, the operator at 1e8 x 32
-// 679 against 675 ms -- k_place_sorted's gather of sort(X)[p] from a random p costs a 64-byte line
-// per 8-byte value once the column outgrows the caches (6.2 ms per 1e8-row column), what the
-// general path's row placement, carrying the value, does not pay.  So the general path stays the
-// default and PBH_STEP4_MAT=msd selects this one (tests prove both equal).
-bool step4_mat_enabled(int64_t n) {
-  const char* e = getenv("PBH_STEP4_MAT");
-  return e && strcmp(e, "msd") == 0 && step4_gen_enabled(n);
-}
 
 int step4_gen_hist(uint32_t* codes, int64_t ldc, const double* cs, int64_t ldcs, int64_t n, const Step4Shared& sh,
                    int c0, int kk, hipStream_t s) {

@@ -42,6 +42,7 @@ enum KernelId {
   kKPlaceMsd,
   kKPlaceGen,
   kKDag,
+  kKTranspose,
   kKCount
 };
 

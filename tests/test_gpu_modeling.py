@@ -191,7 +191,7 @@ def test_unsupported_distribution_fails_loudly(gpu):
 
     # a scipy name with no device kernel: the message names the supported set
     with pytest.raises(NotImplementedError, match=r"no native inverse-CDF kernel.*'weibull_min'"):
-        Distribution("johnsonsu", a=1.0, b=2.0).sample(10, random_state=0)
+        Distribution("vonmises", kappa=2.0).sample(10, random_state=0)
     with pytest.raises(AttributeError):
         Distribution("no_such_distribution").sample(10, random_state=0)
 
