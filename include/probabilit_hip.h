@@ -118,7 +118,15 @@ typedef enum pbh_dist {
   PBH_DIST_BETAPRIME = 73,    /* a, b     r / (1 - r), r = I^-1(q; a, b); 1 / isf - 1 near r = 1 */
   PBH_DIST_DLAPLACE = 74,     /* a, loc (discrete)   log branches, one step down by its cdf */
   PBH_DIST_PLANCK = 75,       /* lambda, loc (discrete)   ceil(-log1p(-q) / lambda - 1), one step down */
-  PBH_DIST_BOLTZMANN = 76     /* lambda, N, loc (discrete) the truncated planck */
+  PBH_DIST_BOLTZMANN = 76,    /* lambda, N, loc (discrete) the truncated planck */
+  PBH_DIST_PEARSON3 = 77,     /* skew     gammaincinv(alpha, q or 1 - q) / beta + zeta; ndtri for |skew| < 1.6e-5 */
+  PBH_DIST_GENNORM = 78,      /* beta     sign(q - 0.5) gammainccinv(1 / beta, (1 + c) - 2 c q)^(1 / beta) */
+  PBH_DIST_HALFGENNORM = 79,  /* beta     gammaincinv(1 / beta, q)^(1 / beta) */
+  PBH_DIST_WRAPCAUCHY = 80,   /* c        2 atan(val tan(pi q)), or 2 pi - 2 atan(val tan(pi (1 - q))) */
+  PBH_DIST_SKEWCAUCHY = 81,   /* a        tan(pi / (1 -+ a) (q - (1 - a) / 2)) (1 -+ a) */
+  PBH_DIST_MOYAL = 82,        /*          -log(2 erfcinv(q)^2), erfcinv(y) = -ndtri(y / 2) / sqrt(2) */
+  PBH_DIST_KAPPA4 = 83,       /* h, k     the four closed forms of kappa4._ppf */
+  PBH_DIST_CRYSTALBALL = 84   /* beta, m  power-law tail below pbeta, ndtri of the gaussian core above */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

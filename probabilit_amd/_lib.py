@@ -22,7 +22,9 @@ DIST_IDS = {"norm": 0, "uniform": 1, "expon": 2, "lognorm": 3, "triang": 4, "gam
             "halfcauchy": 25, "halflogistic": 26, "halfnorm": 27, "arcsine": 28, "hypsecant": 29, "powerlaw": 30, "genpareto": 31, "fisk": 32, "burr": 33, "burr12": 34, "exponweib": 35, "exponpow": 36, "bradford": 37, "anglit": 38, "levy": 39, "levy_l": 40, "gibrat": 41, "invweibull": 42, "loglaplace": 43, "truncexpon": 44, "chi": 45, "maxwell": 46, "nakagami": 47, "dweibull": 48, "kappa3": 49, "genhalflogistic": 50, "alpha": 51, "fatiguelife": 52, "genlogistic": 53, "trapezoid": 54, "erlang": 5, "geom": 55, "randint": 56, "nbinom": 57, "invgamma": 58, "t": 59,
             "trapz": 54, "johnsonsu": 60, "johnsonsb": 61, "powernorm": 62, "laplace_asymmetric": 63, "mielke": 64,
             "truncpareto": 65, "tukeylambda": 66, "gengamma": 67, "loggamma": 68, "dgamma": 69, "f": 70, "rdist": 71,
-            "semicircular": 72, "betaprime": 73, "dlaplace": 74, "planck": 75, "boltzmann": 76}
+            "semicircular": 72, "betaprime": 73, "dlaplace": 74, "planck": 75, "boltzmann": 76,
+            "pearson3": 77, "gennorm": 78, "halfgennorm": 79, "wrapcauchy": 80, "skewcauchy": 81, "moyal": 82,
+            "kappa4": 83, "crystalball": 84}
 
 # pbh_table_kind
 TABLE_INTERP, TABLE_QUANTILE, TABLE_SEARCH = 0, 1, 2

@@ -234,7 +234,7 @@ void attach_table(int dist, const double* t, Params4& p) {
 
 constexpr bool is_closed(int d) {
   return (d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID) || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T ||
-         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME);
+         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME) || (d >= PBH_DIST_PEARSON3 && d <= PBH_DIST_CRYSTALBALL);
 }
 // discrete distributions beyond binom / bernoulli (round 5): p, loc / low, high, loc / n, p, loc;
 // round 6: a, loc (dlaplace) / lambda, loc (planck) / lambda, N, loc (boltzmann)
@@ -246,7 +246,8 @@ constexpr bool is_discrete2(int d) {
 constexpr int closed_shapes(int d) {
   return (d == PBH_DIST_LOGUNIFORM || d == PBH_DIST_BURR || d == PBH_DIST_BURR12 || d == PBH_DIST_EXPONWEIB ||
           d == PBH_DIST_TRAPEZOID || d == PBH_DIST_JOHNSONSU || d == PBH_DIST_JOHNSONSB || d == PBH_DIST_MIELKE ||
-          d == PBH_DIST_TRUNCPARETO || d == PBH_DIST_GENGAMMA || d == PBH_DIST_F || d == PBH_DIST_BETAPRIME)
+          d == PBH_DIST_TRUNCPARETO || d == PBH_DIST_GENGAMMA || d == PBH_DIST_F || d == PBH_DIST_BETAPRIME ||
+          d == PBH_DIST_KAPPA4 || d == PBH_DIST_CRYSTALBALL)
              ? 2
          : (d == PBH_DIST_WEIBULL_MIN || d == PBH_DIST_WEIBULL_MAX || d == PBH_DIST_PARETO || d == PBH_DIST_LOMAX ||
             d == PBH_DIST_GENEXTREME || d == PBH_DIST_GOMPERTZ || d == PBH_DIST_CHI2 || d == PBH_DIST_POWERLAW ||
@@ -256,7 +257,8 @@ constexpr int closed_shapes(int d) {
             d == PBH_DIST_GENHALFLOGISTIC || d == PBH_DIST_ALPHA || d == PBH_DIST_FATIGUELIFE ||
             d == PBH_DIST_GENLOGISTIC || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T || d == PBH_DIST_POWERNORM ||
             d == PBH_DIST_LAPLACE_ASYMMETRIC || d == PBH_DIST_TUKEYLAMBDA || d == PBH_DIST_LOGGAMMA ||
-            d == PBH_DIST_DGAMMA || d == PBH_DIST_RDIST)
+            d == PBH_DIST_DGAMMA || d == PBH_DIST_RDIST || d == PBH_DIST_PEARSON3 || d == PBH_DIST_GENNORM ||
+            d == PBH_DIST_HALFGENNORM || d == PBH_DIST_WRAPCAUCHY || d == PBH_DIST_SKEWCAUCHY)
              ? 1
              : 0;
 }
@@ -369,6 +371,30 @@ __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo,
     lo = -1.0;
     hi = 1.0;
   }
+  // round 6, second set
+  if constexpr (D == PBH_DIST_PEARSON3) return isfinite(s0);  // _argcheck isfinite(skew)
+  if constexpr (D == PBH_DIST_HALFGENNORM) lo = 0.0;
+  if constexpr (D == PBH_DIST_WRAPCAUCHY) {  // support [0, 2 pi], _argcheck 0 < c < 1
+    lo = 0.0;
+    hi = 2.0 * sf::kPi;
+    return s0 > 0.0 && s0 < 1.0;
+  }
+  if constexpr (D == PBH_DIST_SKEWCAUCHY) return fabs(s0) < 1.0;
+  if constexpr (D == PBH_DIST_KAPPA4) {  // _argcheck always true; kappa4._get_support's six cases
+    const double h = s0, k = s1;
+    if (h > 0.0) {
+      lo = k == 0.0 ? log(h) : (1.0 - pow(h, -k)) / k;  // np.float_power(h, -k)
+      hi = k > 0.0 ? 1.0 / k : inf;
+    } else if (h <= 0.0) {
+      lo = k < 0.0 ? 1.0 / k : -inf;
+      hi = k > 0.0 ? 1.0 / k : inf;
+    } else {  // NaN h: no case applies
+      lo = hi = sf::kNaN;
+    }
+    if (k != k) lo = hi = sf::kNaN;
+    return true;
+  }
+  if constexpr (D == PBH_DIST_CRYSTALBALL) return s1 > 1.0 && s0 > 0.0;  // (m > 1) & (beta > 0)
   if constexpr (closed_shapes(D) == 1) return s0 > 0.0;
   if constexpr (closed_shapes(D) == 2) return s0 > 0.0 && s1 > 0.0;
   return true;
@@ -500,6 +526,54 @@ __device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
     const double r = sfx::beta_ppf01(q, s0, s1);
     if (r > 0.9999) return 1 / sfx::beta_ppf01(1.0 - q, s1, s0) - 1;
     return r / (1 - r);
+  }
+  // round 6, second set
+  if constexpr (D == PBH_DIST_PEARSON3) {  // pearson3._preprocess / _ppf (loc 0, scale 1 inside)
+    if (fabs(s0) < 0.000016) return sf::ndtri(q);  // norm2pearson_transition
+    const double beta = 2.0 / (s0 * 1.0), alpha = (1.0 * beta) * (1.0 * beta), zeta = 0.0 - alpha / beta;
+    const double qq = beta < 0.0 ? 1.0 - q : q;  // negative skew: gh-17050
+    return sf::igami(alpha, qq) / beta + zeta;
+  }
+  if constexpr (D == PBH_DIST_GENNORM) {
+    const double c = q > 0.5 ? 1.0 : (q < 0.5 ? -1.0 : 0.0);  // np.sign(x - 0.5)
+    return c * pow(sf::igamci(1.0 / s0, (1.0 + c) - 2.0 * c * q), 1.0 / s0);
+  }
+  if constexpr (D == PBH_DIST_HALFGENNORM) return pow(sf::igami(1.0 / s0, q), 1.0 / s0);
+  if constexpr (D == PBH_DIST_WRAPCAUCHY) {
+    const double val = (1.0 - s0) / (1.0 + s0);
+    if (q < 1.0 / 2) return 2 * atan(val * tan(sf::kPi * q));
+    return 2 * sf::kPi - 2 * atan(val * tan(sf::kPi * (1 - q)));
+  }
+  if constexpr (D == PBH_DIST_SKEWCAUCHY) {  // i = x < _cdf(0, a) = (1 - a) / 2
+    const double a = s0;
+    if (q < (1 - a) / 2) return tan(sf::kPi / (1 - a) * (q - (1 - a) / 2)) * (1 - a);
+    return tan(sf::kPi / (1 + a) * (q - (1 - a) / 2)) * (1 + a);
+  }
+  if constexpr (D == PBH_DIST_MOYAL) {  // scipy's erfcinv(y) = -ndtri(0.5 y) / sqrt(2) (cephes erfinv.c)
+    const double e = -sf::ndtri(0.5 * q) * 0.7071067811865476;
+    return -log(2 * (e * e));
+  }
+  if constexpr (D == PBH_DIST_KAPPA4) {
+    const double h = s0, k = s1;
+    if (h != 0.0 && k != 0.0) return 1.0 / k * (1.0 - pow((1.0 - pow(q, h)) / h, k));
+    if (h == 0.0 && k != 0.0) return 1.0 / k * (1.0 - pow(-log(q), k));
+    if (h != 0.0 && k == 0.0) return -log1p(-pow(q, h)) + log(h);
+    if (h == 0.0 && k == 0.0) return -log(-log(q));
+    return sf::kNaN;  // _lazyselect's default (a NaN shape)
+  }
+  if constexpr (D == PBH_DIST_CRYSTALBALL) {
+    const double beta = s0, m = s1;
+    constexpr double kNormPdfC = 2.5066282746310002;  // np.sqrt(2 * np.pi)
+    // above pbeta the quantile is ndtri(ndtr(-beta) + (p / N - C) / sqrt(2 pi)), whose argument nears 1
+    // as q does: there an ulp of exp(-beta^2 / 2) (numpy's own SIMD exp in scipy) moves x by ~1e-6
+    const double eb = exp(-beta * beta / 2.0);
+    const double Phi = sf::ndtr(beta);
+    const double N0 = 1.0 / (m / beta / (m - 1) * eb + kNormPdfC * Phi);
+    const double pbeta = N0 * (m / beta) * eb / (m - 1);
+    const double C = (m / beta) * eb / (m - 1);
+    const double N = 1 / (C + kNormPdfC * Phi);
+    if (q < pbeta) return m / beta - beta - pow((m - 1) * pow(m / beta, -m) / eb * q / N, 1 / (1 - m));
+    return sf::ndtri(sf::ndtr(-beta) + (1 / kNormPdfC) * (q / N - C));
   }
   return sf::kNaN;
 }
@@ -746,6 +820,14 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_DLAPLACE)
     PBH_EXT(PBH_DIST_PLANCK)
     PBH_EXT(PBH_DIST_BOLTZMANN)
+    PBH_EXT(PBH_DIST_PEARSON3)
+    PBH_EXT(PBH_DIST_GENNORM)
+    PBH_EXT(PBH_DIST_HALFGENNORM)
+    PBH_EXT(PBH_DIST_WRAPCAUCHY)
+    PBH_EXT(PBH_DIST_SKEWCAUCHY)
+    PBH_EXT(PBH_DIST_MOYAL)
+    PBH_EXT(PBH_DIST_KAPPA4)
+    PBH_EXT(PBH_DIST_CRYSTALBALL)
 #undef PBH_EXT
     default:
       return false;

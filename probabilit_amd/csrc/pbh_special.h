@@ -1063,11 +1063,12 @@ struct GammaGuide {
   double z0, h, inv_h;
 };
 
+template <class M = DevMath>
 PBH_HD inline double ndtr(double a) {
   double x = a * 0.70710678118654752440;
   double z = fabs(x);
-  if (z < 1.0) return 0.5 + 0.5 * erf_(x);
-  double y = 0.5 * erfc_(z);
+  if (z < 1.0) return 0.5 + 0.5 * erf_<M>(x);
+  double y = 0.5 * erfc_<M>(z);
   return x > 0 ? 1.0 - y : y;
 }
 

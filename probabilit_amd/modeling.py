@@ -713,7 +713,9 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "laplace_asymmetric": ("kappa",), "mielke": ("k", "s"), "truncpareto": ("b", "c"),
                 "tukeylambda": ("lam",), "gengamma": ("a", "c"), "loggamma": ("c",), "dgamma": ("a",),
                 "f": ("dfn", "dfd"), "rdist": ("c",), "semicircular": (), "betaprime": ("a", "b"),
-                "dlaplace": ("a",), "planck": ("lambda_",), "boltzmann": ("lambda_", "N")}
+                "dlaplace": ("a",), "planck": ("lambda_",), "boltzmann": ("lambda_", "N"),
+                "pearson3": ("skew",), "gennorm": ("beta",), "halfgennorm": ("beta",), "wrapcauchy": ("c",),
+                "skewcauchy": ("a",), "moyal": (), "kappa4": ("h", "k"), "crystalball": ("beta", "m")}
 _DISCRETE = {"poisson", "binom", "bernoulli", "geom", "randint", "nbinom", "dlaplace", "planck", "boltzmann"}
 # distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so
 # that Iman-Conover takes them as generated columns (pbh_ppf.hip k_lhs_sorted_ppf / k_place_gen;

@@ -1,6 +1,6 @@
 """Timing of the reference LHS stream (stream="reference") at n x d: the device decode's wall
 time per call, its attempts and ambiguous-draw count, against the host shuffles.
-python tools/ref_lhs_time.py [n] [d] [reps]"""
+python tools/ref_lhs_time.py [n] [d] [reps] [variant]"""
 import ctypes
 import json
 import sys
@@ -15,6 +15,9 @@ from probabilit_amd import _lib, device, qmc  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+if len(sys.argv) > 4 and sys.argv[4] != "default":  # a library variant (build.py --variant) for A/B runs
+    import os
+    _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), f"libprobabilit_hip_{sys.argv[4]}.so")
 dev = device.device()
 lib = _lib.load()
 
