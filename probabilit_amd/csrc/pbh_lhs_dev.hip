@@ -12,9 +12,8 @@
 //             deviations (closed forms over each mask range, band_table).  A draw whose
 //             decision is the same for every state of the band is decided; the rest
 //             (~1e-3 of the bulk, the whole column tail) are "ambiguous"
-//   walk      the ambiguous draws, in order, by one wave on the device (k_dec_walk, since round 6;
-//             the host walked them before): state = decided accepts before the draw + ambiguous
-//             accepts so far (~3e5 per column at n = 1e7), no host round trip between columns
+//   walk      the ambiguous draws, in order, on the host: state = decided accepts before the
+//             draw + ambiguous accepts so far (a few 10^4 per column at n = 1e7)
 //   finish    every decision re-checked against the rule at the state its prefix implies
 //             (one block scan): all agree <=> the decode is the sequential one, by induction.
 //             The accepted draws give the swap targets j_i; the column's last accept gives
@@ -285,66 +284,6 @@ __global__ __launch_bounds__(kT) void k_dec_compact(DecParams pr, const double2*
   }
 }
 
-// The walk on the device: one wave takes the ambiguous draws 64 at a time, in order.  Inside a
-// chunk, draw k's decision depends on the chunk's entering state plus the accepts of draws 0 .. k-1
-// of the chunk; the wave iterates decisions -> prefix counts (ballot, popcount) -> decisions until
-// nothing changes.  The system is triangular (lane 0 is exact after one round, lane k after k + 1),
-// so the fixed point is unique and is the sequential walk's; a chunk needs a few rounds, as only
-// the draws whose threshold lies within 64 of the state can change.  Chunks are loaded kWB at a
-// time, the next batch in flight while this one is walked.  count > cap (the list was cut short):
-// err bit 8, the attempt fails and is retried / handed to the host.
-constexpr int kWB = 16;
-__device__ __forceinline__ bool walk_decide(uint2 e, uint32_t cur, int64_t N1) {
-  const uint32_t x = e.x;
-  if (!(x >> 31)) return cur < x;
-  const int64_t S = (int64_t)(x & 0x7FFFFFFFu) + cur;
-  const uint32_t i = S < N1 ? (uint32_t)(N1 - S) : 0u;
-  return S < N1 && (e.y & mask_of(i)) <= i;
-}
-
-__global__ __launch_bounds__(64) void k_dec_walk(const uint2* __restrict__ list, const uint32_t* __restrict__ count,
-                                                 int64_t cap, int64_t N1, uint8_t* __restrict__ dec,
-                                                 unsigned long long* __restrict__ total, int32_t* __restrict__ err) {
-  const int lane = threadIdx.x;
-  const int64_t namb = *count;
-  if (lane == 0) atomicAdd(total, (unsigned long long)namb);
-  if (namb > cap) {
-    if (lane == 0) atomicOr(err, 8);
-    return;
-  }
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  uint2 cur[kWB], nxt[kWB];
-#pragma unroll
-  for (int j = 0; j < kWB; ++j) {
-    const int64_t k = (int64_t)j * 64 + lane;
-    cur[j] = k < namb ? list[k] : make_uint2(0u, 0u);
-  }
-  uint32_t extra = 0;
-  for (int64_t base = 0; base < namb; base += kWB * 64) {
-#pragma unroll
-    for (int j = 0; j < kWB; ++j) {
-      const int64_t k = base + (int64_t)(kWB + j) * 64 + lane;
-      nxt[j] = k < namb ? list[k] : make_uint2(0u, 0u);
-    }
-#pragma unroll
-    for (int j = 0; j < kWB; ++j) {
-      const int64_t k = base + (int64_t)j * 64 + lane;
-      const bool valid = k < namb;
-      uint64_t acc = 0, prev;
-      bool a;
-      do {
-        prev = acc;
-        a = valid && walk_decide(cur[j], extra + (uint32_t)__popcll(acc & lt), N1);
-        acc = __ballot(a);
-      } while (acc != prev);
-      if (valid) dec[k] = (uint8_t)a;
-      extra += (uint32_t)__popcll(acc);
-    }
-#pragma unroll
-    for (int j = 0; j < kWB; ++j) cur[j] = nxt[j];
-  }
-}
-
 // per-draw accept flags: the decided ones and the walk's
 __device__ __forceinline__ uint32_t accept_flags(const uint8_t* c, const uint32_t* pre, const uint8_t* dec,
                                                  int64_t nb, uint32_t* sh) {
@@ -559,6 +498,32 @@ int64_t band_table(int64_t n, double ksig, std::vector<double>& band) {
   return tcap;
 }
 
+// pinned staging of the ambiguous draws and their decisions (kept across calls)
+struct Pinned {
+  std::mutex mu;
+  uint2* list = nullptr;
+  uint8_t* dec = nullptr;
+  uint32_t* cnt = nullptr;  // the column's ambiguous count
+  int64_t cap = 0;
+  int ensure(int64_t want) {
+    if (!cnt) PBH_CHECK_HIP(hipHostMalloc((void**)&cnt, 64, hipHostMallocDefault));
+    if (want <= cap) return PBH_OK;
+    if (list) (void)hipHostFree(list);
+    if (dec) (void)hipHostFree(dec);
+    list = nullptr;
+    dec = nullptr;
+    cap = 0;
+    PBH_CHECK_HIP(hipHostMalloc((void**)&list, (size_t)want * sizeof(uint2), hipHostMallocDefault));
+    PBH_CHECK_HIP(hipHostMalloc((void**)&dec, (size_t)want, hipHostMallocDefault));
+    cap = want;
+    return PBH_OK;
+  }
+};
+Pinned& pinned() {
+  static Pinned p;
+  return p;
+}
+
 struct DevBufs {
   hipStream_t s;
   std::vector<void*> v;
@@ -646,7 +611,6 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
   double2* band_dev;
   int64_t* P;
   int32_t *err, *okc;
-  unsigned long long* amb_total;
   u128* pcg_ws;
   PermBufs pb;
   char* sort_ws;
@@ -655,7 +619,6 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
       (st = b.get(&pre, 2 * (pr.nb + 1))) || (st = b.get(&tot2, pr.nb)) || (st = b.get(&pre2, pr.nb + 1)) ||
       (st = b.get(&list, cap)) || (st = b.get(&dec, cap)) || (st = b.get(&band_dev, pr.nband)) ||
       (st = b.get(&P, d + 1)) || (st = b.get(&err, 1)) || (st = b.get(&okc, d)) || (st = b.get(&pcg_ws, 128)) ||
-      (st = b.get(&amb_total, 1)) ||
       (st = b.get(&pb.S, n)) || (st = b.get(&pb.M, n)) ||
       (st = b.get(&sort_ws, sort_workspace_bytes(n))))
     return st;
@@ -670,6 +633,9 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
       if (e) (void)hipEventDestroy(e);
     }
   } evfree{ev};
+  Pinned& pn = pinned();
+  std::lock_guard<std::mutex> lock(pn.mu);
+  if ((st = pn.ensure(std::max<int64_t>(cap, 1 << 16)))) return st;
   // u = rng.uniform(size=(n, d)), draws 0 .. n d - 1 (rewritten by every attempt)
   if ((st = pbh_pcg64_random(state_host, inc_host, 0, n, d, q, ldq, pcg_ws, 128 * sizeof(u128), s))) return st;
   std::vector<int64_t> p_init(d + 1, -1);
@@ -677,8 +643,8 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
   PBH_CHECK_HIP(hipMemcpyAsync(band_dev, band.data(), band.size() * sizeof(double), hipMemcpyHostToDevice, s));
   PBH_CHECK_HIP(hipMemcpyAsync(P, p_init.data(), (d + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   PBH_CHECK_HIP(hipMemsetAsync(err, 0, sizeof(int32_t), s));
-  PBH_CHECK_HIP(hipMemsetAsync(amb_total, 0, sizeof(unsigned long long), s));
   const unsigned nb = (unsigned)pr.nb;
+  int64_t namb_total = 0, last_namb = 0;
   for (int c = 0; c < d; ++c) {
     int32_t* Jc = J + (int64_t)c * n;
     hipLaunchKernelGGL(k_dec_classify, dim3(nb), dim3(kT), 0, s, pr, jt_dev, band_dev, P, c, W, cls, tot, err);
@@ -687,8 +653,48 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
     PBH_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_dec_compact, dim3(nb), dim3(kT), 0, s, pr, band_dev, W, cls, pre, list, cap);
     PBH_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_dec_walk, dim3(1), dim3(64), 0, s, list, pre + 2 * pr.nb + 1, cap, N1, dec, amb_total, err);
-    PBH_CHECK_LAUNCH();
+    // the count and, speculatively, the list up to a little above the previous column's count, in
+    // one round trip (columns differ by a few percent); the rest, if any, in a second
+#ifdef PBH_AB_NO_SPEC  // A/B build: the count first, then the list (two round trips)
+    const int64_t guess = 0;
+    last_namb = 0;
+#else
+    const int64_t guess = std::min<int64_t>(cap, last_namb + last_namb / 16 + 1024);
+#endif
+    PBH_CHECK_HIP(hipMemcpyAsync(pn.cnt, pre + 2 * pr.nb + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (last_namb)
+      PBH_CHECK_HIP(hipMemcpyAsync(pn.list, list, (size_t)guess * sizeof(uint2), hipMemcpyDeviceToHost, s));
+    PBH_CHECK_HIP(hipStreamSynchronize(s));
+    const uint32_t namb = *pn.cnt;
+    if ((int64_t)namb > cap) return PBH_OK;  // too many to walk: the host shuffles
+    namb_total += namb;
+    const int64_t have = last_namb ? guess : 0;
+    last_namb = namb;
+    if (namb) {
+      if ((int64_t)namb > have) {
+        PBH_CHECK_HIP(hipMemcpyAsync(pn.list + have, list + have, (size_t)(namb - have) * sizeof(uint2),
+                                     hipMemcpyDeviceToHost, s));
+        PBH_CHECK_HIP(hipStreamSynchronize(s));
+      }
+      // the walk (k_dec_compact's encoding); decisions past the column's end are never read
+      uint32_t extra = 0;
+      const uint2* L = pn.list;
+      uint8_t* D = pn.dec;
+      for (uint32_t k = 0; k < namb; ++k) {
+        const uint32_t x = L[k].x;
+        uint32_t a;
+        if (!(x >> 31)) {
+          a = extra < x;
+        } else {
+          const int64_t S = (int64_t)(x & 0x7FFFFFFFu) + extra;
+          const uint32_t i = S < N1 ? (uint32_t)(N1 - S) : 0u;
+          a = S < N1 && (L[k].y & mask_of(i)) <= i;
+        }
+        D[k] = (uint8_t)a;
+        extra += a;
+      }
+      PBH_CHECK_HIP(hipMemcpyAsync(dec, pn.dec, namb, hipMemcpyHostToDevice, s));
+    }
     hipLaunchKernelGGL(k_dec_accsum, dim3(nb), dim3(kT), 0, s, pr, cls, pre, dec, tot2);
     PBH_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, tot2, pr.nb, pr.nb, pre2, pr.nb + 1);
@@ -711,12 +717,10 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
   }
   int64_t tail = -1;
   int32_t e = 0;
-  unsigned long long namb_total = 0;
   PBH_CHECK_HIP(hipMemcpyAsync(&tail, P + d, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   PBH_CHECK_HIP(hipMemcpyAsync(&e, err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  PBH_CHECK_HIP(hipMemcpyAsync(&namb_total, amb_total, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));
-  *ambiguous = (int64_t)namb_total;
+  *ambiguous = namb_total;
   *ok = e == 0 && tail >= 0;
   return PBH_OK;
 }
