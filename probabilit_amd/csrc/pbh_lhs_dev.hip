@@ -503,10 +503,8 @@ struct Pinned {
   std::mutex mu;
   uint2* list = nullptr;
   uint8_t* dec = nullptr;
-  uint32_t* cnt = nullptr;  // the column's ambiguous count
   int64_t cap = 0;
   int ensure(int64_t want) {
-    if (!cnt) PBH_CHECK_HIP(hipHostMalloc((void**)&cnt, 64, hipHostMallocDefault));
     if (want <= cap) return PBH_OK;
     if (list) (void)hipHostFree(list);
     if (dec) (void)hipHostFree(dec);
@@ -644,7 +642,7 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
   PBH_CHECK_HIP(hipMemcpyAsync(P, p_init.data(), (d + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   PBH_CHECK_HIP(hipMemsetAsync(err, 0, sizeof(int32_t), s));
   const unsigned nb = (unsigned)pr.nb;
-  int64_t namb_total = 0, last_namb = 0;
+  int64_t namb_total = 0;
   for (int c = 0; c < d; ++c) {
     int32_t* Jc = J + (int64_t)c * n;
     hipLaunchKernelGGL(k_dec_classify, dim3(nb), dim3(kT), 0, s, pr, jt_dev, band_dev, P, c, W, cls, tot, err);
@@ -653,29 +651,15 @@ int decode_attempt(const DecParams& base, const uint64_t* state_host, const uint
     PBH_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_dec_compact, dim3(nb), dim3(kT), 0, s, pr, band_dev, W, cls, pre, list, cap);
     PBH_CHECK_LAUNCH();
-    // the count and, speculatively, the list up to a little above the previous column's count, in
-    // one round trip (columns differ by a few percent); the rest, if any, in a second
-#ifdef PBH_AB_NO_SPEC  // A/B build: the count first, then the list (two round trips)
-    const int64_t guess = 0;
-    last_namb = 0;
-#else
-    const int64_t guess = std::min<int64_t>(cap, last_namb + last_namb / 16 + 1024);
-#endif
-    PBH_CHECK_HIP(hipMemcpyAsync(pn.cnt, pre + 2 * pr.nb + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    if (last_namb)
-      PBH_CHECK_HIP(hipMemcpyAsync(pn.list, list, (size_t)guess * sizeof(uint2), hipMemcpyDeviceToHost, s));
+    uint32_t namb = 0;
+    PBH_CHECK_HIP(hipMemcpyAsync(pn.list, pre + 2 * pr.nb + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     PBH_CHECK_HIP(hipStreamSynchronize(s));
-    const uint32_t namb = *pn.cnt;
+    memcpy(&namb, pn.list, sizeof(uint32_t));
     if ((int64_t)namb > cap) return PBH_OK;  // too many to walk: the host shuffles
     namb_total += namb;
-    const int64_t have = last_namb ? guess : 0;
-    last_namb = namb;
     if (namb) {
-      if ((int64_t)namb > have) {
-        PBH_CHECK_HIP(hipMemcpyAsync(pn.list + have, list + have, (size_t)(namb - have) * sizeof(uint2),
-                                     hipMemcpyDeviceToHost, s));
-        PBH_CHECK_HIP(hipStreamSynchronize(s));
-      }
+      PBH_CHECK_HIP(hipMemcpyAsync(pn.list, list, (size_t)namb * sizeof(uint2), hipMemcpyDeviceToHost, s));
+      PBH_CHECK_HIP(hipStreamSynchronize(s));
       // the walk (k_dec_compact's encoding); decisions past the column's end are never read
       uint32_t extra = 0;
       const uint2* L = pn.list;
