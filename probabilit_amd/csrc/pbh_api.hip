@@ -440,6 +440,13 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
       PBH_CHECK_HIP(hipStreamSynchronize(s));
     }
   }
+  // step 1's scores of a sorted column through the row placement rather than a random scatter
+  // (PBH_SCORES_PLACE=0: the scatter, the comparator), where the placement passes pay: n >= 2^22
+  static const bool scores_place_on = [] {
+    const char* e = getenv("PBH_SCORES_PLACE");
+    return !(e && e[0] == '0');
+  }();
+  const bool scores_placed = scores_place_on && n >= ((int64_t)1 << 22);
   for (int c = 0; c < k; ++c) {
     double* S_c = L.S + (int64_t)c * n;
     double* sx_c = L.sorted_x + (int64_t)c * n;
@@ -505,9 +512,29 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     st = radix_sort_keys(sb, n, s, &buf);
     if (st) return st;
     RankOut out = {};
-    out.scores = S_c;
     out.sorted_x = sx_c;
-    st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+    if (scores_placed) {
+      // the scores in rank order (contiguous), then into row order by the row placement (LSD
+      // passes on the row, 8192-row blocks assembled in LDS): a random 8-byte scatter cost the
+      // rank finish ~4.8x its bytes in HBM writes at 1e8 rows (pmc_traffic_r6p.json)
+      out.scores = L.tmp;
+      st = rank_finish(kModeScoresRank, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+      if (st) return st;
+      PlaceBuffers pb;  // input rows: sb.vals[buf]; pass 1 -> [0], pass 2 -> [1] (the keys are dead)
+      pb.rows[0] = sb.vals[buf ^ 1];
+      pb.vals[0] = (double*)sb.keys[buf ^ 1];
+      pb.rows[1] = sb.vals[buf];
+      pb.vals[1] = (double*)sb.keys[buf];
+      pb.counts = sb.counts;
+      pb.partials = sb.partials;
+      pb.status = sb.status;
+      pb.sweep = &sb.sweep;
+      pb.bases = sb.bases;
+      st = place_by_row(sb.vals[buf], L.tmp, n, S_c, 1, pb, s);
+    } else {
+      out.scores = S_c;
+      st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+    }
     if (st) return st;
     have_sx[c] = 1;
   }

@@ -6,7 +6,9 @@
 
 namespace pbh {
 
-enum RankMode { kModeScores = 0, kModeGather = 1, kModeRanks = 2 };
+// kModeScoresRank: kModeScores with the scores written in rank order, scores[i] for sorted position
+// i (contiguous), for the row placement to put in row order (ic_run's step 1 at large n)
+enum RankMode { kModeScores = 0, kModeGather = 1, kModeRanks = 2, kModeScoresRank = 3 };
 
 struct RankOut {
   // kModeScores: S[row] = ndtri(avg / (n + 1)); sorted_x[i] = value at sorted position i

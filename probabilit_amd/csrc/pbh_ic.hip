@@ -215,6 +215,9 @@ __global__ __launch_bounds__(T) void k_rank_finish(const uint64_t* __restrict__ 
     uint32_t row = sr[pad(p)];
     if constexpr (MODE == kModeScores) {
       out.scores[row] = sf::ppnd16(avg / np1);  // the scores of k_perm_scores (sf::ppnd16)
+    } else if constexpr (MODE == kModeScoresRank) {
+      out.scores[g] = sf::ppnd16(avg / np1);
+      (void)row;
     } else if constexpr (MODE == kModeGather) {
       int64_t idx = (int64_t)avg - 1;
       out.y[(int64_t)row * out.y_rs] = out.sorted_src[idx];
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(T) void k_rank_finish(const uint64_t* __restrict__ 
       out.ranks[row] = avg;
     }
   }
-  if constexpr (MODE == kModeScores) {
+  if constexpr (MODE == kModeScores || MODE == kModeScoresRank) {
     if (out.sorted_x) {
 #pragma unroll
       for (int j = 0; j < IPT; ++j) {
@@ -793,6 +796,11 @@ int rank_finish(int mode, const uint64_t* keys, const uint32_t* rows, int64_t n,
       PBH_TIMED(kKRankScores, s,
                 hipLaunchKernelGGL(k_rank_finish<kModeScores>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, eqprev, n,
                                    tb.prev_head, tb.next_head, out));
+      break;
+    case kModeScoresRank:
+      PBH_TIMED(kKRankScores, s,
+                hipLaunchKernelGGL(k_rank_finish<kModeScoresRank>, dim3((unsigned)nt), dim3(T), 0, s, keys, rows, eqprev,
+                                   n, tb.prev_head, tb.next_head, out));
       break;
     case kModeGather:
       PBH_TIMED(kKRankGather, s,
