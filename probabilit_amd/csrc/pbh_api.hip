@@ -509,8 +509,13 @@ int ic_run(const pbh_ic_args* a, void* stream, int defer) {
     st = load_keys(x_c, x_stride, n, sb.keys[0], L.flag, s);
     if (st) return st;
     int buf = 0;
-    st = radix_sort_keys(sb, n, s, &buf);
+    bool redo = false;
+    st = scores_placed ? radix_sort_keys_top48(sb, n, s, &buf, &redo) : radix_sort_keys(sb, n, s, &buf);
     if (st) return st;
+    if (redo) {  // a long run of keys equal in their top 48 bits: every byte after all
+      if ((st = load_keys(x_c, x_stride, n, sb.keys[0], L.flag, s))) return st;
+      if ((st = radix_sort_keys(sb, n, s, &buf))) return st;
+    }
     RankOut out = {};
     out.sorted_x = sx_c;
     if (scores_placed) {

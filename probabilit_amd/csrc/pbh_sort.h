@@ -51,6 +51,11 @@ void sort_carve(void* ws, int64_t n, SortBuffers& b);
 // the buffer holding the sorted keys / payload.  `stream` ordered; synchronises once to read
 // the digit histogram (pass skipping).  Returns < 0 and sets the last error on failure.
 int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf);
+// The same over bytes 2..7 only, then each run of keys equal in their top 48 bits ordered by the
+// whole key: the same result with two passes fewer when the low bytes vary.  *redo: a run was
+// longer than the fix-up takes (the keys are left partly ordered: load them again and sort with
+// radix_sort_keys).  Synchronises once more than radix_sort_keys.
+int radix_sort_keys_top48(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, bool* redo);
 // In-place exclusive scan of m uint32 counts (partials: scan_partials_count(m) entries).
 int exclusive_scan_u32(uint32_t* a, int64_t m, uint32_t* partials, hipStream_t s);
 // The same on uint32 keys stored in b.keys[0] (reinterpreted), or read from `in` (left

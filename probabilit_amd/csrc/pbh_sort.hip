@@ -878,7 +878,8 @@ void sort_carve(void* ws, int64_t n, SortBuffers& sb) {
 }
 
 template <typename K>
-int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, const K* in = nullptr) {
+int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, const K* in = nullptr,
+                    int skip_low = 0, bool* low_varies = nullptr) {
   constexpr int NB = sizeof(K);
   PBH_REQUIRE(n >= 1 && n < ((int64_t)1 << 32), "radix sort: n out of range");
   const int64_t nt = sort_tiles(n);
@@ -892,9 +893,14 @@ int radix_sort_impl(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, cons
   PBH_CHECK_HIP(hipMemcpyAsync(b.hist_host, b.hist, NB * 256 * 4, hipMemcpyDeviceToHost, s));
   PBH_CHECK_HIP(hipStreamSynchronize(s));
   int passes[8], npass = 0;
+  if (low_varies) *low_varies = false;
   for (int p = 0; p < NB; ++p) {
     int nonzero = 0;
     for (int d = 0; d < 256; ++d) nonzero += b.hist_host[p * 256 + d] != 0;
+    if (nonzero > 1 && p < skip_low) {
+      *low_varies = true;  // left to the caller's fix-up
+      continue;
+    }
     if (nonzero > 1) passes[npass++] = p;
   }
   if (npass == 0) passes[npass++] = 0;  // all keys equal: one pass yields the identity payload
@@ -950,6 +956,57 @@ int radix_sort_keys32_async(SortBuffers& b, int64_t n, int npass, hipStream_t s,
 
 int radix_sort_keys(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf) {
   return radix_sort_impl<uint64_t>(b, n, s, out_buf);
+}
+
+namespace {
+// After the passes over bytes 2..7 only: keys equal in their top 48 bits form runs still in row
+// order; the head of each run orders it by the whole key (insertion sort, rows along).  Runs are
+// rare and short for continuous data (48 bits resolve 2^-36 of a binade); a run longer than
+// kFixCap sets *long_run and the caller sorts the column again with every byte.
+constexpr int64_t kFixCap = 64;
+__global__ __launch_bounds__(256) void k_fix_low16(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                   int64_t n, uint32_t* __restrict__ long_run) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint64_t hk = keys[i] >> 16;
+    if (i > 0 && (keys[i - 1] >> 16) == hk) continue;   // not a run head
+    if (i + 1 >= n || (keys[i + 1] >> 16) != hk) continue;  // alone in its top 48 bits
+    int64_t j = i + 1;
+    while (j < n && (keys[j] >> 16) == hk && j - i <= kFixCap) ++j;
+    if (j - i > kFixCap) {
+      atomicOr(long_run, 1u);
+      continue;
+    }
+    for (int64_t a = i + 1; a < j; ++a) {  // stable insertion sort by the whole key
+      const uint64_t k = keys[a];
+      const uint32_t v = vals[a];
+      int64_t b = a;
+      while (b > i && keys[b - 1] > k) {
+        keys[b] = keys[b - 1];
+        vals[b] = vals[b - 1];
+        --b;
+      }
+      keys[b] = k;
+      vals[b] = v;
+    }
+  }
+}
+}  // namespace
+
+int radix_sort_keys_top48(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, bool* redo) {
+  *redo = false;
+  bool low = false;
+  int st = radix_sort_impl<uint64_t>(b, n, s, out_buf, nullptr, 2, &low);
+  if (st || !low) return st;
+  uint32_t* flag = (uint32_t*)b.hist;  // the histogram is read back already; one word of it
+  PBH_CHECK_HIP(hipMemsetAsync(flag, 0, 4, s));
+  hipLaunchKernelGGL(k_fix_low16, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, b.keys[*out_buf],
+                     b.vals[*out_buf], n, flag);
+  PBH_CHECK_LAUNCH();
+  uint32_t h = 0;
+  PBH_CHECK_HIP(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, s));
+  PBH_CHECK_HIP(hipStreamSynchronize(s));
+  *redo = h != 0;
+  return PBH_OK;
 }
 
 int radix_sort_keys32(SortBuffers& b, int64_t n, hipStream_t s, int* out_buf, const uint32_t* in) {
