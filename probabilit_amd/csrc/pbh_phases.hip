@@ -367,12 +367,37 @@ extern "C" int pbh_ic_column_scores(const double* x, int64_t stride, int64_t n, 
   int st = load_keys(x, stride, n, sb.keys[0], nonfinite_flag, s);
   if (st) return st;
   int buf = 0;
-  st = radix_sort_keys(sb, n, s, &buf);
+  // n >= 2^22: as pbh_iman_conover's step 1 (pbh_api.hip) -- the top 48 key bits sorted and the
+  // runs of equal top bits fixed up, the scores in rank order put in row order by the placement
+  const bool large = n >= ((int64_t)1 << 22);
+  bool redo = false;
+  st = large ? radix_sort_keys_top48(sb, n, s, &buf, &redo) : radix_sort_keys(sb, n, s, &buf);
   if (st) return st;
+  if (redo) {
+    if ((st = load_keys(x, stride, n, sb.keys[0], nonfinite_flag, s))) return st;
+    if ((st = radix_sort_keys(sb, n, s, &buf))) return st;
+  }
   RankOut out = {};
-  out.scores = scores;
   out.sorted_x = sorted_x;
-  st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+  if (large) {
+    double* ranked = (double*)sb.keys[buf ^ 1];  // free after the sort
+    out.scores = ranked;
+    if ((st = rank_finish(kModeScoresRank, sb.keys[buf], sb.vals[buf], n, tb, out, s))) return st;
+    PlaceBuffers pb;  // pass 1 reads (vals[buf], ranked) -> [0]; pass 2 -> [1]: both inputs consumed
+    pb.rows[0] = sb.vals[buf ^ 1];
+    pb.vals[0] = (double*)sb.keys[buf];
+    pb.rows[1] = sb.vals[buf];
+    pb.vals[1] = ranked;
+    pb.counts = sb.counts;
+    pb.partials = sb.partials;
+    pb.status = sb.status;
+    pb.sweep = &sb.sweep;
+    pb.bases = sb.bases;
+    st = place_by_row(sb.vals[buf], ranked, n, scores, 1, pb, s);
+  } else {
+    out.scores = scores;
+    st = rank_finish(kModeScores, sb.keys[buf], sb.vals[buf], n, tb, out, s);
+  }
   if (st) return st;
   PBH_CHECK_HIP(hipStreamSynchronize(s));  // hist_host is read by the sort's copies
   return PBH_OK;

@@ -20,10 +20,24 @@ __global__ __launch_bounds__(256) void k_digit_hist(const K* __restrict__ keys, 
   __shared__ uint32_t h[NB][256];
   for (int i = threadIdx.x; i < NB * 256; i += 256) (&h[0][0])[i] = 0;
   __syncthreads();
+  // A byte every lane of the wave shares (the sign / exponent bytes of data within a binade) is
+  // counted by one atomic of the wave's count instead of 64 atomics on one LDS word, which the LDS
+  // serialises (k_digit_hist<u64> took 0.91 ms per 1e8 keys, 0.88 TB/s, pmc_valu_r6v.json).
+  const int lane = threadIdx.x & 63;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     K k = keys[i];
+    const uint64_t active = __ballot(true);
+    const int leader = __builtin_ctzll(active);
 #pragma unroll
-    for (int p = 0; p < NB; ++p) atomicAdd(&h[p][(k >> (8 * p)) & 255u], 1u);
+    for (int p = 0; p < NB; ++p) {
+      const uint32_t d = (uint32_t)(k >> (8 * p)) & 255u;
+      const uint32_t d0 = (uint32_t)__shfl((int)d, leader, 64);
+      if (__ballot(d == d0) == active) {
+        if (lane == leader) atomicAdd(&h[p][d0], (uint32_t)__popcll(active));
+      } else {
+        atomicAdd(&h[p][d], 1u);
+      }
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < NB * 256; i += 256) {

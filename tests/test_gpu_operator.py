@@ -56,3 +56,29 @@ def test_operator_large_n_paths_bit_exact(gpu):
                                text=True, timeout=600, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
             assert p.returncode == 0, p.stderr[-2000:]
             np.testing.assert_array_equal(np.load(out), Y)
+
+
+def test_column_scores_large_n(gpu):
+    """pbh_ic_column_scores (the row-sharded operator's step 1 on an owned column) at n >= 2^22:
+    the scores within the van der Waerden gate of the oracle's (ndtri of rankdata / (n + 1)), the
+    sorted column exact, for the same columns (a run that takes the redo, short runs, integers)."""
+    import torch
+
+    from oracle import ic as oic
+    from oracle.pipeline import cfg3_corr
+    from probabilit_amd import device
+    from probabilit_amd.distributed import HipPhases
+
+    n = (1 << 22) + 3
+    X = _design(n)
+    ref = oic.iman_conover(X, cfg3_corr(4))["S"]
+    ph = HipPhases()
+    for c in range(X.shape[1]):
+        x = device.to_device(np.ascontiguousarray(X[:, c]))
+        s = torch.empty_like(x)
+        sx = torch.empty_like(x)
+        flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+        ph.column_scores(x, s, sx, flag)
+        np.testing.assert_array_equal(device.to_host(sx), np.sort(X[:, c]))
+        np.testing.assert_allclose(device.to_host(s), ref[:, c], rtol=0, atol=1e-14)
+        assert int(flag.item()) == 0
