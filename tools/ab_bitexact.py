@@ -1,5 +1,5 @@
 """Bit-for-bit check of a library variant against the default on the kernels it changes: norm /
-lognorm sweeps (pbh_ppf) and fused native-LHS columns (Node.sample, method="lhs").
+lognorm / poisson / gamma sweeps (pbh_ppf) and fused native-LHS columns (Node.sample, method="lhs").
 
     python tools/ab_bitexact.py VARIANT     # prints the number of differing elements per case
 """
@@ -22,7 +22,8 @@ from probabilit_amd.modeling import Distribution as D
 q = np.concatenate([np.random.default_rng(5).random(3_000_000), [1e-300, 1e-20, 0.5, 1 - 1e-16, 0.0, 1.0]])
 out = {{}}
 for name, kw in [("norm", dict(loc=0.0, scale=1.0)), ("norm", dict(loc=5.0, scale=2.0)), ("lognorm", dict(s=0.5)),
-                 ("lognorm", dict(s=2.0, loc=-1.0, scale=3.0))]:
+                 ("lognorm", dict(s=2.0, loc=-1.0, scale=3.0)), ("poisson", dict(mu=4.0)), ("poisson", dict(mu=30.0)),
+                 ("poisson", dict(mu=250.0, loc=2.0)), ("gamma", dict(a=2.0))]:
     out[f"ppf_{{name}}_{{sorted(kw.items())}}"] = native.ppf(name, q, **kw)
     out[f"lhs_{{name}}_{{sorted(kw.items())}}"] = D(name, **kw).sample(2_000_003, method="lhs", random_state=9)
 np.savez({path!r}, **out)
