@@ -368,49 +368,6 @@ PBH_DI PoissonTable stage_poisson(const PoissonTable& pt, double* lds) {
   return local;
 }
 
-// The sweeps' table in LDS as (cdf[j], win[j]) pairs: the scan's last 16-byte read (the first j with
-// cdf[j] >= q) brings the window test's operand along, instead of a second LDS read of win[j]
-// (PBH_POISSON_PAIRS=0, A/B build: the two arrays of stage_poisson)
-#ifndef PBH_POISSON_PAIRS
-#define PBH_POISSON_PAIRS 1
-#endif
-struct PoissonPairs {
-  const double2* cw;
-  const int32_t* guide;
-  int64_t len, k_lo;
-};
-PBH_DI PoissonPairs stage_poisson_pairs(const PoissonTable& pt, double* lds) {
-  const int nb = 1 << kPoissonGuideBits;
-  double2* cw = reinterpret_cast<double2*>(lds);
-  int32_t* g = reinterpret_cast<int32_t*>(lds + 2 * pt.len);
-  for (int k = threadIdx.x; k < (int)pt.len; k += blockDim.x) cw[k] = make_double2(pt.cdf[k], pt.win[k]);
-  for (int k = threadIdx.x; k < nb; k += blockDim.x) g[k] = pt.cdf_guide[k];
-  __syncthreads();
-  return PoissonPairs{cw, g, pt.len, pt.k_lo};
-}
-// poisson_ppf_fast (pbh_ppf_core.h) on the pairs: the same decisions, so the same values
-PBH_DI bool poisson_ppf_pairs(double q, double mu, double loc, const PoissonPairs& t, double* x) {
-  const bool cond0 = (mu >= 0.0) && (loc == loc);
-  if (q == 0.0) {
-    *x = -1.0 + loc;
-  } else if (cond0 && q == 1.0) {
-    *x = kInf + loc;
-  } else if (cond0 && q > 0.0 && q < 1.0) {
-    int64_t lo = t.guide[(int)(q * (double)(1 << kPoissonGuideBits))];
-    double2 e = lo < t.len ? t.cw[lo] : make_double2(0.0, 0.0);
-    while (lo < t.len && e.x < q) {
-      ++lo;
-      if (lo < t.len) e = t.cw[lo];
-    }
-    const bool outside = lo == t.len || (lo == 0 && t.k_lo > 0);
-    if (outside || q < e.y || q < cdf::kPoissonDeepTail) return false;
-    *x = (double)(t.k_lo + lo) + loc;
-  } else {
-    *x = kNaN;
-  }
-  return true;
-}
-
 // one atomic per wave: the lanes with sl set append index i to the global list (slow[0] = count)
 __device__ __forceinline__ void append_slow(bool sl, int64_t i, unsigned long long* slow, uint32_t cap) {
   const uint64_t m = __ballot(sl);
@@ -431,11 +388,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_poisson_lds(const double
                                                             double* __restrict__ out, int32_t* flag,
                                                             unsigned long long* __restrict__ slow, uint32_t cap) {
   extern __shared__ double plds[];
-#if PBH_POISSON_PAIRS
-  const PoissonPairs T = stage_poisson_pairs(pt, plds);
-#else
   const PoissonTable T = stage_poisson(pt, plds);
-#endif
   // 4 items per thread per step, their loads issued together (4 independent chains, as in
   // k_place_gen_poisson)
   constexpr int kPer = 4;
@@ -450,12 +403,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_ppf_poisson_lds(const double
     double x[kPer];
     bool ok[kPer];
 #pragma unroll
-    for (int j = 0; j < kPer; ++j)
-#if PBH_POISSON_PAIRS
-      ok[j] = poisson_ppf_pairs(qv[j], prm.val[0], prm.val[1], T, &x[j]);
-#else
-      ok[j] = poisson_ppf_fast(qv[j], prm.val[0], prm.val[1], T, &x[j]);
-#endif
+    for (int j = 0; j < kPer; ++j) ok[j] = poisson_ppf_fast(qv[j], prm.val[0], prm.val[1], T, &x[j]);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int64_t i = b + j * kBlock + threadIdx.x;
@@ -475,11 +423,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_poisson_lds(uint64_t
                                                                 int32_t* flag, unsigned long long* __restrict__ slow,
                                                                 uint32_t cap) {
   extern __shared__ double plds[];
-#if PBH_POISSON_PAIRS
-  const PoissonPairs T = stage_poisson_pairs(pt, plds);
-#else
   const PoissonTable T = stage_poisson(pt, plds);
-#endif
   Philox ph(seed);
   FeistelPerm fp(ph, (uint64_t)n, col);
   bool bad = false;
@@ -490,11 +434,7 @@ __global__ __launch_bounds__(kBlock) PBH_OCC void k_lhs_ppf_poisson_lds(uint64_t
     bool ok = true;
     if (valid) {
       const double q = lhs_quantile(ph, fp, (uint64_t)(row0 + i), col);
-#if PBH_POISSON_PAIRS
-      ok = poisson_ppf_pairs(q, prm.val[0], prm.val[1], T, &x);
-#else
       ok = poisson_ppf_fast(q, prm.val[0], prm.val[1], T, &x);
-#endif
       if (ok) {
         out[i] = x;
         bad |= !isfinite(x);
