@@ -126,7 +126,14 @@ typedef enum pbh_dist {
   PBH_DIST_SKEWCAUCHY = 81,   /* a        tan(pi / (1 -+ a) (q - (1 - a) / 2)) (1 -+ a) */
   PBH_DIST_MOYAL = 82,        /*          -log(2 erfcinv(q)^2), erfcinv(y) = -ndtri(y / 2) / sqrt(2) */
   PBH_DIST_KAPPA4 = 83,       /* h, k     the four closed forms of kappa4._ppf */
-  PBH_DIST_CRYSTALBALL = 84   /* beta, m  power-law tail below pbeta, ndtri of the gaussian core above */
+  PBH_DIST_CRYSTALBALL = 84,  /* beta, m  power-law tail below pbeta, ndtri of the gaussian core above */
+  PBH_DIST_POWERLOGNORM = 85, /* c, s     exp(-ndtri((1 - q)^(1 / c)) s) */
+  PBH_DIST_JF_SKEW_T = 86,    /* a, b     (2 d - 1) sqrt(a + b) / (2 sqrt(d (1 - d))), d = I^-1(q; a, b) */
+  PBH_DIST_FOLDCAUCHY = 87,   /* c        the root of atan(x - c) + atan(x + c) = pi q in closed form */
+  PBH_DIST_FOLDNORM = 88,     /* c        cdf / sf root by bracketed Newton (scipy: brentq on its cdf) */
+  PBH_DIST_COSINE = 89,       /*          the root of x + sin x = pi (2 q - 1) by Newton */
+  PBH_DIST_INVGAUSS = 90,     /* mu       log-cdf / log-sf root in log x by bracketed Newton */
+  PBH_DIST_WALD = 91          /*          invgauss with mu = 1 */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

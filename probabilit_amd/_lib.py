@@ -24,7 +24,8 @@ DIST_IDS = {"norm": 0, "uniform": 1, "expon": 2, "lognorm": 3, "triang": 4, "gam
             "truncpareto": 65, "tukeylambda": 66, "gengamma": 67, "loggamma": 68, "dgamma": 69, "f": 70, "rdist": 71,
             "semicircular": 72, "betaprime": 73, "dlaplace": 74, "planck": 75, "boltzmann": 76,
             "pearson3": 77, "gennorm": 78, "halfgennorm": 79, "wrapcauchy": 80, "skewcauchy": 81, "moyal": 82,
-            "kappa4": 83, "crystalball": 84}
+            "kappa4": 83, "crystalball": 84, "powerlognorm": 85, "jf_skew_t": 86, "foldcauchy": 87, "foldnorm": 88,
+            "cosine": 89, "invgauss": 90, "wald": 91}
 
 # pbh_table_kind
 TABLE_INTERP, TABLE_QUANTILE, TABLE_SEARCH = 0, 1, 2

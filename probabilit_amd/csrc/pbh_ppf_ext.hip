@@ -234,7 +234,7 @@ void attach_table(int dist, const double* t, Params4& p) {
 
 constexpr bool is_closed(int d) {
   return (d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID) || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T ||
-         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME) || (d >= PBH_DIST_PEARSON3 && d <= PBH_DIST_CRYSTALBALL);
+         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME) || (d >= PBH_DIST_PEARSON3 && d <= PBH_DIST_WALD);
 }
 // discrete distributions beyond binom / bernoulli (round 5): p, loc / low, high, loc / n, p, loc;
 // round 6: a, loc (dlaplace) / lambda, loc (planck) / lambda, N, loc (boltzmann)
@@ -247,7 +247,7 @@ constexpr int closed_shapes(int d) {
   return (d == PBH_DIST_LOGUNIFORM || d == PBH_DIST_BURR || d == PBH_DIST_BURR12 || d == PBH_DIST_EXPONWEIB ||
           d == PBH_DIST_TRAPEZOID || d == PBH_DIST_JOHNSONSU || d == PBH_DIST_JOHNSONSB || d == PBH_DIST_MIELKE ||
           d == PBH_DIST_TRUNCPARETO || d == PBH_DIST_GENGAMMA || d == PBH_DIST_F || d == PBH_DIST_BETAPRIME ||
-          d == PBH_DIST_KAPPA4 || d == PBH_DIST_CRYSTALBALL)
+          d == PBH_DIST_KAPPA4 || d == PBH_DIST_CRYSTALBALL || d == PBH_DIST_POWERLOGNORM || d == PBH_DIST_JF_SKEW_T)
              ? 2
          : (d == PBH_DIST_WEIBULL_MIN || d == PBH_DIST_WEIBULL_MAX || d == PBH_DIST_PARETO || d == PBH_DIST_LOMAX ||
             d == PBH_DIST_GENEXTREME || d == PBH_DIST_GOMPERTZ || d == PBH_DIST_CHI2 || d == PBH_DIST_POWERLAW ||
@@ -258,7 +258,8 @@ constexpr int closed_shapes(int d) {
             d == PBH_DIST_GENLOGISTIC || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T || d == PBH_DIST_POWERNORM ||
             d == PBH_DIST_LAPLACE_ASYMMETRIC || d == PBH_DIST_TUKEYLAMBDA || d == PBH_DIST_LOGGAMMA ||
             d == PBH_DIST_DGAMMA || d == PBH_DIST_RDIST || d == PBH_DIST_PEARSON3 || d == PBH_DIST_GENNORM ||
-            d == PBH_DIST_HALFGENNORM || d == PBH_DIST_WRAPCAUCHY || d == PBH_DIST_SKEWCAUCHY)
+            d == PBH_DIST_HALFGENNORM || d == PBH_DIST_WRAPCAUCHY || d == PBH_DIST_SKEWCAUCHY ||
+            d == PBH_DIST_FOLDCAUCHY || d == PBH_DIST_FOLDNORM || d == PBH_DIST_INVGAUSS)
              ? 1
              : 0;
 }
@@ -294,6 +295,131 @@ __device__ __forceinline__ double powm1(double x, double y) {
 // trapezoid._cdf(x, c, d) at x = c and x = d (the middle piece), the breaks of its _ppf
 __device__ __forceinline__ double trapezoid_mid_cdf(double x, double c, double d) {
   return (c + 2.0 * (x - c)) / (d - c + 1.0);
+}
+
+// ---- round 6, third set: quantiles scipy finds by a search (foldcauchy / foldnorm: the generic
+// rv_continuous._ppf, brentq on _cdf to xtol 1e-14; invgauss / wald: Boost's inverse_gaussian
+// quantile, its complement above q = 1/2; cosine: xsf's cosine_invcdf), each solved here to a few
+// ulps by its own method, so they agree with scipy's to its own tolerance
+
+// the x in (lo, hi) with f(x) = t, f increasing (inc) or decreasing (fp(x) its signed derivative): Newton steps kept
+// inside the shrinking bracket, bisection when a step leaves it, until a step moves x by <= 4 ulps
+template <class F, class Fp>
+__device__ __forceinline__ double bracket_newton(F f, Fp fp, double t, double lo, double hi, double x, bool inc) {
+  for (int it = 0; it < 200; ++it) {
+    const double g = f(x) - t;
+    if (g == 0.0) return x;
+    if ((g < 0.0) == inc)
+      lo = x;
+    else
+      hi = x;
+    double xn = x - g / fp(x);
+    if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
+    if (fabs(xn - x) <= 4.0 * 2.220446049250313e-16 * fabs(xn) || !(hi > lo)) return xn;
+    x = xn;
+  }
+  return x;
+}
+
+// foldcauchy: atan(x - c) + atan(x + c) = pi q, x >= 0, is the positive root of
+// sin(th) x^2 + 2 cos(th) x - (1 + c^2) sin(th) = 0, th = pi q (sin / cos of pi q from the nearer
+// end, so that they keep their relative precision as q -> 1)
+__device__ __forceinline__ double foldcauchy_ppf01(double q, double c) {
+  const bool up = q > 0.5;
+  const double r = up ? 1.0 - q : q;  // exact for q > 1/2
+  const double sn = sin(sf::kPi * r), cs = up ? -cos(sf::kPi * r) : cos(sf::kPi * r);
+  const double k = 1.0 + c * c;
+  const double root = sqrt(cs * cs + k * sn * sn);
+  return cs > 0.0 ? k * sn / (cs + root) : (root - cs) / sn;
+}
+
+// foldnorm: scipy's _cdf (0.5 (erf((x - c) / sqrt 2) + erf((x + c) / sqrt 2))) below q = 1/2, its _sf
+// (ndtr(c - x) + ndtr(-x - c)) above, the density phi(x - c) + phi(x + c)
+__device__ __forceinline__ double foldnorm_ppf01(double q, double c) {
+  constexpr double kRs2pi = 0.3989422804014327;  // 1 / sqrt(2 pi)
+  auto pdf = [c](double x) { return kRs2pi * (exp(-0.5 * (x - c) * (x - c)) + exp(-0.5 * (x + c) * (x + c))); };
+  const double hi = c + 40.0;
+  const double x0 = c + fabs(sf::ndtri(0.5 + 0.5 * q));  // the c = 0 answer, shifted
+  if (q <= 0.5) {
+    auto cdf = [c](double x) { return 0.5 * (sf::erf_((x - c) * sfx::kSqrt1_2) + sf::erf_((x + c) * sfx::kSqrt1_2)); };
+    const double xs = fmin(x0, fmax(q / (2.0 * pdf(0.0)), 0.0));
+    return bracket_newton(cdf, pdf, q, 0.0, hi, xs > 0.0 ? xs : 0.5 * hi, true);
+  }
+  auto sfn = [c](double x) { return sfx::ndtr(c - x) + sfx::ndtr(-x - c); };
+  auto dsf = [&pdf](double x) { return -pdf(x); };
+  return bracket_newton(sfn, dsf, 1.0 - q, 0.0, hi, fmin(x0, 0.5 * hi), false);
+}
+
+// invgauss(mu): scipy's _logcdf / _logsf, solved in u = log x (log-concave in u): the quantile below
+// q = 1/2, the complement's above (as scipy, whose lower-tail Boost quantile is inaccurate there);
+// start: the log-normal with the same mean and variance
+__device__ __forceinline__ double invgauss_logcdf(double x, double mu) {
+  const double fac = 1.0 / sqrt(x);
+  const double a = sfx::log_ndtr(fac * ((x / mu) - 1.0));
+  const double b = 2.0 / mu + sfx::log_ndtr(-fac * ((x / mu) + 1.0));
+  return a + log1p(exp(b - a));
+}
+__device__ __forceinline__ double invgauss_logsf(double x, double mu) {
+  const double fac = 1.0 / sqrt(x);
+  const double a = sfx::log_ndtr(-(fac * ((x / mu) - 1.0)));
+  const double b = 2.0 / mu + sfx::log_ndtr(-fac * (x + mu) / mu);
+  return a + log1p(-exp(b - a));
+}
+__device__ __forceinline__ double invgauss_ppf01(double q, double mu) {
+  // log(x pdf(x)) = -log(2 pi x) / 2 - (x - mu)^2 / (2 x mu^2)
+  auto lxpdf = [mu](double x) { return -0.5 * log(2.0 * sf::kPi * x) - (x - mu) * (x - mu) / (2.0 * x * mu * mu); };
+  const double s2 = log1p(mu), u0 = log(mu) - 0.5 * s2 + sqrt(s2) * sf::ndtri(q);
+  const double lo = -744.0, hi = 709.0;
+  const double us = fmin(fmax(u0, lo + 1.0), hi - 1.0);
+  double u;
+  if (q <= 0.5) {
+    auto f = [mu](double v) { return invgauss_logcdf(exp(v), mu); };
+    auto fp = [mu, &lxpdf](double v) {
+      const double x = exp(v);
+      return exp(lxpdf(x) - invgauss_logcdf(x, mu));
+    };
+    u = bracket_newton(f, fp, log(q), lo, hi, us, true);
+  } else {
+    auto f = [mu](double v) { return invgauss_logsf(exp(v), mu); };
+    auto fp = [mu, &lxpdf](double v) {
+      const double x = exp(v);
+      return -exp(lxpdf(x) - invgauss_logsf(x, mu));
+    };
+    u = bracket_newton(f, fp, log1p(-q), lo, hi, us, false);
+  }
+  return exp(u);
+}
+
+// cosine: cdf(x) = (pi + x + sin x) / (2 pi), symmetric about 0.  Central q: x + sin x = pi (2 q - 1)
+// (exact argument for q in [1/4, 3/4]); tails: y = x + pi for min(q, 1 - q), y - sin y = 2 pi q,
+// with its series below y = 1/2 (no cancellation)
+__device__ __forceinline__ double cosine_tail_h(double y) {  // y - sin y
+  if (y >= 0.5) return y - sin(y);
+  const double y2 = y * y;
+  double t = y * y2 / 6.0, s = t;
+  for (int k = 2; k <= 10; ++k) {
+    t *= -y2 / ((2.0 * k) * (2.0 * k + 1.0));
+    s += t;
+  }
+  return s;
+}
+__device__ __forceinline__ double cosine_ppf01(double q) {
+  if (q >= 0.25 && q <= 0.75) {
+    const double t = sf::kPi * (2.0 * q - 1.0);
+    auto f = [](double x) { return x + sin(x); };
+    auto fp = [](double x) { return 1.0 + cos(x); };
+    return bracket_newton(f, fp, t, -sf::kPi, sf::kPi, 0.5 * t, true);
+  }
+  const bool up = q > 0.5;
+  const double p = up ? 1.0 - q : q;  // exact for q > 1/2
+  auto h = [](double y) { return cosine_tail_h(y); };
+  auto hp = [](double y) {
+    const double s = sin(0.5 * y);
+    return 2.0 * s * s;  // 1 - cos y
+  };
+  const double y0 = fmin(cbrt(12.0 * sf::kPi * p), sf::kPi);
+  const double y = bracket_newton(h, hp, 2.0 * sf::kPi * p, 0.0, sf::kPi, y0, true);
+  return up ? sf::kPi - y : y - sf::kPi;
 }
 
 // _argcheck and the support [_a, _b] of scipy's class (rv_continuous default: every shape > 0)
@@ -395,6 +521,16 @@ __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo,
     return true;
   }
   if constexpr (D == PBH_DIST_CRYSTALBALL) return s1 > 1.0 && s0 > 0.0;  // (m > 1) & (beta > 0)
+  // round 6, third set
+  if constexpr (D == PBH_DIST_POWERLOGNORM || D == PBH_DIST_INVGAUSS || D == PBH_DIST_WALD) lo = 0.0;
+  if constexpr (D == PBH_DIST_FOLDCAUCHY || D == PBH_DIST_FOLDNORM) {  // _argcheck c >= 0, support [0, inf)
+    lo = 0.0;
+    return s0 >= 0.0;
+  }
+  if constexpr (D == PBH_DIST_COSINE) {
+    lo = -sf::kPi;
+    hi = sf::kPi;
+  }
   if constexpr (closed_shapes(D) == 1) return s0 > 0.0;
   if constexpr (closed_shapes(D) == 2) return s0 > 0.0 && s1 > 0.0;
   return true;
@@ -575,6 +711,19 @@ __device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
     if (q < pbeta) return m / beta - beta - pow((m - 1) * pow(m / beta, -m) / eb * q / N, 1 / (1 - m));
     return sf::ndtri(sf::ndtr(-beta) + (1 / kNormPdfC) * (q / N - C));
   }
+  // round 6, third set
+  if constexpr (D == PBH_DIST_POWERLOGNORM) return exp(-sf::ndtri(pow(1.0 - q, 1 / s0)) * s1);  // _isf(1 - q)
+  if constexpr (D == PBH_DIST_JF_SKEW_T) {
+    const double d1 = sfx::beta_ppf01(q, s0, s1);
+    const double d2 = (2 * d1 - 1) * sqrt(s0 + s1);
+    const double d3 = 2 * sqrt(d1 * (1 - d1));
+    return d2 / d3;
+  }
+  if constexpr (D == PBH_DIST_FOLDCAUCHY) return foldcauchy_ppf01(q, s0);
+  if constexpr (D == PBH_DIST_FOLDNORM) return foldnorm_ppf01(q, s0);
+  if constexpr (D == PBH_DIST_COSINE) return cosine_ppf01(q);
+  if constexpr (D == PBH_DIST_INVGAUSS) return invgauss_ppf01(q, s0);
+  if constexpr (D == PBH_DIST_WALD) return invgauss_ppf01(q, 1.0);
   return sf::kNaN;
 }
 
@@ -828,6 +977,13 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_MOYAL)
     PBH_EXT(PBH_DIST_KAPPA4)
     PBH_EXT(PBH_DIST_CRYSTALBALL)
+    PBH_EXT(PBH_DIST_POWERLOGNORM)
+    PBH_EXT(PBH_DIST_JF_SKEW_T)
+    PBH_EXT(PBH_DIST_FOLDCAUCHY)
+    PBH_EXT(PBH_DIST_FOLDNORM)
+    PBH_EXT(PBH_DIST_COSINE)
+    PBH_EXT(PBH_DIST_INVGAUSS)
+    PBH_EXT(PBH_DIST_WALD)
 #undef PBH_EXT
     default:
       return false;

@@ -715,7 +715,9 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "f": ("dfn", "dfd"), "rdist": ("c",), "semicircular": (), "betaprime": ("a", "b"),
                 "dlaplace": ("a",), "planck": ("lambda_",), "boltzmann": ("lambda_", "N"),
                 "pearson3": ("skew",), "gennorm": ("beta",), "halfgennorm": ("beta",), "wrapcauchy": ("c",),
-                "skewcauchy": ("a",), "moyal": (), "kappa4": ("h", "k"), "crystalball": ("beta", "m")}
+                "skewcauchy": ("a",), "moyal": (), "kappa4": ("h", "k"), "crystalball": ("beta", "m"),
+                "powerlognorm": ("c", "s"), "jf_skew_t": ("a", "b"), "foldcauchy": ("c",), "foldnorm": ("c",),
+                "cosine": (), "invgauss": ("mu",), "wald": ()}
 _DISCRETE = {"poisson", "binom", "bernoulli", "geom", "randint", "nbinom", "dlaplace", "planck", "boltzmann"}
 # distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so
 # that Iman-Conover takes them as generated columns (pbh_ppf.hip k_lhs_sorted_ppf / k_place_gen;

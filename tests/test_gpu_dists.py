@@ -561,6 +561,67 @@ def test_round6_fused_lhs_and_composite(gpu, name, kw):
         assert_close(got2, ref2, rtol=1e-10, atol=1e-12, what=f"composite {name} {kw}")
 
 
+# round 6, third set: powerlognorm and jf_skew_t (closed forms on ndtri / the beta inverse), cosine,
+# invgauss and wald (scipy: xsf's cosine_invcdf and Boost's quantile, solved here by Newton),
+# foldcauchy (closed form) and foldnorm (Newton).  scipy's foldcauchy / foldnorm ppf is the generic
+# brentq on _cdf (xtol 1e-14): where that cdf is flat to a few ulps (q within ~1e-12 of 0 or 1) its x
+# is any of many; there the device x is accepted when scipy's own cdf maps it back onto q.
+_R6_CONT3 = [("powerlognorm", dict(c=2.14, s=0.446)), ("powerlognorm", dict(c=0.5, s=1.5, loc=1.0)),
+             ("jf_skew_t", dict(a=8.0, b=4.0)), ("jf_skew_t", dict(a=0.7, b=2.5, scale=2.0)),
+             ("foldcauchy", dict(c=4.72)), ("foldcauchy", dict(c=0.0)), ("foldnorm", dict(c=1.95)),
+             ("foldnorm", dict(c=0.0, scale=2.0)), ("cosine", dict()), ("cosine", dict(loc=1.0, scale=0.5)),
+             ("invgauss", dict(mu=0.145)), ("invgauss", dict(mu=3.0)), ("invgauss", dict(mu=25.0)),
+             ("wald", dict()), ("wald", dict(loc=-1.0, scale=2.0))]
+_GENERIC_PPF = ("foldcauchy", "foldnorm")
+
+
+def _check_third(name, kw, q, got, ref, what):
+    import scipy.stats
+
+    if name in _GENERIC_PPF:
+        with np.errstate(all="ignore"):
+            back = getattr(scipy.stats, name)(**kw).cdf(got)
+        loose = (q < 1e-9) | (q > 1 - 1e-9)
+        ok = loose & np.isfinite(got) & (np.abs(back - q) <= 4e-16 + 4 * np.spacing(q))
+        got, ref = got[~ok], ref[~ok]
+    assert_close(got, ref, rtol=1e-10, atol=1e-13, what=what)
+
+
+@pytest.mark.parametrize("name,kw", _R6_CONT3)
+def test_round6_third_set_ppf(gpu, name, kw):
+    import scipy.stats
+
+    from probabilit_amd import native
+
+    q = np.concatenate([_q(20_000, 37), np.linspace(0.01, 0.99, 2001), [-0.5, 1.5, np.nan]])
+    with np.errstate(all="ignore"):
+        ref = getattr(scipy.stats, name)(**kw).ppf(q)
+    got = native.ppf(name, q, **kw)
+    _check_third(name, kw, q, got, ref, f"{name} {kw}")
+
+
+@pytest.mark.parametrize("name,kw", _R6_CONT3)
+def test_round6_third_set_fused_lhs_and_composite(gpu, name, kw):
+    import scipy.stats
+
+    from probabilit_amd import native
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.qmc import seed_from
+
+    n, s = 30_000, 41
+    q = native.fill_lhs(seed_from(s), n, 1)[:, 0]
+    with np.errstate(all="ignore"):
+        ref = getattr(scipy.stats, name)(**kw).ppf(q)
+    got = D(name, **kw).sample(n, method="lhs", random_state=s)
+    _check_third(name, kw, q, got, ref, f"LHS {name} {kw}")
+    loc = np.random.default_rng(5).integers(-3, 4, n).astype(float)
+    kw2 = dict(kw, loc=loc + kw.get("loc", 0.0))
+    with np.errstate(all="ignore"):
+        ref2 = getattr(scipy.stats, name)(**kw2).ppf(q)
+    got2 = native.ppf(name, q, **kw2)
+    assert_close(got2, ref2, rtol=1e-10, atol=1e-12, what=f"composite {name} {kw}")
+
+
 def test_round6_generated_iman_conover(gpu):
     """The round-6 names correlated with method="lhs" take the generated-column path (dlaplace /
     planck / boltzmann with their run heads): bit-identical to the general path on the same native
@@ -576,9 +637,11 @@ def test_round6_generated_iman_conover(gpu):
                 D("planck", lambda_=0.51), D("boltzmann", lambda_=1.4, N=19), D("tukeylambda", lam=3.13),
                 D("betaprime", a=5.0, b=6.0), D("semicircular"), D("trapz", c=0.2, d=0.8),
                 D("pearson3", skew=0.7), D("gennorm", beta=1.3), D("halfgennorm", beta=0.7), D("wrapcauchy", c=0.3),
-                D("skewcauchy", a=0.4), D("moyal"), D("kappa4", h=0.1, k=0.3), D("crystalball", beta=2.0, m=3.0)]
+                D("skewcauchy", a=0.4), D("moyal"), D("kappa4", h=0.1, k=0.3), D("crystalball", beta=2.0, m=3.0),
+                D("powerlognorm", c=2.14, s=0.446), D("jf_skew_t", a=8.0, b=4.0), D("foldcauchy", c=4.72),
+                D("foldnorm", c=1.95), D("cosine"), D("invgauss", mu=0.145), D("wald")]
 
-    n, d = 30_000, 18
+    n, d = 30_000, 25
     C = np.corrcoef(np.random.default_rng(d).normal(size=(d, d + 2)))
     ds = graph()
     root = NoOp(*ds).correlate(*ds, corr_mat=C)
