@@ -133,7 +133,9 @@ typedef enum pbh_dist {
   PBH_DIST_FOLDNORM = 88,     /* c        cdf / sf root by bracketed Newton (scipy: brentq on its cdf) */
   PBH_DIST_COSINE = 89,       /*          the root of x + sin x = pi (2 q - 1) by Newton */
   PBH_DIST_INVGAUSS = 90,     /* mu       log-cdf / log-sf root in log x by bracketed Newton */
-  PBH_DIST_WALD = 91          /*          invgauss with mu = 1 */
+  PBH_DIST_WALD = 91,         /*          invgauss with mu = 1 */
+  PBH_DIST_BETABINOM = 92,    /* n, a, b, loc (discrete)  first k with sum of the pmf over [0, k] >= q */
+  PBH_DIST_HYPERGEOM = 93     /* M, n, N, loc (discrete)  the same over [max(0, N - M + n), min(n, N)] */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

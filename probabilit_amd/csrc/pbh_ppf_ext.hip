@@ -86,6 +86,83 @@ __device__ __forceinline__ double discrete_from_table(double q, const double* cd
   return lo < len ? (double)lo : -1.0;
 }
 
+// betabinom (n, a, b) and hypergeom (M, n, N) (round 6): scipy's generic discrete ppf, the smallest k
+// of the support with cdf(k) >= q (_drv2_ppfsingle's bisection), cdf(k) the sum of the pmf over
+// [lo, k] (rv_discrete._cdf_single; hypergeom._cdf is Boost's sum of its pdf).  Summed here in order
+// from lo, by the per-draw loop and the scalar-parameter table alike, so the two answer the same; the
+// pmf as scipy's betabinom._logpmf writes it, log C(a, b) = -log(a + 1) - betaln(a - b + 1, b + 1).
+// The outputs equal scipy's except where q lies within the summation's rounding (~1e-15) of a CDF value.
+PBH_HD inline double lchoose(double a, double b) { return -log(a + 1.0) - sfx::lbeta(a - b + 1.0, b + 1.0); }
+
+// _argcheck and the support [lo, hi]
+PBH_HD inline bool sum_bounds(int d, double s0, double s1, double s2, double* lo, double* hi) {
+  if (d == PBH_DIST_BETABINOM) {
+    *lo = 0.0;
+    *hi = s0;
+    return s0 >= 0.0 && s0 == floor(s0) && s1 > 0.0 && s2 > 0.0;
+  }
+  *lo = fmax(s2 - (s0 - s1), 0.0);  // hypergeom: M, n, N
+  *hi = fmin(s1, s2);
+  return s0 > 0.0 && s1 >= 0.0 && s2 >= 0.0 && s1 <= s0 && s2 <= s0 && s0 == floor(s0) && s1 == floor(s1) &&
+         s2 == floor(s2);
+}
+
+template <int D>
+__device__ __forceinline__ double sum_pmf(double k, double s0, double s1, double s2) {
+  if constexpr (D == PBH_DIST_BETABINOM)
+    return exp(lchoose(s0, k) + sfx::lbeta(k + s1, s0 - k + s2) - sfx::lbeta(s1, s2));
+  else
+    return exp(lchoose(s1, k) + lchoose(s0 - s1, s2 - k) - lchoose(s0, s2));
+}
+
+// hypergeom above q = 1/2 follows Boost's cdf there, 1 - (the pmf summed from the top down to k + 1):
+// the first k with fl(1 - S(k)) >= q, scanned down from hi (summed from lo, the pmf's rounding would
+// overshoot 1 by ~1e-13 and move q = 1 - 2^-53's answer by several values)
+template <int D>
+__device__ __forceinline__ double sum_ppf01(double q, double s0, double s1, double s2, double lo, double hi) {
+  if (D == PBH_DIST_HYPERGEOM && q > 0.5) {
+    double k = hi, S = 0.0;
+    while (k > lo) {
+      const double S2 = S + sum_pmf<D>(k, s0, s1, s2);
+      if (!(1.0 - S2 >= q)) break;
+      S = S2;
+      k -= 1.0;
+    }
+    return k;
+  }
+  double k = lo, c = sum_pmf<D>(lo, s0, s1, s2);
+  while (c < q && k < hi) {
+    k += 1.0;
+    c += sum_pmf<D>(k, s0, s1, s2);
+  }
+  return k;
+}
+
+// the table of these two: pmf(lo + i) in parallel, then one thread sums them in the per-draw loops'
+// orders: cdf[i] from lo up, and the complement the q > 1/2 search compares with 1 - q: 1 - cdf[i],
+// or for hypergeom 1 - fl(1 - S(i)) with S summed from the top (exact: fl(1 - S) >= 1/2 there)
+template <int D>
+__global__ void k_sum_pmf(double s0, double s1, double s2, double lo, int len, double* __restrict__ pmf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < len) pmf[i] = sum_pmf<D>(lo + (double)i, s0, s1, s2);
+}
+__global__ void k_sum_cdf(int len, int from_top, double* __restrict__ cdf, double* __restrict__ ccdf) {
+  if (threadIdx.x || blockIdx.x) return;
+  if (from_top) {
+    double S = 0.0;
+    for (int i = len - 1; i >= 0; --i) {
+      ccdf[i] = 1.0 - (1.0 - S);
+      S += cdf[i];
+    }
+  }
+  double c = 0.0;
+  for (int i = 0; i < len; ++i) {
+    c += cdf[i];
+    cdf[i] = c;
+    if (!from_top) ccdf[i] = 1.0 - c;
+  }
+}
+
 // the beta guide for scalar (a, b) (sfx::BetaGuide): nodes, then the midpoint check
 __global__ void k_beta_guide(double a, double b, double lb, double* z, double* d1, double* d2) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -117,6 +194,11 @@ int discrete_table_len(int dist, const double* v) {
     return (int)v[0] + 1;
   }
   if (dist == PBH_DIST_BERNOULLI) return (v[0] >= 0.0 && v[0] <= 1.0) ? 2 : 0;
+  if (dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM) {  // v: the three shapes
+    double lo, hi;
+    if (!sum_bounds(dist, v[0], v[1], v[2], &lo, &hi) || !(hi - lo + 1.0 <= kDiscreteTableMax)) return 0;
+    return (int)(hi - lo) + 1;
+  }
   if (dist == PBH_DIST_NBINOM) {
     if (!(v[0] > 0.0 && v[1] > 0.0 && v[1] < 1.0 && v[0] < 1e6 && v[1] > 1e-4)) return 0;
     const double top = sfx::nbinom_ppf01(1.0 - 0x1p-40, v[0], v[1]);
@@ -142,6 +224,36 @@ double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t 
   if (is_gamma_family(dist) || dist == PBH_DIST_INVGAMMA) {
     if (dist != PBH_DIST_MAXWELL && (nparams < 1 || params[0].ptr)) return nullptr;
     return gamma_guide_table(gamma_family_a(dist, nparams ? params[0].value : 0.0), s);
+  }
+  if (dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM) {
+    if (nparams < 3 || params[0].ptr || params[1].ptr || params[2].ptr) return nullptr;
+    const double v[3] = {params[0].value, params[1].value, params[2].value};
+    const int len = discrete_table_len(dist, v);
+    if (len <= 0) return nullptr;
+    double lo, hi;
+    (void)sum_bounds(dist, v[0], v[1], v[2], &lo, &hi);
+    auto build = [=](double* t, hipStream_t st) {
+      const double hdr = (double)len;
+      if (hipMemcpyAsync(t, &hdr, sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess) return false;
+      const dim3 g((unsigned)((len + 255) / 256)), b(256);
+      if (dist == PBH_DIST_BETABINOM)
+        hipLaunchKernelGGL(k_sum_pmf<PBH_DIST_BETABINOM>, g, b, 0, st, v[0], v[1], v[2], lo, len, t + 1);
+      else
+        hipLaunchKernelGGL(k_sum_pmf<PBH_DIST_HYPERGEOM>, g, b, 0, st, v[0], v[1], v[2], lo, len, t + 1);
+      hipLaunchKernelGGL(k_sum_cdf, dim3(1), dim3(64), 0, st, len, dist == PBH_DIST_HYPERGEOM ? 1 : 0, t + 1,
+                         t + 1 + len);
+      return hipGetLastError() == hipSuccess;
+    };
+    const size_t bytes = (size_t)(2 * len + 1) * sizeof(double);
+    const double key[4] = {(double)dist, v[0], v[1], v[2]};
+    if (double* t = cached_table(kTabDiscrete, key, 4, bytes, s, build)) return t;
+    double* t = nullptr;
+    if (hipMallocAsync((void**)&t, bytes, s) != hipSuccess) return nullptr;
+    if (!build(t, s)) {
+      (void)hipFreeAsync(t, s);
+      return nullptr;
+    }
+    return t;
   }
   if (dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_NBINOM) {
     const int ns = dist == PBH_DIST_BERNOULLI ? 1 : 2;
@@ -224,6 +336,9 @@ void attach_table(int dist, const double* t, Params4& p) {
     const double a = gamma_family_a(dist, p.val[0]);
     p.gg = sf::GammaGuide{t, t + m, t + 2 * m, t + 3 * m, m, sf::kGammaGuideZ0, sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
     p.ga = sf::gamma_aux(a);
+  } else if (dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM) {
+    p.dlen = discrete_table_len(dist, p.val);
+    p.dt = p.dlen > 0 ? t + 1 : nullptr;
   } else if (dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_NBINOM) {
     const int ns = dist == PBH_DIST_BERNOULLI ? 1 : 2;
     p.dlen = discrete_table_len(dist, p.val);  // the same length the table was built with
@@ -240,7 +355,7 @@ constexpr bool is_closed(int d) {
 // round 6: a, loc (dlaplace) / lambda, loc (planck) / lambda, N, loc (boltzmann)
 constexpr bool is_discrete2(int d) {
   return d == PBH_DIST_GEOM || d == PBH_DIST_RANDINT || d == PBH_DIST_NBINOM || d == PBH_DIST_DLAPLACE ||
-         d == PBH_DIST_PLANCK || d == PBH_DIST_BOLTZMANN;
+         d == PBH_DIST_PLANCK || d == PBH_DIST_BOLTZMANN || d == PBH_DIST_BETABINOM || d == PBH_DIST_HYPERGEOM;
 }
 
 constexpr int closed_shapes(int d) {
@@ -778,6 +893,18 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
       if (!(lam > 0.0 && N > 0.0 && N == floor(N) && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
       if (q == 1.0) return N - 1.0 + loc;
       return sfx::boltzmann_ppf01(q, lam, N) + loc;
+    } else if constexpr (D == PBH_DIST_BETABINOM || D == PBH_DIST_HYPERGEOM) {
+      const double s0 = p.at(0, i), s1 = p.at(1, i), s2 = p.at(2, i), loc = p.at(3, i);
+      double lo, hi;
+      const bool ok = sum_bounds(D, s0, s1, s2, &lo, &hi) && loc == loc;
+      if (q == 0.0) return lo - 1.0 + loc;
+      if (!ok || !(q >= 0.0 && q <= 1.0)) return nan;
+      if (q == 1.0) return hi + loc;
+      if (p.dt) {
+        const double k = discrete_from_table(q, p.dt, p.dlen);
+        if (k >= 0.0) return lo + k + loc;
+      }
+      return sum_ppf01<D>(q, s0, s1, s2, lo, hi) + loc;
     } else {  // nbinom
       const double n = p.at(0, i), pp = p.at(1, i), loc = p.at(2, i);
       if (q == 0.0) return -1.0 + loc;
@@ -862,7 +989,8 @@ struct LhsCol {
 constexpr int kExtLdsTab = 512;
 template <int D>
 constexpr bool ext_table_discrete() {
-  return D == PBH_DIST_BINOM || D == PBH_DIST_BERNOULLI || D == PBH_DIST_NBINOM;
+  return D == PBH_DIST_BINOM || D == PBH_DIST_BERNOULLI || D == PBH_DIST_NBINOM || D == PBH_DIST_BETABINOM ||
+         D == PBH_DIST_HYPERGEOM;
 }
 
 template <int D, bool LHS>
@@ -984,6 +1112,8 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_COSINE)
     PBH_EXT(PBH_DIST_INVGAUSS)
     PBH_EXT(PBH_DIST_WALD)
+    PBH_EXT(PBH_DIST_BETABINOM)
+    PBH_EXT(PBH_DIST_HYPERGEOM)
 #undef PBH_EXT
     default:
       return false;
@@ -1246,7 +1376,8 @@ int ext_nparams(int dist) {
     return 2;
   if (dist == PBH_DIST_BINOM || dist == PBH_DIST_RANDINT || dist == PBH_DIST_NBINOM || dist == PBH_DIST_BOLTZMANN)
     return 3;
-  if (dist == PBH_DIST_BETA || dist == PBH_DIST_TRUNCNORM) return 4;
+  if (dist == PBH_DIST_BETA || dist == PBH_DIST_TRUNCNORM || dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM)
+    return 4;
   if (is_closed(dist)) return closed_shapes(dist) + 2;
   return -1;
 }
@@ -1296,6 +1427,13 @@ void discrete_span(int dist, const double* val, double* span, double* loc) {
       if (val[0] > 0.0 && val[1] > 0.0) *span = val[1];
       *loc = val[2];
       break;
+    case PBH_DIST_BETABINOM:
+    case PBH_DIST_HYPERGEOM: {
+      double lo, hi;
+      if (sum_bounds(dist, val[0], val[1], val[2], &lo, &hi)) *span = hi - lo + 1.0;
+      *loc = val[3];
+      break;
+    }
     default:
       break;
   }

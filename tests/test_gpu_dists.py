@@ -622,6 +622,33 @@ def test_round6_third_set_fused_lhs_and_composite(gpu, name, kw):
     assert_close(got2, ref2, rtol=1e-10, atol=1e-12, what=f"composite {name} {kw}")
 
 
+# round 6: betabinom and hypergeom, scipy's generic discrete ppf (the first k with cdf(k) >= q, cdf the
+# sum of the pmf): exact, with scalar parameters (the CDF table) and per row (the per-draw sum)
+_R6_DISCRETE3 = [("betabinom", dict(n=20, a=2.5, b=1.5)), ("betabinom", dict(n=200, a=0.6, b=3.0, loc=1)),
+                 ("hypergeom", dict(M=50, n=12, N=20)), ("hypergeom", dict(M=500, n=300, N=150, loc=-2))]
+
+
+@pytest.mark.parametrize("name,kw", _R6_DISCRETE3)
+def test_round6_summed_discrete_ppf(gpu, name, kw):
+    import scipy.stats
+
+    from probabilit_amd import native
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.qmc import seed_from
+
+    q = np.concatenate([_q(20_000, 43), np.linspace(0.01, 0.99, 2001), [-0.5, 1.5, np.nan]])
+    ref = getattr(scipy.stats, name)(**kw).ppf(q)
+    np.testing.assert_array_equal(native.ppf(name, q, **kw), ref)
+    # fused with the native LHS, and with a per-row loc (no table: the per-draw sum)
+    n, s = 30_000, 47
+    ql = native.fill_lhs(seed_from(s), n, 1)[:, 0]
+    np.testing.assert_array_equal(D(name, **kw).sample(n, method="lhs", random_state=s),
+                                  getattr(scipy.stats, name)(**kw).ppf(ql))
+    loc = np.random.default_rng(7).integers(-3, 4, n).astype(float)
+    kw2 = dict(kw, loc=loc + kw.get("loc", 0.0))
+    np.testing.assert_array_equal(native.ppf(name, ql, **kw2), getattr(scipy.stats, name)(**kw2).ppf(ql))
+
+
 def test_round6_generated_iman_conover(gpu):
     """The round-6 names correlated with method="lhs" take the generated-column path (dlaplace /
     planck / boltzmann with their run heads): bit-identical to the general path on the same native
@@ -639,9 +666,10 @@ def test_round6_generated_iman_conover(gpu):
                 D("pearson3", skew=0.7), D("gennorm", beta=1.3), D("halfgennorm", beta=0.7), D("wrapcauchy", c=0.3),
                 D("skewcauchy", a=0.4), D("moyal"), D("kappa4", h=0.1, k=0.3), D("crystalball", beta=2.0, m=3.0),
                 D("powerlognorm", c=2.14, s=0.446), D("jf_skew_t", a=8.0, b=4.0), D("foldcauchy", c=4.72),
-                D("foldnorm", c=1.95), D("cosine"), D("invgauss", mu=0.145), D("wald")]
+                D("foldnorm", c=1.95), D("cosine"), D("invgauss", mu=0.145), D("wald"),
+                D("betabinom", n=20, a=2.5, b=1.5), D("hypergeom", M=50, n=12, N=20)]
 
-    n, d = 30_000, 25
+    n, d = 30_000, 27
     C = np.corrcoef(np.random.default_rng(d).normal(size=(d, d + 2)))
     ds = graph()
     root = NoOp(*ds).correlate(*ds, corr_mat=C)
