@@ -135,7 +135,8 @@ typedef enum pbh_dist {
   PBH_DIST_INVGAUSS = 90,     /* mu       log-cdf / log-sf root in log x by bracketed Newton */
   PBH_DIST_WALD = 91,         /*          invgauss with mu = 1 */
   PBH_DIST_BETABINOM = 92,    /* n, a, b, loc (discrete)  first k with sum of the pmf over [0, k] >= q */
-  PBH_DIST_HYPERGEOM = 93     /* M, n, N, loc (discrete)  the same over [max(0, N - M + n), min(n, N)] */
+  PBH_DIST_HYPERGEOM = 93,    /* M, n, N, loc (discrete)  the same over [max(0, N - M + n), min(n, N)] */
+  PBH_DIST_SKEWNORM = 94      /* a        cdf / sf root by bracketed Newton, Owen's T by Gauss-Legendre */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

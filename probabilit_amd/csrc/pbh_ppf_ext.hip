@@ -349,7 +349,7 @@ void attach_table(int dist, const double* t, Params4& p) {
 
 constexpr bool is_closed(int d) {
   return (d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID) || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T ||
-         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME) || (d >= PBH_DIST_PEARSON3 && d <= PBH_DIST_WALD);
+         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME) || (d >= PBH_DIST_PEARSON3 && d <= PBH_DIST_WALD) || d == PBH_DIST_SKEWNORM;
 }
 // discrete distributions beyond binom / bernoulli (round 5): p, loc / low, high, loc / n, p, loc;
 // round 6: a, loc (dlaplace) / lambda, loc (planck) / lambda, N, loc (boltzmann)
@@ -374,7 +374,7 @@ constexpr int closed_shapes(int d) {
             d == PBH_DIST_LAPLACE_ASYMMETRIC || d == PBH_DIST_TUKEYLAMBDA || d == PBH_DIST_LOGGAMMA ||
             d == PBH_DIST_DGAMMA || d == PBH_DIST_RDIST || d == PBH_DIST_PEARSON3 || d == PBH_DIST_GENNORM ||
             d == PBH_DIST_HALFGENNORM || d == PBH_DIST_WRAPCAUCHY || d == PBH_DIST_SKEWCAUCHY ||
-            d == PBH_DIST_FOLDCAUCHY || d == PBH_DIST_FOLDNORM || d == PBH_DIST_INVGAUSS)
+            d == PBH_DIST_FOLDCAUCHY || d == PBH_DIST_FOLDNORM || d == PBH_DIST_INVGAUSS || d == PBH_DIST_SKEWNORM)
              ? 1
              : 0;
 }
@@ -537,6 +537,52 @@ __device__ __forceinline__ double cosine_ppf01(double q) {
   return up ? sf::kPi - y : y - sf::kPi;
 }
 
+// skewnorm(a): scipy's ppf is Boost's skew_normal quantile, Newton on cdf(x) = Phi(x) - 2 T(x, a)
+// (T: Owen's function).  Solved here the same way, the complement sf(x) = Phi(-x) + 2 T(x, a) above
+// q = 1/2.  Boost's own cdf loses its relative precision in the left tail for a > 0 (scipy's _cdf
+// says so and patches it; its _ppf does not), so the two agree to 1e-10 for q in [1e-6, 1 - 1e-6].
+// Owen's T(h, a) = (1 / 2 pi) int_0^a exp(-h^2 (1 + x^2) / 2) / (1 + x^2) dx for 0 <= a <= 1 by
+// 20-point Gauss-Legendre (the integrand's poles at +-i lie a unit from [0, 1]: ~1e-18 for the h
+// where the cdf needs T to full precision), and beyond by Owen's identity
+// T(h, a) = (Phi(h) Q(ah) + Phi(ah) Q(h)) / 2 - T(ah, 1 / a), h >= 0 (Q = 1 - Phi, no cancellation).
+__device__ __forceinline__ double owens_t01(double h, double a) {
+  const double T[10] = {0.07652652113349734, 0.2277858511416451, 0.37370608871541955, 0.5108670019508271,
+                        0.636053680726515,   0.7463319064601508, 0.8391169718222188,  0.9122344282513258,
+                        0.9639719272779138,  0.9931285991850949};
+  const double W[10] = {0.15275338713072578, 0.14917298647260366, 0.14209610931838187, 0.13168863844917653,
+                        0.11819453196151825, 0.10193011981724026, 0.08327674157670467, 0.06267204833410944,
+                        0.04060142980038622, 0.017614007139153273};
+  const double hh = -0.5 * h * h;
+  double acc = 0.0;
+  for (int i = 0; i < 10; ++i) {
+    const double xp = 0.5 * a * (1.0 + T[i]), xm = 0.5 * a * (1.0 - T[i]);
+    const double up = 1.0 + xp * xp, um = 1.0 + xm * xm;
+    acc += W[i] * (exp(hh * up) / up + exp(hh * um) / um);
+  }
+  return acc * (0.25 * a / sf::kPi);
+}
+__device__ __forceinline__ double owens_t(double h, double a) {
+  const double sg = a < 0.0 ? -1.0 : 1.0;  // T(h, -a) = -T(h, a), T(-h, a) = T(h, a)
+  a = fabs(a);
+  h = fabs(h);
+  if (a <= 1.0) return sg * owens_t01(h, a);
+  const double ah = a * h;
+  const double v = 0.5 * (sfx::ndtr(h) * sfx::ndtr(-ah) + sfx::ndtr(ah) * sfx::ndtr(-h)) - owens_t01(ah, 1.0 / a);
+  return sg * v;
+}
+__device__ __forceinline__ double skewnorm_ppf01(double q, double a) {
+  constexpr double kRs2pi = 0.3989422804014327;  // 1 / sqrt(2 pi)
+  auto pdf = [a](double x) { return 2.0 * kRs2pi * exp(-0.5 * x * x) * sfx::ndtr(a * x); };
+  const double x0 = fmin(fmax(sf::ndtri(q) + a / sqrt(1.0 + a * a) * 0.7978845608028654, -39.0), 39.0);
+  if (q <= 0.5) {
+    auto cdf = [a](double x) { return sfx::ndtr(x) - 2.0 * owens_t(x, a); };
+    return bracket_newton(cdf, pdf, q, -40.0, 40.0, x0, true);
+  }
+  auto sfn = [a](double x) { return sfx::ndtr(-x) + 2.0 * owens_t(x, a); };
+  auto dsf = [&pdf](double x) { return -pdf(x); };
+  return bracket_newton(sfn, dsf, 1.0 - q, -40.0, 40.0, x0, false);
+}
+
 // _argcheck and the support [_a, _b] of scipy's class (rv_continuous default: every shape > 0)
 template <int D>
 __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo, double& hi) {
@@ -642,6 +688,7 @@ __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo,
     lo = 0.0;
     return s0 >= 0.0;
   }
+  if constexpr (D == PBH_DIST_SKEWNORM) return isfinite(s0);  // _argcheck isfinite(a)
   if constexpr (D == PBH_DIST_COSINE) {
     lo = -sf::kPi;
     hi = sf::kPi;
@@ -839,6 +886,7 @@ __device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
   if constexpr (D == PBH_DIST_COSINE) return cosine_ppf01(q);
   if constexpr (D == PBH_DIST_INVGAUSS) return invgauss_ppf01(q, s0);
   if constexpr (D == PBH_DIST_WALD) return invgauss_ppf01(q, 1.0);
+  if constexpr (D == PBH_DIST_SKEWNORM) return skewnorm_ppf01(q, s0);
   return sf::kNaN;
 }
 
@@ -1114,6 +1162,7 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_WALD)
     PBH_EXT(PBH_DIST_BETABINOM)
     PBH_EXT(PBH_DIST_HYPERGEOM)
+    PBH_EXT(PBH_DIST_SKEWNORM)
 #undef PBH_EXT
     default:
       return false;

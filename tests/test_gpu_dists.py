@@ -649,6 +649,33 @@ def test_round6_summed_discrete_ppf(gpu, name, kw):
     np.testing.assert_array_equal(native.ppf(name, ql, **kw2), getattr(scipy.stats, name)(**kw2).ppf(ql))
 
 
+@pytest.mark.parametrize("kw", [dict(a=4.0), dict(a=-3.0, loc=1.0), dict(a=0.5, scale=2.0), dict(a=25.0),
+                                dict(a=0.0)])
+def test_skewnorm_ppf(gpu, kw):
+    """skewnorm: scipy's ppf is Boost's quantile on its cdf Phi(x) - 2 T(x, a), whose left tail loses
+    its relative precision for a > 0 (scipy's _cdf says so and patches it, its _ppf does not): compared
+    at 1e-10 for q in [1e-6, 1 - 1e-6]; the edges as rv_continuous.ppf has them."""
+    import scipy.stats
+
+    from probabilit_amd import native
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.qmc import seed_from
+
+    q = np.concatenate([_q(20_000, 53), np.linspace(0.01, 0.99, 2001), [-0.5, 1.5, np.nan]])
+    ref = scipy.stats.skewnorm(**kw).ppf(q)
+    got = native.ppf("skewnorm", q, **kw)
+    mid = (q >= 1e-6) & (q <= 1 - 1e-6)
+    assert_close(got[mid], ref[mid], rtol=1e-10, atol=1e-13, what=f"skewnorm {kw}")
+    edge = ~mid & ~((q > 0) & (q < 1))
+    np.testing.assert_array_equal(got[edge], ref[edge])
+    assert np.all(np.isfinite(got[~mid & (q > 0) & (q < 1)]))
+    n, s = 30_000, 59
+    ql = native.fill_lhs(seed_from(s), n, 1)[:, 0]
+    lm = (ql >= 1e-6) & (ql <= 1 - 1e-6)
+    got = D("skewnorm", **kw).sample(n, method="lhs", random_state=s)
+    assert_close(got[lm], scipy.stats.skewnorm(**kw).ppf(ql[lm]), rtol=1e-10, atol=1e-13, what=f"LHS skewnorm {kw}")
+
+
 def test_round6_generated_iman_conover(gpu):
     """The round-6 names correlated with method="lhs" take the generated-column path (dlaplace /
     planck / boltzmann with their run heads): bit-identical to the general path on the same native
@@ -667,9 +694,9 @@ def test_round6_generated_iman_conover(gpu):
                 D("skewcauchy", a=0.4), D("moyal"), D("kappa4", h=0.1, k=0.3), D("crystalball", beta=2.0, m=3.0),
                 D("powerlognorm", c=2.14, s=0.446), D("jf_skew_t", a=8.0, b=4.0), D("foldcauchy", c=4.72),
                 D("foldnorm", c=1.95), D("cosine"), D("invgauss", mu=0.145), D("wald"),
-                D("betabinom", n=20, a=2.5, b=1.5), D("hypergeom", M=50, n=12, N=20)]
+                D("betabinom", n=20, a=2.5, b=1.5), D("hypergeom", M=50, n=12, N=20), D("skewnorm", a=4.0)]
 
-    n, d = 30_000, 27
+    n, d = 30_000, 28
     C = np.corrcoef(np.random.default_rng(d).normal(size=(d, d + 2)))
     ds = graph()
     root = NoOp(*ds).correlate(*ds, corr_mat=C)
