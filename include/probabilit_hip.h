@@ -136,7 +136,11 @@ typedef enum pbh_dist {
   PBH_DIST_WALD = 91,         /*          invgauss with mu = 1 */
   PBH_DIST_BETABINOM = 92,    /* n, a, b, loc (discrete)  first k with sum of the pmf over [0, k] >= q */
   PBH_DIST_HYPERGEOM = 93,    /* M, n, N, loc (discrete)  the same over [max(0, N - M + n), min(n, N)] */
-  PBH_DIST_SKEWNORM = 94      /* a        cdf / sf root by bracketed Newton, Owen's T by Gauss-Legendre */
+  PBH_DIST_SKEWNORM = 94,     /* a        cdf / sf root by bracketed Newton, Owen's T by Gauss-Legendre */
+  PBH_DIST_RECIPINVGAUSS = 95, /* mu      1 / invgauss's (1 - q)-quantile */
+  PBH_DIST_EXPONNORM = 96,    /* K        cdf / sf root by bracketed Newton */
+  PBH_DIST_ARGUS = 97,        /* chi      cdf / sf root by bracketed Newton, sf from gammainc(1.5, .) */
+  PBH_DIST_KSTWOBIGN = 98     /*          kolmogci: theta-series cdf / alternating-series sf root */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

@@ -349,7 +349,7 @@ void attach_table(int dist, const double* t, Params4& p) {
 
 constexpr bool is_closed(int d) {
   return (d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID) || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T ||
-         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME) || (d >= PBH_DIST_PEARSON3 && d <= PBH_DIST_WALD) || d == PBH_DIST_SKEWNORM;
+         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME) || (d >= PBH_DIST_PEARSON3 && d <= PBH_DIST_WALD) || (d >= PBH_DIST_SKEWNORM && d <= PBH_DIST_KSTWOBIGN);
 }
 // discrete distributions beyond binom / bernoulli (round 5): p, loc / low, high, loc / n, p, loc;
 // round 6: a, loc (dlaplace) / lambda, loc (planck) / lambda, N, loc (boltzmann)
@@ -374,7 +374,8 @@ constexpr int closed_shapes(int d) {
             d == PBH_DIST_LAPLACE_ASYMMETRIC || d == PBH_DIST_TUKEYLAMBDA || d == PBH_DIST_LOGGAMMA ||
             d == PBH_DIST_DGAMMA || d == PBH_DIST_RDIST || d == PBH_DIST_PEARSON3 || d == PBH_DIST_GENNORM ||
             d == PBH_DIST_HALFGENNORM || d == PBH_DIST_WRAPCAUCHY || d == PBH_DIST_SKEWCAUCHY ||
-            d == PBH_DIST_FOLDCAUCHY || d == PBH_DIST_FOLDNORM || d == PBH_DIST_INVGAUSS || d == PBH_DIST_SKEWNORM)
+            d == PBH_DIST_FOLDCAUCHY || d == PBH_DIST_FOLDNORM || d == PBH_DIST_INVGAUSS || d == PBH_DIST_SKEWNORM ||
+            d == PBH_DIST_RECIPINVGAUSS || d == PBH_DIST_EXPONNORM || d == PBH_DIST_ARGUS)
              ? 1
              : 0;
 }
@@ -480,29 +481,108 @@ __device__ __forceinline__ double invgauss_logsf(double x, double mu) {
   const double b = 2.0 / mu + sfx::log_ndtr(-fac * (x + mu) / mu);
   return a + log1p(-exp(b - a));
 }
-__device__ __forceinline__ double invgauss_ppf01(double q, double mu) {
+// the x with cdf(x) = t (upper: sf(x) = t), t <= 1/2
+__device__ __forceinline__ double invgauss_solve(double mu, double t, bool upper) {
   // log(x pdf(x)) = -log(2 pi x) / 2 - (x - mu)^2 / (2 x mu^2)
   auto lxpdf = [mu](double x) { return -0.5 * log(2.0 * sf::kPi * x) - (x - mu) * (x - mu) / (2.0 * x * mu * mu); };
-  const double s2 = log1p(mu), u0 = log(mu) - 0.5 * s2 + sqrt(s2) * sf::ndtri(q);
+  const double s2 = log1p(mu), u0 = log(mu) - 0.5 * s2 + sqrt(s2) * sf::ndtri(upper ? 1.0 - t : t);
   const double lo = -744.0, hi = 709.0;
   const double us = fmin(fmax(u0, lo + 1.0), hi - 1.0);
   double u;
-  if (q <= 0.5) {
+  if (!upper) {
     auto f = [mu](double v) { return invgauss_logcdf(exp(v), mu); };
     auto fp = [mu, &lxpdf](double v) {
       const double x = exp(v);
       return exp(lxpdf(x) - invgauss_logcdf(x, mu));
     };
-    u = bracket_newton(f, fp, log(q), lo, hi, us, true);
+    u = bracket_newton(f, fp, log(t), lo, hi, us, true);
   } else {
     auto f = [mu](double v) { return invgauss_logsf(exp(v), mu); };
     auto fp = [mu, &lxpdf](double v) {
       const double x = exp(v);
       return -exp(lxpdf(x) - invgauss_logsf(x, mu));
     };
-    u = bracket_newton(f, fp, log1p(-q), lo, hi, us, false);
+    u = bracket_newton(f, fp, log(t), lo, hi, us, false);
   }
   return exp(u);
+}
+__device__ __forceinline__ double invgauss_ppf01(double q, double mu) {
+  return q <= 0.5 ? invgauss_solve(mu, q, false) : invgauss_solve(mu, 1.0 - q, true);
+}
+// recipinvgauss(mu) is 1 / invgauss(mu): its q-quantile is 1 / invgauss's (1 - q)-quantile, solved on
+// the side that keeps q exact (scipy: brentq on recipinvgauss._cdf)
+__device__ __forceinline__ double recipinvgauss_ppf01(double q, double mu) {
+  return 1.0 / (q <= 0.5 ? invgauss_solve(mu, q, true) : invgauss_solve(mu, 1.0 - q, false));
+}
+
+// exponnorm(K) (scipy: brentq on _cdf): cdf = Phi(x) - exp(e(x)), sf = Phi(-x) + exp(e(x)),
+// e(x) = (0.5 / K - x) / K + log_ndtr(x - 1 / K), density exp(e(x)) / K
+__device__ __forceinline__ double exponnorm_ppf01(double q, double K) {
+  const double invK = 1.0 / K;
+  auto e = [invK](double x) { return invK * (0.5 * invK - x) + sfx::log_ndtr(x - invK); };
+  auto pdf = [invK, e](double x) { return exp(e(x)) * invK; };
+  const double lo = -40.0, hi = 40.0 + 40.0 * K;
+  const double x0 = fmin(fmax(sf::ndtri(q) + K, lo + 1.0), hi - 1.0);
+  if (q <= 0.5) {
+    auto cdf = [e](double x) { return sfx::ndtr(x) - exp(e(x)); };
+    return bracket_newton(cdf, pdf, q, lo, hi, x0, true);
+  }
+  auto sfn = [e](double x) { return sfx::ndtr(-x) + exp(e(x)); };
+  auto dsf = [&pdf](double x) { return -pdf(x); };
+  return bracket_newton(sfn, dsf, 1.0 - q, lo, hi, x0, false);
+}
+
+// argus(chi) (scipy: brentq on _cdf = 1 - _sf): sf = Psi(chi sqrt((1 - x)(1 + x))) / Psi(chi),
+// Psi(c) = gammainc(1.5, c^2 / 2) / 2, density from scipy's _logpdf
+__device__ __forceinline__ double argus_ppf01(double q, double chi) {
+  auto psi = [](double c) { return sf::igam(1.5, c * c / 2) / 2; };
+  const double pc = psi(chi);
+  const double A = 3 * log(chi) - 0.9189385332046727 - log(pc);  // _norm_pdf_logC = log(sqrt(2 pi))
+  auto pdf = [chi, A](double x) { return exp(A + log(x) + 0.5 * log1p(-x * x) - chi * chi * (1.0 - x * x) / 2); };
+  auto sfn = [chi, pc, psi](double x) { return psi(chi * sqrt((1 - x) * (1 + x))) / pc; };
+  if (q <= 0.5) {
+    auto cdf = [&sfn](double x) { return 1.0 - sfn(x); };
+    return bracket_newton(cdf, pdf, q, 0.0, 1.0, 0.5, true);
+  }
+  auto dsf = [&pdf](double x) { return -pdf(x); };
+  return bracket_newton(sfn, dsf, 1.0 - q, 0.0, 1.0, 0.5, false);
+}
+
+// kstwobign (scipy: kolmogci, the inverse of the Kolmogorov distribution's cdf): below x = 0.82 the
+// cdf's theta-function form sqrt(2 pi) / x sum exp(-(2k - 1)^2 pi^2 / (8 x^2)), above it the
+// complement 2 sum (-1)^(k - 1) exp(-2 k^2 x^2); the quantile on the side that keeps q exact
+__device__ __forceinline__ double kolmog_cdf_small(double x) {
+  double s = 0.0;
+  const double w = -sf::kPi * sf::kPi / (8.0 * x * x);
+  for (int k = 1; k <= 4; ++k) s += exp((2.0 * k - 1) * (2.0 * k - 1) * w);
+  return 2.5066282746310002 / x * s;
+}
+__device__ __forceinline__ double kolmog_sf_large(double x) {
+  double s = 0.0, sg = 1.0;
+  for (int k = 1; k <= 10; ++k, sg = -sg) s += sg * exp(-2.0 * k * k * x * x);
+  return 2.0 * s;
+}
+__device__ __forceinline__ double kolmog_pdf(double x) {
+  if (x < 0.82) {
+    const double a = sf::kPi * sf::kPi / 8.0;
+    double s = 0.0;
+    for (int k = 1; k <= 4; ++k) {
+      const double ak = (2.0 * k - 1) * (2.0 * k - 1) * a;
+      s += exp(-ak / (x * x)) * (2.0 * ak / (x * x * x * x) - 1.0 / (x * x));
+    }
+    return 2.5066282746310002 * s;
+  }
+  double s = 0.0, sg = 1.0;
+  for (int k = 1; k <= 10; ++k, sg = -sg) s += sg * k * k * exp(-2.0 * k * k * x * x);
+  return 8.0 * x * s;
+}
+__device__ __forceinline__ double kstwobign_ppf01(double q) {
+  auto cdf = [](double x) { return x < 0.82 ? kolmog_cdf_small(x) : 1.0 - kolmog_sf_large(x); };
+  auto sfn = [](double x) { return x < 0.82 ? 1.0 - kolmog_cdf_small(x) : kolmog_sf_large(x); };
+  auto pdf = [](double x) { return kolmog_pdf(x); };
+  auto dsf = [](double x) { return -kolmog_pdf(x); };
+  if (q <= 0.5) return bracket_newton(cdf, pdf, q, 0.02, 10.0, 0.8, true);
+  return bracket_newton(sfn, dsf, 1.0 - q, 0.02, 10.0, 1.0, false);
 }
 
 // cosine: cdf(x) = (pi + x + sin x) / (2 pi), symmetric about 0.  Central q: x + sin x = pi (2 q - 1)
@@ -689,6 +769,11 @@ __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo,
     return s0 >= 0.0;
   }
   if constexpr (D == PBH_DIST_SKEWNORM) return isfinite(s0);  // _argcheck isfinite(a)
+  if constexpr (D == PBH_DIST_RECIPINVGAUSS || D == PBH_DIST_KSTWOBIGN) lo = 0.0;
+  if constexpr (D == PBH_DIST_ARGUS) {
+    lo = 0.0;
+    hi = 1.0;
+  }
   if constexpr (D == PBH_DIST_COSINE) {
     lo = -sf::kPi;
     hi = sf::kPi;
@@ -887,6 +972,10 @@ __device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
   if constexpr (D == PBH_DIST_INVGAUSS) return invgauss_ppf01(q, s0);
   if constexpr (D == PBH_DIST_WALD) return invgauss_ppf01(q, 1.0);
   if constexpr (D == PBH_DIST_SKEWNORM) return skewnorm_ppf01(q, s0);
+  if constexpr (D == PBH_DIST_RECIPINVGAUSS) return recipinvgauss_ppf01(q, s0);
+  if constexpr (D == PBH_DIST_EXPONNORM) return exponnorm_ppf01(q, s0);
+  if constexpr (D == PBH_DIST_ARGUS) return argus_ppf01(q, s0);
+  if constexpr (D == PBH_DIST_KSTWOBIGN) return kstwobign_ppf01(q);
   return sf::kNaN;
 }
 
@@ -1163,6 +1252,10 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_BETABINOM)
     PBH_EXT(PBH_DIST_HYPERGEOM)
     PBH_EXT(PBH_DIST_SKEWNORM)
+    PBH_EXT(PBH_DIST_RECIPINVGAUSS)
+    PBH_EXT(PBH_DIST_EXPONNORM)
+    PBH_EXT(PBH_DIST_ARGUS)
+    PBH_EXT(PBH_DIST_KSTWOBIGN)
 #undef PBH_EXT
     default:
       return false;

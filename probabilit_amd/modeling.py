@@ -718,7 +718,7 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "skewcauchy": ("a",), "moyal": (), "kappa4": ("h", "k"), "crystalball": ("beta", "m"),
                 "powerlognorm": ("c", "s"), "jf_skew_t": ("a", "b"), "foldcauchy": ("c",), "foldnorm": ("c",),
                 "cosine": (), "invgauss": ("mu",), "wald": (), "betabinom": ("n", "a", "b"), "hypergeom": ("M", "n", "N"),
-                "skewnorm": ("a",)}
+                "skewnorm": ("a",), "recipinvgauss": ("mu",), "exponnorm": ("K",), "argus": ("chi",), "kstwobign": ()}
 _DISCRETE = {"poisson", "binom", "bernoulli", "geom", "randint", "nbinom", "dlaplace", "planck", "boltzmann", "betabinom",
              "hypergeom"}
 # distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so

@@ -571,8 +571,10 @@ _R6_CONT3 = [("powerlognorm", dict(c=2.14, s=0.446)), ("powerlognorm", dict(c=0.
              ("foldcauchy", dict(c=4.72)), ("foldcauchy", dict(c=0.0)), ("foldnorm", dict(c=1.95)),
              ("foldnorm", dict(c=0.0, scale=2.0)), ("cosine", dict()), ("cosine", dict(loc=1.0, scale=0.5)),
              ("invgauss", dict(mu=0.145)), ("invgauss", dict(mu=3.0)), ("invgauss", dict(mu=25.0)),
-             ("wald", dict()), ("wald", dict(loc=-1.0, scale=2.0))]
-_GENERIC_PPF = ("foldcauchy", "foldnorm")
+             ("wald", dict()), ("wald", dict(loc=-1.0, scale=2.0)), ("recipinvgauss", dict(mu=0.63)),
+             ("recipinvgauss", dict(mu=4.0, loc=0.5)), ("exponnorm", dict(K=1.5)), ("exponnorm", dict(K=0.2, scale=3.0)),
+             ("argus", dict(chi=1.0)), ("argus", dict(chi=4.0)), ("kstwobign", dict()), ("kstwobign", dict(loc=1.0))]
+_GENERIC_PPF = ("foldcauchy", "foldnorm", "recipinvgauss", "exponnorm", "argus")
 
 
 def _check_third(name, kw, q, got, ref, what):
@@ -694,9 +696,10 @@ def test_round6_generated_iman_conover(gpu):
                 D("skewcauchy", a=0.4), D("moyal"), D("kappa4", h=0.1, k=0.3), D("crystalball", beta=2.0, m=3.0),
                 D("powerlognorm", c=2.14, s=0.446), D("jf_skew_t", a=8.0, b=4.0), D("foldcauchy", c=4.72),
                 D("foldnorm", c=1.95), D("cosine"), D("invgauss", mu=0.145), D("wald"),
-                D("betabinom", n=20, a=2.5, b=1.5), D("hypergeom", M=50, n=12, N=20), D("skewnorm", a=4.0)]
+                D("betabinom", n=20, a=2.5, b=1.5), D("hypergeom", M=50, n=12, N=20), D("skewnorm", a=4.0),
+                D("recipinvgauss", mu=0.63), D("exponnorm", K=1.5), D("argus", chi=1.0), D("kstwobign")]
 
-    n, d = 30_000, 28
+    n, d = 30_000, 32
     C = np.corrcoef(np.random.default_rng(d).normal(size=(d, d + 2)))
     ds = graph()
     root = NoOp(*ds).correlate(*ds, corr_mat=C)
