@@ -637,6 +637,10 @@ constexpr int kBinCap = 32;
 // per item; a bucket whose runs hold more than kFQCap items reads the rest from global memory):
 // faster standalone, but the default without it measured ~2 ms per step faster in the pipeline.
 constexpr int kFQCap = 512;
+#ifndef PBH_FINISH_NT
+#define PBH_FINISH_NT 512  // threads of k_finish_q; 1024 (two items of each bucket per thread, 16-wave
+                           // barriers) measured 120 against 113-116 ms per step (profiles/r06/ab_finish_nt_r6fn.log)
+#endif
 
 template <int BINS, int FB>
 union FinishQLds {
@@ -654,7 +658,7 @@ union FinishQLds {
 // Q = false: no queue, the run members read the CS values of their run from global memory in
 // pass 2 (as k_finish_ah does in its one loop)
 template <int BINS, int NT, bool Q = true>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 8 : 4))) void k_finish_q(
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 512 ? 8 : 4))) void k_finish_q(
     const uint16_t* __restrict__ keys, const uint32_t* __restrict__ rows, const double* __restrict__ x,
     const uint32_t* __restrict__ start, int s_top, uint32_t* __restrict__ gcur, int cpad, uint64_t* __restrict__ out,
     int32_t* __restrict__ flags, const int32_t* __restrict__ state) {
@@ -664,7 +668,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
   constexpr int kPer = BINS / NT;
   constexpr int kIt = kBucketCap2 / NT;  // items of a bucket per thread
   __shared__ FinishQLds<BINS, FB> L;
-  __shared__ uint32_t gcnt[256], goff[264], gbase[256];
+  __shared__ uint32_t gcnt[256], goff[256 + NT / 64], gbase[256];
   __shared__ int bad;
   __shared__ uint32_t nq;
   const int t = threadIdx.x;
@@ -1212,7 +1216,7 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     // output were measured and removed: profiles/r03/, r04/README_ab.md)
     uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
     PBH_TIMED(kKFinish, s,
-              hipLaunchKernelGGL((k_finish_q<2048, 512, false>), dim3(65536 / 2), dim3(512), 0, s, cb.keys16,
+              hipLaunchKernelGGL((k_finish_q<2048, PBH_FINISH_NT, false>), dim3(65536 / 2), dim3(PBH_FINISH_NT), 0, s, cb.keys16,
                                  cb.rows2, cs, start, s_top, gc, cur_pad(), cb.pairs[0], sh.flags + c, state));
   }
   PBH_CHECK_LAUNCH();
