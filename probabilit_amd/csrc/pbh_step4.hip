@@ -637,6 +637,10 @@ constexpr int kBinCap = 32;
 // per item; a bucket whose runs hold more than kFQCap items reads the rest from global memory):
 // faster standalone, but the default without it measured ~2 ms per step faster in the pipeline.
 constexpr int kFQCap = 512;
+#ifndef PBH_FINISH_BINS
+#define PBH_FINISH_BINS 2048  // counting bins of k_finish_q (4096: 113.8-114.4 against 113.5-114.8 ms per
+                              // step, no gain: profiles/r06/ab_finish_bins_r6fb.log)
+#endif
 #ifndef PBH_FINISH_NT
 #define PBH_FINISH_NT 512  // threads of k_finish_q; 1024 (two items of each bucket per thread, 16-wave
                            // barriers) measured 120 against 113-116 ms per step (profiles/r06/ab_finish_nt_r6fn.log)
@@ -1216,7 +1220,7 @@ int step4_gen_column(int c, const uint32_t* codes, const double* cs, int64_t n, 
     // output were measured and removed: profiles/r03/, r04/README_ab.md)
     uint32_t* gc = sh.curF + (int64_t)c * 8 * 256 * cur_pad();
     PBH_TIMED(kKFinish, s,
-              hipLaunchKernelGGL((k_finish_q<2048, PBH_FINISH_NT, false>), dim3(65536 / 2), dim3(PBH_FINISH_NT), 0, s, cb.keys16,
+              hipLaunchKernelGGL((k_finish_q<PBH_FINISH_BINS, PBH_FINISH_NT, false>), dim3(65536 / 2), dim3(PBH_FINISH_NT), 0, s, cb.keys16,
                                  cb.rows2, cs, start, s_top, gc, cur_pad(), cb.pairs[0], sh.flags + c, state));
   }
   PBH_CHECK_LAUNCH();
