@@ -140,7 +140,9 @@ typedef enum pbh_dist {
   PBH_DIST_RECIPINVGAUSS = 95, /* mu      1 / invgauss's (1 - q)-quantile */
   PBH_DIST_EXPONNORM = 96,    /* K        cdf / sf root by bracketed Newton */
   PBH_DIST_ARGUS = 97,        /* chi      cdf / sf root by bracketed Newton, sf from gammainc(1.5, .) */
-  PBH_DIST_KSTWOBIGN = 98     /*          kolmogci: theta-series cdf / alternating-series sf root */
+  PBH_DIST_KSTWOBIGN = 98,    /*          kolmogci: theta-series cdf / alternating-series sf root */
+  PBH_DIST_NHYPERGEOM = 99,   /* M, n, r, loc (discrete)  first k with sum of the pmf over [0, k] >= q */
+  PBH_DIST_YULESIMON = 100    /* alpha, loc (discrete)  first k >= 1 with 1 - k B(k, alpha + 1) >= q */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

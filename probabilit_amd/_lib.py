@@ -26,7 +26,8 @@ DIST_IDS = {"norm": 0, "uniform": 1, "expon": 2, "lognorm": 3, "triang": 4, "gam
             "pearson3": 77, "gennorm": 78, "halfgennorm": 79, "wrapcauchy": 80, "skewcauchy": 81, "moyal": 82,
             "kappa4": 83, "crystalball": 84, "powerlognorm": 85, "jf_skew_t": 86, "foldcauchy": 87, "foldnorm": 88,
             "cosine": 89, "invgauss": 90, "wald": 91, "betabinom": 92, "hypergeom": 93, "skewnorm": 94,
-            "recipinvgauss": 95, "exponnorm": 96, "argus": 97, "kstwobign": 98}
+            "recipinvgauss": 95, "exponnorm": 96, "argus": 97, "kstwobign": 98,
+            "nhypergeom": 99, "yulesimon": 100}
 
 # pbh_table_kind
 TABLE_INTERP, TABLE_QUANTILE, TABLE_SEARCH = 0, 1, 2

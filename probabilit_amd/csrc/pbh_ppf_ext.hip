@@ -101,6 +101,12 @@ PBH_HD inline bool sum_bounds(int d, double s0, double s1, double s2, double* lo
     *hi = s0;
     return s0 >= 0.0 && s0 == floor(s0) && s1 > 0.0 && s2 > 0.0;
   }
+  if (d == PBH_DIST_NHYPERGEOM) {  // M, n, r: support [0, n]
+    *lo = 0.0;
+    *hi = s1;
+    return s1 >= 0.0 && s1 <= s0 && s2 >= 0.0 && s2 <= s0 - s1 && s0 == floor(s0) && s1 == floor(s1) &&
+           s2 == floor(s2);
+  }
   *lo = fmax(s2 - (s0 - s1), 0.0);  // hypergeom: M, n, N
   *hi = fmin(s1, s2);
   return s0 > 0.0 && s1 >= 0.0 && s2 >= 0.0 && s1 <= s0 && s2 <= s0 && s0 == floor(s0) && s1 == floor(s1) &&
@@ -111,7 +117,12 @@ template <int D>
 __device__ __forceinline__ double sum_pmf(double k, double s0, double s1, double s2) {
   if constexpr (D == PBH_DIST_BETABINOM)
     return exp(lchoose(s0, k) + sfx::lbeta(k + s1, s0 - k + s2) - sfx::lbeta(s1, s2));
-  else
+  else if constexpr (D == PBH_DIST_NHYPERGEOM) {  // scipy nhypergeom._logpmf (M, n, r); 1 at r = k = 0
+    if (s2 == 0.0 && k == 0.0) return 1.0;
+    const double M = s0, n = s1, r = s2;
+    return exp(-sfx::lbeta(k + 1, r) + sfx::lbeta(k + r, 1) - sfx::lbeta(n - k + 1, M - r - n + 1) +
+               sfx::lbeta(M - r - k + 1, 1) + sfx::lbeta(n + 1, M - n + 1) - sfx::lbeta(M + 1, 1));
+  } else
     return exp(lchoose(s1, k) + lchoose(s0 - s1, s2 - k) - lchoose(s0, s2));
 }
 
@@ -136,6 +147,47 @@ __device__ __forceinline__ double sum_ppf01(double q, double s0, double s1, doub
     c += sum_pmf<D>(k, s0, s1, s2);
   }
   return k;
+}
+
+// yulesimon(alpha) (round 6): scipy's generic discrete ppf on its closed cdf 1 - k B(k, alpha + 1)
+// (support k >= 1), rv_discrete._drv2_ppfsingle step for step: b grows from max(100 q, 10) by doubling
+// steps until cdf(b) >= q, then bisection with c = int((a + b) / 2) from a = 1, which returns the
+// first c it meets with cdf(c) == q -- near q = 1 the cdf rounds to q over a run of k, and scipy's
+// answer is the one its bisection path lands on, not the smallest
+__device__ __forceinline__ double yulesimon_cdf(double k, double a) { return 1.0 - k * sfx::beta_fn(k, a + 1.0); }
+__device__ __forceinline__ double yulesimon_ppf01(double q, double al) {
+  double b = fmax(100.0 * q, 10.0), step = 10.0, qb = 1.0;
+  for (int it = 0; it < 1100; ++it) {
+    if (!(b < sf::kInf)) {
+      qb = 1.0;
+      break;
+    }
+    qb = yulesimon_cdf(b, al);
+    if (qb < q) {
+      b += step;
+      step *= 2.0;
+    } else {
+      break;
+    }
+  }
+  double a = 1.0, qa = yulesimon_cdf(1.0, al);
+  for (int i = 0; i < 2046; ++i) {
+    if (qa == q) return a;
+    if (qb == q) return b;
+    if (b <= a + 1) return qa > q ? a : b;
+    const double c = trunc((a + b) / 2.0);
+    const double qc = yulesimon_cdf(c, al);
+    if (qc < q) {
+      a = c;
+      qa = qc;
+    } else if (qc > q) {
+      b = c;
+      qb = qc;
+    } else {
+      return c;
+    }
+  }
+  return sf::kNaN;
 }
 
 // the table of these two: pmf(lo + i) in parallel, then one thread sums them in the per-draw loops'
@@ -194,7 +246,7 @@ int discrete_table_len(int dist, const double* v) {
     return (int)v[0] + 1;
   }
   if (dist == PBH_DIST_BERNOULLI) return (v[0] >= 0.0 && v[0] <= 1.0) ? 2 : 0;
-  if (dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM) {  // v: the three shapes
+  if (dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM || dist == PBH_DIST_NHYPERGEOM) {  // v: the three shapes
     double lo, hi;
     if (!sum_bounds(dist, v[0], v[1], v[2], &lo, &hi) || !(hi - lo + 1.0 <= kDiscreteTableMax)) return 0;
     return (int)(hi - lo) + 1;
@@ -225,7 +277,7 @@ double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t 
     if (dist != PBH_DIST_MAXWELL && (nparams < 1 || params[0].ptr)) return nullptr;
     return gamma_guide_table(gamma_family_a(dist, nparams ? params[0].value : 0.0), s);
   }
-  if (dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM) {
+  if (dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM || dist == PBH_DIST_NHYPERGEOM) {
     if (nparams < 3 || params[0].ptr || params[1].ptr || params[2].ptr) return nullptr;
     const double v[3] = {params[0].value, params[1].value, params[2].value};
     const int len = discrete_table_len(dist, v);
@@ -238,6 +290,8 @@ double* build_table(int dist, const pbh_param* params, int nparams, hipStream_t 
       const dim3 g((unsigned)((len + 255) / 256)), b(256);
       if (dist == PBH_DIST_BETABINOM)
         hipLaunchKernelGGL(k_sum_pmf<PBH_DIST_BETABINOM>, g, b, 0, st, v[0], v[1], v[2], lo, len, t + 1);
+      else if (dist == PBH_DIST_NHYPERGEOM)
+        hipLaunchKernelGGL(k_sum_pmf<PBH_DIST_NHYPERGEOM>, g, b, 0, st, v[0], v[1], v[2], lo, len, t + 1);
       else
         hipLaunchKernelGGL(k_sum_pmf<PBH_DIST_HYPERGEOM>, g, b, 0, st, v[0], v[1], v[2], lo, len, t + 1);
       hipLaunchKernelGGL(k_sum_cdf, dim3(1), dim3(64), 0, st, len, dist == PBH_DIST_HYPERGEOM ? 1 : 0, t + 1,
@@ -336,7 +390,7 @@ void attach_table(int dist, const double* t, Params4& p) {
     const double a = gamma_family_a(dist, p.val[0]);
     p.gg = sf::GammaGuide{t, t + m, t + 2 * m, t + 3 * m, m, sf::kGammaGuideZ0, sf::kGammaGuideH, 1.0 / sf::kGammaGuideH};
     p.ga = sf::gamma_aux(a);
-  } else if (dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM) {
+  } else if (dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM || dist == PBH_DIST_NHYPERGEOM) {
     p.dlen = discrete_table_len(dist, p.val);
     p.dt = p.dlen > 0 ? t + 1 : nullptr;
   } else if (dist == PBH_DIST_BINOM || dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_NBINOM) {
@@ -355,7 +409,8 @@ constexpr bool is_closed(int d) {
 // round 6: a, loc (dlaplace) / lambda, loc (planck) / lambda, N, loc (boltzmann)
 constexpr bool is_discrete2(int d) {
   return d == PBH_DIST_GEOM || d == PBH_DIST_RANDINT || d == PBH_DIST_NBINOM || d == PBH_DIST_DLAPLACE ||
-         d == PBH_DIST_PLANCK || d == PBH_DIST_BOLTZMANN || d == PBH_DIST_BETABINOM || d == PBH_DIST_HYPERGEOM;
+         d == PBH_DIST_PLANCK || d == PBH_DIST_BOLTZMANN || d == PBH_DIST_BETABINOM || d == PBH_DIST_HYPERGEOM ||
+         d == PBH_DIST_NHYPERGEOM || d == PBH_DIST_YULESIMON;
 }
 
 constexpr int closed_shapes(int d) {
@@ -1030,7 +1085,13 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
       if (!(lam > 0.0 && N > 0.0 && N == floor(N) && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
       if (q == 1.0) return N - 1.0 + loc;
       return sfx::boltzmann_ppf01(q, lam, N) + loc;
-    } else if constexpr (D == PBH_DIST_BETABINOM || D == PBH_DIST_HYPERGEOM) {
+    } else if constexpr (D == PBH_DIST_YULESIMON) {  // support [1, inf), _argcheck alpha > 0
+      const double a = p.at(0, i), loc = p.at(1, i);
+      if (q == 0.0) return 0.0 + loc;
+      if (!(a > 0.0 && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
+      if (q == 1.0) return inf + loc;
+      return yulesimon_ppf01(q, a) + loc;
+    } else if constexpr (D == PBH_DIST_BETABINOM || D == PBH_DIST_HYPERGEOM || D == PBH_DIST_NHYPERGEOM) {
       const double s0 = p.at(0, i), s1 = p.at(1, i), s2 = p.at(2, i), loc = p.at(3, i);
       double lo, hi;
       const bool ok = sum_bounds(D, s0, s1, s2, &lo, &hi) && loc == loc;
@@ -1127,7 +1188,7 @@ constexpr int kExtLdsTab = 512;
 template <int D>
 constexpr bool ext_table_discrete() {
   return D == PBH_DIST_BINOM || D == PBH_DIST_BERNOULLI || D == PBH_DIST_NBINOM || D == PBH_DIST_BETABINOM ||
-         D == PBH_DIST_HYPERGEOM;
+         D == PBH_DIST_HYPERGEOM || D == PBH_DIST_NHYPERGEOM;
 }
 
 template <int D, bool LHS>
@@ -1256,6 +1317,8 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_EXPONNORM)
     PBH_EXT(PBH_DIST_ARGUS)
     PBH_EXT(PBH_DIST_KSTWOBIGN)
+    PBH_EXT(PBH_DIST_NHYPERGEOM)
+    PBH_EXT(PBH_DIST_YULESIMON)
 #undef PBH_EXT
     default:
       return false;
@@ -1514,11 +1577,12 @@ Params4 scalar_params(int dist, const double* val, int np, const double* table) 
 }  // namespace
 
 int ext_nparams(int dist) {
-  if (dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_GEOM || dist == PBH_DIST_DLAPLACE || dist == PBH_DIST_PLANCK)
+  if (dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_GEOM || dist == PBH_DIST_DLAPLACE || dist == PBH_DIST_PLANCK ||
+      dist == PBH_DIST_YULESIMON)
     return 2;
   if (dist == PBH_DIST_BINOM || dist == PBH_DIST_RANDINT || dist == PBH_DIST_NBINOM || dist == PBH_DIST_BOLTZMANN)
     return 3;
-  if (dist == PBH_DIST_BETA || dist == PBH_DIST_TRUNCNORM || dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM)
+  if (dist == PBH_DIST_BETA || dist == PBH_DIST_TRUNCNORM || dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM || dist == PBH_DIST_NHYPERGEOM)
     return 4;
   if (is_closed(dist)) return closed_shapes(dist) + 2;
   return -1;
@@ -1570,7 +1634,8 @@ void discrete_span(int dist, const double* val, double* span, double* loc) {
       *loc = val[2];
       break;
     case PBH_DIST_BETABINOM:
-    case PBH_DIST_HYPERGEOM: {
+    case PBH_DIST_HYPERGEOM:
+    case PBH_DIST_NHYPERGEOM: {
       double lo, hi;
       if (sum_bounds(dist, val[0], val[1], val[2], &lo, &hi)) *span = hi - lo + 1.0;
       *loc = val[3];

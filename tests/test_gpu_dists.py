@@ -627,7 +627,9 @@ def test_round6_third_set_fused_lhs_and_composite(gpu, name, kw):
 # round 6: betabinom and hypergeom, scipy's generic discrete ppf (the first k with cdf(k) >= q, cdf the
 # sum of the pmf): exact, with scalar parameters (the CDF table) and per row (the per-draw sum)
 _R6_DISCRETE3 = [("betabinom", dict(n=20, a=2.5, b=1.5)), ("betabinom", dict(n=200, a=0.6, b=3.0, loc=1)),
-                 ("hypergeom", dict(M=50, n=12, N=20)), ("hypergeom", dict(M=500, n=300, N=150, loc=-2))]
+                 ("hypergeom", dict(M=50, n=12, N=20)), ("hypergeom", dict(M=500, n=300, N=150, loc=-2)),
+                 ("nhypergeom", dict(M=40, n=12, r=8)), ("nhypergeom", dict(M=300, n=120, r=30, loc=1)),
+                 ("yulesimon", dict(alpha=3.5)), ("yulesimon", dict(alpha=11.0, loc=-1))]
 
 
 @pytest.mark.parametrize("name,kw", _R6_DISCRETE3)
@@ -697,9 +699,10 @@ def test_round6_generated_iman_conover(gpu):
                 D("powerlognorm", c=2.14, s=0.446), D("jf_skew_t", a=8.0, b=4.0), D("foldcauchy", c=4.72),
                 D("foldnorm", c=1.95), D("cosine"), D("invgauss", mu=0.145), D("wald"),
                 D("betabinom", n=20, a=2.5, b=1.5), D("hypergeom", M=50, n=12, N=20), D("skewnorm", a=4.0),
-                D("recipinvgauss", mu=0.63), D("exponnorm", K=1.5), D("argus", chi=1.0), D("kstwobign")]
+                D("recipinvgauss", mu=0.63), D("exponnorm", K=1.5), D("argus", chi=1.0), D("kstwobign"),
+                D("nhypergeom", M=40, n=12, r=8), D("yulesimon", alpha=3.5)]
 
-    n, d = 30_000, 32
+    n, d = 30_000, 34
     C = np.corrcoef(np.random.default_rng(d).normal(size=(d, d + 2)))
     ds = graph()
     root = NoOp(*ds).correlate(*ds, corr_mat=C)
