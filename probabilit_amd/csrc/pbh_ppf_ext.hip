@@ -17,6 +17,7 @@
 #include <math.h>
 
 #include "pbh_error.h"
+#include "pbh_glibc.h"
 #include "pbh_table_cache.h"
 #include "pbh_ppf_ext.h"
 #include "pbh_rng.h"
@@ -177,6 +178,75 @@ __device__ __forceinline__ double yulesimon_ppf01(double q, double al) {
     if (b <= a + 1) return qa > q ? a : b;
     const double c = trunc((a + b) / 2.0);
     const double qc = yulesimon_cdf(c, al);
+    if (qc < q) {
+      a = c;
+      qa = qc;
+    } else if (qc > q) {
+      b = c;
+      qb = qc;
+    } else {
+      return c;
+    }
+  }
+  return sf::kNaN;
+}
+
+// zipfian(a, n) (round 6): scipy's generic discrete ppf (_drv2_ppfsingle step for step, the finite
+// support [1, n]: no bracket search) on its closed cdf H(k, a) / H(n, a), H the generalized harmonic
+// number: zeta(a, 1) - zeta(a, k + 1) for a > 1 (Cephes' Hurwitz zeta, Euler-Maclaurin with its
+// twelve Bernoulli terms), else the sum of 1 / i^a from i = k down to 1 -- over glibc's pow restated,
+// as scipy's compiled zeta and numpy's power call it, so the cdf is scipy's to the bit
+__device__ __forceinline__ double hurwitz_zeta(double x, double q) {
+  const double A[12] = {12.0, -720.0, 30240.0, -1209600.0, 47900160.0, -1.8924375803183791606e9, 7.47242496e10,
+                        -2.950130727918164224e12, 1.1646782814350067249e14, -4.5979787224074726105e15,
+                        1.8152105401943546773e17, -7.1661652561756670113e18};
+  constexpr double kMachEp = 1.11022302462515654042e-16;
+  if (x == 1.0) return sf::kInf;
+  if (q > 1e8) return (1 / (x - 1) + 1 / (2 * q)) * glibc::pow(q, 1 - x);
+  double s = glibc::pow(q, -x), a = q, b = 0.0;
+  int i = 0;
+  while (i < 9 || a <= 9.0) {
+    i += 1;
+    a += 1.0;
+    b = glibc::pow(a, -x);
+    s += b;
+    if (fabs(b / s) < kMachEp) return s;
+  }
+  const double w = a;
+  s += b * w / (x - 1.0);
+  s -= 0.5 * b;
+  a = 1.0;
+  double k = 0.0;
+  for (i = 0; i < 12; ++i) {
+    a *= x + k;
+    b /= w;
+    double t = a * b / A[i];
+    s = s + t;
+    t = fabs(t / s);
+    if (t < kMachEp) return s;
+    k += 1.0;
+    a *= x + k;
+    b /= w;
+    k += 1.0;
+  }
+  return s;
+}
+__device__ __forceinline__ double gen_harmonic(double k, double a) {
+  if (a > 1) return hurwitz_zeta(a, 1.0) - hurwitz_zeta(a, k + 1);
+  double out = 0.0;
+  for (double i = k; i > 0.0; i -= 1.0) out += 1 / glibc::pow(i, a);
+  return out;
+}
+__device__ __forceinline__ double zipfian_ppf01(double q, double al, double n) {
+  const double hn = gen_harmonic(n, al);
+  auto cdf = [al, hn](double k) { return gen_harmonic(k, al) / hn; };
+  double a = 1.0, qa = cdf(1.0), b = n, qb = 1.0;
+  for (int i = 0; i < 2046; ++i) {
+    if (qa == q) return a;
+    if (qb == q) return b;
+    if (b <= a + 1) return qa > q ? a : b;
+    const double c = trunc((a + b) / 2.0);
+    const double qc = cdf(c);
     if (qc < q) {
       a = c;
       qa = qc;
@@ -410,7 +480,7 @@ constexpr bool is_closed(int d) {
 constexpr bool is_discrete2(int d) {
   return d == PBH_DIST_GEOM || d == PBH_DIST_RANDINT || d == PBH_DIST_NBINOM || d == PBH_DIST_DLAPLACE ||
          d == PBH_DIST_PLANCK || d == PBH_DIST_BOLTZMANN || d == PBH_DIST_BETABINOM || d == PBH_DIST_HYPERGEOM ||
-         d == PBH_DIST_NHYPERGEOM || d == PBH_DIST_YULESIMON;
+         d == PBH_DIST_NHYPERGEOM || d == PBH_DIST_YULESIMON || d == PBH_DIST_ZIPFIAN;
 }
 
 constexpr int closed_shapes(int d) {
@@ -1085,6 +1155,12 @@ __device__ __forceinline__ double ppf_ext_one(double q, const Params4& p, int64_
       if (!(lam > 0.0 && N > 0.0 && N == floor(N) && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
       if (q == 1.0) return N - 1.0 + loc;
       return sfx::boltzmann_ppf01(q, lam, N) + loc;
+    } else if constexpr (D == PBH_DIST_ZIPFIAN) {  // support [1, n], _argcheck a >= 0, n > 0 integral
+      const double a = p.at(0, i), nn = p.at(1, i), loc = p.at(2, i);
+      if (q == 0.0) return 0.0 + loc;
+      if (!(a >= 0.0 && nn > 0.0 && nn == floor(nn) && loc == loc) || !(q >= 0.0 && q <= 1.0)) return nan;
+      if (q == 1.0) return nn + loc;
+      return zipfian_ppf01(q, a, nn) + loc;
     } else if constexpr (D == PBH_DIST_YULESIMON) {  // support [1, inf), _argcheck alpha > 0
       const double a = p.at(0, i), loc = p.at(1, i);
       if (q == 0.0) return 0.0 + loc;
@@ -1319,6 +1395,7 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_KSTWOBIGN)
     PBH_EXT(PBH_DIST_NHYPERGEOM)
     PBH_EXT(PBH_DIST_YULESIMON)
+    PBH_EXT(PBH_DIST_ZIPFIAN)
 #undef PBH_EXT
     default:
       return false;
@@ -1580,7 +1657,8 @@ int ext_nparams(int dist) {
   if (dist == PBH_DIST_BERNOULLI || dist == PBH_DIST_GEOM || dist == PBH_DIST_DLAPLACE || dist == PBH_DIST_PLANCK ||
       dist == PBH_DIST_YULESIMON)
     return 2;
-  if (dist == PBH_DIST_BINOM || dist == PBH_DIST_RANDINT || dist == PBH_DIST_NBINOM || dist == PBH_DIST_BOLTZMANN)
+  if (dist == PBH_DIST_BINOM || dist == PBH_DIST_RANDINT || dist == PBH_DIST_NBINOM || dist == PBH_DIST_BOLTZMANN ||
+      dist == PBH_DIST_ZIPFIAN)
     return 3;
   if (dist == PBH_DIST_BETA || dist == PBH_DIST_TRUNCNORM || dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM || dist == PBH_DIST_NHYPERGEOM)
     return 4;
@@ -1631,6 +1709,10 @@ void discrete_span(int dist, const double* val, double* span, double* loc) {
       break;
     case PBH_DIST_BOLTZMANN:
       if (val[0] > 0.0 && val[1] > 0.0) *span = val[1];
+      *loc = val[2];
+      break;
+    case PBH_DIST_ZIPFIAN:
+      if (val[0] >= 0.0 && val[1] > 0.0) *span = val[1];
       *loc = val[2];
       break;
     case PBH_DIST_BETABINOM:

@@ -89,7 +89,7 @@ inline bool gen_discrete(int dist) {
          dist == PBH_DIST_GEOM || dist == PBH_DIST_RANDINT || dist == PBH_DIST_NBINOM ||
          dist == PBH_DIST_DLAPLACE || dist == PBH_DIST_PLANCK || dist == PBH_DIST_BOLTZMANN ||
          dist == PBH_DIST_BETABINOM || dist == PBH_DIST_HYPERGEOM || dist == PBH_DIST_NHYPERGEOM ||
-         dist == PBH_DIST_YULESIMON;
+         dist == PBH_DIST_YULESIMON || dist == PBH_DIST_ZIPFIAN;
 }
 int gen_create(uint64_t seed, int64_t n, int col, int dist, const pbh_param* params, int nparams, GenColumn** out,
                hipStream_t s);

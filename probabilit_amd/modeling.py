@@ -719,9 +719,10 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "powerlognorm": ("c", "s"), "jf_skew_t": ("a", "b"), "foldcauchy": ("c",), "foldnorm": ("c",),
                 "cosine": (), "invgauss": ("mu",), "wald": (), "betabinom": ("n", "a", "b"), "hypergeom": ("M", "n", "N"),
                 "skewnorm": ("a",), "recipinvgauss": ("mu",), "exponnorm": ("K",), "argus": ("chi",), "kstwobign": (),
-                "nhypergeom": ("M", "n", "r"), "yulesimon": ("alpha",)}
+                "nhypergeom": ("M", "n", "r"), "yulesimon": ("alpha",),
+                "zipfian": ("a", "n")}
 _DISCRETE = {"poisson", "binom", "bernoulli", "geom", "randint", "nbinom", "dlaplace", "planck", "boltzmann", "betabinom",
-             "hypergeom", "nhypergeom", "yulesimon"}
+             "hypergeom", "nhypergeom", "yulesimon", "zipfian"}
 # distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so
 # that Iman-Conover takes them as generated columns (pbh_ppf.hip k_lhs_sorted_ppf / k_place_gen;
 # the extended set pbh_ppf_ext.hip k_ext_sorted / k_ext_place): every distribution with a kernel

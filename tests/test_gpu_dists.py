@@ -680,6 +680,24 @@ def test_skewnorm_ppf(gpu, kw):
     assert_close(got[lm], scipy.stats.skewnorm(**kw).ppf(ql[lm]), rtol=1e-10, atol=1e-13, what=f"LHS skewnorm {kw}")
 
 
+@pytest.mark.parametrize("kw,m", [(dict(a=1.25, n=10), 3000), (dict(a=0.6, n=30, loc=2), 600), (dict(a=2.5, n=1000), 2000),
+                                  (dict(a=0.0, n=7), 2000)])
+def test_zipfian_ppf(gpu, kw, m):
+    """zipfian: scipy's bisection on H(k, a) / H(n, a), exact (scipy's own ppf is a Python loop per q,
+    so m quantiles per case)."""
+    import scipy.stats
+
+    from probabilit_amd import native
+    from probabilit_amd.modeling import Distribution as D
+    from probabilit_amd.qmc import seed_from
+
+    q = np.concatenate([_q(m, 61), np.linspace(0.01, 0.99, 99), [-0.5, 1.5, np.nan]])
+    np.testing.assert_array_equal(native.ppf("zipfian", q, **kw), scipy.stats.zipfian(**kw).ppf(q))
+    ql = native.fill_lhs(seed_from(67), m, 1)[:, 0]
+    np.testing.assert_array_equal(D("zipfian", **kw).sample(m, method="lhs", random_state=67),
+                                  scipy.stats.zipfian(**kw).ppf(ql))
+
+
 def test_round6_generated_iman_conover(gpu):
     """The round-6 names correlated with method="lhs" take the generated-column path (dlaplace /
     planck / boltzmann with their run heads): bit-identical to the general path on the same native
@@ -700,9 +718,9 @@ def test_round6_generated_iman_conover(gpu):
                 D("foldnorm", c=1.95), D("cosine"), D("invgauss", mu=0.145), D("wald"),
                 D("betabinom", n=20, a=2.5, b=1.5), D("hypergeom", M=50, n=12, N=20), D("skewnorm", a=4.0),
                 D("recipinvgauss", mu=0.63), D("exponnorm", K=1.5), D("argus", chi=1.0), D("kstwobign"),
-                D("nhypergeom", M=40, n=12, r=8), D("yulesimon", alpha=3.5)]
+                D("nhypergeom", M=40, n=12, r=8), D("yulesimon", alpha=3.5), D("zipfian", a=1.25, n=10)]
 
-    n, d = 30_000, 34
+    n, d = 30_000, 35
     C = np.corrcoef(np.random.default_rng(d).normal(size=(d, d + 2)))
     ds = graph()
     root = NoOp(*ds).correlate(*ds, corr_mat=C)
