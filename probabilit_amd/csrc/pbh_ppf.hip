@@ -2638,7 +2638,10 @@ extern "C" int pbh_lhs_ppf_columns(const pbh_ic_column* cols, int32_t k, int64_t
     PBH_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
     return PBH_OK;
   };
-  const int nl = nts < k ? nts : k;
+  // below 2^20 rows a column's kernel is a few microseconds: the lanes' events (create, record,
+  // wait, destroy on each side) would cost more host time than the overlap saves, and the setup
+  // tables are cached after the first call, so the columns go on the caller's stream in order
+  const int nl = nrows < ((int64_t)1 << 20) ? 1 : (nts < k ? nts : k);
   for (int i = 0; i < nl; ++i) {
     ts[i] = nl > 1 ? step4_side_stream(i) : s;
     if (!ts[i]) ts[i] = s;
