@@ -143,7 +143,8 @@ typedef enum pbh_dist {
   PBH_DIST_KSTWOBIGN = 98,    /*          kolmogci: theta-series cdf / alternating-series sf root */
   PBH_DIST_NHYPERGEOM = 99,   /* M, n, r, loc (discrete)  first k with sum of the pmf over [0, k] >= q */
   PBH_DIST_YULESIMON = 100,   /* alpha, loc (discrete)  first k >= 1 with 1 - k B(k, alpha + 1) >= q */
-  PBH_DIST_ZIPFIAN = 101      /* a, n, loc (discrete)  scipy's bisection on H(k, a) / H(n, a) */
+  PBH_DIST_ZIPFIAN = 101,     /* a, n, loc (discrete)  scipy's bisection on H(k, a) / H(n, a) */
+  PBH_DIST_REL_BREITWIGNER = 102 /* rho   cdf root by bracketed Newton (scipy's complex-form cdf) */
 } pbh_dist;
 
 /* A distribution parameter: a scalar (ptr == NULL) or a length-n device vector of float64

@@ -27,7 +27,8 @@ DIST_IDS = {"norm": 0, "uniform": 1, "expon": 2, "lognorm": 3, "triang": 4, "gam
             "kappa4": 83, "crystalball": 84, "powerlognorm": 85, "jf_skew_t": 86, "foldcauchy": 87, "foldnorm": 88,
             "cosine": 89, "invgauss": 90, "wald": 91, "betabinom": 92, "hypergeom": 93, "skewnorm": 94,
             "recipinvgauss": 95, "exponnorm": 96, "argus": 97, "kstwobign": 98,
-            "nhypergeom": 99, "yulesimon": 100, "zipfian": 101}
+            "nhypergeom": 99, "yulesimon": 100, "zipfian": 101,
+            "rel_breitwigner": 102}
 
 # pbh_table_kind
 TABLE_INTERP, TABLE_QUANTILE, TABLE_SEARCH = 0, 1, 2

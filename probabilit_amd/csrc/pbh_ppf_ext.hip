@@ -473,7 +473,7 @@ void attach_table(int dist, const double* t, Params4& p) {
 
 constexpr bool is_closed(int d) {
   return (d >= PBH_DIST_WEIBULL_MIN && d <= PBH_DIST_TRAPEZOID) || d == PBH_DIST_INVGAMMA || d == PBH_DIST_T ||
-         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME) || (d >= PBH_DIST_PEARSON3 && d <= PBH_DIST_WALD) || (d >= PBH_DIST_SKEWNORM && d <= PBH_DIST_KSTWOBIGN);
+         (d >= PBH_DIST_JOHNSONSU && d <= PBH_DIST_BETAPRIME) || (d >= PBH_DIST_PEARSON3 && d <= PBH_DIST_WALD) || (d >= PBH_DIST_SKEWNORM && d <= PBH_DIST_KSTWOBIGN) || d == PBH_DIST_REL_BREITWIGNER;
 }
 // discrete distributions beyond binom / bernoulli (round 5): p, loc / low, high, loc / n, p, loc;
 // round 6: a, loc (dlaplace) / lambda, loc (planck) / lambda, N, loc (boltzmann)
@@ -500,7 +500,8 @@ constexpr int closed_shapes(int d) {
             d == PBH_DIST_DGAMMA || d == PBH_DIST_RDIST || d == PBH_DIST_PEARSON3 || d == PBH_DIST_GENNORM ||
             d == PBH_DIST_HALFGENNORM || d == PBH_DIST_WRAPCAUCHY || d == PBH_DIST_SKEWCAUCHY ||
             d == PBH_DIST_FOLDCAUCHY || d == PBH_DIST_FOLDNORM || d == PBH_DIST_INVGAUSS || d == PBH_DIST_SKEWNORM ||
-            d == PBH_DIST_RECIPINVGAUSS || d == PBH_DIST_EXPONNORM || d == PBH_DIST_ARGUS)
+            d == PBH_DIST_RECIPINVGAUSS || d == PBH_DIST_EXPONNORM || d == PBH_DIST_ARGUS ||
+            d == PBH_DIST_REL_BREITWIGNER)
              ? 1
              : 0;
 }
@@ -788,6 +789,45 @@ __device__ __forceinline__ double skewnorm_ppf01(double q, double a) {
   return bracket_newton(sfn, dsf, 1.0 - q, -40.0, 40.0, x0, false);
 }
 
+// rel_breitwigner(rho) (scipy: brentq on _cdf): scipy's complex form of the cdf,
+// min(2 C Im(sqrt(-1 + i / rho) atan(x / sqrt(-rho (rho + i)))), 1), C = sqrt(2 / (1 + sqrt(1 +
+// 1 / rho^2))) / pi, in real arithmetic with the principal branches (sqrt by halves, atan(z) =
+// -(i / 2) (log(1 + i z) - log(1 - i z)) away from its cuts: z lies in the first quadrant here);
+// density C' / (((x - rho)(x + rho) / rho)^2 + 1)
+__device__ __forceinline__ void csqrt_(double re, double im, double* ore, double* oim) {
+  const double r = hypot(re, im);
+  if (re >= 0.0) {
+    const double t = sqrt((r + re) / 2);
+    *ore = t;
+    *oim = t != 0.0 ? im / (2 * t) : 0.0;
+  } else {
+    const double t = sqrt((r - re) / 2);
+    *ore = fabs(im) / (2 * t);
+    *oim = copysign(t, im);
+  }
+}
+__device__ __forceinline__ double rel_breitwigner_cdf(double x, double rho) {
+  const double C = sqrt(2 / (1 + sqrt(1 + 1 / (rho * rho)))) / sf::kPi;
+  double s1r, s1i, wr, wi;
+  csqrt_(-1.0, 1 / rho, &s1r, &s1i);
+  csqrt_(-rho * rho, -rho, &wr, &wi);
+  const double den = wr * wr + wi * wi;
+  const double zr = x * wr / den, zi = -x * wi / den;  // x / w
+  const double l1r = log(hypot(1 - zi, zr)), l1i = atan2(zr, 1 - zi);    // log(1 + i z)
+  const double l2r = log(hypot(1 + zi, -zr)), l2i = atan2(-zr, 1 + zi);  // log(1 - i z)
+  const double ar = (l1i - l2i) / 2, ai = -(l1r - l2r) / 2;             // atan(z)
+  return fmin(C * 2 * (s1r * ai + s1i * ar), 1.0);
+}
+__device__ __forceinline__ double rel_breitwigner_ppf01(double q, double rho) {
+  const double C2 = sqrt(2 * (1 + 1 / (rho * rho)) / (1 + sqrt(1 + 1 / (rho * rho)))) * 2 / sf::kPi;
+  auto pdf = [rho, C2](double x) {
+    const double u = (x - rho) * (x + rho) / rho;
+    return C2 / (u * u + 1);
+  };
+  auto cdf = [rho](double x) { return rel_breitwigner_cdf(x, rho); };
+  return bracket_newton(cdf, pdf, q, 0.0, 1e12, rho, true);
+}
+
 // _argcheck and the support [_a, _b] of scipy's class (rv_continuous default: every shape > 0)
 template <int D>
 __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo, double& hi) {
@@ -894,7 +934,7 @@ __device__ __forceinline__ bool closed_support(double s0, double s1, double& lo,
     return s0 >= 0.0;
   }
   if constexpr (D == PBH_DIST_SKEWNORM) return isfinite(s0);  // _argcheck isfinite(a)
-  if constexpr (D == PBH_DIST_RECIPINVGAUSS || D == PBH_DIST_KSTWOBIGN) lo = 0.0;
+  if constexpr (D == PBH_DIST_RECIPINVGAUSS || D == PBH_DIST_KSTWOBIGN || D == PBH_DIST_REL_BREITWIGNER) lo = 0.0;
   if constexpr (D == PBH_DIST_ARGUS) {
     lo = 0.0;
     hi = 1.0;
@@ -1101,6 +1141,7 @@ __device__ __forceinline__ double closed_ppf01(double q, double s0, double s1) {
   if constexpr (D == PBH_DIST_EXPONNORM) return exponnorm_ppf01(q, s0);
   if constexpr (D == PBH_DIST_ARGUS) return argus_ppf01(q, s0);
   if constexpr (D == PBH_DIST_KSTWOBIGN) return kstwobign_ppf01(q);
+  if constexpr (D == PBH_DIST_REL_BREITWIGNER) return rel_breitwigner_ppf01(q, s0);
   return sf::kNaN;
 }
 
@@ -1396,6 +1437,7 @@ bool dispatch_ext(int dist, F&& f) {
     PBH_EXT(PBH_DIST_NHYPERGEOM)
     PBH_EXT(PBH_DIST_YULESIMON)
     PBH_EXT(PBH_DIST_ZIPFIAN)
+    PBH_EXT(PBH_DIST_REL_BREITWIGNER)
 #undef PBH_EXT
     default:
       return false;

@@ -720,7 +720,7 @@ _DIST_SHAPES = {"norm": (), "uniform": (), "expon": (), "lognorm": ("s",), "tria
                 "cosine": (), "invgauss": ("mu",), "wald": (), "betabinom": ("n", "a", "b"), "hypergeom": ("M", "n", "N"),
                 "skewnorm": ("a",), "recipinvgauss": ("mu",), "exponnorm": ("K",), "argus": ("chi",), "kstwobign": (),
                 "nhypergeom": ("M", "n", "r"), "yulesimon": ("alpha",),
-                "zipfian": ("a", "n")}
+                "zipfian": ("a", "n"), "rel_breitwigner": ("rho",)}
 _DISCRETE = {"poisson", "binom", "bernoulli", "geom", "randint", "nbinom", "dlaplace", "planck", "boltzmann", "betabinom",
              "hypergeom", "nhypergeom", "yulesimon", "zipfian"}
 # distributions with a fused native-LHS + inverse-CDF kernel and a stratum-ordered generator, so

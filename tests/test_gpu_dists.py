@@ -573,8 +573,9 @@ _R6_CONT3 = [("powerlognorm", dict(c=2.14, s=0.446)), ("powerlognorm", dict(c=0.
              ("invgauss", dict(mu=0.145)), ("invgauss", dict(mu=3.0)), ("invgauss", dict(mu=25.0)),
              ("wald", dict()), ("wald", dict(loc=-1.0, scale=2.0)), ("recipinvgauss", dict(mu=0.63)),
              ("recipinvgauss", dict(mu=4.0, loc=0.5)), ("exponnorm", dict(K=1.5)), ("exponnorm", dict(K=0.2, scale=3.0)),
-             ("argus", dict(chi=1.0)), ("argus", dict(chi=4.0)), ("kstwobign", dict()), ("kstwobign", dict(loc=1.0))]
-_GENERIC_PPF = ("foldcauchy", "foldnorm", "recipinvgauss", "exponnorm", "argus")
+             ("argus", dict(chi=1.0)), ("argus", dict(chi=4.0)), ("kstwobign", dict()), ("kstwobign", dict(loc=1.0)),
+             ("rel_breitwigner", dict(rho=36.545)), ("rel_breitwigner", dict(rho=0.4, scale=2.0))]
+_GENERIC_PPF = ("foldcauchy", "foldnorm", "recipinvgauss", "exponnorm", "argus", "rel_breitwigner")
 
 
 def _check_third(name, kw, q, got, ref, what):
@@ -718,9 +719,10 @@ def test_round6_generated_iman_conover(gpu):
                 D("foldnorm", c=1.95), D("cosine"), D("invgauss", mu=0.145), D("wald"),
                 D("betabinom", n=20, a=2.5, b=1.5), D("hypergeom", M=50, n=12, N=20), D("skewnorm", a=4.0),
                 D("recipinvgauss", mu=0.63), D("exponnorm", K=1.5), D("argus", chi=1.0), D("kstwobign"),
-                D("nhypergeom", M=40, n=12, r=8), D("yulesimon", alpha=3.5), D("zipfian", a=1.25, n=10)]
+                D("nhypergeom", M=40, n=12, r=8), D("yulesimon", alpha=3.5), D("zipfian", a=1.25, n=10),
+                D("rel_breitwigner", rho=36.545)]
 
-    n, d = 30_000, 35
+    n, d = 30_000, 36
     C = np.corrcoef(np.random.default_rng(d).normal(size=(d, d + 2)))
     ds = graph()
     root = NoOp(*ds).correlate(*ds, corr_mat=C)
